@@ -1,0 +1,317 @@
+"""CPU (numpy) restatement of the reference's DINO-SVT forward/loss hot path.
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the CHECKER.  The product never calls it.
+
+Parity status: PINNED.  tests/test_oracle_golden.py checks every function below
+against the golden vectors in tests/golden/*.npz, which tests/golden/make_golden.py
+produced by running the reference code itself (torch 2.10 CPU, fp32).
+
+Every function cites the reference file:line it restates.  Arrays are float32 in,
+float32 out; matmuls accumulate in float32 (BLAS), the loss in float64.
+"""
+import math
+
+import numpy as np
+from scipy.special import erf
+
+LN_EPS = 1e-6  # partial(nn.LayerNorm, eps=1e-6): models/timesformer.py:386, 596
+
+
+# --------------------------------------------------------------------------- primitives
+def layer_norm(x, w, b, eps=LN_EPS):
+    """nn.LayerNorm over the last dim (biased variance)."""
+    x = x.astype(np.float32)
+    mu = x.mean(-1, keepdims=True, dtype=np.float64)
+    var = ((x - mu) ** 2).mean(-1, keepdims=True, dtype=np.float64)
+    return (((x - mu) / np.sqrt(var + eps)) * w + b).astype(np.float32)
+
+
+def gelu(x):
+    """nn.GELU() default = exact erf form (models/timesformer.py:37, 42)."""
+    return (0.5 * x * (1.0 + erf(x / np.sqrt(2.0)))).astype(np.float32)
+
+
+def linear(x, w, b=None):
+    y = x @ w.T
+    if b is not None:
+        y = y + b
+    return y.astype(np.float32)
+
+
+def softmax(x, axis=-1):
+    m = x.max(axis, keepdims=True)
+    e = np.exp(x - m)
+    return e / e.sum(axis, keepdims=True)
+
+
+def attention(x, sd, prefix, num_heads):
+    """Attention.forward  models/timesformer.py:68-87 (with_qkv=True, dropout 0).
+    x: [B, L, C] -> [B, L, C]."""
+    B, L, C = x.shape
+    d = C // num_heads
+    qkv = linear(x, sd[prefix + ".qkv.weight"], sd[prefix + ".qkv.bias"])
+    qkv = qkv.reshape(B, L, 3, num_heads, d).transpose(2, 0, 3, 1, 4)
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    attn = softmax((q @ k.transpose(0, 1, 3, 2)) * np.float32(d ** -0.5))
+    o = (attn @ v).transpose(0, 2, 1, 3).reshape(B, L, C).astype(np.float32)
+    return linear(o, sd[prefix + ".proj.weight"], sd[prefix + ".proj.bias"]), attn
+
+
+def mlp(x, sd, prefix):
+    """Mlp.forward  models/timesformer.py:46-52."""
+    h = gelu(linear(x, sd[prefix + ".fc1.weight"], sd[prefix + ".fc1.bias"]))
+    return linear(h, sd[prefix + ".fc2.weight"], sd[prefix + ".fc2.bias"])
+
+
+def nearest_index(out_size, in_size):
+    """torch upsample_nearest source index (ATen UpSample.h nearest_idx): float32 scale
+    in/out, floorf(dst*scale), clamp.  Used by the pos/time-embed resize at
+    models/timesformer.py:299 and :316."""
+    if out_size == in_size:
+        return np.arange(out_size)
+    if out_size == 2 * in_size:
+        return np.arange(out_size) >> 1
+    scale = np.float32(in_size) / np.float32(out_size)
+    idx = np.floor(np.arange(out_size, dtype=np.float32) * scale).astype(np.int64)
+    return np.minimum(idx, in_size - 1)
+
+
+# --------------------------------------------------------------------------- TimeSformer
+def patch_embed(x, w, b, patch=16):
+    """PatchEmbed.forward  models/timesformer.py:203-209: conv k=s=patch as im2col GEMM.
+    x [B,3,T,H,W] -> ([(B*T), N, C], T, W_patches)."""
+    B, Cin, T, H, W = x.shape
+    Hp, Wp = H // patch, W // patch
+    xt = x.transpose(0, 2, 1, 3, 4).reshape(B * T, Cin, H, W)
+    cols = xt[:, :, :Hp * patch, :Wp * patch].reshape(B * T, Cin, Hp, patch, Wp, patch)
+    cols = cols.transpose(0, 2, 4, 1, 3, 5).reshape(B * T, Hp * Wp, Cin * patch * patch)
+    y = cols @ w.reshape(w.shape[0], -1).T + b
+    return y.astype(np.float32), T, Wp
+
+
+def resized_pos_embed(pos, Hp, Wp):
+    """pos-embed nearest resize  models/timesformer.py:291-305. pos [1,1+P*P,C] -> [1+Hp*Wp, C]."""
+    if pos.shape[1] == 1 + Hp * Wp:
+        return pos[0]
+    P = int(math.sqrt(pos.shape[1] - 1))
+    grid = pos[0, 1:].reshape(P, P, -1)
+    ri, ci = nearest_index(Hp, P), nearest_index(Wp, P)
+    new = grid[ri][:, ci].reshape(Hp * Wp, -1)
+    return np.concatenate([pos[0, :1], new], 0)
+
+
+def resized_time_embed(temb, T):
+    """time-embed nearest resize  models/timesformer.py:313-320. temb [1,T0,C] -> [T, C]."""
+    return temb[0][nearest_index(T, temb.shape[1])]
+
+
+def block_divided(x, sd, i, B, T, W, num_heads):
+    """Block.forward divided_space_time  models/timesformer.py:116-185 (drop_path = id, eval).
+    x [B, 1+N*T, C], token 1+n*T+t = patch n of frame t."""
+    p = "blocks.%d." % i
+    _, L, C = x.shape
+    N = (L - 1) // T
+    # temporal (127-137): (b h w) t m
+    xt = x[:, 1:].reshape(B * N, T, C)
+    r, _ = attention(layer_norm(xt, sd[p + "temporal_norm1.weight"], sd[p + "temporal_norm1.bias"]),
+                     sd, p + "temporal_attn", num_heads)
+    r = linear(r.reshape(B, N * T, C), sd[p + "temporal_fc.weight"], sd[p + "temporal_fc.bias"])
+    xt = x[:, 1:] + r
+    # spatial (140-159): (b t) (h w) m with CLS replicated per frame
+    cls0 = x[:, :1]
+    xs = xt.reshape(B, N, T, C).transpose(0, 2, 1, 3).reshape(B * T, N, C)
+    xs = np.concatenate([np.repeat(cls0, T, axis=1).reshape(B * T, 1, C), xs], 1)
+    rs, _ = attention(layer_norm(xs, sd[p + "norm1.weight"], sd[p + "norm1.bias"]), sd, p + "attn", num_heads)
+    # CLS: mean over frames (162-164); patches back to (h w t) order (172-175)
+    cls = rs[:, 0].reshape(B, T, C).mean(1, keepdims=True)
+    res = rs[:, 1:].reshape(B, T, N, C).transpose(0, 2, 1, 3).reshape(B, N * T, C)
+    x = np.concatenate([cls0, xt], 1) + np.concatenate([cls, res], 1)      # 181
+    x = x + mlp(layer_norm(x, sd[p + "norm2.weight"], sd[p + "norm2.bias"]), sd, p + "mlp")  # 184
+    return x.astype(np.float32)
+
+
+def block_plain(x, sd, i, num_heads):
+    """Block.forward space_only / joint_space_time  models/timesformer.py:120-123."""
+    p = "blocks.%d." % i
+    r, _ = attention(layer_norm(x, sd[p + "norm1.weight"], sd[p + "norm1.bias"]), sd, p + "attn", num_heads)
+    x = x + r
+    return (x + mlp(layer_norm(x, sd[p + "norm2.weight"], sd[p + "norm2.bias"]), sd, p + "mlp")).astype(np.float32)
+
+
+def embed_tokens(sd, x, attention_type="divided_space_time"):
+    """forward_features token assembly  models/timesformer.py:285-323."""
+    B = x.shape[0]
+    tok, T, Wp = patch_embed(x, sd["patch_embed.proj.weight"], sd["patch_embed.proj.bias"])
+    BT, Np, C = tok.shape
+    Hp = Np // Wp
+    pos = resized_pos_embed(sd["pos_embed"], Hp, Wp)
+    cls = sd["cls_token"][0, 0] + pos[0]
+    tok = tok + pos[1:][None]
+    if attention_type == "space_only":
+        return np.concatenate([np.broadcast_to(cls, (BT, 1, C)), tok], 1).astype(np.float32), T, Wp
+    tok = tok.reshape(B, T, Np, C).transpose(0, 2, 1, 3)          # (b n) t m
+    tok = tok + resized_time_embed(sd["time_embed"], T)[None, None]
+    tok = tok.reshape(B, Np * T, C)                                 # b (n t) m
+    return np.concatenate([np.broadcast_to(cls, (B, 1, C)), tok], 1).astype(np.float32), T, Wp
+
+
+def forward_features(sd, x, num_heads, attention_type="divided_space_time", get_all=False, depth=None):
+    """VisionTransformer.forward_features  models/timesformer.py:285-345 (eval mode).
+    Returns the normed CLS [B, C] (or all tokens when get_all)."""
+    B = x.shape[0]
+    h, T, W = embed_tokens(sd, x, attention_type)
+    if depth is None:
+        depth = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("blocks."))
+    for i in range(depth):
+        if attention_type == "divided_space_time":
+            h = block_divided(h, sd, i, B, T, W, num_heads)
+        else:
+            h = block_plain(h, sd, i, num_heads)
+    if attention_type == "space_only":                              # 338-340
+        h = h.reshape(B, T, h.shape[1], h.shape[2]).mean(1)
+    h = layer_norm(h, sd["norm.weight"], sd["norm.bias"])
+    return h if get_all else h[:, 0]
+
+
+# --------------------------------------------------------------------------- 2-D ViT
+def _cubic_coeffs(t, A=-0.75):
+    def c1(x):
+        return ((A + 2) * x - (A + 3)) * x * x + 1
+
+    def c2(x):
+        return ((A * x - 5 * A) * x + 8 * A) * x - 4 * A
+    return np.stack([c2(t + 1), c1(t), c1(1 - t), c2(2 - t)], -1)
+
+
+def bicubic_resize(img, scale_h, scale_w):
+    """F.interpolate(mode='bicubic', scale_factor=..., align_corners=False) on [C,H,W]
+    (ATen upsample_bicubic2d: src = (dst+0.5)/scale - 0.5, A=-0.75, clamped taps)."""
+    C, H, W = img.shape
+    OH, OW = int(math.floor(H * scale_h)), int(math.floor(W * scale_w))
+
+    def taps(out, inp, scale):
+        s = np.float32(1.0 / scale)
+        src = s * (np.arange(out, dtype=np.float32) + np.float32(0.5)) - np.float32(0.5)
+        i0 = np.floor(src).astype(np.int64)
+        coef = _cubic_coeffs((src - i0).astype(np.float64))
+        idx = np.clip(i0[:, None] + np.arange(-1, 3)[None], 0, inp - 1)
+        return idx, coef
+    ri, rc = taps(OH, H, scale_h)
+    ci, cc = taps(OW, W, scale_w)
+    rows = (img[:, ri, :] * rc[None, :, :, None]).sum(2)           # [C, OH, W]
+    return (rows[:, :, ci] * cc[None, None]).sum(-1).astype(np.float32)
+
+
+def vit2d_forward(sd, x, num_heads, patch=16):
+    """vision_transformer.py:196-214 (prepare_tokens + blocks + norm, CLS)."""
+    B, _, w, h = x.shape
+    C = sd["cls_token"].shape[-1]
+    tok, _, _ = patch_embed(x[:, :, None], sd["patch_embed.proj.weight"], sd["patch_embed.proj.bias"], patch)
+    pos = sd["pos_embed"]
+    N = pos.shape[1] - 1
+    if tok.shape[1] == N and w == h:                                 # interpolate_pos_encoding 174-194
+        pe = pos[0]
+    else:
+        w0, h0 = w // patch + 0.1, h // patch + 0.1
+        s = int(math.sqrt(N))
+        grid = pos[0, 1:].reshape(s, s, C).transpose(2, 0, 1)
+        g2 = bicubic_resize(grid, w0 / math.sqrt(N), h0 / math.sqrt(N))
+        pe = np.concatenate([pos[0, :1], g2.transpose(1, 2, 0).reshape(-1, C)], 0)
+    hcur = np.concatenate([np.broadcast_to(sd["cls_token"][0], (B, 1, C)), tok], 1) + pe[None]
+    depth = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("blocks."))
+    for i in range(depth):
+        hcur = block_plain(hcur.astype(np.float32), sd, i, num_heads)
+    return layer_norm(hcur, sd["norm.weight"], sd["norm.bias"])[:, 0]
+
+
+# --------------------------------------------------------------------------- DINO head / loss
+def dino_head(sd, x, nlayers=3):
+    """DINOHead.forward  vision_transformer.py:278-282 (GELU MLP, L2 normalize, weight-norm)."""
+    h = x
+    for idx in range(0, 2 * (nlayers - 1) + 1, 2):
+        h = linear(h, sd["mlp.%d.weight" % idx], sd["mlp.%d.bias" % idx])
+        if idx < 2 * (nlayers - 1):
+            h = gelu(h)
+    n = np.sqrt((h.astype(np.float64) ** 2).sum(-1, keepdims=True))
+    h = (h / np.maximum(n, 1e-12)).astype(np.float32)               # F.normalize eps=1e-12
+    v = sd["last_layer.weight_v"]
+    wn = v * (sd["last_layer.weight_g"] / np.sqrt((v.astype(np.float64) ** 2).sum(1, keepdims=True)))
+    return linear(h, wn.astype(np.float32))
+
+
+def teacher_temp_schedule(warmup_teacher_temp, teacher_temp, warmup_epochs, nepochs):
+    """train_ssl.py:627-631."""
+    return np.concatenate((np.linspace(warmup_teacher_temp, teacher_temp, warmup_epochs),
+                           np.ones(nepochs - warmup_epochs) * teacher_temp))
+
+
+def dino_loss(student, teacher, center, ncrops, temp, global_crops=2, student_temp=0.1,
+              center_momentum=0.9, world_size=1, teacher_sum_all=None):
+    """DINOLoss.forward + update_center  train_ssl.py:633-691 (two_token=False).
+    Returns (loss, new_center).  teacher_sum_all: the all-reduced column sum when
+    world_size > 1 (defaults to this rank's sum)."""
+    s = student.astype(np.float64) / student_temp
+    s_chunks = np.split(s, ncrops)
+    q = softmax((teacher.astype(np.float64) - center) / temp)
+    q_chunks = np.split(q, global_crops)
+    total, n = 0.0, 0
+    for iq, qq in enumerate(q_chunks):
+        for v in range(len(s_chunks)):
+            if v == iq:
+                continue
+            sv = s_chunks[v]
+            lsm = sv - sv.max(-1, keepdims=True)
+            lsm = lsm - np.log(np.exp(lsm).sum(-1, keepdims=True))
+            total += np.sum(-qq * lsm, -1).mean()
+            n += 1
+    loss = total / n
+    colsum = teacher.astype(np.float64).sum(0, keepdims=True) if teacher_sum_all is None else teacher_sum_all
+    batch_center = colsum / (len(teacher) * world_size)
+    new_center = center * center_momentum + batch_center * (1 - center_momentum)
+    return np.float32(loss), new_center.astype(np.float32)
+
+
+def pair_loss(student, teacher, center, teacher_temp=0.02, student_temp=0.3):
+    """dino_similarity.DINOLoss.forward  dino_similarity.py:129-135, one value per row
+    (the caller at dino_similarity.py:87-88 invokes it per frame on 1-D CLS rows)."""
+    q = softmax((teacher.astype(np.float64) - center) / teacher_temp)
+    s = student.astype(np.float64) / student_temp
+    lsm = s - s.max(-1, keepdims=True)
+    lsm = lsm - np.log(np.exp(lsm).sum(-1, keepdims=True))
+    return np.sum(-q * lsm, -1).astype(np.float32)
+
+
+# --------------------------------------------------------------------------- frame scoring
+def view_windows(F, local_size, global_size):
+    """get_views_of_video_same_size  datasets_custom/dino_loss_loader.py:126-171 as index
+    windows: for frame i returns (j, k, l, m, padded_len) so that local = frames[j:k]
+    zero-padded to padded_len, global = frames[l:m]."""
+    loc, glob = local_size // 2, global_size // 2
+    if F < global_size:
+        global_size = F
+    out = []
+    for i in range(F):
+        j, k, l, m = i - loc, i + loc + 1, i - glob, i + glob
+        if j < 0:
+            j, k = 0, local_size
+        if k >= F:
+            k, j = F, F - local_size
+        if l < 0:
+            l, m = 0, global_size
+        if m >= F:
+            m, l = F, F - global_size
+        out.append((j, k, l, m, global_size))
+    return out
+
+
+def view_index_map(F, local_size, global_size):
+    """1-based frame index per (view, slot), 0 = zero padding; views interleaved
+    (local_0, global_0, local_1, ...) exactly like dino_loss_loader.py:164-171."""
+    w = view_windows(F, local_size, global_size)
+    G = w[0][4]
+    out = np.zeros((2 * F, G), np.int32)
+    for i, (j, k, l, m, _) in enumerate(w):
+        out[2 * i, :k - j] = np.arange(j, k) + 1
+        out[2 * i + 1, :m - l] = np.arange(l, m) + 1
+    return out

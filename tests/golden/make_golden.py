@@ -1,0 +1,196 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Runs ONLY in the build container (needs /root/reference, read-only).  Nothing on the
+GPU box or in the product reads /root/reference; the outputs of this script are
+committed as small .npz files (inputs are NOT stored: they are regenerated from
+seeds by oracle/params.py, which is bit-reproducible).
+
+Import recipe:
+  * /root/reference on sys.path, a stub package `models` whose __path__ points at
+    /root/reference/models (skips models/__init__.py -> timm import);
+  * `DINOLoss` (train_ssl.py:602-691), the pairwise `DINOLoss`
+    (dino_similarity.py:120-135) and `get_views_of_video_same_size`
+    (datasets_custom/dino_loss_loader.py:126-171) are pulled out of their source
+    files with `ast` and exec'd, because importing those modules drags in
+    torchvision/kornia/av which are not installed;
+  * `update_center` needs a process group: gloo, world_size 1.
+
+Usage:  python tests/golden/make_golden.py
+"""
+import ast
+import os
+import sys
+import types
+from functools import partial
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+from oracle import params as P  # noqa: E402
+
+sys.path.insert(0, REF)
+_models = types.ModuleType("models")
+_models.__path__ = [os.path.join(REF, "models")]
+sys.modules["models"] = _models
+import models.timesformer as ref_tsf  # noqa: E402
+import vision_transformer as ref_vit  # noqa: E402
+
+
+def _extract(path, names):
+    """exec the named top-level defs/classes of a reference source file."""
+    src = open(path).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and n.name in names]
+    assert len(keep) == len(names), (path, names)
+    mod = ast.Module(body=keep, type_ignores=[])
+    import torch.distributed as dist
+    ns = {"torch": torch, "nn": nn, "F": F, "np": np, "dist": dist}
+    exec(compile(mod, path, "exec"), ns)
+    return ns
+
+
+def _load(model, sd):
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected, unexpected
+    assert not [m for m in missing if not m.startswith("head")], missing
+
+
+def tsf_model(seed, **kw):
+    kw.setdefault("num_classes", 0)
+    m = ref_tsf.VisionTransformer(
+        img_size=kw.get("img_size", 224), patch_size=16, num_classes=kw["num_classes"],
+        embed_dim=kw.get("embed_dim", 768), depth=kw.get("depth", 12), num_heads=kw.get("num_heads", 12),
+        mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_rate=0.,
+        attn_drop_rate=0., drop_path_rate=0.1, num_frames=kw.get("num_frames", 8),
+        attention_type=kw.get("attention_type", "divided_space_time"))
+    sd = P.timesformer_state(seed, embed_dim=kw.get("embed_dim", 768), depth=kw.get("depth", 12),
+                             num_heads=kw.get("num_heads", 12), img_size=kw.get("img_size", 224),
+                             num_frames=kw.get("num_frames", 8),
+                             attention_type=kw.get("attention_type", "divided_space_time"))
+    _load(m, sd)
+    return m.eval()
+
+
+def run(m, x, **kw):
+    with torch.no_grad():
+        return m.forward_features(torch.from_numpy(x), **kw).numpy()
+
+
+def main():
+    torch.set_num_threads(os.cpu_count())
+    out = {}
+
+    # ---- 1. config-1 tiny divided ViT (C=192, h=3, 12 blocks, 4 frames, 112^2) ----
+    tiny = tsf_model(1, embed_dim=192, num_heads=3, img_size=112, num_frames=4)
+    xg = P.clip(101, (2, 3, 4, 112, 112))
+    xl = P.clip(102, (2, 3, 4, 64, 64))
+    xt3 = P.clip(103, (1, 3, 3, 112, 112))
+    out["tiny_div"] = dict(cls_g=run(tiny, xg), all_g=run(tiny, xg, get_all=True),
+                           cls_l=run(tiny, xl), cls_t3=run(tiny, xt3))
+    # block-level probe: tokens entering block 0 and leaving block 0
+    cap = {}
+    h0 = tiny.blocks[0].register_forward_hook(lambda mod, i, o: cap.update(inp=i[0].numpy().copy(), out=o.numpy().copy()))
+    run(tiny, xg)
+    h0.remove()
+    out["tiny_div"].update(blk0_in=cap["inp"], blk0_out=cap["out"])
+
+    # ---- 2. ViT-B/16 divided (the north-star backbone) ----
+    base = tsf_model(2)
+    xs = P.clip(201, (2, 3, 8, 32, 32))
+    d = dict(cls_small=run(base, xs), all_small=run(base, xs, get_all=True))
+    for name, shape, seed in [("cls_224", (1, 3, 8, 224, 224), 202), ("cls_96", (1, 3, 8, 96, 96), 203),
+                              ("cls_t3", (1, 3, 3, 224, 224), 204), ("cls_t30", (1, 3, 30, 224, 224), 205)]:
+        d[name] = run(base, P.clip(seed, shape))
+    out["base_div"] = d
+
+    # ---- 3. joint space-time + space-only variants (config 4 family, small shapes) ----
+    joint = tsf_model(3, attention_type="joint_space_time")
+    out["base_joint"] = dict(cls_small=run(joint, P.clip(301, (1, 3, 4, 64, 64))))
+    sonly = tsf_model(4, attention_type="space_only")
+    out["base_sonly"] = dict(cls_small=run(sonly, P.clip(401, (2, 3, 4, 64, 64))))
+
+    # ---- 4. 2-D ViT (vision_transformer.py vit_tiny), incl. bicubic pos interp ----
+    v2 = ref_vit.vit_tiny(patch_size=16, img_size=[64])
+    _load(v2, P.vit2d_state(5, embed_dim=192, img_size=64))
+    v2.eval()
+    with torch.no_grad():
+        out["vit2d_tiny"] = dict(cls_64=v2(torch.from_numpy(P.clip(501, (2, 3, 64, 64)))).numpy(),
+                                 cls_48=v2(torch.from_numpy(P.clip(502, (2, 3, 48, 48)))).numpy())
+
+    # ---- 5. DINO heads ----
+    def head(seed, in_dim, out_dim, x):
+        hd = ref_vit.DINOHead(in_dim, out_dim)
+        _load(hd, P.dino_head_state(seed, in_dim, out_dim))
+        with torch.no_grad():
+            return hd(torch.from_numpy(x)).numpy()
+    out["head"] = dict(tiny=head(6, 192, 4096, P.clip(601, (6, 192))),
+                       base=head(7, 768, 65536, P.clip(701, (2, 768))))
+
+    # ---- 6. DINOLoss (train) + center EMA; pairwise loss; views ----
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    ns = _extract(os.path.join(REF, "train_ssl.py"), ["DINOLoss"])
+    TL = ns["DINOLoss"]
+    # config-1 shape: ncrops=2, global_crops=1 (SURVEY §5 defect 4), B=2
+    l1 = TL(4096, 2, 0.04, 0.04, 0, 100, global_crops=1)
+    s1 = torch.from_numpy(P.uniform(801, (4, 4096)))
+    t1 = torch.from_numpy(P.uniform(802, (2, 4096)))
+    loss1 = l1(s1, t1, 0).item()
+    # config-2 shape: ncrops=8 (2 global + 6 local), out_dim 65536, warm-up schedule, B=2, two steps
+    l2 = TL(65536, 8, 0.04, 0.07, 30, 100)
+    s2a = torch.from_numpy(P.uniform(803, (16, 65536)))
+    t2a = torch.from_numpy(P.uniform(804, (4, 65536)))
+    s2b = torch.from_numpy(P.uniform(805, (16, 65536)))
+    t2b = torch.from_numpy(P.uniform(806, (4, 65536)))
+    la = l2(s2a, t2a, 0).item()
+    lb = l2(s2b, t2b, 10).item()
+    out["loss"] = dict(cfg1_loss=np.float32(loss1), cfg1_center=l1.center.numpy().copy(),
+                       cfg2_loss=np.array([la, lb], np.float32), cfg2_center=l2.center.numpy().copy(),
+                       cfg2_temp_sched=np.asarray(l2.teacher_temp_schedule, np.float64))
+
+    ns2 = _extract(os.path.join(REF, "dino_similarity.py"), ["DINOLoss"])
+    PL = ns2["DINOLoss"](out_dim=768, teacher_temp=0.02, student_temp=0.3)
+    sp = torch.from_numpy(P.clip(901, (10, 768)))
+    tp = torch.from_numpy(P.clip(902, (10, 768)))
+    out["pair_loss"] = dict(loss=np.array([PL.forward(sp[k], tp[k]).item() for k in range(10)], np.float32))
+
+    ns3 = _extract(os.path.join(REF, "datasets_custom", "dino_loss_loader.py"), ["get_views_of_video_same_size"])
+    gv = ns3["get_views_of_video_same_size"]
+    vd = {}
+    for F_, loc, glob in [(3, 3, 30), (5, 3, 30), (29, 3, 30), (30, 3, 30), (31, 3, 30), (45, 3, 30), (12, 3, 10), (12, 5, 10)]:
+        frames = torch.arange(1, F_ + 1, dtype=torch.float32).view(F_, 1, 1, 1).expand(F_, 3, 2, 2).contiguous()
+        views = gv(frames, loc, glob)
+        vd["F%d_%d_%d" % (F_, loc, glob)] = views[:, 0, :, 0, 0].numpy().astype(np.int32)
+    out["views"] = vd
+
+    # ---- 7. config-1 end-to-end DINO step (MultiCropWrapper semantics, eval mode) ----
+    hd = ref_vit.DINOHead(192, 4096)
+    _load(hd, P.dino_head_state(6, 192, 4096))
+    with torch.no_grad():
+        g_in = torch.from_numpy(P.clip(1001, (2, 3, 4, 112, 112)))
+        l_in = torch.from_numpy(P.clip(1002, (2, 3, 4, 64, 64)))
+        feats = torch.cat([tiny(g_in), tiny(l_in)])       # one backbone call per resolution group
+        s_out = hd(feats)
+        t_out = hd(tiny(g_in))
+    l3 = TL(4096, 2, 0.04, 0.04, 0, 100, global_crops=1)
+    e2e_loss = l3(s_out, t_out, 0).item()
+    out["e2e_cfg1"] = dict(student=s_out.numpy(), teacher=t_out.numpy(), loss=np.float32(e2e_loss),
+                           center=l3.center.numpy().copy())
+    dist.destroy_process_group()
+
+    for name, arrays in out.items():
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, torch_version=np.array(torch.__version__), **arrays)
+        print("wrote", path, os.path.getsize(path))
+
+
+if __name__ == "__main__":
+    main()
