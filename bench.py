@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""bench.py -- DINO-SVT forward + loss throughput on MI355X (BASELINE.json metric).
+
+One STEP = the DINO fwd+loss of `--clips` multi-crop video clips per GPU (config 2):
+  teacher: ViT-B/16 divided-ST backbone on the 2 global 8x224^2 crops of every clip,
+  student: the same backbone architecture (own weights) on 2 global + 6 local 8x96^2 crops
+           (MultiCropWrapper: one call per resolution group),
+  DINOHead(768 -> 65536) on both, DINOLoss(ncrops=8) incl. the center update, whose teacher
+  column sum is all-reduced over RCCL when N > 1.
+value = clips/s over ALL ranks (weak scaling: `--clips` per GPU), inputs resident in HBM.
+
+Usage:  python bench.py [--gpus N --steps K --warmup W]
+        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "dino-video-summarization-transformer_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "clips/sec (8-frame 224², ViT-B/16 DINO fwd+loss) at 1/2/4/8 MI355X; % MFMA roofline"
+PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3}   # dense, MI355X_MICROARCH.md chip table (2.4 GHz)
+IMAGENET_MEAN = (0.45, 0.45, 0.45)             # DATA.MEAN / STD defaults of the reference loader
+IMAGENET_STD = (0.225, 0.225, 0.225)
+
+
+# ----------------------------------------------------------------- algorithmic FLOPs
+def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16):
+    """2*M*N*K over every matmul of one divided-ST clip forward, counted as the reference
+    executes it (CLS replicated T times in the spatial branch).  8x224^2: 391.7 GFLOP,
+    8x96^2: 70.7 GFLOP (391.66 / 70.70 from torch.utils.flop_counter)."""
+    N = (S // patch) ** 2
+    d = C // heads
+    R = N * T
+    rows_s = T * (1 + N)
+    L = 1 + N * T
+    per_block = (2 * R * C * 3 * C + 4 * N * heads * T * T * d + 2 * 2 * R * C * C          # temporal
+                 + 2 * rows_s * C * 3 * C + 4 * T * heads * (1 + N) ** 2 * d + 2 * rows_s * C * C  # spatial
+                 + 2 * 2 * L * C * mlp * C)                                                  # MLP
+    return depth * per_block + 2 * R * (3 * patch * patch) * C
+
+
+def head_flops(in_dim=768, hidden=2048, bottleneck=256, out_dim=65536):
+    return 2 * (in_dim * hidden + hidden * hidden + hidden * bottleneck + bottleneck * out_dim)
+
+
+def clip_flops(n_global=2, n_local=6):
+    """teacher (2 global) + student (2 global + 6 local) + heads on every crop row."""
+    g, l = vit_fwd_flops(8, 224), vit_fwd_flops(8, 96)
+    return 2 * n_global * g + n_local * l + (2 * n_global + n_local) * head_flops()
+
+
+# ----------------------------------------------------------------- CPU baseline (oracle)
+def cpu_baseline(budget_s=10.0, max_clips=4):
+    """The oracle's numpy fp32 restatement (the checker, never the product) timed on the
+    host cores on a bounded sample: whole multi-crop clips, fwd + heads + loss."""
+    from oracle import dsvt_oracle as O
+    from oracle import params as P
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    sd_s, sd_t = P.timesformer_state(11), P.timesformer_state(12)
+    hsd = P.dino_head_state(13, 768, 65536)
+    center = np.zeros((1, 65536), np.float32)
+    done, t_all = 0, 0.0
+    while done < max_clips and (t_all < budget_s or done == 0):
+        gl = [P.clip(100 + 8 * done + i, (1, 3, 8, 224, 224)) for i in range(2)]
+        lo = [P.clip(102 + 8 * done + i, (1, 3, 8, 96, 96)) for i in range(6)]
+        t0 = time.perf_counter()
+        fs = np.concatenate([O.forward_features(sd_s, np.concatenate(gl), 12),
+                             O.forward_features(sd_s, np.concatenate(lo), 12)])
+        s_out = O.dino_head(hsd, fs)
+        t_out = O.dino_head(hsd, O.forward_features(sd_t, np.concatenate(gl), 12))
+        _, center = O.dino_loss(s_out, t_out, center, 8, 0.04)
+        t_all += time.perf_counter() - t0
+        done += 1
+    return {"value": round(done / t_all, 4), "unit": "clips/s", "cores": int(cores), "kind": "port",
+            "sample": "%d clip(s) x (teacher 2x8x224^2 + student 2x8x224^2 + 6x8x96^2 + DINOHead(65536) + "
+                      "DINOLoss), numpy fp32 oracle, %.1f s" % (done, t_all)}
+
+
+# ----------------------------------------------------------------- models / data
+def build(dtype, device, seed=0):
+    from functools import partial
+
+    import torch.nn as nn
+
+    from dsvt.loss import DINOLoss
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+
+    def net():
+        bb = VisionTransformer(img_size=224, patch_size=16, num_classes=0, embed_dim=768, depth=12, num_heads=12,
+                               mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                               drop_path_rate=0.1, num_frames=8, attention_type="divided_space_time")
+        hd = DINOHead(768, 65536, norm_last_layer=True)
+        bb.dsvt_dtype = hd.dsvt_dtype = dtype
+        return MultiCropWrapper(bb, hd)
+
+    torch.manual_seed(seed)
+    student = net()
+    teacher = net()
+    teacher.load_state_dict(student.state_dict())          # train_ssl.py:330-333
+    # random-init stand-in for the SVT weights: the temporal branch must not be a no-op
+    # (reference zero-inits temporal_fc, SURVEY §5 defect 3)
+    with torch.no_grad():
+        for m in (student, teacher):
+            for blk in m.backbone.blocks:
+                blk.temporal_fc.weight.normal_(0, 0.02)
+            m.backbone.time_embed.normal_(0, 0.02)
+    for p in list(student.parameters()) + list(teacher.parameters()):
+        p.requires_grad_(False)
+    student = student.to(device).eval()
+    teacher = teacher.to(device).eval()
+    loss = DINOLoss(65536, 8, 0.04, 0.04, 0, 100).to(device)
+    return student, teacher, loss
+
+
+def synthetic_crops(clips, device, seed):
+    """U8 uniform frames -> /255 -> (x - mean)/std, NCTHW fp32, resident on the GPU."""
+    g = torch.Generator(device=device).manual_seed(seed)
+
+    def crop(S):
+        x = torch.randint(0, 256, (clips, 3, 8, S, S), generator=g, device=device, dtype=torch.uint8).float()
+        return ((x / 255.0 - IMAGENET_MEAN[0]) / IMAGENET_STD[0]).contiguous()
+    return [crop(224) for _ in range(2)] + [crop(96) for _ in range(6)]
+
+
+# ----------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=8, help="multi-crop clips per GPU per step (config 2: 8)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=device)   # RCCL over xGMI
+
+    from dsvt import ops
+    from dsvt._lib import PROBE_GEMM
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    student, teacher, dino_loss = build(dtype, device)
+    crops = synthetic_crops(args.clips, device, seed=1234 + rank)
+
+    def step():
+        with torch.no_grad():
+            s_out = student(crops)             # 2 backbone calls + head on (2+6)*clips rows
+            t_out = teacher(crops[:2])         # 1 backbone call + head on 2*clips rows
+            return dino_loss(s_out, t_out, 0)  # loss + center (RCCL all-reduce when N > 1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    if not args.no_probe:
+        ops.probe_enable(PROBE_GEMM, 1 << 16)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    loss_val = float(loss.item())
+
+    roofline = None
+    if not args.no_probe:
+        ms, work, fam, tag = ops.probe_read(1 << 16)
+        ops.probe_disable()
+        if len(ms):
+            by_tag = {}
+            for t, m_, w_ in zip(tag, ms, work):
+                a = by_tag.setdefault(int(t), [0, 0.0, 0.0])
+                a[0] += 1
+                a[1] += float(m_)
+                a[2] += float(w_)
+            dom = max(by_tag, key=lambda t: by_tag[t][1])
+            n, tms, tfl = by_tag[dom]
+            achieved = tfl / (tms * 1e-3) / 1e12          # = (flops per launch) / (avg launch time)
+            peak = PEAK_TFLOPS[args.dtype]
+            all_ms = float(np.sum(ms))
+            roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(achieved / peak, 4), "traffic": None,
+                        "kernel": ops.GEMM_KERNEL_NAMES[dom], "launches": n,
+                        "avg_launch_us": round(tms / n * 1e3, 2),
+                        "flops_per_launch": tfl / n,
+                        "gemm_share_of_step": round(all_ms / (elapsed * 1e3), 3),
+                        "all_gemm_tflops": round(float(np.sum(work)) / (all_ms * 1e-3) / 1e12, 1)}
+
+    value = world * args.clips * args.steps / elapsed
+    step_ms = elapsed / args.steps * 1e3
+    step_tflops = value * clip_flops() / 1e12
+    out = {"metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+           "config": {"workload": "DINO-SVT fwd+loss: per clip teacher ViT-B/16 divided-ST on 2x8x224^2 global "
+                                  "crops + student on 2x8x224^2 + 6x8x96^2 crops, DINOHead(768->65536), "
+                                  "DINOLoss(ncrops=8) + center all-reduce",
+                      "clips_per_gpu": args.clips, "global_batch": world * args.clips,
+                      "gflop_per_clip": round(clip_flops() / 1e9, 1), "parallelism": "dp%d" % world,
+                      "weights": "random init (torch seed 0)"},
+           "step_roofline": {"achieved": round(step_tflops, 1), "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
+                             "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4)},
+           "roofline": roofline, "loss": round(loss_val, 5)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,292 @@
+// Attention kernels of the divided space-time block (and the plain/joint variants).
+//
+// attn_seq_bf16 (K6/K10, perf mode): flash-style, one workgroup = 4 waves = 64 queries of
+//   one (sequence, head); K/V streamed through a 2-stage LDS ring in 64-key chunks
+//   (register-staged: the rows are GATHERED -- the spatial sequence (b,t) is the CLS row
+//   plus every T-th token row of X -- so they cannot use lane-linear LDS-DMA), online
+//   softmax in fp32.  S^T = K.Q^T is issued with K as the MFMA A operand so each lane
+//   holds 16 scores of ONE query: the row max / sum are in-register + 2 cross-lane xors,
+//   and the probabilities feed O^T = V^T.P^T directly as the B operand (k order permuted
+//   to match); V^T fragments come from ds_read_b64_tr_b16 transposed LDS reads.
+// attn_seq_f32 (parity mode): same decomposition on the fp32 VALU, one query per lane.
+// attn_temporal (K5): T <= 64 tokens per sequence, all heads of a group staged in LDS,
+//   16 lanes per (head, query), online softmax; HBM-bound.
+#include <math.h>
+
+#include "common.h"
+
+namespace dsvt {
+
+__device__ __forceinline__ int64_t tok_row(const AttnParams& p, int64_t b, int64_t t, int64_t i) {
+  return b * p.L + (i == 0 ? 0 : 1 + (i - 1) * p.tok_stride + t);
+}
+
+// ---------------------------------------------------------------- bf16 MFMA flash kernel
+constexpr int KV_ROW = 72;  // bf16 per LDS row: 64 + 8 pad (144 B rows: conflict-light b128 + tr reads)
+
+__global__ __launch_bounds__(256) void attn_seq_bf16(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t kv[2][2][64 * KV_ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t seq = blockIdx.z, b = seq / p.tin, t = seq % p.tin;
+  const int h = blockIdx.y;
+  const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  const bf16_t* qkv = (const bf16_t*)p.qkv;
+  const int64_t C = p.C;
+
+  int64_t qi = q0 + r16;
+  if (qi > p.seqlen - 1) qi = p.seqlen - 1;
+  const bf16_t* qrow = qkv + tok_row(p, b, t, qi) * p.ld_qkv + h * 64;
+  const sv8 qf0 = *reinterpret_cast<const sv8*>(qrow + g * 8);
+  const sv8 qf1 = *reinterpret_cast<const sv8*>(qrow + 32 + g * 8);
+
+  const int nchunks = (int)((p.seqlen + 63) / 64);
+  // K/V staging: thread owns 16-B pieces pc = tid and tid + 256 of the 64x128 B chunk
+  const int row_a = tid >> 3, row_b = (tid + 256) >> 3, ch = tid & 7;
+  uint4 ka, kb, va, vb;
+#define DSVT_LOAD_CHUNK(c)                                                              \
+  {                                                                                     \
+    int64_t kia = (int64_t)(c) * 64 + row_a, kib = (int64_t)(c) * 64 + row_b;           \
+    kia = kia < p.seqlen ? kia : p.seqlen - 1;                                          \
+    kib = kib < p.seqlen ? kib : p.seqlen - 1;                                          \
+    const bf16_t* pa = qkv + tok_row(p, b, t, kia) * p.ld_qkv + C + h * 64 + ch * 8;    \
+    const bf16_t* pb_ = qkv + tok_row(p, b, t, kib) * p.ld_qkv + C + h * 64 + ch * 8;   \
+    ka = *reinterpret_cast<const uint4*>(pa);                                           \
+    va = *reinterpret_cast<const uint4*>(pa + C);                                       \
+    kb = *reinterpret_cast<const uint4*>(pb_);                                          \
+    vb = *reinterpret_cast<const uint4*>(pb_ + C);                                      \
+  }
+#define DSVT_STORE_CHUNK(st)                                                            \
+  {                                                                                     \
+    *reinterpret_cast<uint4*>(&kv[st][0][row_a * KV_ROW + ch * 8]) = ka;                \
+    *reinterpret_cast<uint4*>(&kv[st][1][row_a * KV_ROW + ch * 8]) = va;                \
+    *reinterpret_cast<uint4*>(&kv[st][0][row_b * KV_ROW + ch * 8]) = kb;                \
+    *reinterpret_cast<uint4*>(&kv[st][1][row_b * KV_ROW + ch * 8]) = vb;                \
+  }
+
+  float m = -INFINITY, l = 0.f;
+  fv4 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = fv4{0.f, 0.f, 0.f, 0.f};
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  DSVT_LOAD_CHUNK(0);
+  DSVT_STORE_CHUNK(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int st = c & 1;
+    if (c + 1 < nchunks) DSVT_LOAD_CHUNK(c + 1);
+    const bf16_t* Ks = kv[st][0];
+    const bf16_t* Vs = kv[st][1];
+
+    // S^T tiles: s[kt][j] = score(query q0 + r16, key c*64 + kt*16 + 4g + j)
+    fv4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const bf16_t* kr = Ks + (kt * 16 + r16) * KV_ROW + g * 8;
+      const sv8 k0 = *reinterpret_cast<const sv8*>(kr);
+      const sv8 k1 = *reinterpret_cast<const sv8*>(kr + 32);
+      fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t key = (int64_t)c * 64 + kt * 16 + 4 * g + j;
+        const float v = key < p.seqlen ? s[kt][j] * sl2 : -INFINITY;
+        s[kt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = exp2f(s[kt][j] - mn);
+        s[kt][j] = e;
+        rs += e;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+
+    // O^T += V^T . P^T over two 32-key steps; k-slot (g, jj): jj<4 -> key tile 2st2, jj>=4 -> 2st2+1
+#pragma unroll
+    for (int st2 = 0; st2 < 2; ++st2) {
+      sv8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[2 * st2][j]);
+        pb[4 + j] = (short)f2bf(s[2 * st2 + 1][j]);
+      }
+      const int vr0 = (2 * st2) * 16 + 4 * g + (r16 >> 2);
+      const int vr1 = vr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr0 * KV_ROW + col));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr1 * KV_ROW + col));
+        const sv8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+      }
+    }
+    if (c + 1 < nchunks) DSVT_STORE_CHUNK(st ^ 1);
+    __syncthreads();
+  }
+
+#undef DSVT_LOAD_CHUNK
+#undef DSVT_STORE_CHUNK
+  // lane holds O[query q0 + r16][d = dt*16 + 4g + 0..3]
+  const int64_t qo = q0 + r16;
+  if (qo < p.seqlen) {
+    const float inv = 1.0f / l;
+    if (qo == 0 && p.cls_aux) {
+      float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    } else {
+      bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fp32 VALU (parity mode)
+__global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
+  __shared__ float ks[64][65], vs[64][65];
+  const int lane = threadIdx.x;
+  const int64_t seq = blockIdx.z, b = seq / p.tin, t = seq % p.tin;
+  const int h = blockIdx.y;
+  const float* qkv = (const float*)p.qkv;
+  const int64_t C = p.C;
+  const int64_t qi = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t qc = qi < p.seqlen ? qi : p.seqlen - 1;
+  float q[64], o[64];
+  const float* qrow = qkv + tok_row(p, b, t, qc) * p.ld_qkv + h * 64;
+#pragma unroll
+  for (int d = 0; d < 64; ++d) { q[d] = qrow[d]; o[d] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  const int nchunks = (int)((p.seqlen + 63) / 64);
+  for (int c = 0; c < nchunks; ++c) {
+    __syncthreads();
+    int64_t ki = (int64_t)c * 64 + lane;
+    if (ki > p.seqlen - 1) ki = p.seqlen - 1;
+    const float* base = qkv + tok_row(p, b, t, ki) * p.ld_qkv + h * 64;
+    for (int d = 0; d < 64; ++d) { ks[lane][d] = base[C + d]; vs[lane][d] = base[2 * C + d]; }
+    __syncthreads();
+    const int64_t rem = p.seqlen - (int64_t)c * 64;
+    const int nk = rem < 64 ? (int)rem : 64;
+    for (int j = 0; j < nk; ++j) {
+      float sdot = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) sdot = fmaf(q[d], ks[j][d], sdot);
+      const float sc = sdot * p.scale;
+      const float mn = fmaxf(m, sc);
+      const float corr = expf(m - mn), pe = expf(sc - mn);
+      l = l * corr + pe;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) o[d] = fmaf(pe, vs[j][d], o[d] * corr);
+      m = mn;
+    }
+  }
+  if (qi < p.seqlen) {
+    const float inv = 1.0f / l;
+    float* dst = (qi == 0 && p.cls_aux) ? p.cls_aux + seq * C + h * 64
+                                        : (float*)p.out + tok_row(p, b, t, qi) * p.ld_out + h * 64;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) dst[d] = o[d] * inv;
+  }
+}
+
+hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
+  dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)(p.nb * p.tin));
+  if (dtype == 0) attn_seq_bf16<<<grid, 256, 0, s>>>(p);
+  else attn_seq_f32<<<grid, 64, 0, s>>>(p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- temporal attention
+// grid (nseq, ceil(heads/G)); LDS holds [T][3][G][64] of the sequence's q/k/v for the
+// workgroup's G heads.  Work item = (head hh, query i), 16 lanes each, 4 dims per lane.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_temporal_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                            int Tf, int heads, int G, int64_t C, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char dyn_smem[];
+  T* sm = reinterpret_cast<T*>(dyn_smem);
+  const int tid = threadIdx.x;
+  const int64_t sq = blockIdx.x;
+  const int h0 = blockIdx.y * G;
+  const int gh = (heads - h0) < G ? (heads - h0) : G;
+  constexpr int PER = Elem<T>::PER16;
+  const int seg_pieces = 64 / PER;  // 16-B pieces per 64-elem head segment
+  const int total = Tf * 3 * gh * seg_pieces;
+  for (int pc = tid; pc < total; pc += 256) {
+    const int piece = pc % seg_pieces;
+    const int rest = pc / seg_pieces;
+    const int hh = rest % gh, which = (rest / gh) % 3, tt = rest / (gh * 3);
+    const T* src = qkv + (sq * Tf + tt) * 3 * C + which * C + (int64_t)(h0 + hh) * 64 + piece * PER;
+    T* dst = sm + (((int64_t)tt * 3 + which) * G + hh) * 64 + piece * PER;
+    *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+  }
+  __syncthreads();
+  const int sub = tid & 15, d0 = sub * 4;
+  const int items = gh * Tf;
+  for (int it = tid >> 4; it < items; it += 16) {
+    const int hh = it % gh, i = it / gh;
+    float q[4], o[4] = {0.f, 0.f, 0.f, 0.f};
+    load4(sm + (((int64_t)i * 3 + 0) * G + hh) * 64 + d0, q);
+    float m = -INFINITY, l = 0.f;
+    for (int j = 0; j < Tf; ++j) {
+      float k[4], v[4];
+      load4(sm + (((int64_t)j * 3 + 1) * G + hh) * 64 + d0, k);
+      float part = q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3];
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+      part += __shfl_xor(part, 8, 64);
+      const float sc = part * scale;
+      const float mn = fmaxf(m, sc);
+      const float corr = expf(m - mn), pe = expf(sc - mn);
+      load4(sm + (((int64_t)j * 3 + 2) * G + hh) * 64 + d0, v);
+      l = l * corr + pe;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaf(pe, v[e], o[e] * corr);
+      m = mn;
+    }
+    const float inv = 1.0f / l;
+    store4(out + (sq * Tf + i) * C + (int64_t)(h0 + hh) * 64 + d0, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+  }
+}
+
+hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T, int64_t heads,
+                                int64_t C, float scale, hipStream_t s) {
+  const int64_t esz = dtype == 0 ? 2 : 4;
+  const int64_t per_head = T * 3 * 64 * esz;
+  int64_t G = (48 * 1024) / per_head;
+  if (G < 1) G = 1;
+  if (G > heads) G = heads;
+  const size_t smem = (size_t)(per_head * G);
+  dim3 grid((unsigned)nseq, (unsigned)((heads + G - 1) / G));
+  if (dtype == 0)
+    attn_temporal_kernel<bf16_t><<<grid, 256, smem, s>>>((const bf16_t*)qkv, (bf16_t*)out, (int)T, (int)heads, (int)G, C, scale);
+  else
+    attn_temporal_kernel<float><<<grid, 256, smem, s>>>((const float*)qkv, (float*)out, (int)T, (int)heads, (int)G, C, scale);
+  return hipGetLastError();
+}
+
+}  // namespace dsvt

@@ -1,0 +1,370 @@
+// extern "C" boundary: argument validation, error reporting, launch-probe bookkeeping.
+// Every entry point checks the shapes/alignments its kernels assume BEFORE launching (a
+// mis-shaped launch would fault the GPU), returns non-zero on error and never aborts.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/dsvt.h"
+#include "internal.h"
+
+using namespace dsvt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return 1;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return 2;
+}
+
+#define REQUIRE(cond, ...) \
+  do {                     \
+    if (!(cond)) return fail(__VA_ARGS__); \
+  } while (0)
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+int64_t esize(int dtype) { return dtype == DSVT_BF16 ? 2 : 4; }
+
+// ---- launch probe (diagnostic) ----
+struct Probe {
+  int mask = 0, cap = 0, count = 0;
+  std::vector<hipEvent_t> ev0, ev1;
+  std::vector<double> work;
+  std::vector<int32_t> fam, tag;
+  void clear() {
+    for (auto e : ev0) (void)hipEventDestroy(e);
+    for (auto e : ev1) (void)hipEventDestroy(e);
+    ev0.clear(); ev1.clear(); work.clear(); fam.clear(); tag.clear();
+    mask = cap = count = 0;
+  }
+} g_probe;
+
+template <typename F>
+int probed(int family, double work, hipStream_t s, const char* where, F&& launch, int tag = 0) {
+  const bool on = (g_probe.mask & family) && g_probe.count < g_probe.cap;
+  if (on) (void)hipEventRecord(g_probe.ev0[g_probe.count], s);
+  hipError_t e = launch();
+  if (e != hipSuccess) return hip_fail(e, where);
+  if (on) {
+    (void)hipEventRecord(g_probe.ev1[g_probe.count], s);
+    g_probe.work[g_probe.count] = work;
+    g_probe.fam[g_probe.count] = family;
+    g_probe.tag[g_probe.count] = tag;
+    g_probe.count++;
+  }
+  return 0;
+}
+
+// GEMM instantiation id: gemm_kernel<T = dtype ? float : bf16, EPI = epi, OUT_F32 = f32>
+int gemm_tag(int dtype, int epi, int out_f32) {
+  const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
+  return dtype * 16 + epi * 2 + f32;
+}
+
+void norm_map(int64_t& rpg, int64_t& gstride, int64_t& goff) {
+  if (rpg <= 0) { rpg = INT64_MAX; gstride = 0; goff = 0; }
+}
+
+int check_gemm(int dtype, int epi, const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+               const void* out, int64_t ldo, int64_t M, int64_t N, int64_t K) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "gemm: bad dtype %d", dtype);
+  REQUIRE(epi >= 0 && epi <= 3, "gemm: bad epilogue %d", epi);
+  REQUIRE(A && W && out, "gemm: null pointer");
+  REQUIRE(M > 0 && N > 0 && K > 0, "gemm: empty problem M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
+  REQUIRE((K * esize(dtype)) % 128 == 0, "gemm: K=%lld must be a multiple of %d", (long long)K, dtype == DSVT_BF16 ? 64 : 32);
+  REQUIRE(N % 4 == 0, "gemm: N=%lld must be a multiple of 4", (long long)N);
+  REQUIRE(lda >= K && ldw >= K && (lda * esize(dtype)) % 16 == 0 && (ldw * esize(dtype)) % 16 == 0,
+          "gemm: lda/ldw must be >= K and 16-byte multiples");
+  REQUIRE(ldo >= N && ldo % 4 == 0, "gemm: ldo must be >= N and a multiple of 4");
+  REQUIRE(aligned16(A) && aligned16(W) && aligned16(out) && (!bias || aligned16(bias)),
+          "gemm: pointers must be 16-byte aligned");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dsvt_version(void) { return DSVT_ABI_VERSION; }
+const char* dsvt_last_error(void) { return g_err.c_str(); }
+
+int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K) {
+  const int64_t es = esize(dtype);
+  auto up = [](int64_t b) { return (b + 255) / 256 * 256; };
+  switch (op) {
+    case DSVT_WS_LN_GEMM: return up(M * K * es);
+    case DSVT_WS_PATCH_EMBED: return up(M * K * es);
+    case DSVT_WS_ATTN_SPATIAL: return up(M * N * 4);
+    case DSVT_WS_DINO_LOSS: {  // M = B, N = ncrops, K = global_crops
+      const int64_t rt = K * M, rs = N * M, np = K * (N - 1) * M;
+      return up((2 * rt + 2 * rs + np) * 4);
+    }
+    case DSVT_WS_PAIR_LOSS: return up(4 * M * 4);
+    default: return -1;
+  }
+}
+
+int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, const void* W, int64_t ldw,
+                  const float* bias, void* out, int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg,
+                  int64_t gstride, int64_t goff, void* stream) {
+  if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
+  REQUIRE(epilogue != 3, "gemm: the patch epilogue is reachable only through dsvt_patch_embed_fwd");
+  norm_map(rpg, gstride, goff);
+  GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
+                [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
+                gemm_tag(dtype, epilogue, out_f32));
+}
+
+int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const float* gamma, const float* beta,
+                       int64_t rows, int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "layernorm: bad dtype");
+  REQUIRE(x && y && gamma && beta, "layernorm: null pointer");
+  REQUIRE(rows > 0 && C > 0 && C % 64 == 0 && C <= 1024, "layernorm: need 0 < C <= 1024, C %% 64 == 0 (C=%lld)", (long long)C);
+  REQUIRE(aligned16(x) && aligned16(y) && aligned16(gamma) && aligned16(beta), "layernorm: pointers must be 16-byte aligned");
+  norm_map(rpg, gstride, goff);
+  const double bytes = (double)rows * C * (4 + (out_f32 || dtype == DSVT_F32 ? 4 : 2));
+  return probed(DSVT_PROBE_NORM, bytes, (hipStream_t)stream, "dsvt_layernorm_fwd", [&] {
+    return launch_layernorm(dtype, out_f32, x, y, gamma, beta, rows, C, rpg, gstride, goff, eps, (hipStream_t)stream);
+  });
+}
+
+int dsvt_ln_gemm_fwd(int dtype, int epilogue, int out_f32, const float* x, int64_t in_rpg, int64_t in_gstride,
+                     int64_t in_goff, const float* gamma, const float* beta, float eps, const void* W, const float* bias,
+                     void* out, int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride,
+                     int64_t goff, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_GEMM, dtype, M, N, K),
+          "ln_gemm: workspace too small (%lld < %lld)", (long long)workspace_bytes,
+          (long long)dsvt_workspace_bytes(DSVT_WS_LN_GEMM, dtype, M, N, K));
+  if (int e = check_gemm(dtype, epilogue, workspace, K, W, K, bias, out, ldo, M, N, K)) return e;
+  if (int e = dsvt_layernorm_fwd(dtype, 0, x, workspace, gamma, beta, M, K, in_rpg, in_gstride, in_goff, eps, stream))
+    return e;
+  return dsvt_gemm_fwd(dtype, epilogue, out_f32, workspace, K, W, K, bias, out, ldo, M, N, K, rpg, gstride, goff, stream);
+}
+
+int dsvt_patch_embed_fwd(int dtype, int tokens_order, const float* x, int64_t B, int64_t Cin, int64_t T, int64_t H,
+                         int64_t W, int64_t patch, const void* w, const float* bias, const float* cls_token,
+                         const float* pos_embed, const int32_t* pos_index, const float* time_embed,
+                         const int32_t* time_index, int64_t C, float* X, const int32_t* frame_index,
+                         void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "patch_embed: bad dtype");
+  REQUIRE(patch == 16, "patch_embed: only patch_size 16 is supported (got %lld)", (long long)patch);
+  REQUIRE(tokens_order == DSVT_TOKENS_NT || tokens_order == DSVT_TOKENS_FRAME, "patch_embed: bad tokens_order");
+  REQUIRE(x && w && bias && cls_token && pos_embed && pos_index && X, "patch_embed: null pointer");
+  REQUIRE(tokens_order == DSVT_TOKENS_FRAME || (time_embed && time_index), "patch_embed: NT order needs time_embed");
+  REQUIRE(B > 0 && Cin > 0 && T > 0 && H >= 16 && W >= 16 && W % 4 == 0 && C % 4 == 0,
+          "patch_embed: bad shape B=%lld Cin=%lld T=%lld H=%lld W=%lld C=%lld", (long long)B, (long long)Cin,
+          (long long)T, (long long)H, (long long)W, (long long)C);
+  REQUIRE(aligned16(x), "patch_embed: x must be 16-byte aligned");
+  const int64_t Hp = H / 16, Wp = W / 16, Np = Hp * Wp, K = Cin * 256, M = B * T * Np;
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_PATCH_EMBED, dtype, M, C, K),
+          "patch_embed: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int nt = tokens_order == DSVT_TOKENS_NT;
+  if (hipError_t e = launch_im2col(dtype, nt, x, workspace, B, Cin, T, H, W, Hp, Wp, frame_index, s))
+    return hip_fail(e, "im2col");
+  GemmParams p{};
+  p.A = workspace; p.lda = K; p.W = w; p.ldw = K; p.bias = bias; p.out = X; p.ldo = C;
+  p.M = M; p.N = C; p.K = K;
+  if (nt) { p.rpg = Np * T; p.gstride = 1 + Np * T; p.goff = 1; p.T = T; p.temb = time_embed; p.tidx = time_index; }
+  else { p.rpg = Np; p.gstride = 1 + Np; p.goff = 1; p.T = 1; p.temb = nullptr; p.tidx = nullptr; }
+  p.pos = pos_embed; p.pidx = pos_index;
+  if (int e = check_gemm(dtype, EPI_PATCH, workspace, K, w, K, bias, X, C, M, C, K)) return e;
+  int rc = probed(DSVT_PROBE_GEMM, 2.0 * M * C * K, s, "patch_embed gemm",
+                  [&] { return launch_gemm(p, dtype, EPI_PATCH, 1, s); }, gemm_tag(dtype, EPI_PATCH, 1));
+  if (rc) return rc;
+  const int64_t rows = nt ? B : B * T, stride = (nt ? 1 + Np * T : 1 + Np) * C;
+  if (hipError_t e = launch_cls_init(X, cls_token, pos_embed, rows, stride, C, s)) return hip_fail(e, "cls_init");
+  return 0;
+}
+
+int dsvt_pos_bicubic_fwd(const float* pos_embed, float* out, int64_t s, int64_t OH, int64_t OW, int64_t C,
+                         double scale_h, double scale_w, void* stream) {
+  REQUIRE(pos_embed && out && s > 0 && OH > 0 && OW > 0 && C > 0 && scale_h > 0 && scale_w > 0,
+          "pos_bicubic: bad args");
+  hipError_t e = launch_pos_bicubic(pos_embed, out, s, OH, OW, C, (float)(1.0 / scale_h), (float)(1.0 / scale_w),
+                                    (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "pos_bicubic");
+}
+
+int dsvt_attn_temporal_fwd(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T, int64_t heads,
+                           int64_t head_dim, float scale, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_temporal: bad dtype");
+  REQUIRE(qkv && out && aligned16(qkv) && aligned16(out), "attn_temporal: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_temporal: head_dim must be 64 (got %lld)", (long long)head_dim);
+  REQUIRE(nseq > 0 && T >= 1 && T <= 64 && heads >= 1, "attn_temporal: need nseq > 0, 1 <= T <= 64");
+  const int64_t C = heads * 64;
+  const double flops = 4.0 * nseq * heads * T * T * 64;
+  return probed(DSVT_PROBE_ATTN_TEMPORAL, flops, (hipStream_t)stream, "dsvt_attn_temporal_fwd", [&] {
+    return launch_attn_temporal(dtype, qkv, out, nseq, T, heads, C, scale, (hipStream_t)stream);
+  });
+}
+
+int dsvt_attn_spatial_fwd(int dtype, const void* qkv, void* out, int64_t B, int64_t T, int64_t L, int64_t heads,
+                          int64_t head_dim, float scale, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial: bad dtype");
+  REQUIRE(qkv && out && aligned16(qkv) && aligned16(out), "attn_spatial: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_spatial: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial: need (L-1) %% T == 0");
+  const int64_t C = heads * 64;
+  REQUIRE(workspace && aligned16(workspace) &&
+              workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_SPATIAL, dtype, B * T, C, 0),
+          "attn_spatial: workspace too small");
+  AttnParams p{qkv, 3 * C, out, C, (float*)workspace, B, T, L, T, 1 + (L - 1) / T, heads, C, scale};
+  hipStream_t s = (hipStream_t)stream;
+  const double flops = 4.0 * B * T * heads * (double)p.seqlen * p.seqlen * 64;
+  int rc = probed(DSVT_PROBE_ATTN_SPATIAL, flops, s, "dsvt_attn_spatial_fwd", [&] { return launch_attn_seq(dtype, p, s); });
+  if (rc) return rc;
+  if (hipError_t e = launch_cls_mean(dtype, (const float*)workspace, out, B, T, L, C, s)) return hip_fail(e, "cls_mean");
+  return 0;
+}
+
+int dsvt_attn_joint_fwd(int dtype, const void* qkv, void* out, int64_t nb, int64_t L, int64_t heads, int64_t head_dim,
+                        float scale, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_joint: bad dtype");
+  REQUIRE(qkv && out && aligned16(qkv) && aligned16(out), "attn_joint: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_joint: head_dim must be 64");
+  REQUIRE(nb > 0 && L > 0, "attn_joint: empty problem");
+  const int64_t C = heads * 64;
+  AttnParams p{qkv, 3 * C, out, C, nullptr, nb, 1, L, 1, L, heads, C, scale};
+  hipStream_t s = (hipStream_t)stream;
+  const double flops = 4.0 * nb * heads * (double)L * L * 64;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, s, "dsvt_attn_joint_fwd", [&] { return launch_attn_seq(dtype, p, s); });
+}
+
+int dsvt_frame_mean_fwd(const float* x, float* y, int64_t B, int64_t T, int64_t rowlen, void* stream) {
+  REQUIRE(x && y && B > 0 && T > 0 && rowlen > 0, "frame_mean: bad args");
+  hipError_t e = launch_frame_mean(x, y, B, T, rowlen, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "frame_mean");
+}
+
+int dsvt_cast_fwd(int dtype, const float* x, void* y, int64_t n, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "cast: bad dtype");
+  REQUIRE(x && y && aligned16(x) && n % 4 == 0 && ((uintptr_t)y & 7) == 0, "cast: need aligned pointers, n %% 4 == 0");
+  hipError_t e = launch_cast(dtype, x, y, n, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "cast");
+}
+
+int dsvt_dino_head_norm_fwd(int dtype, const float* x, void* y, int64_t rows, int64_t D, float eps, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "head_norm: bad dtype");
+  REQUIRE(x && y && aligned16(x) && aligned16(y) && rows > 0 && D > 0 && D % 4 == 0, "head_norm: bad args");
+  return probed(DSVT_PROBE_NORM, (double)rows * D * (4 + esize(dtype)), (hipStream_t)stream, "dsvt_dino_head_norm_fwd",
+                [&] { return launch_l2norm(dtype, x, y, rows, D, eps, (hipStream_t)stream); });
+}
+
+int dsvt_weight_norm_fwd(int dtype, const float* v, const float* g, void* w, int64_t rows, int64_t D, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "weight_norm: bad dtype");
+  REQUIRE(v && g && w && aligned16(v) && aligned16(w) && rows > 0 && D > 0 && D % 4 == 0, "weight_norm: bad args");
+  return probed(DSVT_PROBE_NORM, (double)rows * D * (4 + esize(dtype)), (hipStream_t)stream, "dsvt_weight_norm_fwd",
+                [&] { return launch_weight_norm(dtype, v, g, w, rows, D, (hipStream_t)stream); });
+}
+
+int dsvt_dino_loss_fwd(const float* student, const float* teacher, const float* center, int64_t B, int64_t ncrops,
+                       int64_t global_crops, int64_t D, float student_temp, float teacher_temp, float* loss_out,
+                       float* teacher_colsum, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(student && teacher && center && loss_out && teacher_colsum, "dino_loss: null pointer");
+  REQUIRE(aligned16(student) && aligned16(teacher) && aligned16(center), "dino_loss: pointers must be 16-byte aligned");
+  REQUIRE(B > 0 && D > 0 && D % 4 == 0, "dino_loss: bad shape");
+  REQUIRE(global_crops >= 1 && ncrops >= global_crops, "dino_loss: need 1 <= global_crops <= ncrops");
+  REQUIRE(ncrops >= 2, "dino_loss: no loss terms (ncrops == 1): the reference divides by zero here");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_DINO_LOSS, 1, B, ncrops, global_crops),
+          "dino_loss: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rt = global_crops * B, rs = ncrops * B, np = global_crops * (ncrops - 1) * B;
+  float* ws = (float*)workspace;
+  float *t_m = ws, *t_z = ws + rt, *s_m = ws + 2 * rt, *s_z = ws + 2 * rt + rs, *ce = ws + 2 * rt + 2 * rs;
+  const double bytes = 4.0 * D * (rt + rs + np * 2);
+  return probed(DSVT_PROBE_LOSS, bytes, s, "dsvt_dino_loss_fwd", [&]() -> hipError_t {
+    hipError_t e;
+    if ((e = launch_softmax_stats(teacher, center, 1.0f / teacher_temp, rt, D, t_m, t_z, s))) return e;
+    if ((e = launch_softmax_stats(student, nullptr, 1.0f / student_temp, rs, D, s_m, s_z, s))) return e;
+    if ((e = launch_pair_ce(student, teacher, center, nullptr, np, B, ncrops, global_crops, D, 1.0f / student_temp,
+                            1.0f / teacher_temp, t_m, t_z, s_m, s_z, ce, s)))
+      return e;
+    const double n_terms = (double)global_crops * (ncrops - 1);
+    if ((e = launch_loss_reduce(ce, np, (float)(1.0 / (n_terms * B)), loss_out, s))) return e;
+    return launch_colsum(teacher, rt, D, teacher_colsum, s);
+  });
+}
+
+int dsvt_dino_pair_loss_fwd(const float* student, const float* teacher, const float* center, int64_t rows, int64_t D,
+                            float student_temp, float teacher_temp, float* out, void* workspace,
+                            int64_t workspace_bytes, void* stream) {
+  REQUIRE(student && teacher && out, "pair_loss: null pointer");
+  REQUIRE(aligned16(student) && aligned16(teacher) && (!center || aligned16(center)), "pair_loss: misaligned");
+  REQUIRE(rows > 0 && D > 0 && D % 4 == 0, "pair_loss: bad shape");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_PAIR_LOSS, 1, rows, 0, 0),
+          "pair_loss: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  return probed(DSVT_PROBE_LOSS, 8.0 * rows * D, s, "dsvt_dino_pair_loss_fwd", [&]() -> hipError_t {
+    hipError_t e;
+    if ((e = launch_softmax_stats(teacher, center, 1.0f / teacher_temp, rows, D, ws, ws + rows, s))) return e;
+    if ((e = launch_softmax_stats(student, nullptr, 1.0f / student_temp, rows, D, ws + 2 * rows, ws + 3 * rows, s)))
+      return e;
+    return launch_pair_ce(student, teacher, center, nullptr, rows, 1, 1, 0, D, 1.0f / student_temp,
+                          1.0f / teacher_temp, ws, ws + rows, ws + 2 * rows, ws + 3 * rows, out, s);
+  });
+}
+
+int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentum, float inv_count, void* stream) {
+  REQUIRE(center && colsum && D > 0, "center_ema: bad args");
+  hipError_t e = launch_center_ema(center, colsum, D, momentum, inv_count, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "center_ema");
+}
+
+int dsvt_probe_enable(int mask, int capacity) {
+  g_probe.clear();
+  REQUIRE(capacity > 0 && capacity <= (1 << 20), "probe: bad capacity");
+  g_probe.ev0.resize(capacity);
+  g_probe.ev1.resize(capacity);
+  for (int i = 0; i < capacity; ++i) {
+    if (hipEventCreate(&g_probe.ev0[i]) != hipSuccess || hipEventCreate(&g_probe.ev1[i]) != hipSuccess) {
+      g_probe.ev0.resize(i); g_probe.ev1.resize(i);
+      g_probe.clear();
+      return fail("probe: hipEventCreate failed");
+    }
+  }
+  g_probe.work.assign(capacity, 0.0);
+  g_probe.fam.assign(capacity, 0);
+  g_probe.tag.assign(capacity, 0);
+  g_probe.cap = capacity;
+  g_probe.mask = mask;
+  return 0;
+}
+
+int dsvt_probe_disable(void) {
+  g_probe.clear();
+  return 0;
+}
+
+int dsvt_probe_read(float* ms, double* work, int32_t* family, int32_t* tag, int capacity) {
+  const int n = g_probe.count < capacity ? g_probe.count : capacity;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(g_probe.ev1[i]) != hipSuccess) return -fail("probe: event sync failed");
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, g_probe.ev0[i], g_probe.ev1[i]);
+    if (ms) ms[i] = t;
+    if (work) work[i] = g_probe.work[i];
+    if (family) family[i] = g_probe.fam[i];
+    if (tag) tag[i] = g_probe.tag[i];
+  }
+  g_probe.count = 0;
+  return n;
+}
+
+}  // extern "C"

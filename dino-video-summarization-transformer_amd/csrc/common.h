@@ -1,0 +1,74 @@
+// Shared device helpers for the DINO-SVT gfx950 kernels.
+// Storage types: bf16 is carried as raw `unsigned short` bits (perf mode), float is the
+// fp32 parity mode.  All accumulation is fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "internal.h"
+
+typedef unsigned short bf16_t;
+typedef short sv8 __attribute__((ext_vector_type(8)));   // 8 x bf16 MFMA operand (4 VGPRs)
+typedef short sv4 __attribute__((ext_vector_type(4)));   // 4 x bf16 (tr-read result)
+typedef float fv4 __attribute__((ext_vector_type(4)));   // 4 x fp32 accumulator
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+__device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((unsigned)u) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN preserved
+  return __builtin_bit_cast(bf16_t, h);
+}
+
+// Generic element <-> float conversion for the two storage types.
+template <typename T> struct Elem;
+template <> struct Elem<bf16_t> {
+  static constexpr int PER16 = 8;  // elements per 16-byte piece
+  __device__ __forceinline__ static float to_f(bf16_t v) { return bf2f(v); }
+  __device__ __forceinline__ static bf16_t from_f(float v) { return f2bf(v); }
+};
+template <> struct Elem<float> {
+  static constexpr int PER16 = 4;
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
+};
+
+// Store 4 consecutive values (converted to T): 8 B for bf16, 16 B for fp32.
+__device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, float d) {
+  uint2 u;
+  u.x = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+  u.y = (unsigned)f2bf(c) | ((unsigned)f2bf(d) << 16);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void load4(const bf16_t* p, float* v) {
+  uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void load4(const float* p, float* v) {
+  float4 f = *reinterpret_cast<const float4*>(p);
+  v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// Output-row map used by every kernel that writes into the [B, L, C] token tensor:
+//   row(m) = (m / rpg) * gstride + goff + (m % rpg)
+// identity: rpg = huge, gstride = 0, goff = 0.
+__device__ __forceinline__ long map_row(long m, long rpg, long gstride, long goff) {
+  return (m / rpg) * gstride + goff + (m % rpg);
+}

@@ -1,0 +1,212 @@
+// MFMA GEMM with fused epilogues for every nn.Linear / Conv2d(k=s=16) on the hot path.
+//
+//   out = A[M,K] . W[N,K]^T  (+ bias, GELU, residual add into the fp32 token tensor X,
+//                             or the patch-embed pos/time-embed add)
+//
+// Tiling (gfx950): 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each a
+// 64x64 sub-tile = 4x4 MFMA 16x16 tiles).  K advances 128 BYTES per stage (64 bf16 or
+// 32 fp32), staged global->LDS with `global_load_lds_dwordx4` (16 B/lane, no VGPR round
+// trip) into a 2-stage ring (64 KB LDS), XOR-swizzled on the SOURCE address so the
+// ds_read_b128 fragment reads are bank-conflict free (chunk' = chunk ^ ((row>>1)&7)).
+//
+// bf16: v_mfma_f32_16x16x32_bf16.  fp32 parity mode: v_mfma_f32_16x16x4_f32 (exact fp32
+// products), with the K order inside a stage permuted (lane group g owns k = 8g..8g+7).
+//
+// The MFMA is issued "swapped" (W fragment as the A operand) so each lane ends with 4
+// CONSECUTIVE output columns of one row: the epilogue does 16-B (fp32) / 8-B (bf16)
+// vector loads/stores.  Workgroup ids are remapped so the N-tiles of one M-tile run on the
+// same XCD (its A panel then stays in that XCD's L2).
+#include "common.h"
+
+namespace dsvt {
+
+constexpr int BM = 128, BN = 128, BKB = 128;  // tile rows, tile cols, K bytes per stage
+constexpr int TILE_BYTES = BM * BKB;           // 16 KB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // A + W
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+// Issue the global->LDS copy of one [128 rows][128 bytes] tile (16 x 1 KB pieces, 4 per
+// wave).  Rows beyond `rows` re-read the last row (results masked in the epilogue).
+__device__ __forceinline__ void stage_tile(const char* __restrict__ g, int64_t ld_bytes,
+                                           int64_t row0, int64_t rows, int64_t kbyte0,
+                                           char* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int cl = lane & 7;
+    int64_t gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const char* src = g + gr * ld_bytes + kbyte0 + ((cl ^ swz(r)) << 4);
+    __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ const char* lds_chunk(const char* tile, int r, int c) {
+  return tile + r * BKB + ((c ^ swz(r)) << 4);
+}
+
+template <typename T> struct TileMMA;
+
+template <> struct TileMMA<bf16_t> {
+  __device__ __forceinline__ static void run(const char* At, const char* Wt, fv4 (&acc)[4][4],
+                                             int wm, int wn, int lane) {
+    const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      sv8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const sv8*>(lds_chunk(At, wm * 64 + i * 16 + r16, ks * 4 + g));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *reinterpret_cast<const sv8*>(lds_chunk(Wt, wn * 64 + j * 16 + r16, ks * 4 + g));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+  }
+};
+
+template <> struct TileMMA<float> {
+  __device__ __forceinline__ static void run(const char* At, const char* Wt, fv4 (&acc)[4][4],
+                                             int wm, int wn, int lane) {
+    const int r16 = lane & 15, g = lane >> 4;
+    fv4 a[4][2], b[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + i * 16 + r16;
+      a[i][0] = *reinterpret_cast<const fv4*>(lds_chunk(At, r, 2 * g));
+      a[i][1] = *reinterpret_cast<const fv4*>(lds_chunk(At, r, 2 * g + 1));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wn * 64 + j * 16 + r16;
+      b[j][0] = *reinterpret_cast<const fv4*>(lds_chunk(Wt, r, 2 * g));
+      b[j][1] = *reinterpret_cast<const fv4*>(lds_chunk(Wt, r, 2 * g + 1));
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][s >> 2][s & 3], a[i][s >> 2][s & 3],
+                                                          acc[i][j], 0, 0, 0);
+  }
+};
+
+template <typename T, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap: consecutive workgroup ids of one XCD walk the N-tiles of
+  // one M-tile (blocks b and b+8 share an XCD under round-robin dispatch).
+  const int tilesN = (int)((p.N + BN - 1) / BN);
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int64_t m0 = (int64_t)(wg / tilesN) * BM;
+  const int64_t n0 = (int64_t)(wg % tilesN) * BN;
+
+  const char* A = (const char*)p.A;
+  const char* W = (const char*)p.W;
+  const int64_t lda_b = p.lda * (int64_t)sizeof(T), ldw_b = p.ldw * (int64_t)sizeof(T);
+  const int nk = (int)((p.K * (int64_t)sizeof(T)) / BKB);
+
+  fv4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile(A, lda_b, m0, p.M, 0, smem, wave, lane);
+  stage_tile(W, ldw_b, n0, p.N, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+      stage_tile(A, lda_b, m0, p.M, (int64_t)(kt + 1) * BKB, nxt, wave, lane);
+      stage_tile(W, ldw_b, n0, p.N, (int64_t)(kt + 1) * BKB, nxt + TILE_BYTES, wave, lane);
+    }
+    TileMMA<T>::run(cur, cur + TILE_BYTES, acc, wm, wn, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + 0..3]
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + wm * 64 + i * 16 + r16;
+    if (m >= p.M) continue;
+    const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
+      if (n >= p.N) continue;
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if (p.bias) {
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+        v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
+      }
+      if constexpr (EPI == EPI_GELU) {
+        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+      }
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
+        if constexpr (OUT_F32)
+          store4((float*)p.out + orow * p.ldo + n, v0, v1, v2, v3);
+        else
+          store4((T*)p.out + orow * p.ldo + n, v0, v1, v2, v3);
+      } else if constexpr (EPI == EPI_RESID) {
+        float4* xo = reinterpret_cast<float4*>((float*)p.out + orow * p.ldo + n);
+        float4 x = *xo;
+        x.x += v0; x.y += v1; x.z += v2; x.w += v3;
+        *xo = x;
+      } else {  // EPI_PATCH
+        const int64_t rr = m % p.rpg;
+        const int64_t np = rr / p.T, t = rr % p.T;
+        const float4 pe = *reinterpret_cast<const float4*>(p.pos + (1 + (int64_t)p.pidx[np]) * p.N + n);
+        v0 += pe.x; v1 += pe.y; v2 += pe.z; v3 += pe.w;
+        if (p.temb) {
+          const float4 te = *reinterpret_cast<const float4*>(p.temb + (int64_t)p.tidx[t] * p.N + n);
+          v0 += te.x; v1 += te.y; v2 += te.z; v3 += te.w;
+        }
+        store4((float*)p.out + orow * p.ldo + n, v0, v1, v2, v3);
+      }
+    }
+  }
+}
+
+template <typename T>
+static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
+  const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  dim3 grid((unsigned)tiles), block(256);
+  switch (epi) {
+    case EPI_BIAS:
+      if (out_f32) gemm_kernel<T, EPI_BIAS, true><<<grid, block, 0, s>>>(p);
+      else gemm_kernel<T, EPI_BIAS, false><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_GELU:
+      if (out_f32) gemm_kernel<T, EPI_GELU, true><<<grid, block, 0, s>>>(p);
+      else gemm_kernel<T, EPI_GELU, false><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_RESID: gemm_kernel<T, EPI_RESID, true><<<grid, block, 0, s>>>(p); break;
+    case EPI_PATCH: gemm_kernel<T, EPI_PATCH, true><<<grid, block, 0, s>>>(p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
+  return dtype == 0 ? launch_t<bf16_t>(p, epi, out_f32, s) : launch_t<float>(p, epi, out_f32, s);
+}
+
+}  // namespace dsvt

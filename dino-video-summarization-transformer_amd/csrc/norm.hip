@@ -1,0 +1,281 @@
+// Row-wise normalizations and the small layout kernels of the hot path.
+//   LayerNorm (K3), F.normalize + weight-norm (K12), im2col for PatchEmbed (K1),
+//   CLS token init (K2), CLS mean over frames (K8), dtype cast.
+// All are HBM-bound: one wave per row, 16-B vector loads where the row length allows.
+#include "common.h"
+
+namespace dsvt {
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row; VEC: C % 256 == 0 (float4 per lane per 256 cols), else C % 64 == 0.
+template <typename OutT, bool VEC>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, OutT* __restrict__ y,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int64_t rows,
+                                                        int C, int64_t rpg, int64_t gstride,
+                                                        int64_t goff, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* xr = x + map_row(r, rpg, gstride, goff) * C;
+  OutT* yr = y + r * C;
+  float v[16];
+  float s = 0.f;
+  if constexpr (VEC) {
+    const int n4 = C >> 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < n4) {
+        float4 f = *reinterpret_cast<const float4*>(xr + i * 256 + lane * 4);
+        v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+        s += (f.x + f.y) + (f.z + f.w);
+      }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < 4 * n4) { v[i] -= mean; q += v[i] * v[i]; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < n4) {
+        const int c = i * 256 + lane * 4;
+        const float4 gg = *reinterpret_cast<const float4*>(gamma + c);
+        const float4 bb = *reinterpret_cast<const float4*>(beta + c);
+        store4(yr + c, v[4 * i] * rstd * gg.x + bb.x, v[4 * i + 1] * rstd * gg.y + bb.y,
+               v[4 * i + 2] * rstd * gg.z + bb.z, v[4 * i + 3] * rstd * gg.w + bb.w);
+      }
+  } else {
+    const int n = C >> 6;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) { v[i] = xr[i * 64 + lane]; s += v[i]; }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) { v[i] -= mean; q += v[i] * v[i]; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) {
+        const int c = i * 64 + lane;
+        yr[c] = Elem<OutT>::from_f(v[i] * rstd * gamma[c] + beta[c]);
+      }
+  }
+}
+
+template <typename OutT>
+static hipError_t ln_t(const float* x, OutT* y, const float* g, const float* b, int64_t rows, int64_t C,
+                       int64_t rpg, int64_t gstride, int64_t goff, float eps, hipStream_t s) {
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  if (C % 256 == 0)
+    layernorm_kernel<OutT, true><<<grid, block, 0, s>>>(x, y, g, b, rows, (int)C, rpg, gstride, goff, eps);
+  else
+    layernorm_kernel<OutT, false><<<grid, block, 0, s>>>(x, y, g, b, rows, (int)C, rpg, gstride, goff, eps);
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
+                            const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
+                            int64_t goff, float eps, hipStream_t s) {
+  if (dtype == 1 || out_f32) return ln_t<float>(x, (float*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
+  return ln_t<bf16_t>(x, (bf16_t*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
+}
+
+// ---------------------------------------------------------------- L2 row norms
+// MODE 0: F.normalize  y = x / max(||x||, eps)          (vision_transformer.py:280)
+// MODE 1: weight_norm  y = x * (g[r] / ||x||)           (torch._weight_norm, dim=0)
+template <typename OutT, int MODE>
+__global__ __launch_bounds__(256) void rownorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                      OutT* __restrict__ y, int64_t rows, int D, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* xr = x + r * D;
+  OutT* yr = y + r * D;
+  float s = 0.f;
+  for (int c = lane * 4; c < D; c += 256) {
+    const float4 f = *reinterpret_cast<const float4*>(xr + c);
+    s += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+  }
+  const float nrm = sqrtf(wave_sum(s));
+  const float sc = MODE == 0 ? 1.0f / fmaxf(nrm, eps) : g[r] / nrm;
+  for (int c = lane * 4; c < D; c += 256) {
+    const float4 f = *reinterpret_cast<const float4*>(xr + c);
+    store4(yr + c, f.x * sc, f.y * sc, f.z * sc, f.w * sc);
+  }
+}
+
+hipError_t launch_l2norm(int dtype, const float* x, void* y, int64_t rows, int64_t D, float eps, hipStream_t s) {
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  if (dtype == 0) rownorm_kernel<bf16_t, 0><<<grid, block, 0, s>>>(x, nullptr, (bf16_t*)y, rows, (int)D, eps);
+  else rownorm_kernel<float, 0><<<grid, block, 0, s>>>(x, nullptr, (float*)y, rows, (int)D, eps);
+  return hipGetLastError();
+}
+
+hipError_t launch_weight_norm(int dtype, const float* v, const float* g, void* w, int64_t rows, int64_t D,
+                              hipStream_t s) {
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  if (dtype == 0) rownorm_kernel<bf16_t, 1><<<grid, block, 0, s>>>(v, g, (bf16_t*)w, rows, (int)D, 0.f);
+  else rownorm_kernel<float, 1><<<grid, block, 0, s>>>(v, g, (float*)w, rows, (int)D, 0.f);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- cast fp32 -> T
+template <typename OutT>
+__global__ void cast_kernel(const float* __restrict__ x, OutT* __restrict__ y, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 f = reinterpret_cast<const float4*>(x)[i];
+    store4(y + 4 * i, f.x, f.y, f.z, f.w);
+  }
+}
+
+hipError_t launch_cast(int dtype, const float* x, void* y, int64_t n, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  unsigned blocks = (unsigned)((n4 + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return hipSuccess;
+  if (dtype == 0) cast_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, (bf16_t*)y, n4);
+  else cast_kernel<float><<<blocks, 256, 0, s>>>(x, (float*)y, n4);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- im2col (PatchEmbed)
+// A[m][k], k = c*256 + kh*16 + kw; order_nt: m = (b*Np + np)*T + t, else m = (b*T + t)*Np + np.
+// One thread per 4 consecutive kw (one float4 of the input row).
+// fidx (nullable): x is a frame bank [F][Cin][H][W]; frame t of clip b = fidx[b*Tf + t], -1 = zeros.
+template <typename T>
+__global__ void im2col_kernel(const float* __restrict__ x, T* __restrict__ a, int64_t total, int Cin, int Tf,
+                              int H, int W, int Hp, int Wp, int order_nt, const int32_t* __restrict__ fidx) {
+  const int K = Cin * 256, kq = K / 4, Np = Hp * Wp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / kq;
+    const int k = (int)(i % kq) * 4;
+    const int c = k >> 8, kh = (k >> 4) & 15, kw = k & 15;
+    int64_t b; int t, np;
+    if (order_nt) { t = (int)(m % Tf); np = (int)((m / Tf) % Np); b = m / ((int64_t)Tf * Np); }
+    else { np = (int)(m % Np); t = (int)((m / Np) % Tf); b = m / ((int64_t)Tf * Np); }
+    const int ph = np / Wp, pw = np % Wp;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fidx) {
+      const int fi = fidx[b * Tf + t];
+      if (fi >= 0) f = *reinterpret_cast<const float4*>(x + ((((int64_t)fi * Cin + c) * H + ph * 16 + kh) * (int64_t)W + pw * 16 + kw));
+    } else {
+      f = *reinterpret_cast<const float4*>(x + ((((b * Cin + c) * Tf + t) * H + ph * 16 + kh) * (int64_t)W + pw * 16 + kw));
+    }
+    store4(a + m * K + k, f.x, f.y, f.z, f.w);
+  }
+}
+
+hipError_t launch_im2col(int dtype, int order_nt, const float* x, void* a, int64_t B, int64_t Cin, int64_t T,
+                         int64_t H, int64_t W, int64_t Hp, int64_t Wp, const int32_t* fidx, hipStream_t s) {
+  const int64_t total = B * T * Hp * Wp * Cin * 64;
+  unsigned blocks = (unsigned)((total + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  if (dtype == 0)
+    im2col_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, (bf16_t*)a, total, (int)Cin, (int)T, (int)H, (int)W, (int)Hp, (int)Wp, order_nt, fidx);
+  else
+    im2col_kernel<float><<<blocks, 256, 0, s>>>(x, (float*)a, total, (int)Cin, (int)T, (int)H, (int)W, (int)Hp, (int)Wp, order_nt, fidx);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- bicubic pos-embed resize
+// ATen upsample_bicubic2d (align_corners=False, scale given): real = inv_scale*(dst+0.5)-0.5,
+// idx = min(floor(real), size-1), t = clamp(real-idx, 0, 1), taps idx-1..idx+2 clamped,
+// A = -0.75; interpolate along x for 4 rows, then along y (same op order as ATen's CPU loop).
+__device__ __forceinline__ void cubic_coeffs(float t, float* c) {
+  const float A = -0.75f;
+  float x1 = t;
+  c[0] = ((A * (x1 + 1.f) - 5.f * A) * (x1 + 1.f) + 8.f * A) * (x1 + 1.f) - 4.f * A;
+  c[1] = ((A + 2.f) * x1 - (A + 3.f)) * x1 * x1 + 1.f;
+  float x2 = 1.f - t;
+  c[2] = ((A + 2.f) * x2 - (A + 3.f)) * x2 * x2 + 1.f;
+  c[3] = ((A * (x2 + 1.f) - 5.f * A) * (x2 + 1.f) + 8.f * A) * (x2 + 1.f) - 4.f * A;
+}
+
+__global__ void pos_bicubic_kernel(const float* __restrict__ pos, float* __restrict__ out, int sg, int OH, int OW,
+                                   int C, float inv_h, float inv_w) {
+  const int o = blockIdx.x;  // 0 = CLS row
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    if (o == 0) { out[c] = pos[c]; continue; }
+    const int oy = (o - 1) / OW, ox = (o - 1) % OW;
+    const float ry = inv_h * ((float)oy + 0.5f) - 0.5f, rx = inv_w * ((float)ox + 0.5f) - 0.5f;
+    int iy = (int)floorf(ry); iy = iy < sg - 1 ? iy : sg - 1;
+    int ix = (int)floorf(rx); ix = ix < sg - 1 ? ix : sg - 1;
+    const float ty = fminf(fmaxf(ry - iy, 0.f), 1.f), tx = fminf(fmaxf(rx - ix, 0.f), 1.f);
+    float cy[4], cx[4], rows[4];
+    cubic_coeffs(ty, cy);
+    cubic_coeffs(tx, cx);
+    for (int i = 0; i < 4; ++i) {
+      int yy = iy - 1 + i; yy = yy < 0 ? 0 : (yy > sg - 1 ? sg - 1 : yy);
+      float v[4];
+      for (int j = 0; j < 4; ++j) {
+        int xx = ix - 1 + j; xx = xx < 0 ? 0 : (xx > sg - 1 ? sg - 1 : xx);
+        v[j] = pos[(int64_t)(1 + yy * sg + xx) * C + c];
+      }
+      rows[i] = v[0] * cx[0] + v[1] * cx[1] + v[2] * cx[2] + v[3] * cx[3];
+    }
+    out[(int64_t)o * C + c] = rows[0] * cy[0] + rows[1] * cy[1] + rows[2] * cy[2] + rows[3] * cy[3];
+  }
+}
+
+hipError_t launch_pos_bicubic(const float* pos, float* out, int64_t sgrid, int64_t OH, int64_t OW, int64_t C,
+                              float inv_h, float inv_w, hipStream_t s) {
+  pos_bicubic_kernel<<<(unsigned)(1 + OH * OW), 256, 0, s>>>(pos, out, (int)sgrid, (int)OH, (int)OW, (int)C, inv_h, inv_w);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- CLS rows
+// X[r*stride + c] = cls[c] + pos0[c]   (timesformer.py:288-305: cat(cls) then + pos_embed[0])
+__global__ void cls_init_kernel(float* __restrict__ X, const float* __restrict__ cls, const float* __restrict__ pos0,
+                                int64_t rows, int64_t stride, int C) {
+  const int64_t r = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) X[r * stride + c] = cls[c] + pos0[c];
+}
+
+hipError_t launch_cls_init(float* X, const float* cls, const float* pos0, int64_t rows, int64_t stride, int64_t C,
+                           hipStream_t s) {
+  cls_init_kernel<<<(unsigned)rows, 256, 0, s>>>(X, cls, pos0, rows, stride, (int)C);
+  return hipGetLastError();
+}
+
+// out[b*L][c] = mean_t aux[(b*T + t)][c]  (timesformer.py:162-164; proj is affine, so the
+// mean is taken before it -- see DESIGN.md)
+template <typename T>
+__global__ void cls_mean_kernel(const float* __restrict__ aux, T* __restrict__ out, int Tf, int64_t L, int C) {
+  const int64_t b = blockIdx.x;
+  const float inv = 1.0f / Tf;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < Tf; ++t) s += aux[(b * Tf + t) * C + c];
+    out[b * L * C + c] = Elem<T>::from_f(s * inv);
+  }
+}
+
+hipError_t launch_cls_mean(int dtype, const float* aux, void* out, int64_t B, int64_t T, int64_t L, int64_t C,
+                           hipStream_t s) {
+  if (dtype == 0) cls_mean_kernel<bf16_t><<<(unsigned)B, 256, 0, s>>>(aux, (bf16_t*)out, (int)T, L, (int)C);
+  else cls_mean_kernel<float><<<(unsigned)B, 256, 0, s>>>(aux, (float*)out, (int)T, L, (int)C);
+  return hipGetLastError();
+}
+
+// y[b][i] = mean_t x[(b*T + t)][i]   (space_only prediction average, timesformer.py:338-340)
+__global__ void frame_mean_kernel(const float* __restrict__ x, float* __restrict__ y, int Tf, int64_t rowlen) {
+  const int64_t b = blockIdx.y;
+  const float inv = 1.0f / Tf;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rowlen; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < Tf; ++t) s += x[(b * Tf + t) * rowlen + i];
+    y[b * rowlen + i] = s * inv;
+  }
+}
+
+hipError_t launch_frame_mean(const float* x, float* y, int64_t B, int64_t T, int64_t rowlen, hipStream_t s) {
+  unsigned bx = (unsigned)((rowlen + 255) / 256);
+  if (bx > 1024) bx = 1024;
+  frame_mean_kernel<<<dim3(bx, (unsigned)B), 256, 0, s>>>(x, y, (int)T, rowlen);
+  return hipGetLastError();
+}
+
+}  // namespace dsvt

@@ -1,0 +1,79 @@
+"""ctypes binding of the gfx950 C-ABI library (include/dsvt.h -> libdsvt.so).
+
+There is NO fallback: if the library is missing or cannot be loaded, every op raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DSVT_LIB", os.path.join(_HERE, "libdsvt.so"))
+
+BF16, F32 = 0, 1
+EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID = 0, 1, 2
+TOKENS_NT, TOKENS_FRAME = 0, 1
+PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
+WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
+
+_i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+# name -> (restype, argtypes); must mirror include/dsvt.h exactly (tests/test_capi_symbols.py)
+SIGNATURES = {
+    "dsvt_version": (_i32, []),
+    "dsvt_last_error": (ctypes.c_char_p, []),
+    "dsvt_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
+    "dsvt_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
+                             _i64, _i64, _i64, _p]),
+    "dsvt_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_ln_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _i64, _i64, _p, _p, _f32, _p, _p, _p, _i64,
+                                _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
+    "dsvt_patch_embed_fwd": (_i32, [_i32, _i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p,
+                                    _p, _p, _p, _i64, _p, _p, _p, _i64, _p]),
+    "dsvt_pos_bicubic_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _p]),
+    "dsvt_attn_temporal_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_attn_spatial_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
+    "dsvt_attn_joint_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_frame_mean_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
+    "dsvt_cast_fwd": (_i32, [_i32, _p, _p, _i64, _p]),
+    "dsvt_dino_head_norm_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _f32, _p]),
+    "dsvt_weight_norm_fwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _p]),
+    "dsvt_dino_loss_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _f32, _f32, _p, _p, _p, _i64, _p]),
+    "dsvt_dino_pair_loss_fwd": (_i32, [_p, _p, _p, _i64, _i64, _f32, _f32, _p, _p, _i64, _p]),
+    "dsvt_center_ema": (_i32, [_p, _p, _i64, _f32, _f32, _p]),
+    "dsvt_probe_enable": (_i32, [_i32, _i32]),
+    "dsvt_probe_disable": (_i32, []),
+    "dsvt_probe_read": (_i32, [_p, _p, _p, _p, _i32]),
+}
+
+
+class DsvtError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libdsvt.so once; raise loudly if it is absent (no CPU / eager fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DsvtError("libdsvt.so not found at %s -- run `python -c 'import __graft_entry__ as g; "
+                            "g.build()'` (or make -C dino-video-summarization-transformer_amd/csrc)" % LIB_PATH)
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.dsvt_version() != 1:
+            raise DsvtError("libdsvt ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point; non-zero status -> DsvtError with dsvt_last_error()."""
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        raise DsvtError("%s failed (%d): %s" % (name, rc, L.dsvt_last_error().decode()))
+    return rc

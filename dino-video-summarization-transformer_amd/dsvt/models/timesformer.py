@@ -1,0 +1,403 @@
+"""TimeSformer ViT (divided space-time / joint / space-only) on the gfx950 kernels.
+
+Drop-in for models/timesformer.py of the reference: same constructor signatures
+(`VisionTransformer` :212-276, `TimeSformer` :404-426, `get_vit_base_patch16_224`
+:592-609), same sub-module names, hence the same 247 state_dict keys (ViT-B, no head),
+so SVT checkpoints load unchanged.  The nn.Linear / nn.LayerNorm / nn.Conv2d children
+are parameter containers only: forward never calls them -- it runs the token tensor
+through libdsvt.so (dsvt.ops).
+
+Storage precision: `model.dsvt_dtype` (torch.bfloat16 = bf16 MFMA perf mode, default;
+torch.float32 = fp32 parity mode).  The residual token stream is always fp32.
+"""
+import math
+from functools import partial
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .._lib import EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, TOKENS_FRAME, TOKENS_NT, WS_ATTN_SPATIAL, \
+    WS_LN_GEMM, WS_PATCH_EMBED, DsvtError
+from ..weights import WeightCache
+from .vit_utils import DropPath, to_2tuple, trunc_normal_
+
+_DEFAULT_DTYPE = [torch.bfloat16]
+
+
+def set_default_dtype(dtype):
+    """Storage precision for models created afterwards (torch.bfloat16 | torch.float32)."""
+    assert dtype in (torch.bfloat16, torch.float32)
+    _DEFAULT_DTYPE[0] = dtype
+
+
+def nearest_index(out_size, in_size):
+    """ATen upsample_nearest source index (float32 scale = in/out, floorf, clamp), the rule
+    behind F.interpolate(mode='nearest') at models/timesformer.py:299 and :316."""
+    if out_size == in_size:
+        return np.arange(out_size)
+    if out_size == 2 * in_size:
+        return np.arange(out_size) >> 1
+    scale = np.float32(in_size) / np.float32(out_size)
+    idx = np.floor(np.arange(out_size, dtype=np.float32) * scale).astype(np.int64)
+    return np.minimum(idx, in_size - 1)
+
+
+class Mlp(nn.Module):
+    """models/timesformer.py:36-52 (parameter container)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+
+class Attention(nn.Module):
+    """models/timesformer.py:55-87 (parameter container; math in dsvt attention kernels)."""
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, qk_scale=None, attn_drop=0., proj_drop=0., with_qkv=True):
+        super().__init__()
+        if not with_qkv:
+            raise NotImplementedError("Attention(with_qkv=False) is not on the DINO-SVT path")
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        if head_dim != 64:
+            raise NotImplementedError("dsvt kernels are specialised for head_dim 64 (ViT-Ti/S/B); got %d" % head_dim)
+        self.scale = qk_scale or head_dim ** -0.5
+        self.with_qkv = with_qkv
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.attn_drop = nn.Dropout(attn_drop)
+
+
+class Block(nn.Module):
+    """models/timesformer.py:90-185."""
+
+    def __init__(self, dim, num_heads, mlp_ratio=4., qkv_bias=False, qk_scale=None, drop=0., attn_drop=0.,
+                 drop_path=0.1, act_layer=nn.GELU, norm_layer=nn.LayerNorm, attention_type='divided_space_time'):
+        super().__init__()
+        self.attention_type = attention_type
+        self.class_tokens = 1
+        assert attention_type in ['divided_space_time', 'space_only', 'joint_space_time']
+        self.norm1 = norm_layer(dim)
+        self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                              attn_drop=attn_drop, proj_drop=drop)
+        if attention_type == 'divided_space_time':
+            self.temporal_norm1 = norm_layer(dim)
+            self.temporal_attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                                           attn_drop=attn_drop, proj_drop=drop)
+            self.temporal_fc = nn.Linear(dim, dim)
+        self.drop_path = DropPath(drop_path) if drop_path > 0. else nn.Identity()
+        self.norm2 = norm_layer(dim)
+        self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+
+    # -------------------------------------------------------------- HIP forward
+    def run(self, X, ctx):
+        """One block on the fp32 token tensor X (in place).  ctx: per-forward buffers."""
+        w = ctx.w
+        C, heads = ctx.C, self.attn.num_heads
+        eps1, eps2 = self.norm1.eps, self.norm2.eps
+        if self.attention_type == 'divided_space_time':
+            B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
+            R = B * Np * T
+            patch_map = (Np * T, L, 1)          # compact patch row m -> X row b*L + 1 + m % (Np*T)
+            ta = self.temporal_attn
+            # temporal: LN -> qkv (timesformer.py:127-131)
+            ops.ln_gemm(X, patch_map, R, self.temporal_norm1.weight, self.temporal_norm1.bias,
+                        self.temporal_norm1.eps, w(ta.qkv.weight), ta.qkv.bias, ctx.qkv, ctx.ws)
+            ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
+            ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)                 # proj (:83)
+            ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X,        # fc + residual
+                     epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)                       # (:133-135)
+            # spatial with CLS replicate/mean (:139-181)
+            ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, eps1, w(self.attn.qkv.weight),
+                        self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
+        else:
+            nb, L = ctx.nb, ctx.L
+            ops.ln_gemm(X, None, nb * L, self.norm1.weight, self.norm1.bias, eps1, w(self.attn.qkv.weight),
+                        self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            ops.attn_joint(ctx.qkv, ctx.o, nb, L, heads, self.attn.scale)
+        rows = ctx.rows
+        ops.gemm(ctx.o, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
+        # MLP (:184)
+        ops.ln_gemm(X, None, rows, self.norm2.weight, self.norm2.bias, eps2, w(self.mlp.fc1.weight),
+                    self.mlp.fc1.bias, ctx.hid, ctx.ws, epilogue=EPI_BIAS_GELU)
+        ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
+
+
+class PatchEmbed(nn.Module):
+    """models/timesformer.py:188-209 (Conv2d k=s=patch is an im2col GEMM in dsvt)."""
+
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, embed_dim=768):
+        super().__init__()
+        img_size = to_2tuple(img_size)
+        patch_size = to_2tuple(patch_size)
+        self.img_size = img_size
+        self.patch_size = patch_size
+        self.num_patches = (img_size[1] // patch_size[1]) * (img_size[0] // patch_size[0])
+        self.proj = nn.Conv2d(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size)
+
+
+class _Ctx:
+    """Per-forward scratch buffers (torch caching allocator = plumbing)."""
+
+
+class VisionTransformer(nn.Module):
+    """models/timesformer.py:212-364."""
+
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, num_classes=1000, embed_dim=768, depth=12,
+                 num_heads=12, mlp_ratio=4., qkv_bias=False, qk_scale=None, drop_rate=0., attn_drop_rate=0.,
+                 drop_path_rate=0.1, hybrid_backbone=None, norm_layer=nn.LayerNorm, num_frames=8,
+                 attention_type='divided_space_time', dropout=0.):
+        super().__init__()
+        if patch_size != 16:
+            raise NotImplementedError("dsvt patch embedding is specialised for patch_size 16")
+        self.attention_type = attention_type
+        self.depth = depth
+        self.dropout = nn.Dropout(dropout)
+        self.num_classes = num_classes
+        self.num_features = self.embed_dim = embed_dim
+        self.patch_embed = PatchEmbed(img_size=img_size, patch_size=patch_size, in_chans=in_chans, embed_dim=embed_dim)
+        num_patches = self.patch_embed.num_patches
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, num_patches + 1, embed_dim))
+        self.pos_drop = nn.Dropout(p=drop_rate)
+        if self.attention_type != 'space_only':
+            self.time_embed = nn.Parameter(torch.zeros(1, num_frames, embed_dim))
+            self.time_drop = nn.Dropout(p=drop_rate)
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, self.depth)]
+        self.blocks = nn.ModuleList([
+            Block(dim=embed_dim, num_heads=num_heads, mlp_ratio=mlp_ratio, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                  drop=drop_rate, attn_drop=attn_drop_rate, drop_path=dpr[i], norm_layer=norm_layer,
+                  attention_type=self.attention_type)
+            for i in range(self.depth)])
+        self.norm = norm_layer(embed_dim)
+        self.head = nn.Linear(embed_dim, num_classes) if num_classes > 0 else nn.Identity()
+        self._drop_rates = (drop_rate, attn_drop_rate, dropout)
+
+        trunc_normal_(self.pos_embed, std=.02)
+        trunc_normal_(self.cls_token, std=.02)
+        self.apply(self._init_weights)
+        if self.attention_type == 'divided_space_time':
+            # reference quirk kept for init parity (:255-263): the counter first hits the
+            # ModuleList itself, so EVERY block's temporal_fc is zero-initialised
+            i = 0
+            for m in self.blocks.modules():
+                if 'Block' in str(m):
+                    if i > 0:
+                        nn.init.constant_(m.temporal_fc.weight, 0)
+                        nn.init.constant_(m.temporal_fc.bias, 0)
+                    i += 1
+        self.dsvt_dtype = _DEFAULT_DTYPE[0]
+        self._wcache = WeightCache()
+        self._index_cache = {}
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Linear):
+            trunc_normal_(m.weight, std=.02)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    @torch.jit.ignore
+    def no_weight_decay(self):
+        return {'pos_embed', 'cls_token', 'time_embed'}
+
+    def get_classifier(self):
+        return self.head
+
+    def reset_classifier(self, num_classes, global_pool=''):
+        self.num_classes = num_classes
+        self.head = nn.Linear(self.embed_dim, num_classes) if num_classes > 0 else nn.Identity()
+
+    # -------------------------------------------------------------- helpers
+    def _indices(self, Hp, Wp, T, device):
+        key = (Hp, Wp, T, device)
+        if key not in self._index_cache:
+            P = int(math.isqrt(self.pos_embed.shape[1] - 1))
+            if self.pos_embed.shape[1] == 1 + Hp * Wp:
+                pidx = np.arange(Hp * Wp)
+            else:  # nearest resize of the PxP grid (timesformer.py:292-303)
+                ri, ci = nearest_index(Hp, P), nearest_index(Wp, P)
+                pidx = (ri[:, None] * P + ci[None, :]).reshape(-1)
+            tidx = None
+            if self.attention_type != 'space_only':
+                tidx = torch.from_numpy(nearest_index(T, self.time_embed.shape[1]).astype(np.int32)).to(device)
+            self._index_cache[key] = (torch.from_numpy(pidx.astype(np.int32)).to(device), tidx)
+        return self._index_cache[key]
+
+    def _check_supported(self, x):
+        if not getattr(x, "is_cuda", False) or not self.pos_embed.is_cuda:
+            raise DsvtError("dsvt VisionTransformer runs only on the GPU (no CPU fallback): move model and input "
+                            "to cuda")
+        if self.training:
+            if any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0 for b in self.blocks):
+                raise NotImplementedError("training-mode stochastic depth (DropPath) is not implemented in the "
+                                          "dsvt forward yet; call .eval() (SURVEY §8(f))")
+            if any(r > 0 for r in self._drop_rates):
+                raise NotImplementedError("dropout > 0 is not supported by the dsvt forward")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("dsvt backward is not implemented yet (SURVEY §8(f) rank 1): run the "
+                                      "forward under torch.no_grad() or freeze the parameters")
+
+    # -------------------------------------------------------------- forward
+    def forward_features(self, x, get_all=False, get_attn=False, out=None):
+        """models/timesformer.py:285-345 on libdsvt.so.  `x` may also be a LIST of clip
+        tensors of one shape (MultiCropWrapper groups: no torch.cat copy); `out` optionally
+        receives the [B, C] CLS features in place."""
+        clips = list(x) if isinstance(x, (list, tuple)) else [x]
+        B = sum(c.shape[0] for c in clips)
+        shape = tuple(clips[0].shape[1:])
+        if any(tuple(c.shape[1:]) != shape for c in clips):
+            raise ValueError("all clips of one forward must share (C, T, H, W)")
+        srcs = [(c, None, c.shape[0]) for c in clips]
+        return self._forward_sources(srcs, B, shape[1], shape[2], shape[3], shape[0], get_all, get_attn, out)
+
+    def forward_frame_bank(self, frames, frame_index, B, T, get_all=False, out=None):
+        """Clips gathered from a frame bank [F, Cin, H, W] by frame_index [B*T] int32 (-1 =
+        zero frame) inside the patch-embed kernel (frame scoring: the per-frame local/global
+        views of dino_loss_loader.py:126-171 are never materialized)."""
+        _, Cin, H, W = frames.shape
+        return self._forward_sources([(frames, frame_index, B)], B, T, H, W, Cin, get_all, False, out)
+
+    def _forward_sources(self, srcs, B, T, H, W, Cin, get_all, get_attn, out):
+        if get_attn:
+            raise NotImplementedError("get_attn (attention-probability export) is not on the hot path yet")
+        for src, _, _ in srcs:
+            self._check_supported(src)
+        mode = self.dsvt_dtype
+        w = self._wcache.getter(mode)
+        Hp, Wp = H // 16, W // 16
+        Np = Hp * Wp
+        C = self.embed_dim
+        dev = srcs[0][0].device
+        pidx, tidx = self._indices(Hp, Wp, T, dev)
+        ctx = _Ctx()
+        ctx.w, ctx.C, ctx.B, ctx.T, ctx.Np = w, C, B, T, Np
+        if self.attention_type == 'space_only':
+            ctx.nb, ctx.L, order, rows_per_clip = B * T, 1 + Np, TOKENS_FRAME, T * (1 + Np)
+        else:
+            ctx.nb, ctx.L, order, rows_per_clip = B, 1 + Np * T, TOKENS_NT, 1 + Np * T
+        ctx.rows = ctx.nb * ctx.L
+        X = torch.empty(ctx.rows, C, device=dev, dtype=torch.float32)
+        pe_rows = max(b for _, _, b in srcs) * T * Np
+        ws_bytes = max(ops.workspace_bytes(WS_LN_GEMM, mode, ctx.rows, 0, C),
+                       ops.workspace_bytes(WS_PATCH_EMBED, mode, pe_rows, C, Cin * 256))
+        ctx.ws = torch.empty(ws_bytes // 2, device=dev, dtype=torch.bfloat16)
+        row0 = 0
+        for src, fidx, nb in srcs:          # K1+K2 per source, straight into its rows of X
+            xs = src.float().contiguous()
+            ops.patch_embed(xs, w(self.patch_embed.proj.weight, flat=True), self.patch_embed.proj.bias,
+                            self.cls_token, self.pos_embed, pidx,
+                            None if order == TOKENS_FRAME else self.time_embed, tidx,
+                            X[row0 * rows_per_clip:(row0 + nb) * rows_per_clip], ctx.ws, order,
+                            frame_index=fidx, clip_shape=(nb, T))
+            row0 += nb
+        ctx.qkv = torch.empty(ctx.rows, 3 * C, device=dev, dtype=mode)
+        ctx.o = torch.empty(ctx.rows, C, device=dev, dtype=mode)
+        ctx.hid = torch.empty(ctx.rows, self.blocks[0].mlp.fc1.out_features, device=dev, dtype=mode)
+        if self.attention_type == 'divided_space_time':
+            ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
+            nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
+            ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+        for blk in self.blocks:
+            blk.run(X, ctx)
+        L = ctx.L
+        if self.attention_type == 'space_only':      # mean over frames (:338-340)
+            Xm = torch.empty(B * L, C, device=dev, dtype=torch.float32)
+            ops.frame_mean(X, Xm, B, T, L * C)
+            X = Xm
+        if get_all:
+            res = torch.empty(B, L, C, device=dev, dtype=torch.float32) if out is None else out
+            return ops.layernorm(X, B * L, C, self.norm.weight, self.norm.bias, self.norm.eps, res)
+        res = torch.empty(B, C, device=dev, dtype=torch.float32) if out is None else out
+        return ops.layernorm(X, B, C, self.norm.weight, self.norm.bias, self.norm.eps, res, rowmap=(1, L, 0))
+
+    def forward(self, x, use_head=False):
+        x = self.forward_features(x)
+        if use_head:
+            if isinstance(self.head, nn.Linear):
+                mode = self.dsvt_dtype
+                w = self._wcache.getter(mode)
+                a = torch.empty(x.shape[0], x.shape[1], device=x.device, dtype=mode)
+                ops.cast(x, a)
+                out = torch.empty(x.shape[0], self.head.out_features, device=x.device, dtype=torch.float32)
+                return ops.gemm(a, w(self.head.weight), self.head.bias, out, out_f32=True)
+        return x
+
+    def get_intermediate_layers(self, x, n=1):
+        return [self.forward_features(x, get_all=True)]
+
+
+def _state_dict_pretrained(model, pretrained_model):
+    from ..checkpoint import load_pretrained
+    load_pretrained(model, pretrained_model)
+
+
+class vit_base_patch16_224(nn.Module):
+    """models/timesformer.py:379-401 (local checkpoints only; no URL fetch)."""
+
+    def __init__(self, cfg, **kwargs):
+        super().__init__()
+        self.pretrained = True
+        patch_size = 16
+        self.model = VisionTransformer(img_size=cfg.DATA.TRAIN_CROP_SIZE, num_classes=cfg.MODEL.NUM_CLASSES,
+                                       patch_size=patch_size, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4,
+                                       qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_rate=0.,
+                                       attn_drop_rate=0., drop_path_rate=0.1, num_frames=cfg.DATA.NUM_FRAMES,
+                                       attention_type=cfg.TIMESFORMER.ATTENTION_TYPE, **kwargs)
+        self.attention_type = cfg.TIMESFORMER.ATTENTION_TYPE
+        self.num_patches = (cfg.DATA.TRAIN_CROP_SIZE // patch_size) * (cfg.DATA.TRAIN_CROP_SIZE // patch_size)
+        if cfg.TIMESFORMER.PRETRAINED_MODEL:
+            _state_dict_pretrained(self.model, cfg.TIMESFORMER.PRETRAINED_MODEL)
+
+    def forward(self, x):
+        return self.model(x)
+
+
+class TimeSformer(nn.Module):
+    """models/timesformer.py:404-426 (local checkpoints only; no URL fetch)."""
+
+    def __init__(self, img_size=224, patch_size=16, num_classes=400, num_frames=8,
+                 attention_type='divided_space_time', pretrained_model='', **kwargs):
+        super().__init__()
+        self.pretrained = True
+        self.model = VisionTransformer(img_size=img_size, num_classes=num_classes, patch_size=patch_size,
+                                       embed_dim=768, depth=12, num_heads=12, mlp_ratio=4, qkv_bias=True,
+                                       norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_rate=0.,
+                                       attn_drop_rate=0., drop_path_rate=0.1, num_frames=num_frames,
+                                       attention_type=attention_type, **kwargs)
+        self.attention_type = attention_type
+        self.num_patches = (img_size // patch_size) * (img_size // patch_size)
+        if pretrained_model:
+            _state_dict_pretrained(self.model, pretrained_model)
+
+    def forward(self, x):
+        return self.model(x)
+
+
+def get_vit_base_patch16_224(cfg, no_head=False, **kwargs):
+    """models/timesformer.py:592-609.  `cfg` needs DATA.TRAIN_CROP_SIZE, DATA.NUM_FRAMES,
+    MODEL.NUM_CLASSES, TIMESFORMER.ATTENTION_TYPE, TIMESFORMER.PRETRAINED_MODEL."""
+    patch_size = 16
+    vit = VisionTransformer(img_size=cfg.DATA.TRAIN_CROP_SIZE, num_classes=cfg.MODEL.NUM_CLASSES,
+                            patch_size=patch_size, embed_dim=768, depth=12, num_heads=12, mlp_ratio=4,
+                            qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_rate=0.,
+                            attn_drop_rate=0., drop_path_rate=0.1, num_frames=cfg.DATA.NUM_FRAMES,
+                            attention_type=cfg.TIMESFORMER.ATTENTION_TYPE, **kwargs)
+    vit.attention_type = cfg.TIMESFORMER.ATTENTION_TYPE
+    vit.num_patches = (cfg.DATA.TRAIN_CROP_SIZE // patch_size) * (cfg.DATA.TRAIN_CROP_SIZE // patch_size)
+    if cfg.TIMESFORMER.PRETRAINED_MODEL:
+        _state_dict_pretrained(vit, cfg.TIMESFORMER.PRETRAINED_MODEL)
+    if no_head:
+        vit.head = None
+    return vit

@@ -1,0 +1,204 @@
+"""Tensor-level wrappers over the C-ABI.  torch is used only for device memory and the
+current HIP stream; every computation is a libdsvt.so kernel.
+
+Storage dtype ("mode"): torch.bfloat16 (perf) or torch.float32 (parity).  The token
+tensor X, LayerNorm/softmax statistics and losses are always fp32.
+"""
+import torch
+
+from . import _lib
+from ._lib import call
+
+INT64_MAX = (1 << 63) - 1
+
+
+def _dt(mode):
+    if mode == torch.bfloat16:
+        return _lib.BF16
+    if mode == torch.float32:
+        return _lib.F32
+    raise ValueError("dsvt storage dtype must be torch.bfloat16 or torch.float32, got %s" % (mode,))
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _check(t, dtype, name):
+    if not t.is_cuda:
+        raise _lib.DsvtError("%s must be a GPU tensor (no CPU fallback)" % name)
+    if t.dtype != dtype:
+        raise _lib.DsvtError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise _lib.DsvtError("%s must be contiguous" % name)
+
+
+def workspace_bytes(op, mode, M, N, K):
+    return int(_lib.lib().dsvt_workspace_bytes(op, _dt(mode), M, N, K))
+
+
+def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=None):
+    """out[row(m)] (op)= a[m] . w^T (+bias ...); a [M,K] mode, w [N,K] mode."""
+    mode = w.dtype
+    _check(a, mode, "A")
+    _check(w, mode, "W")
+    M = a.shape[0] if M is None else M
+    K = a.shape[-1]
+    N = w.shape[0]
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    call("dsvt_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
+         _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _stream())
+    return out
+
+
+def ln_gemm(x, in_rowmap, M, ln_w, ln_b, eps, w, bias, out, ws, epilogue=_lib.EPI_BIAS, out_f32=False,
+            rowmap=None):
+    """LayerNorm(rows of fp32 x through in_rowmap) -> GEMM with epilogue."""
+    mode = w.dtype
+    _check(x, torch.float32, "x")
+    K = x.shape[-1]
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    irpg, igs, igo = in_rowmap if in_rowmap is not None else (0, 0, 0)
+    call("dsvt_ln_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(x), irpg, igs, igo, _ptr(ln_w), _ptr(ln_b),
+         float(eps), _ptr(w), _ptr(bias), _ptr(out), out.shape[-1], M, w.shape[0], K, rpg, gs, go, _ptr(ws),
+         ws.numel() * ws.element_size(), _stream())
+    return out
+
+
+def layernorm(x, rows, C, ln_w, ln_b, eps, out, rowmap=None, out_f32=True):
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    mode = out.dtype if out.dtype in (torch.bfloat16, torch.float32) else torch.float32
+    call("dsvt_layernorm_fwd", _dt(mode), int(out_f32), _ptr(x), _ptr(out), _ptr(ln_w), _ptr(ln_b), rows, C,
+         rpg, gs, go, float(eps), _stream())
+    return out
+
+
+def patch_embed(x, w_mode, bias, cls_token, pos_embed, pos_index, time_embed, time_index, X, ws, tokens_order,
+                frame_index=None, clip_shape=None):
+    """x [B,Cin,T,H,W] fp32; or, with frame_index [B*T] int32, a frame bank [F,Cin,H,W] read
+    through the index (clip_shape = (B, T))."""
+    _check(x, torch.float32, "x")
+    if frame_index is None:
+        B, Cin, T, H, W = x.shape
+    else:
+        _check(frame_index, torch.int32, "frame_index")
+        (B, T), (_, Cin, H, W) = clip_shape, x.shape
+    call("dsvt_patch_embed_fwd", _dt(w_mode.dtype), tokens_order, _ptr(x), B, Cin, T, H, W, 16, _ptr(w_mode),
+         _ptr(bias), _ptr(cls_token), _ptr(pos_embed), _ptr(pos_index), _ptr(time_embed), _ptr(time_index),
+         w_mode.shape[0], _ptr(X), _ptr(frame_index), _ptr(ws), ws.numel() * ws.element_size(), _stream())
+    return X
+
+
+def pos_bicubic(pos_embed, out, s, OH, OW, scale_h, scale_w):
+    _check(pos_embed, torch.float32, "pos_embed")
+    call("dsvt_pos_bicubic_fwd", _ptr(pos_embed.contiguous()), _ptr(out), s, OH, OW, pos_embed.shape[-1],
+         float(scale_h), float(scale_w), _stream())
+    return out
+
+
+def attn_temporal(qkv, out, nseq, T, heads, scale):
+    call("dsvt_attn_temporal_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), nseq, T, heads, 64, float(scale), _stream())
+    return out
+
+
+def attn_spatial(qkv, out, B, T, L, heads, scale, ws):
+    call("dsvt_attn_spatial_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), B, T, L, heads, 64, float(scale), _ptr(ws),
+         ws.numel() * ws.element_size(), _stream())
+    return out
+
+
+def attn_joint(qkv, out, nb, L, heads, scale):
+    call("dsvt_attn_joint_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), nb, L, heads, 64, float(scale), _stream())
+    return out
+
+
+def frame_mean(x, y, B, T, rowlen):
+    call("dsvt_frame_mean_fwd", _ptr(x), _ptr(y), B, T, rowlen, _stream())
+    return y
+
+
+def cast(x, out):
+    _check(x, torch.float32, "x")
+    call("dsvt_cast_fwd", _dt(out.dtype), _ptr(x), _ptr(out), x.numel(), _stream())
+    return out
+
+
+def head_norm(x, out, eps=1e-12):
+    _check(x, torch.float32, "x")
+    call("dsvt_dino_head_norm_fwd", _dt(out.dtype), _ptr(x), _ptr(out), x.shape[0], x.shape[1], float(eps), _stream())
+    return out
+
+
+def weight_norm(v, g, out):
+    _check(v, torch.float32, "weight_v")
+    call("dsvt_weight_norm_fwd", _dt(out.dtype), _ptr(v), _ptr(g.contiguous()), _ptr(out), v.shape[0], v.shape[1],
+         _stream())
+    return out
+
+
+def dino_loss(student, teacher, center, B, ncrops, global_crops, student_temp, teacher_temp):
+    """Returns (loss [1] fp32 device tensor, teacher column sum [D] fp32)."""
+    _check(student, torch.float32, "student_output")
+    _check(teacher, torch.float32, "teacher_output")
+    D = student.shape[-1]
+    dev = student.device
+    loss = torch.empty(1, device=dev, dtype=torch.float32)
+    colsum = torch.empty(D, device=dev, dtype=torch.float32)
+    nbytes = workspace_bytes(_lib.WS_DINO_LOSS, torch.float32, B, ncrops, global_crops)
+    ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+    c = center.reshape(-1).contiguous()
+    call("dsvt_dino_loss_fwd", _ptr(student), _ptr(teacher), _ptr(c), B, ncrops, global_crops, D,
+         float(student_temp), float(teacher_temp), _ptr(loss), _ptr(colsum), _ptr(ws), nbytes, _stream())
+    return loss, colsum
+
+
+def pair_loss(student, teacher, center, student_temp, teacher_temp):
+    _check(student, torch.float32, "student_output")
+    _check(teacher, torch.float32, "teacher_output")
+    rows, D = student.shape
+    out = torch.empty(rows, device=student.device, dtype=torch.float32)
+    nbytes = workspace_bytes(_lib.WS_PAIR_LOSS, torch.float32, rows, 0, 0)
+    ws = torch.empty(nbytes // 4, device=student.device, dtype=torch.float32)
+    c = None if center is None else center.reshape(-1).contiguous()
+    call("dsvt_dino_pair_loss_fwd", _ptr(student), _ptr(teacher), _ptr(c), rows, D, float(student_temp),
+         float(teacher_temp), _ptr(out), _ptr(ws), nbytes, _stream())
+    return out
+
+
+def center_ema(center, colsum, momentum, inv_count):
+    call("dsvt_center_ema", _ptr(center), _ptr(colsum), colsum.numel(), float(momentum), float(inv_count), _stream())
+    return center
+
+
+# ---------------------------------------------------------------- measurement probe
+def probe_enable(mask, capacity=65536):
+    call("dsvt_probe_enable", mask, capacity)
+
+
+def probe_disable():
+    call("dsvt_probe_disable")
+
+
+def probe_read(capacity=65536):
+    import ctypes
+    import numpy as np
+    ms = np.zeros(capacity, np.float32)
+    work = np.zeros(capacity, np.float64)
+    fam = np.zeros(capacity, np.int32)
+    tag = np.zeros(capacity, np.int32)
+    vp = ctypes.c_void_p
+    n = _lib.lib().dsvt_probe_read(ms.ctypes.data_as(vp), work.ctypes.data_as(vp), fam.ctypes.data_as(vp),
+                                   tag.ctypes.data_as(vp), capacity)
+    if n < 0:
+        raise _lib.DsvtError(_lib.lib().dsvt_last_error().decode())
+    return ms[:n], work[:n], fam[:n], tag[:n]
+
+
+GEMM_KERNEL_NAMES = {  # probe tag -> rocprofv3 kernel name prefix (template instantiation)
+    t: "void dsvt::gemm_kernel<%s, %d, %s>" % ("float" if t >= 16 else "unsigned short", (t % 16) // 2,
+                                                "true" if t % 2 else "false")
+    for t in range(32)}

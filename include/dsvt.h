@@ -1,0 +1,184 @@
+/*
+ * dsvt.h -- C-ABI of the MI355X (gfx950) DINO-SVT forward/loss hot path.
+ *
+ * The reference (Luke-537/Dino-Video-Summarization-Transformer) has no FFI: its hot path
+ * is the PyTorch module API.  These entry points are what that API's implicit device
+ * kernels become (SURVEY.md §2.2 K1-K14, §8(b) "What the C-ABI replacement must export").
+ * Each entry point names the reference code it replaces.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + sizes, no framework types; `stream` is a hipStream_t;
+ *   - dtype selects the activation/weight STORAGE type: DSVT_BF16 (perf mode: bf16 MFMA,
+ *     fp32 accumulate) or DSVT_F32 (parity mode: fp32 MFMA / fp32 VALU). The residual
+ *     token stream X, LayerNorm statistics, softmax statistics and losses are always fp32;
+ *   - return 0 on success, non-zero on error; dsvt_last_error() gives the text
+ *     (thread-local).  Nothing aborts, nothing allocates device memory: scratch space is
+ *     a caller-provided workspace sized by dsvt_workspace_bytes();
+ *   - all kernels are asynchronous on `stream` and safe to capture into a hipGraph.
+ *
+ * Token layout of X (models/timesformer.py:312, :322): X[b][i][c], i = 0 is CLS,
+ * i = 1 + n*T + t is patch n of frame t ('b (n t) m').  Row maps: an operation that
+ * reads or writes X through a row map uses  row(m) = (m / rpg) * gstride + goff + m % rpg.
+ */
+#ifndef DSVT_H
+#define DSVT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSVT_ABI_VERSION 1
+
+#define DSVT_BF16 0
+#define DSVT_F32 1
+
+/* GEMM epilogues (out = A[M,K] . W[N,K]^T, i.e. nn.Linear with weight [out,in]) */
+#define DSVT_EPI_BIAS 0       /* out[row(m)] = acc + bias                  (Linear)          */
+#define DSVT_EPI_BIAS_GELU 1  /* out[row(m)] = GELU_erf(acc + bias)        (Mlp.fc1 + act)   */
+#define DSVT_EPI_BIAS_RESID 2 /* X[row(m)]  += acc + bias   (fp32 X)       (residual adds)   */
+
+/* token orders for patch embedding */
+#define DSVT_TOKENS_NT 0      /* divided / joint: X[b][1 + n*T + t]   (timesformer.py:312-323)  */
+#define DSVT_TOKENS_FRAME 1   /* space_only / 2-D ViT: X[b*T + t][1 + n] (timesformer.py:288-306) */
+
+/* probe families (bit mask) */
+#define DSVT_PROBE_GEMM 1
+#define DSVT_PROBE_ATTN_SPATIAL 2
+#define DSVT_PROBE_ATTN_TEMPORAL 4
+#define DSVT_PROBE_NORM 8
+#define DSVT_PROBE_LOSS 16
+
+/* workspace ops */
+#define DSVT_WS_LN_GEMM 1
+#define DSVT_WS_PATCH_EMBED 2
+#define DSVT_WS_ATTN_SPATIAL 3
+#define DSVT_WS_DINO_LOSS 4
+#define DSVT_WS_PAIR_LOSS 5
+
+int dsvt_version(void);
+const char *dsvt_last_error(void);
+
+/* Scratch bytes needed by an op (M,N,K meaning per op: LN_GEMM: rows, -, K;
+ * PATCH_EMBED: patch rows, -, Cin*p*p; ATTN_SPATIAL: B*T, C, -; DINO_LOSS: pairs, rows, -;
+ * PAIR_LOSS: rows, -, -). */
+int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K);
+
+/* K4/K7/K9/K12: MFMA GEMM with fused epilogue.
+ * Replaces nn.Linear in Attention.qkv/proj (models/timesformer.py:63-64, 71, 83),
+ * temporal_fc (:108, :133), Mlp.fc1/act/fc2 (:41-52) and DINOHead.mlp / last_layer
+ * (vision_transformer.py:255-281).  Requires K % 64 == 0 (bf16) / K % 32 == 0 (f32),
+ * N % 4 == 0.  A rows are contiguous with stride lda (elements of dtype); W [N,K]
+ * contiguous with stride ldw; out stride ldo (elements). out_f32 selects fp32 output for
+ * EPI_BIAS / EPI_BIAS_GELU (otherwise dtype). */
+int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
+                  int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N,
+                  int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void *stream);
+
+/* K3: LayerNorm(eps) over rows of fp32 X read through a row map, written compact
+ * (rows x C) in dtype (or fp32 when out_f32).  nn.LayerNorm(eps=1e-6) at
+ * models/timesformer.py:99,105,112,131,159,184,245,342. */
+int dsvt_layernorm_fwd(int dtype, int out_f32, const float *x, void *y, const float *gamma,
+                       const float *beta, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
+                       int64_t goff, float eps, void *stream);
+
+/* K3+K4 / K3+K9: LayerNorm prologue + GEMM (norm1->qkv, temporal_norm1->temporal qkv,
+ * norm2->fc1: models/timesformer.py:131, :159, :184).  x rows read through (in_rpg,
+ * in_gstride, in_goff); the normalized rows go through `workspace`. */
+int dsvt_ln_gemm_fwd(int dtype, int epilogue, int out_f32, const float *x, int64_t in_rpg,
+                     int64_t in_gstride, int64_t in_goff, const float *gamma, const float *beta,
+                     float eps, const void *W, const float *bias, void *out, int64_t ldo,
+                     int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
+                     void *workspace, int64_t workspace_bytes, void *stream);
+
+/* K1+K2: PatchEmbed (Conv2d k=s=16 as im2col GEMM, models/timesformer.py:203-209) fused
+ * with the CLS concat, pos-embed add (nearest-resized via pos_index, :288-306) and
+ * time-embed add (nearest-resized via time_index, :309-323).  x is [B,Cin,T,H,W] fp32.
+ * w is the conv weight [C, Cin*16*16] in dtype; pos_embed [1+P*P, C] fp32 with
+ * pos_index[Np] indexing the P*P grid; time_embed [T0, C] (NULL for space_only) with
+ * time_index[T].  Writes X fp32: tokens_order DSVT_TOKENS_NT -> [B, 1+Np*T, C],
+ * DSVT_TOKENS_FRAME -> [B*T, 1+Np, C].  frame_index (nullable): x is then a frame bank
+ * [F, Cin, H, W] and frame t of clip b is x[frame_index[b*T + t]] (-1 = zero frame) -- the
+ * per-frame local/global views of datasets_custom/dino_loss_loader.py:126-171 without
+ * materializing them. */
+int dsvt_patch_embed_fwd(int dtype, int tokens_order, const float *x, int64_t B, int64_t Cin,
+                         int64_t T, int64_t H, int64_t W, int64_t patch, const void *w,
+                         const float *bias, const float *cls_token, const float *pos_embed,
+                         const int32_t *pos_index, const float *time_embed,
+                         const int32_t *time_index, int64_t C, float *X,
+                         const int32_t *frame_index, void *workspace, int64_t workspace_bytes,
+                         void *stream);
+
+/* vision_transformer.py:174-194 interpolate_pos_encoding: bicubic (A=-0.75,
+ * align_corners=False, scale_factor semantics of ATen upsample_bicubic2d) resize of the
+ * s x s patch grid of pos_embed [1+s*s, C] to out [1+OH*OW, C] (row 0 = CLS pos copied). */
+int dsvt_pos_bicubic_fwd(const float *pos_embed, float *out, int64_t s, int64_t OH, int64_t OW,
+                         int64_t C, double scale_h, double scale_w, void *stream);
+
+/* K5: temporal attention of the divided block (models/timesformer.py:127-131 via
+ * Attention.forward :68-87).  qkv compact [(nseq*T), 3C] (sequence = (b,n), T rows each),
+ * out [(nseq*T), C].  head_dim must be 64, T <= 64. */
+int dsvt_attn_temporal_fwd(int dtype, const void *qkv, void *out, int64_t nseq, int64_t T,
+                           int64_t heads, int64_t head_dim, float scale, void *stream);
+
+/* K6+K8: spatial attention of the divided block with the CLS replicate / mean over
+ * frames (models/timesformer.py:139-175).  qkv rows follow X's token layout
+ * ([B*L, 3C]); sequence (b,t) = {CLS row b*L} U {row b*L + 1 + n*T + t}.  Patch outputs go
+ * to out at the same rows; the CLS output is the mean over t, written to row b*L.
+ * workspace: >= dsvt_workspace_bytes(DSVT_WS_ATTN_SPATIAL, ., B*T, C, 0). */
+int dsvt_attn_spatial_fwd(int dtype, const void *qkv, void *out, int64_t B, int64_t T, int64_t L,
+                          int64_t heads, int64_t head_dim, float scale, void *workspace,
+                          int64_t workspace_bytes, void *stream);
+
+/* K10: plain (joint space-time / space-only / 2-D ViT) attention over each of nb
+ * contiguous sequences of L rows (models/timesformer.py:120-123, vision_transformer.py:80-92). */
+int dsvt_attn_joint_fwd(int dtype, const void *qkv, void *out, int64_t nb, int64_t L,
+                        int64_t heads, int64_t head_dim, float scale, void *stream);
+
+/* CLS mean over frames for space_only (models/timesformer.py:338-340) and dtype casts. */
+int dsvt_frame_mean_fwd(const float *x, float *y, int64_t B, int64_t T, int64_t rowlen,
+                        void *stream);
+int dsvt_cast_fwd(int dtype, const float *x, void *y, int64_t n, void *stream);
+
+/* K12 pieces: F.normalize(x, dim=-1, p=2, eps) (vision_transformer.py:280) and the
+ * weight-norm of DINOHead.last_layer (w = g * v / ||v||_row, :267-269). */
+int dsvt_dino_head_norm_fwd(int dtype, const float *x, void *y, int64_t rows, int64_t D,
+                            float eps, void *stream);
+int dsvt_weight_norm_fwd(int dtype, const float *v, const float *g, void *w, int64_t rows,
+                         int64_t D, void *stream);
+
+/* K13+K14: DINOLoss.forward (train_ssl.py:633-671, two_token=False).  student
+ * [ncrops*B, D], teacher [global_crops*B, D], center [D], all fp32.  Writes the scalar
+ * loss to loss_out[0] (device) and the teacher column sum (pre all-reduce,
+ * train_ssl.py:686) to teacher_colsum[D].  No host sync. */
+int dsvt_dino_loss_fwd(const float *student, const float *teacher, const float *center,
+                       int64_t B, int64_t ncrops, int64_t global_crops, int64_t D,
+                       float student_temp, float teacher_temp, float *loss_out,
+                       float *teacher_colsum, void *workspace, int64_t workspace_bytes,
+                       void *stream);
+
+/* dino_similarity.DINOLoss (dino_similarity.py:129-135), one loss per row pair -- the
+ * per-frame importance score (dino_similarity.py:87-88). */
+int dsvt_dino_pair_loss_fwd(const float *student, const float *teacher, const float *center,
+                            int64_t rows, int64_t D, float student_temp, float teacher_temp,
+                            float *out, void *workspace, int64_t workspace_bytes, void *stream);
+
+/* K14: center = center*momentum + colsum*(1-momentum)*inv_count (train_ssl.py:687-691,
+ * after the caller's all-reduce of colsum). */
+int dsvt_center_ema(float *center, const float *colsum, int64_t D, float momentum,
+                    float inv_count, void *stream);
+
+/* Measurement probe: when enabled, every launch of a family in `mask` is bracketed by a
+ * pair of hipEvents on its own stream (diagnostic; not thread-safe). */
+int dsvt_probe_enable(int mask, int capacity);
+int dsvt_probe_disable(void);
+/* Synchronizes the recorded events; fills per-launch ms, algorithmic work (FLOP for
+ * GEMM/attention, bytes for norm/loss), family and tag (GEMM: kernel instantiation id =
+ * dtype*16 + epilogue*2 + fp32_out, epilogue 3 = patch embed).  Returns the number of
+ * launches (negative on error). */
+int dsvt_probe_read(float *ms, double *work, int32_t *family, int32_t *tag, int capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSVT_H */

@@ -193,8 +193,8 @@ def bicubic_resize(img, scale_h, scale_w):
     def taps(out, inp, scale):
         s = np.float32(1.0 / scale)
         src = s * (np.arange(out, dtype=np.float32) + np.float32(0.5)) - np.float32(0.5)
-        i0 = np.floor(src).astype(np.int64)
-        coef = _cubic_coeffs((src - i0).astype(np.float64))
+        i0 = np.minimum(np.floor(src).astype(np.int64), inp - 1)          # guard_index_and_lambda
+        coef = _cubic_coeffs(np.clip(src - i0, 0.0, 1.0).astype(np.float64))
         idx = np.clip(i0[:, None] + np.arange(-1, 3)[None], 0, inp - 1)
         return idx, coef
     ri, rc = taps(OH, H, scale_h)

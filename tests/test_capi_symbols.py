@@ -1,0 +1,81 @@
+"""The C-ABI library loads and exports exactly what include/dsvt.h declares; host-side
+argument validation rejects bad shapes before any kernel launch.  CPU only: no entry point
+that would launch a kernel is called here."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "dsvt.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dsvt_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from dsvt import _lib
+    return _lib.lib()
+
+
+def test_header_symbols_exported(L):
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_python_binding_covers_header():
+    from dsvt._lib import SIGNATURES
+    assert sorted(SIGNATURES) == header_functions()
+
+
+def test_binding_arity_matches_header():
+    from dsvt._lib import SIGNATURES
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name, (_, args) in SIGNATURES.items():
+        m = re.search(r"\b%s\s*\(([^)]*)\)" % name, src)
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), (name, len(params), len(args))
+
+
+def test_version_and_workspace(L):
+    assert L.dsvt_version() == 1
+    from dsvt import _lib
+    assert L.dsvt_workspace_bytes(_lib.WS_LN_GEMM, _lib.BF16, 1000, 0, 768) >= 1000 * 768 * 2
+    assert L.dsvt_workspace_bytes(_lib.WS_LN_GEMM, _lib.F32, 1000, 0, 768) >= 1000 * 768 * 4
+    assert L.dsvt_workspace_bytes(99, 0, 1, 1, 1) == -1
+
+
+def test_validation_rejects_before_launch(L):
+    from dsvt import _lib
+    fake = ctypes.c_void_p(256)
+    # K not a multiple of 64 (bf16)
+    rc = L.dsvt_gemm_fwd(_lib.BF16, 0, 0, fake, 100, fake, 100, None, fake, 64, 16, 64, 100, 0, 0, 0, None)
+    assert rc == 1 and b"multiple of 64" in L.dsvt_last_error()
+    # head_dim must be 64
+    rc = L.dsvt_attn_temporal_fwd(_lib.BF16, fake, fake, 4, 8, 3, 32, ctypes.c_float(0.1), None)
+    assert rc == 1 and b"head_dim" in L.dsvt_last_error()
+    # T > 64 rejected
+    rc = L.dsvt_attn_temporal_fwd(_lib.BF16, fake, fake, 4, 65, 3, 64, ctypes.c_float(0.1), None)
+    assert rc == 1
+    # ncrops == 1: the reference divides by zero (SURVEY §5 defect 4)
+    rc = L.dsvt_dino_loss_fwd(fake, fake, fake, 2, 1, 1, 64, ctypes.c_float(.1), ctypes.c_float(.04), fake, fake,
+                              fake, 1 << 20, None)
+    assert rc == 1 and b"ncrops" in L.dsvt_last_error()
+    # LayerNorm width limits
+    rc = L.dsvt_layernorm_fwd(_lib.BF16, 0, fake, fake, fake, fake, 4, 100, 0, 0, 0, ctypes.c_float(1e-6), None)
+    assert rc == 1
+
+
+def test_ops_raise_with_dsvt_error(L):
+    import torch
+    from dsvt import ops, DsvtError
+    with pytest.raises(DsvtError):
+        ops.cast(torch.zeros(8), torch.zeros(8, dtype=torch.bfloat16))   # CPU tensors: no fallback

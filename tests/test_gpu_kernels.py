@@ -1,0 +1,271 @@
+"""Kernel-level parity on the GPU: every libdsvt.so op vs a float64 numpy reference of the
+same op computed from the same (storage-rounded) inputs.
+
+Tolerances: fp32 parity mode 2e-5 relative; bf16 mode bounded by the bf16 rounding of the
+output (2^-8 relative) plus fp32 accumulation."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dsvt_oracle as O
+
+pytestmark = pytest.mark.gpu
+DT = [torch.float32, torch.bfloat16]
+RTOL = {torch.float32: 2e-5, torch.bfloat16: 1.2e-2}
+
+
+def dev():
+    return torch.device("cuda:0")
+
+
+def rnd(shape, seed, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+def to(x, dtype):
+    return torch.from_numpy(x).to(dev()).to(dtype).contiguous()
+
+
+def back(t):
+    return t.float().cpu().numpy().astype(np.float64)
+
+
+def check(got, ref, dtype, what=""):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert np.isfinite(got).all(), what
+    err = np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-6)
+    assert err < RTOL[dtype], "%s rel err %.3g" % (what, err)
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (37, 192, 192), (128, 768, 768), (300, 2304, 768),
+                                   (77, 3072, 3072), (129, 256, 2048)])
+def test_gemm_bias_gelu(dtype, M, N, K):
+    from dsvt import ops
+    from dsvt._lib import EPI_BIAS, EPI_BIAS_GELU
+    a, w, b = rnd((M, K), 1), rnd((N, K), 2, 0.05), rnd((N,), 3)
+    A, W, Bt = to(a, dtype), to(w, dtype), to(b, torch.float32)
+    ref = back(A) @ back(W).T + b
+    for epi, f in ((EPI_BIAS, lambda v: v), (EPI_BIAS_GELU, O.gelu)):
+        for out_f32 in (False, True):
+            out = torch.empty(M, N, device=dev(), dtype=torch.float32 if out_f32 else dtype)
+            ops.gemm(A, W, Bt, out, epilogue=epi, out_f32=out_f32)
+            torch.cuda.synchronize()
+            check(back(out), f(ref), dtype, "gemm epi=%d f32out=%d" % (epi, out_f32))
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_gemm_residual_rowmap(dtype):
+    """X[b*L + 1 + m % (Np*T)] += A.W^T + bias; CLS rows untouched (temporal_fc epilogue)."""
+    from dsvt import ops
+    from dsvt._lib import EPI_BIAS_RESID
+    B, Np, T, C = 3, 5, 4, 192
+    L, R = 1 + Np * T, B * Np * T
+    a, w, b = rnd((R, C), 4), rnd((C, C), 5, 0.05), rnd((C,), 6)
+    x0 = rnd((B * L, C), 7)
+    A, W = to(a, dtype), to(w, dtype)
+    X = to(x0, torch.float32)
+    ops.gemm(A, W, to(b, torch.float32), X, epilogue=EPI_BIAS_RESID, rowmap=(Np * T, L, 1))
+    torch.cuda.synchronize()
+    ref = x0.astype(np.float64).copy()
+    rows = (np.arange(R) // (Np * T)) * L + 1 + np.arange(R) % (Np * T)
+    ref[rows] += back(A) @ back(W).T + b
+    check(back(X), ref, dtype, "resid")
+    np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("C", [192, 384, 768])
+def test_layernorm_rowmap(dtype, C):
+    from dsvt import ops
+    B, L = 3, 11
+    x = rnd((B * L, C), 8, 3.0) + 0.5
+    g, bb = 1 + rnd((C,), 9, 0.1), rnd((C,), 10, 0.1)
+    X = to(x, torch.float32)
+    out = torch.empty(B * (L - 1), C, device=dev(), dtype=dtype)
+    ops.layernorm(X, B * (L - 1), C, to(g, torch.float32), to(bb, torch.float32), 1e-6, out,
+                  rowmap=(L - 1, L, 1), out_f32=False)
+    torch.cuda.synchronize()
+    rows = (np.arange(B * (L - 1)) // (L - 1)) * L + 1 + np.arange(B * (L - 1)) % (L - 1)
+    check(back(out), O.layer_norm(x[rows], g, bb), dtype, "ln")
+
+
+# ------------------------------------------------------------------ attention references
+def attn_ref(q, k, v, scale):
+    s = (q @ k.T) * scale
+    p = np.exp(s - s.max(-1, keepdims=True))
+    return (p / p.sum(-1, keepdims=True)) @ v
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("T,heads", [(1, 3), (3, 12), (4, 3), (8, 12), (30, 12), (64, 1)])
+def test_attn_temporal(dtype, T, heads):
+    from dsvt import ops
+    nseq, C = 7, heads * 64
+    qkv = rnd((nseq * T, 3 * C), 11, 1.5)
+    Q = to(qkv, dtype)
+    out = torch.empty(nseq * T, C, device=dev(), dtype=dtype)
+    ops.attn_temporal(Q, out, nseq, T, heads, 0.125)
+    torch.cuda.synchronize()
+    q3 = back(Q)
+    ref = np.zeros((nseq * T, C))
+    for s in range(nseq):
+        r = slice(s * T, (s + 1) * T)
+        for h in range(heads):
+            c = slice(h * 64, (h + 1) * 64)
+            ref[r, c] = attn_ref(q3[r, c], q3[r, C + h * 64:C + (h + 1) * 64], q3[r, 2 * C + h * 64:2 * C + (h + 1) * 64],
+                                 0.125)
+    check(back(out), ref, dtype, "temporal")
+
+
+def spatial_ref(qkv, B, T, L, heads, scale):
+    C = heads * 64
+    N = (L - 1) // T
+    out = np.zeros((B * L, C))
+    for b in range(B):
+        cls_acc = np.zeros(C)
+        for t in range(T):
+            rows = np.concatenate([[b * L], b * L + 1 + np.arange(N) * T + t])
+            for h in range(heads):
+                c = slice(h * 64, (h + 1) * 64)
+                o = attn_ref(qkv[rows, h * 64:(h + 1) * 64], qkv[rows, C + h * 64:C + (h + 1) * 64],
+                             qkv[rows, 2 * C + h * 64:2 * C + (h + 1) * 64], scale)
+                out[rows[1:], c] = o[1:]
+                cls_acc[c] += o[0]
+        out[b * L] = cls_acc / T
+    return out
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,T,N,heads", [(2, 1, 4, 3), (2, 3, 36, 12), (1, 8, 196, 12), (2, 4, 49, 3),
+                                         (1, 2, 150, 1)])
+def test_attn_spatial_cls_mean(dtype, B, T, N, heads):
+    from dsvt import ops
+    from dsvt._lib import WS_ATTN_SPATIAL
+    C, L = heads * 64, 1 + N * T
+    qkv = rnd((B * L, 3 * C), 12, 1.5)
+    Q = to(qkv, dtype)
+    out = torch.zeros(B * L, C, device=dev(), dtype=dtype)
+    ws = torch.empty(ops.workspace_bytes(WS_ATTN_SPATIAL, dtype, B * T, C, 0) // 4, device=dev())
+    ops.attn_spatial(Q, out, B, T, L, heads, 0.125, ws)
+    torch.cuda.synchronize()
+    check(back(out), spatial_ref(back(Q), B, T, L, heads, 0.125), dtype, "spatial")
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("nb,L,heads", [(2, 5, 3), (1, 65, 12), (2, 197, 3), (1, 300, 2), (1, 1569, 1)])
+def test_attn_joint(dtype, nb, L, heads):
+    from dsvt import ops
+    C = heads * 64
+    qkv = rnd((nb * L, 3 * C), 13, 1.5)
+    Q = to(qkv, dtype)
+    out = torch.empty(nb * L, C, device=dev(), dtype=dtype)
+    ops.attn_joint(Q, out, nb, L, heads, 0.125)
+    torch.cuda.synchronize()
+    q3 = back(Q)
+    ref = np.zeros((nb * L, C))
+    for b in range(nb):
+        r = slice(b * L, (b + 1) * L)
+        for h in range(heads):
+            ref[r, h * 64:(h + 1) * 64] = attn_ref(q3[r, h * 64:(h + 1) * 64], q3[r, C + h * 64:C + (h + 1) * 64],
+                                                   q3[r, 2 * C + h * 64:2 * C + (h + 1) * 64], 0.125)
+    check(back(out), ref, dtype, "joint")
+
+
+def test_attn_softmax_spike():
+    """Force the online-softmax rescale branch: one key far above the rest in a LATE chunk."""
+    from dsvt import ops
+    nb, L, heads = 1, 200, 1
+    qkv = rnd((L, 192), 14, 0.5)
+    qkv[:, :64] = 1.0
+    qkv[190, 64:128] = 40.0        # key 190 (chunk 3) dominates every query
+    for dtype in DT:
+        Q = to(qkv, dtype)
+        out = torch.empty(L, 64, device=dev(), dtype=dtype)
+        ops.attn_joint(Q, out, nb, L, heads, 0.125)
+        torch.cuda.synchronize()
+        q3 = back(Q)
+        check(back(out), attn_ref(q3[:, :64], q3[:, 64:128], q3[:, 128:], 0.125), dtype, "spike")
+
+
+# ------------------------------------------------------------------ patch embedding
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("shape", [(2, 3, 4, 112, 112), (1, 3, 3, 64, 64), (2, 3, 8, 32, 48)])
+def test_patch_embed_tokens(dtype, shape):
+    """im2col GEMM + CLS + nearest pos/time resize == oracle.embed_tokens."""
+    from oracle import params as P
+    from dsvt import ops
+    from dsvt._lib import TOKENS_NT, WS_PATCH_EMBED
+    from dsvt.models.timesformer import nearest_index
+    sd = P.timesformer_state(21, embed_dim=192, depth=1, num_heads=3, img_size=112, num_frames=4)
+    x = P.clip(22, shape)
+    ref, T, Wp = O.embed_tokens(sd, x)
+    B, Cin, T, H, W = shape
+    Hp, Wp = H // 16, W // 16
+    P_ = 7
+    pidx = (nearest_index(Hp, P_)[:, None] * P_ + nearest_index(Wp, P_)[None, :]).reshape(-1)
+    tidx = nearest_index(T, 4)
+    X = torch.empty(B * (1 + Hp * Wp * T), 192, device=dev())
+    ws = torch.empty(ops.workspace_bytes(WS_PATCH_EMBED, dtype, B * T * Hp * Wp, 192, 768) // 2, device=dev(),
+                     dtype=torch.bfloat16)
+    w = to(sd["patch_embed.proj.weight"].reshape(192, -1), dtype)
+    ops.patch_embed(to(x, torch.float32), w, to(sd["patch_embed.proj.bias"], torch.float32),
+                    to(sd["cls_token"], torch.float32), to(sd["pos_embed"], torch.float32),
+                    torch.from_numpy(pidx.astype(np.int32)).to(dev()), to(sd["time_embed"], torch.float32),
+                    torch.from_numpy(tidx.astype(np.int32)).to(dev()), X, ws, TOKENS_NT)
+    torch.cuda.synchronize()
+    check(back(X).reshape(ref.shape), ref, dtype, "patch_embed")
+
+
+def test_pos_bicubic_matches_oracle():
+    from dsvt import ops
+    pos = rnd((1, 1 + 14 * 14, 64), 23)
+    for (oh, ow) in [(6, 6), (3, 5), (20, 20)]:
+        out = torch.empty(1 + oh * ow, 64, device=dev())
+        ops.pos_bicubic(to(pos, torch.float32), out, 14, oh, ow, (oh + 0.1) / 14, (ow + 0.1) / 14)
+        torch.cuda.synchronize()
+        grid = pos[0, 1:].reshape(14, 14, 64).transpose(2, 0, 1)
+        ref = O.bicubic_resize(grid, (oh + 0.1) / 14, (ow + 0.1) / 14).transpose(1, 2, 0).reshape(-1, 64)
+        check(back(out)[1:], ref, torch.float32, "bicubic %dx%d" % (oh, ow))
+        np.testing.assert_array_equal(back(out)[0], pos[0, 0])
+
+
+# ------------------------------------------------------------------ head pieces / loss
+@pytest.mark.parametrize("dtype", DT)
+def test_head_norm_weight_norm(dtype):
+    from dsvt import ops
+    x = rnd((9, 256), 24)
+    v, g = rnd((300, 256), 25, 0.02), 1 + rnd((300, 1), 26, 0.1)
+    y = torch.empty(9, 256, device=dev(), dtype=dtype)
+    ops.head_norm(to(x, torch.float32), y)
+    w = torch.empty(300, 256, device=dev(), dtype=dtype)
+    ops.weight_norm(to(v, torch.float32), to(g, torch.float32), w)
+    torch.cuda.synchronize()
+    check(back(y), x / np.linalg.norm(x, axis=1, keepdims=True), dtype, "l2norm")
+    check(back(w), v * g / np.linalg.norm(v.astype(np.float64), axis=1, keepdims=True), dtype, "wnorm")
+
+
+def test_dino_loss_center_golden():
+    from oracle import params as P
+    from dsvt.loss import DINOLoss
+    f = np.load("tests/golden/loss.npz")
+    l1 = DINOLoss(4096, 2, 0.04, 0.04, 0, 100, global_crops=1).to(dev())
+    v = l1(to(P.uniform(801, (4, 4096)), torch.float32), to(P.uniform(802, (2, 4096)), torch.float32), 0)
+    np.testing.assert_allclose(v.item(), f["cfg1_loss"], rtol=2e-5)
+    np.testing.assert_allclose(back(l1.center), f["cfg1_center"], rtol=1e-5, atol=1e-7)
+    l2 = DINOLoss(65536, 8, 0.04, 0.07, 30, 100).to(dev())
+    la = l2(to(P.uniform(803, (16, 65536)), torch.float32), to(P.uniform(804, (4, 65536)), torch.float32), 0)
+    lb = l2(to(P.uniform(805, (16, 65536)), torch.float32), to(P.uniform(806, (4, 65536)), torch.float32), 10)
+    np.testing.assert_allclose([la.item(), lb.item()], f["cfg2_loss"], rtol=2e-5)
+    np.testing.assert_allclose(back(l2.center), f["cfg2_center"], rtol=1e-5, atol=1e-7)
+
+
+def test_pair_loss_golden():
+    from oracle import params as P
+    from dsvt.loss import PairwiseDINOLoss
+    pl = PairwiseDINOLoss(768, 0.02, 0.3).to(dev())
+    got = back(pl.per_row(to(P.clip(901, (10, 768)), torch.float32), to(P.clip(902, (10, 768)), torch.float32)))
+    np.testing.assert_allclose(got, np.load("tests/golden/pair_loss.npz")["loss"], rtol=2e-5, atol=1e-5)

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: each stage under its own time limit; stop at the first crash, abort,
+# fault or timeout (exit status other than 0 = pass / 1 = test failures or Python error).
+# usage: tools/gpu_session.sh stage [stage ...]
+#   stages: kernels model smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name exited $rc"; exit $rc; fi
+}
+for stage in "$@"; do
+  case $stage in
+    kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -q -x -rf ;;
+    model)   run model 1200 python -m pytest tests/test_gpu_model.py -q -rf -s ;;
+    gputests) run gputests 1500 python -m pytest tests -m gpu -q -rf ;;
+    smoke)   run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   run bench 900 python bench.py ;;
+    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe &&
+             run pmc2 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe ;;
+    *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done
