@@ -327,6 +327,12 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
   return e == hipSuccess ? 0 : hip_fail(e, "center_ema");
 }
 
+int dsvt_set_gemm_variant(int variant) {
+  REQUIRE(variant >= 0 && variant <= 3, "gemm variant must be 0..3");
+  set_gemm_variant(variant);
+  return 0;
+}
+
 int dsvt_probe_enable(int mask, int capacity) {
   g_probe.clear();
   REQUIRE(capacity > 0 && capacity <= (1 << 20), "probe: bad capacity");

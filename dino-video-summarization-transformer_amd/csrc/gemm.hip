@@ -205,8 +205,26 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
   return hipGetLastError();
 }
 
+static int g_gemm_variant = 0;  // 0 auto, 1 = 128x128, 2 = 256x256 big, 3 = 256x128 big
+
+void set_gemm_variant(int v) { g_gemm_variant = v; }
+
+// Kernel choice: the 512-thread large-tile kernel for the big bf16 projections, the
+// 128x128 kernel for small M (DINO head) and the fp32 parity mode.
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
-  return dtype == 0 ? launch_t<bf16_t>(p, epi, out_f32, s) : launch_t<float>(p, epi, out_f32, s);
+  if (dtype == 0) {
+    int v = g_gemm_variant;
+    if (v == 0) {
+      v = 1;
+      if (p.M >= 1024 && p.N % 128 == 0) {
+        const int64_t t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+        v = (p.N % 256 == 0 && t256 >= 768) ? 2 : 3;
+      }
+    }
+    if (v == 2 || v == 3) return launch_gemm_big(p, v, epi, out_f32, s);
+    return launch_t<bf16_t>(p, epi, out_f32, s);
+  }
+  return launch_t<float>(p, epi, out_f32, s);
 }
 
 }  // namespace dsvt

@@ -20,6 +20,8 @@ struct GemmParams {
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_PATCH = 3 };
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s);
+hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
+void set_gemm_variant(int v);
 
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,

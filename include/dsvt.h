@@ -168,6 +168,10 @@ int dsvt_dino_pair_loss_fwd(const float *student, const float *teacher, const fl
 int dsvt_center_ema(float *center, const float *colsum, int64_t D, float momentum,
                     float inv_count, void *stream);
 
+/* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
+ * 1 = 128x128 / 4-wave kernel, 2 = 256x256 / 8-wave, 3 = 256x128 / 8-wave.  Process-global. */
+int dsvt_set_gemm_variant(int variant);
+
 /* Measurement probe: when enabled, every launch of a family in `mask` is bracketed by a
  * pair of hipEvents on its own stream (diagnostic; not thread-safe). */
 int dsvt_probe_enable(int mask, int capacity);

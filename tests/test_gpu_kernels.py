@@ -39,12 +39,25 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "v128", "v256x256", "v256x128"])
+def gemm_variant(request):
+    """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
+    from dsvt import _lib
+    _lib.call("dsvt_set_gemm_variant", request.param)
+    yield request.param
+    _lib.call("dsvt_set_gemm_variant", 0)
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("M,N,K", [(1, 64, 64), (37, 192, 192), (128, 768, 768), (300, 2304, 768),
-                                   (77, 3072, 3072), (129, 256, 2048)])
-def test_gemm_bias_gelu(dtype, M, N, K):
+                                   (77, 3072, 3072), (129, 256, 2048), (1100, 384, 128), (2500, 768, 768)])
+def test_gemm_bias_gelu(dtype, M, N, K, gemm_variant):
     from dsvt import ops
     from dsvt._lib import EPI_BIAS, EPI_BIAS_GELU
+    if dtype == torch.float32 and gemm_variant:
+        pytest.skip("variants are bf16-only")
+    if dtype == torch.float32 and K % 32:
+        pytest.skip("fp32 needs K % 32 == 0")
     a, w, b = rnd((M, K), 1), rnd((N, K), 2, 0.05), rnd((N,), 3)
     A, W, Bt = to(a, dtype), to(w, dtype), to(b, torch.float32)
     ref = back(A) @ back(W).T + b
@@ -57,11 +70,14 @@ def test_gemm_bias_gelu(dtype, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", DT)
-def test_gemm_residual_rowmap(dtype):
+@pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8)])
+def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     """X[b*L + 1 + m % (Np*T)] += A.W^T + bias; CLS rows untouched (temporal_fc epilogue)."""
     from dsvt import ops
     from dsvt._lib import EPI_BIAS_RESID
-    B, Np, T, C = 3, 5, 4, 192
+    if dtype == torch.float32 and gemm_variant:
+        pytest.skip("variants are bf16-only")
+    C = 192
     L, R = 1 + Np * T, B * Np * T
     a, w, b = rnd((R, C), 4), rnd((C, C), 5, 0.05), rnd((C,), 6)
     x0 = rnd((B * L, C), 7)

@@ -1,0 +1,72 @@
+"""GEMM micro-benchmark on the hot-path shapes (bf16, one process, interleaved variants).
+
+Usage: python tools/gemm_bench.py [variant ...]     (variants are DSVT_GEMM_VARIANT values;
+        default: the library's auto choice only).  Prints TFLOP/s per shape and variant and
+        a max-abs-diff check of every variant against variant "old" (128x128 kernel)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dino-video-summarization-transformer_amd"))
+
+import torch  # noqa: E402
+
+from dsvt import _lib, ops  # noqa: E402
+
+M_G, M_L = 16 * 1569, 48 * 289       # rows of the global (16 clips) / local (48 clips) backbone calls
+SHAPES = [  # (name, M, N, K, epilogue)
+    ("qkv_g", M_G, 2304, 768, _lib.EPI_BIAS),
+    ("proj_g", M_G, 768, 768, _lib.EPI_BIAS_RESID),
+    ("fc1_g", M_G, 3072, 768, _lib.EPI_BIAS_GELU),
+    ("fc2_g", M_G, 768, 3072, _lib.EPI_BIAS_RESID),
+    ("qkv_l", M_L, 2304, 768, _lib.EPI_BIAS),
+    ("fc1_l", M_L, 3072, 768, _lib.EPI_BIAS_GELU),
+    ("head", 64, 65536, 256, _lib.EPI_BIAS),
+]
+
+
+def set_variant(v):
+    _lib.lib().dsvt_set_gemm_variant(int(v))
+
+
+def run(M, N, K, epi, reps=20):
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    A = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g)
+    out_dtype = torch.float32 if epi == _lib.EPI_BIAS_RESID else torch.bfloat16
+    out = torch.zeros(M, N, device=dev, dtype=out_dtype)
+    ops.gemm(A, W, b, out, epilogue=epi)
+    torch.cuda.synchronize()
+    first = out.clone()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ops.gemm(A, W, b, out, epilogue=epi)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return 2.0 * M * N * K / (ms * 1e-3) / 1e12, ms, first
+
+
+def main():
+    variants = [int(v) for v in sys.argv[1:]] or [0]
+    print("%-7s %6s %6s %5s | " % ("shape", "M", "N", "K") + " | ".join("v%d TF/s (us)" % v for v in variants))
+    for name, M, N, K, epi in SHAPES:
+        cells, ref = [], None
+        for v in variants:
+            set_variant(v)
+            tf, ms, out = run(M, N, K, epi)
+            if ref is None:
+                ref = out.float()
+                d = 0.0
+            else:
+                d = (out.float() - ref).abs().max().item()
+            cells.append("%7.1f (%7.1f) d=%.1e" % (tf, ms * 1e3, d))
+        print("%-7s %6d %6d %5d | " % (name, M, N, K) + " | ".join(cells), flush=True)
+    set_variant(0)
+
+
+if __name__ == "__main__":
+    main()
