@@ -328,7 +328,8 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 }
 
 int dsvt_set_gemm_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 3, "gemm variant must be 0..3");
+  REQUIRE((variant >= 0 && variant <= 13) || variant == 14 || variant == 24 || variant == 34,
+          "gemm variant must be 0..13 (14/24/34: ablation builds)");
   set_gemm_variant(variant);
   return 0;
 }

@@ -215,13 +215,12 @@ hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hip
   if (dtype == 0) {
     int v = g_gemm_variant;
     if (v == 0) {
-      v = 1;
-      if (p.M >= 1024 && p.N % 128 == 0) {
-        const int64_t t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-        v = (p.N % 256 == 0 && t256 >= 768) ? 2 : 3;
-      }
+      // measured on MI355X (tools/gemm_bench.py): wide outputs (qkv N=2304, fc1 N=3072) ->
+      // persistent staggered 256x128 (2 WGs/CU, store tail overlapped); N <= 1024 (proj,
+      // temporal_fc, fc2) and small M (DINO head) -> 128x128 (finer tiles, better fill)
+      v = (p.M >= 2048 && p.N >= 2048 && p.N % 128 == 0) ? 10 : 1;
     }
-    if (v == 2 || v == 3) return launch_gemm_big(p, v, epi, out_f32, s);
+    if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
     return launch_t<bf16_t>(p, epi, out_f32, s);
   }
   return launch_t<float>(p, epi, out_f32, s);

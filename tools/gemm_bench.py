@@ -50,10 +50,34 @@ def run(M, N, K, epi, reps=20):
     return 2.0 * M * N * K / (ms * 1e-3) / 1e12, ms, first
 
 
+def torch_ref(M, N, K, reps=20):
+    """hipBLASLt through torch (F.linear, bf16) on the same shape: a known-good reference."""
+    dev = torch.device("cuda")
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    torch.nn.functional.linear(A, W, b)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.nn.functional.linear(A, W, b)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return 2.0 * M * N * K / (ms * 1e-3) / 1e12, ms
+
+
 def main():
     variants = [int(v) for v in sys.argv[1:]] or [0]
+    print("hipBLASLt (torch F.linear bf16):")
+    for name, M, N, K, epi in SHAPES:
+        tf, ms = torch_ref(M, N, K)
+        print("  %-7s %6d %6d %5d  %7.1f TF/s (%7.1f us)" % (name, M, N, K, tf, ms * 1e3), flush=True)
     print("%-7s %6s %6s %5s | " % ("shape", "M", "N", "K") + " | ".join("v%d TF/s (us)" % v for v in variants))
     for name, M, N, K, epi in SHAPES:
+        if any(v >= 10 for v in variants):
+            epi = _lib.EPI_BIAS          # ablation builds exist for EPI_BIAS only
         cells, ref = [], None
         for v in variants:
             set_variant(v)
