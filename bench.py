@@ -34,10 +34,12 @@ IMAGENET_STD = (0.225, 0.225, 0.225)
 
 
 # ----------------------------------------------------------------- algorithmic FLOPs
-def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16):
+def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16, folded=False):
     """2*M*N*K over every matmul of one divided-ST clip forward, counted as the reference
     executes it (CLS replicated T times in the spatial branch).  8x224^2: 391.7 GFLOP,
-    8x96^2: 70.7 GFLOP (391.66 / 70.70 from torch.utils.flop_counter)."""
+    8x96^2: 70.7 GFLOP (391.66 / 70.70 from torch.utils.flop_counter).
+    folded=True: what dsvt executes -- temporal proj and temporal_fc folded into one GEMM
+    (VisionTransformer.fold_temporal_fc), i.e. one 2*R*C*C GEMM less per block."""
     N = (S // patch) ** 2
     d = C // heads
     R = N * T
@@ -46,6 +48,8 @@ def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16):
     per_block = (2 * R * C * 3 * C + 4 * N * heads * T * T * d + 2 * 2 * R * C * C          # temporal
                  + 2 * rows_s * C * 3 * C + 4 * T * heads * (1 + N) ** 2 * d + 2 * rows_s * C * C  # spatial
                  + 2 * 2 * L * C * mlp * C)                                                  # MLP
+    if folded:
+        per_block -= 2 * R * C * C
     return depth * per_block + 2 * R * (3 * patch * patch) * C
 
 
@@ -53,9 +57,9 @@ def head_flops(in_dim=768, hidden=2048, bottleneck=256, out_dim=65536):
     return 2 * (in_dim * hidden + hidden * hidden + hidden * bottleneck + bottleneck * out_dim)
 
 
-def clip_flops(n_global=2, n_local=6):
+def clip_flops(n_global=2, n_local=6, folded=False):
     """teacher (2 global) + student (2 global + 6 local) + heads on every crop row."""
-    g, l = vit_fwd_flops(8, 224), vit_fwd_flops(8, 96)
+    g, l = vit_fwd_flops(8, 224, folded=folded), vit_fwd_flops(8, 96, folded=folded)
     return 2 * n_global * g + n_local * l + (2 * n_global + n_local) * head_flops()
 
 
@@ -88,6 +92,22 @@ def cpu_baseline(budget_s=10.0, max_clips=4):
     return {"value": round(done / t_all, 4), "unit": "clips/s", "cores": int(cores), "kind": "port",
             "sample": "%d clip(s) x (teacher 2x8x224^2 + student 2x8x224^2 + 6x8x96^2 + DINOHead(65536) + "
                       "DINOLoss), numpy fp32 oracle, %.1f s" % (done, t_all)}
+
+
+def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "pmc_traffic.json")):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this same
+    bench command, gfx950 FETCH x2 correction applied); None when no summary matches."""
+    try:
+        with open(path) as f:
+            kernels = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    hits = [v for k, v in kernels.items() if k.startswith(kernel_prefix)]
+    if not hits:
+        return None
+    calls = sum(h["calls"] for h in hits)
+    return round(sum(h["traffic_bytes"] * h["calls"] for h in hits) / calls)
 
 
 # ----------------------------------------------------------------- models / data
@@ -209,9 +229,10 @@ def main():
             achieved = tfl / (tms * 1e-3) / 1e12          # = (flops per launch) / (avg launch time)
             peak = PEAK_TFLOPS[args.dtype]
             all_ms = float(np.sum(ms))
+            kname = ops.gemm_kernel_name(dom)
             roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                        "frac": round(achieved / peak, 4), "traffic": None,
-                        "kernel": ops.GEMM_KERNEL_NAMES[dom], "launches": n,
+                        "frac": round(achieved / peak, 4), "traffic": pmc_traffic(kname),
+                        "kernel": kname, "launches": n,
                         "avg_launch_us": round(tms / n * 1e3, 2),
                         "flops_per_launch": tfl / n,
                         "gemm_share_of_step": round(all_ms / (elapsed * 1e3), 3),
@@ -219,7 +240,8 @@ def main():
 
     value = world * args.clips * args.steps / elapsed
     step_ms = elapsed / args.steps * 1e3
-    step_tflops = value * clip_flops() / 1e12
+    folded = student.backbone.fold_temporal_fc
+    step_tflops = value * clip_flops(folded=folded) / 1e12        # FLOPs the GPU executed
     out = {"metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
@@ -227,10 +249,15 @@ def main():
                                   "crops + student on 2x8x224^2 + 6x8x96^2 crops, DINOHead(768->65536), "
                                   "DINOLoss(ncrops=8) + center all-reduce",
                       "clips_per_gpu": args.clips, "global_batch": world * args.clips,
-                      "gflop_per_clip": round(clip_flops() / 1e9, 1), "parallelism": "dp%d" % world,
+                      "gflop_per_clip": round(clip_flops() / 1e9, 1),
+                      "executed_gflop_per_clip": round(clip_flops(folded=folded) / 1e9, 1),
+                      "parallelism": "dp%d" % world,
                       "weights": "random init (torch seed 0)"},
-           "step_roofline": {"achieved": round(step_tflops, 1), "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
-                             "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4)},
+           "step_roofline": {"achieved": round(step_tflops / world, 1), "peak": PEAK_TFLOPS[args.dtype],
+                             "unit": "TFLOP/s per GPU", "flops": "executed",
+                             "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4),
+                             "frac_reference_flops": round(value * clip_flops() / 1e12 / world
+                                                           / PEAK_TFLOPS[args.dtype], 4)},
            "roofline": roofline, "loss": round(loss_val, 5)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()

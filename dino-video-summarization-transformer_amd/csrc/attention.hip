@@ -273,8 +273,124 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- bf16 register kernel, T <= 8
+// 16 lanes own one (sequence, head); lane `sub` holds dims 4*sub..4*sub+3 of q/k/v for all
+// T tokens (8-B loads: a wave reads 4 heads x 128 B = 512 B contiguous per token and role,
+// all 3*TP loads issued before any use -> deep memory-level parallelism, no LDS).
+// S = Q K^T: each lane forms TP*TP partial dots over its 4 dims; a butterfly reduce-scatter
+// over the 16 lanes (masks 8,4,2,1: NV/2+NV/4+.. shuffles instead of 4*NV) leaves lane sub with
+// the VPL = TP*TP/16 fully-reduced scores idx = sub*VPL + k (row i = idx / TP).  Softmax runs
+// in-lane plus a LPR-lane max/sum; the reverse butterfly all-gathers P for the P.V product.
+template <int TP>
+__global__ __launch_bounds__(256) void attn_temporal_reg(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                         int64_t groups, int Tf, int heads, int64_t C, float sl2) {
+  constexpr int NV = TP * TP, VPL = NV / 16, LPR = TP / VPL;
+  static_assert(NV >= 16 && NV % 16 == 0, "TP must be 4 or 8");
+  const int64_t grp = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15;
+  if (grp >= groups) return;  // the whole 16-lane group leaves together
+  const int64_t sq = grp / heads;
+  const int h = (int)(grp % heads);
+  const bf16_t* base = qkv + sq * Tf * 3 * C + (int64_t)h * 64 + sub * 4;
+  uint2 rq[TP], rk[TP], rv[TP];
+#pragma unroll
+  for (int t = 0; t < TP; ++t) {
+    const int tt = t < Tf ? t : Tf - 1;
+    const bf16_t* r = base + (int64_t)tt * 3 * C;
+    rq[t] = *reinterpret_cast<const uint2*>(r);
+    rk[t] = *reinterpret_cast<const uint2*>(r + C);
+    rv[t] = *reinterpret_cast<const uint2*>(r + 2 * C);
+  }
+  float vals[NV];
+#pragma unroll
+  for (int i = 0; i < TP; ++i) {
+    const float q0 = bf16_lo(rq[i].x), q1 = bf16_hi(rq[i].x), q2 = bf16_lo(rq[i].y), q3 = bf16_hi(rq[i].y);
+#pragma unroll
+    for (int j = 0; j < TP; ++j)
+      vals[i * TP + j] = q0 * bf16_lo(rk[j].x) + q1 * bf16_hi(rk[j].x) + q2 * bf16_lo(rk[j].y) + q3 * bf16_hi(rk[j].y);
+  }
+  // reduce-scatter: after the stage with mask m the lane keeps the half selected by (sub & m)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int mask = 8 >> s, half = NV >> (s + 1);
+    const bool hi = (sub & mask) != 0;
+#pragma unroll
+    for (int k = 0; k < half; ++k) {
+      const float mine = hi ? vals[half + k] : vals[k];
+      const float oth = hi ? vals[k] : vals[half + k];
+      vals[k] = mine + __shfl_xor(oth, mask, 64);
+    }
+  }
+  // lane holds scores idx = sub*VPL + k: row i = sub / LPR, key j = (sub % LPR)*VPL + k
+  const int j0 = (sub % LPR) * VPL;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    vals[k] = (j0 + k < Tf) ? vals[k] * sl2 : -INFINITY;
+    mx = fmaxf(mx, vals[k]);
+  }
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    vals[k] = exp2f(vals[k] - mx);
+    sum += vals[k];
+  }
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) sum += __shfl_xor(sum, m, 64);
+  const float inv = 1.0f / sum;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) vals[k] *= inv;
+  // all-gather P (reverse butterfly: blocks stay in natural index order)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int mask = 1 << s, n = VPL << s;
+    const bool hi = (sub & mask) != 0;
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+      const float recv = __shfl_xor(vals[k], mask, 64);
+      const float mine = vals[k];
+      vals[k] = hi ? recv : mine;
+      vals[n + k] = hi ? mine : recv;
+    }
+  }
+  float vf[TP][4];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) {
+    vf[j][0] = bf16_lo(rv[j].x); vf[j][1] = bf16_hi(rv[j].x);
+    vf[j][2] = bf16_lo(rv[j].y); vf[j][3] = bf16_hi(rv[j].y);
+  }
+  bf16_t* obase = out + sq * Tf * C + (int64_t)h * 64 + sub * 4;
+#pragma unroll
+  for (int i = 0; i < TP; ++i) {
+    if (i >= Tf) break;
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const float pj = vals[i * TP + j];
+      o0 = fmaf(pj, vf[j][0], o0); o1 = fmaf(pj, vf[j][1], o1);
+      o2 = fmaf(pj, vf[j][2], o2); o3 = fmaf(pj, vf[j][3], o3);
+    }
+    uint2 w;
+    w.x = pack_bf16x2(o0, o1);
+    w.y = pack_bf16x2(o2, o3);
+    *reinterpret_cast<uint2*>(obase + (int64_t)i * C) = w;
+  }
+}
+
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T, int64_t heads,
                                 int64_t C, float scale, hipStream_t s) {
+  if (dtype == 0 && T <= 8) {
+    const int64_t groups = nseq * heads;
+    const unsigned blocks = (unsigned)((groups * 16 + 255) / 256);
+    const float sl2 = scale * 1.4426950408889634f;
+    if (T <= 4)
+      attn_temporal_reg<4><<<blocks, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, groups, (int)T, (int)heads, C, sl2);
+    else
+      attn_temporal_reg<8><<<blocks, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, groups, (int)T, (int)heads, C, sl2);
+    return hipGetLastError();
+  }
   const int64_t esz = dtype == 0 ? 2 : 4;
   const int64_t per_head = T * 3 * 64 * esz;
   int64_t G = (48 * 1024) / per_head;

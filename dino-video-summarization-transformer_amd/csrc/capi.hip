@@ -70,9 +70,11 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
 }
 
 // GEMM instantiation id: gemm_kernel<T = dtype ? float : bf16, EPI = epi, OUT_F32 = f32>
-int gemm_tag(int dtype, int epi, int out_f32) {
+// probe tag of a GEMM launch: variant * 32 + dtype * 16 + epilogue * 2 + fp32-output, so the
+// host can name the exact kernel instantiation rocprofv3 reports (dsvt/ops.py gemm_kernel_name)
+int gemm_tag(const GemmParams& p, int dtype, int epi, int out_f32) {
   const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
-  return dtype * 16 + epi * 2 + f32;
+  return gemm_variant_for(p, dtype, epi) * 32 + dtype * 16 + epi * 2 + f32;
 }
 
 void norm_map(int64_t& rpg, int64_t& gstride, int64_t& goff) {
@@ -127,7 +129,7 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t l
   GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
                 [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
-                gemm_tag(dtype, epilogue, out_f32));
+                gemm_tag(p, dtype, epilogue, out_f32));
 }
 
 int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const float* gamma, const float* beta,
@@ -185,7 +187,7 @@ int dsvt_patch_embed_fwd(int dtype, int tokens_order, const float* x, int64_t B,
   p.pos = pos_embed; p.pidx = pos_index;
   if (int e = check_gemm(dtype, EPI_PATCH, workspace, K, w, K, bias, X, C, M, C, K)) return e;
   int rc = probed(DSVT_PROBE_GEMM, 2.0 * M * C * K, s, "patch_embed gemm",
-                  [&] { return launch_gemm(p, dtype, EPI_PATCH, 1, s); }, gemm_tag(dtype, EPI_PATCH, 1));
+                  [&] { return launch_gemm(p, dtype, EPI_PATCH, 1, s); }, gemm_tag(p, dtype, EPI_PATCH, 1));
   if (rc) return rc;
   const int64_t rows = nt ? B : B * T, stride = (nt ? 1 + Np * T : 1 + Np) * C;
   if (hipError_t e = launch_cls_init(X, cls_token, pos_embed, rows, stride, C, s)) return hip_fail(e, "cls_init");

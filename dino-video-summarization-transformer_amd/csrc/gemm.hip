@@ -205,24 +205,26 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
   return hipGetLastError();
 }
 
-static int g_gemm_variant = 0;  // 0 auto, 1 = 128x128, 2 = 256x256 big, 3 = 256x128 big
+static int g_gemm_variant = 0;  // 0 = auto; otherwise forced (tools/gemm_bench.py, tests)
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
-// Kernel choice: the 512-thread large-tile kernel for the big bf16 projections, the
-// 128x128 kernel for small M (DINO head) and the fp32 parity mode.
+// Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, >= 2: gemm_big.hip variants).
+// Measured on MI355X (tools/gemm_bench.py): wide bf16 outputs (qkv N=2304, fc1 N=3072) ->
+// persistent staggered 256x128 (v10: 2 WGs/CU, the store tail overlaps the next tile's
+// prologue); N <= 1024 (proj, temporal_fc, fc2), small M (DINO head) and the patch GEMM ->
+// 128x128 (finer tiles, better fill of 256 CUs).
+int gemm_variant_for(const GemmParams& p, int dtype, int epi) {
+  if (dtype != 0) return 0;
+  if (epi == EPI_PATCH) return 1;
+  if (g_gemm_variant) return g_gemm_variant;
+  return (p.M >= 2048 && p.N >= 2048 && p.N % 128 == 0) ? 10 : 1;
+}
+
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
-  if (dtype == 0) {
-    int v = g_gemm_variant;
-    if (v == 0) {
-      // measured on MI355X (tools/gemm_bench.py): wide outputs (qkv N=2304, fc1 N=3072) ->
-      // persistent staggered 256x128 (2 WGs/CU, store tail overlapped); N <= 1024 (proj,
-      // temporal_fc, fc2) and small M (DINO head) -> 128x128 (finer tiles, better fill)
-      v = (p.M >= 2048 && p.N >= 2048 && p.N % 128 == 0) ? 10 : 1;
-    }
-    if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
-    return launch_t<bf16_t>(p, epi, out_f32, s);
-  }
+  const int v = gemm_variant_for(p, dtype, epi);
+  if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
+  if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);
   return launch_t<float>(p, epi, out_f32, s);
 }
 

@@ -112,9 +112,13 @@ class Block(nn.Module):
             ops.ln_gemm(X, patch_map, R, self.temporal_norm1.weight, self.temporal_norm1.bias,
                         self.temporal_norm1.eps, w(ta.qkv.weight), ta.qkv.bias, ctx.qkv, ctx.ws)
             ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
-            ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)                 # proj (:83)
-            ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X,        # fc + residual
-                     epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)                       # (:133-135)
+            if ctx.fold_temporal:   # temporal_fc(proj(o)) as one GEMM (WeightCache.folded) + residual
+                wf, bf = ctx.fold(self.temporal_fc, ta.proj)
+                ops.gemm(ctx.o, wf, bf, X, epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)
+            else:
+                ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)             # proj (:83)
+                ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X,    # fc + residual
+                         epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)                   # (:133-135)
             # spatial with CLS replicate/mean (:139-181)
             ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, eps1, w(self.attn.qkv.weight),
                         self.attn.qkv.bias, ctx.qkv, ctx.ws)
@@ -196,6 +200,9 @@ class VisionTransformer(nn.Module):
                         nn.init.constant_(m.temporal_fc.bias, 0)
                     i += 1
         self.dsvt_dtype = _DEFAULT_DTYPE[0]
+        # fold temporal_attn.proj and temporal_fc into one Linear (exact algebra, one GEMM less
+        # per block); False runs the two GEMMs of the reference literally
+        self.fold_temporal_fc = True
         self._wcache = WeightCache()
         self._index_cache = {}
 
@@ -305,8 +312,11 @@ class VisionTransformer(nn.Module):
         ctx.qkv = torch.empty(ctx.rows, 3 * C, device=dev, dtype=mode)
         ctx.o = torch.empty(ctx.rows, C, device=dev, dtype=mode)
         ctx.hid = torch.empty(ctx.rows, self.blocks[0].mlp.fc1.out_features, device=dev, dtype=mode)
+        ctx.fold_temporal = self.fold_temporal_fc
+        ctx.fold = lambda outer, inner: self._wcache.folded(mode, outer, inner)
         if self.attention_type == 'divided_space_time':
-            ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
+            if not ctx.fold_temporal:
+                ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
             nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
             ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
         for blk in self.blocks:

@@ -198,7 +198,16 @@ def probe_read(capacity=65536):
     return ms[:n], work[:n], fam[:n], tag[:n]
 
 
-GEMM_KERNEL_NAMES = {  # probe tag -> rocprofv3 kernel name prefix (template instantiation)
-    t: "void dsvt::gemm_kernel<%s, %d, %s>" % ("float" if t >= 16 else "unsigned short", (t % 16) // 2,
-                                                "true" if t % 2 else "false")
-    for t in range(32)}
+def gemm_kernel_name(tag):
+    """probe tag (variant*32 + dtype*16 + epi*2 + f32, csrc/capi.hip gemm_tag) -> the
+    rocprofv3 kernel-name prefix of that template instantiation."""
+    variant, rest = divmod(int(tag), 32)
+    epi, f32 = (rest % 16) // 2, "true" if rest % 2 else "false"
+    if variant == 0:
+        return "void dsvt::gemm_kernel<float, %d, %s>" % (epi, f32)
+    if variant == 1:
+        return "void dsvt::gemm_kernel<unsigned short, %d, %s>" % (epi, f32)
+    persist = {9: "256, 128, 2, 2, 3, %d, %s, false", 10: "256, 128, 2, 2, 3, %d, %s, true"}
+    if variant in persist:
+        return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
+    return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)

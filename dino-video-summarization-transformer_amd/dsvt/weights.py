@@ -32,5 +32,32 @@ class WeightCache:
             return out
         return get
 
+    def folded(self, mode, outer, inner):
+        """outer(inner(x)) for two nn.Linear with nothing between them, as ONE Linear:
+        W = Wo.Wi, b = Wo.bi + bo, formed in fp32 on the dsvt GEMM (then cast to `mode`) and
+        cached until any of the four parameters changes.  Used for the temporal branch
+        proj -> temporal_fc of the divided block (timesformer.py:83, 133-135: dropout 0)."""
+        params = (outer.weight, outer.bias, inner.weight, inner.bias)
+        stamp = tuple((p._version, p.data_ptr()) for p in params)
+        key = ("fold", id(outer), id(inner), mode)
+        ent = self._c.get(key)
+        if ent is not None and ent[0] == stamp:
+            return ent[1]
+        wo, bo, wi, bi = (p.detach().float().contiguous() for p in params)
+        dev = wo.device
+        wi_t = wi.t().contiguous()                       # [in_i, out_i]: the GEMM's W[n][k] = Wi[k][n]
+        w32 = torch.empty(wo.shape[0], wi.shape[1], device=dev, dtype=torch.float32)
+        ops.gemm(wo, wi_t, None, w32)                    # W[m][n] = sum_k Wo[m][k] Wi[k][n]
+        b32 = torch.empty(1, wo.shape[0], device=dev, dtype=torch.float32)
+        ops.gemm(bi.reshape(1, -1), wo, bo, b32)         # b[n] = sum_k bi[k] Wo[n][k] + bo[n]
+        b32 = b32.reshape(-1)
+        if mode == torch.float32:
+            w = w32
+        else:
+            w = torch.empty(w32.shape, device=dev, dtype=mode)
+            ops.cast(w32, w)
+        self._c[key] = (stamp, (w, b32))
+        return w, b32
+
     def clear(self):
         self._c.clear()

@@ -178,7 +178,8 @@ int dsvt_probe_enable(int mask, int capacity);
 int dsvt_probe_disable(void);
 /* Synchronizes the recorded events; fills per-launch ms, algorithmic work (FLOP for
  * GEMM/attention, bytes for norm/loss), family and tag (GEMM: kernel instantiation id =
- * dtype*16 + epilogue*2 + fp32_out, epilogue 3 = patch embed).  Returns the number of
+ * variant*32 + dtype*16 + epilogue*2 + fp32_out; variant 0 = fp32 128x128, 1 = bf16 128x128,
+ * 10 = bf16 persistent 256x128; epilogue 3 = patch embed).  Returns the number of
  * launches (negative on error). */
 int dsvt_probe_read(float *ms, double *work, int32_t *family, int32_t *tag, int capacity);
 

@@ -88,6 +88,30 @@ def test_base_divided_golden(base_sd, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
+def test_base_divided_unfolded_golden(base_sd, dtype, tol):
+    """fold_temporal_fc=False runs temporal proj and temporal_fc as the reference's two
+    GEMMs (timesformer.py:83, 133-135); both paths must meet the same golden bar, and the
+    folded weight must follow parameter updates (cache keyed on the four params' versions)."""
+    f = g("base_div")
+    m = tsf(base_sd, dtype)
+    x = cu(P.clip(202, (1, 3, 8, 224, 224)))
+    with torch.no_grad():
+        m.fold_temporal_fc = False
+        e_lit = rel(m(x).cpu(), f["cls_224"])
+        m.fold_temporal_fc = True
+        e_fold = rel(m(x).cpu(), f["cls_224"])
+        y0 = m(x).clone()
+        m.blocks[3].temporal_fc.weight.mul_(1.5)      # invalidates the cached fold
+        y1 = m(x)
+        m.fold_temporal_fc = False
+        y2 = m(x)
+    print("unfolded", dtype, e_lit, "folded", e_fold)
+    assert e_lit < tol and e_fold < tol
+    assert (y1 - y0).abs().max().item() > 0
+    assert rel(y1.cpu(), y2.cpu()) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
 def test_joint_and_space_only_golden(dtype, tol):
     with torch.no_grad():
         mj = tsf(P.timesformer_state(3, attention_type="joint_space_time"), dtype, attention_type="joint_space_time")
