@@ -170,15 +170,13 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from dsvt import dist as ddist
+    from dsvt import ops
+
+    rank, world, local_rank = ddist.env_ranks()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=device)   # RCCL over xGMI
-
-    from dsvt import ops
+    rank, world = ddist.init_from_env(device)          # 'nccl' = RCCL over xGMI when world > 1
     from dsvt._lib import PROBE_GEMM
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -206,11 +204,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    elapsed = ddist.max_over_ranks(time.perf_counter() - t0, device)
     loss_val = float(loss.item())
 
     roofline = None

@@ -8,11 +8,11 @@
 """
 import numpy as np
 import torch
-import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
 from ._lib import DsvtError
+from .dist import center_batch_sum
 
 
 def _fp32(t, name):
@@ -59,13 +59,10 @@ class DINOLoss(nn.Module):
     def update_center(self, colsum, rows):
         """train_ssl.py:673-691: all-reduce (RCCL 'nccl' backend on ROCm) of the teacher column
         sum, then center = m*center + (1-m)*sum/(rows*world)."""
-        world = 1
-        if dist.is_available() and dist.is_initialized():
-            dist.all_reduce(colsum)
-            world = dist.get_world_size()
+        scale = center_batch_sum(colsum, rows)
         if self.center.dtype != torch.float32 or not self.center.is_contiguous():
             self.center = self.center.float().contiguous()
-        ops.center_ema(self.center, colsum, self.center_momentum, 1.0 / (rows * world))
+        ops.center_ema(self.center, colsum, self.center_momentum, scale)
 
 
 class PairwiseDINOLoss(nn.Module):
