@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the backbone calls one after another (no stream overlap)")
     args = ap.parse_args()
 
     from dsvt import dist as ddist
@@ -183,10 +185,14 @@ def main():
     student, teacher, dino_loss = build(dtype, device)
     crops = synthetic_crops(args.clips, device, seed=1234 + rank)
 
+    from dsvt.utils import dino_forward
+    student.concurrent_groups = teacher.concurrent_groups = not args.serial
+
     def step():
         with torch.no_grad():
-            s_out = student(crops)             # 2 backbone calls + head on (2+6)*clips rows
-            t_out = teacher(crops[:2])         # 1 backbone call + head on 2*clips rows
+            # student: 2 backbone calls (224 / 96 groups) + head on (2+6)*clips rows; teacher:
+            # 1 backbone call + head on 2*clips rows -- three independent calls, overlapped
+            s_out, t_out = dino_forward(student, teacher, crops, concurrent=not args.serial)
             return dino_loss(s_out, t_out, 0)  # loss + center (RCCL all-reduce when N > 1)
 
     for _ in range(args.warmup):

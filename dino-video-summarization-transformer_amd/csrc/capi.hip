@@ -74,7 +74,7 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
 // host can name the exact kernel instantiation rocprofv3 reports (dsvt/ops.py gemm_kernel_name)
 int gemm_tag(const GemmParams& p, int dtype, int epi, int out_f32) {
   const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
-  return gemm_variant_for(p, dtype, epi) * 32 + dtype * 16 + epi * 2 + f32;
+  return gemm_variant_for(p, dtype, epi, out_f32) * 32 + dtype * 16 + epi * 2 + f32;
 }
 
 void norm_map(int64_t& rpg, int64_t& gstride, int64_t& goff) {

@@ -27,6 +27,21 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
 }
 
+// Two adjacent 16x16 fp32 fragments (cols 16j.. and 16(j+1).. of one row) -> 8 contiguous bf16
+// per lane for ONE 16-byte store: a v_permlane16_swap per packed dword gives lane group g the
+// columns {g0: 0-7, g1: 16-23, g2: 8-15, g3: 24-31} of the 32-column span (offset pair_off(g)).
+// Cross-lane: call with the whole wave active; predicate only the store.
+__device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
+  const unsigned a0 = (unsigned)f2bf(a[0]) | ((unsigned)f2bf(a[1]) << 16);
+  const unsigned a1 = (unsigned)f2bf(a[2]) | ((unsigned)f2bf(a[3]) << 16);
+  const unsigned b0 = (unsigned)f2bf(b[0]) | ((unsigned)f2bf(b[1]) << 16);
+  const unsigned b1 = (unsigned)f2bf(b[2]) | ((unsigned)f2bf(b[3]) << 16);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+  return make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+__device__ __forceinline__ int pair_off(int g) { return ((g & 1) << 4) | ((g >> 1) << 3); }
+
 // Generic element <-> float conversion for the two storage types.
 template <typename T> struct Elem;
 template <> struct Elem<bf16_t> {
@@ -71,7 +86,22 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU, 0.5 x (1 + erf(x / sqrt2)) (nn.GELU default).  erf by Abramowitz & Stegun
+// 7.1.26 (|abs err| <= 1.5e-7): 1 - erf(z) = t P(t) exp(-z^2), t = 1 / (1 + 0.3275911 z), z >= 0.
+// ~14 VALU ops (one v_rcp, one v_exp) instead of ~35 for the libm erff: this runs on every
+// fc1 output element, in the epilogue of the largest GEMM.  1 + erf(-z) = t P(t) exp(-z^2) is
+// formed directly for x < 0, so the negative tail has no cancellation.
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float tail = p * t * __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);  // 1 - erf(z)
+  const float one_plus_erf = x >= 0.f ? 2.0f - tail : tail;
+  return 0.5f * x * one_plus_erf;
+}
 
 // Output-row map used by every kernel that writes into the [B, L, C] token tensor:
 //   row(m) = (m / rpg) * gstride + goff + (m % rpg)

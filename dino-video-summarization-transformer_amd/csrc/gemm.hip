@@ -214,7 +214,7 @@ void set_gemm_variant(int v) { g_gemm_variant = v; }
 // persistent staggered 256x128 (v10: 2 WGs/CU, the store tail overlaps the next tile's
 // prologue); N <= 1024 (proj, temporal_fc, fc2), small M (DINO head) and the patch GEMM ->
 // 128x128 (finer tiles, better fill of 256 CUs).
-int gemm_variant_for(const GemmParams& p, int dtype, int epi) {
+int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
   if (g_gemm_variant) return g_gemm_variant;
@@ -222,7 +222,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi) {
 }
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
-  const int v = gemm_variant_for(p, dtype, epi);
+  const int v = gemm_variant_for(p, dtype, epi, out_f32);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);
   return launch_t<float>(p, epi, out_f32, s);

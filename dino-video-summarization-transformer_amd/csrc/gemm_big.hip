@@ -36,18 +36,8 @@ __device__ __forceinline__ void wait_stages(int k) {
 }
 
 
-// Store two adjacent 16x16 fragments (cols 16j.., 16(j+1).. of row `row`) as bf16 with ONE
-// 16-byte store per lane: a v_permlane16_swap per packed dword gives lane group g the 8
-// contiguous columns {g0: 0-7, g1: 16-23, g2: 8-15, g3: 24-31} of the 32-column span.
 __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int g) {
-  const unsigned a0 = (unsigned)f2bf(a[0]) | ((unsigned)f2bf(a[1]) << 16);
-  const unsigned a1 = (unsigned)f2bf(a[2]) | ((unsigned)f2bf(a[3]) << 16);
-  const unsigned b0 = (unsigned)f2bf(b[0]) | ((unsigned)f2bf(b[1]) << 16);
-  const unsigned b1 = (unsigned)f2bf(b[2]) | ((unsigned)f2bf(b[3]) << 16);
-  const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
-  const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
-  const int off = ((g & 1) << 4) | ((g >> 1) << 3);
-  *reinterpret_cast<uint4*>(span + off) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  *reinterpret_cast<uint4*>(span + pair_off(g)) = pack_pair_bf16(a, b);
 }
 
 // Direct (register) epilogue shared by the big and persistent kernels.

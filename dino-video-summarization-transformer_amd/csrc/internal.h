@@ -20,7 +20,7 @@ struct GemmParams {
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_PATCH = 3 };
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s);
-int gemm_variant_for(const GemmParams& p, int dtype, int epi);  // the kernel launch_gemm dispatches
+int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // the kernel launch_gemm dispatches
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 void set_gemm_variant(int v);
 

@@ -1,6 +1,54 @@
-"""Drop-in for utils.utils.MultiCropWrapper (utils/utils.py:564-609)."""
+"""Drop-in for utils.utils.MultiCropWrapper (utils/utils.py:564-609), plus the concurrent
+teacher/student forward of one DINO step."""
 import torch
 import torch.nn as nn
+
+_SIDE_STREAMS = {}
+
+
+def side_stream(device, slot):
+    """A persistent non-default HIP stream per (device, slot), created on first use."""
+    key = (torch.device(device), slot)
+    st = _SIDE_STREAMS.get(key)
+    if st is None:
+        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=key[0])
+    return st
+
+
+def run_concurrent(thunks, device, slot0=0):
+    """Run independent GPU work items on separate streams: thunk 0 on the current stream,
+    thunk i on side stream slot0+i-1; every side stream first waits for the current
+    stream's prior work, and the current stream waits for all of them before returning.
+    Kernels of the different items then overlap on the chip (one backbone call's last,
+    partly-filled wave of tiles runs beside another's full waves)."""
+    cur = torch.cuda.current_stream(device)
+    results, used = [None] * len(thunks), []
+    for i, fn in enumerate(thunks):
+        if i == 0:
+            continue
+        st = side_stream(device, slot0 + i - 1)
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            results[i] = fn()
+        used.append(st)
+    if thunks:
+        results[0] = thunks[0]()
+    for st in used:
+        cur.wait_stream(st)
+    for r in results:                      # outputs made on side streams are consumed on `cur`
+        if isinstance(r, torch.Tensor) and r.is_cuda:
+            r.record_stream(cur)
+    return results
+
+
+def dino_forward(student, teacher, images, n_global=2, concurrent=True):
+    """train_ssl.py:523-527: teacher on the `n_global` global views, student on all views.
+    The two networks are independent, so their backbone calls run concurrently."""
+    if not concurrent:
+        return student(images), teacher(images[:n_global])
+    s_out, t_out = run_concurrent([lambda: student(images), lambda: teacher(images[:n_global])],
+                                  images[0].device, slot0=8)
+    return s_out, t_out
 
 
 class MultiCropWrapper(nn.Module):
@@ -9,8 +57,9 @@ class MultiCropWrapper(nn.Module):
     takes the group as a list and writes every crop's tokens straight into one token tensor,
     and the features of all groups land in one preallocated buffer."""
 
-    def __init__(self, backbone, head, vary_fr=False):
+    def __init__(self, backbone, head, vary_fr=False, concurrent_groups=True):
         super().__init__()
+        self.concurrent_groups = concurrent_groups
         if hasattr(backbone, 'fc'):
             backbone.fc, backbone.head = nn.Identity(), nn.Identity()
         self.backbone = backbone
@@ -35,11 +84,20 @@ class MultiCropWrapper(nn.Module):
                     idx_crops.append(i)
         total = sum(inp.shape[0] for inp in x)
         feats = torch.empty(total, self.backbone.embed_dim, device=x[0].device, dtype=torch.float32)
-        start, row = 0, 0
+        jobs, start, row = [], 0, 0
         for end in idx_crops:
             group = x[start:end]
             n = sum(g.shape[0] for g in group)
-            self.backbone.forward_features(group, out=feats[row:row + n], **kwargs)
+            jobs.append((group, feats[row:row + n]))
             row += n
             start = end
+
+        def job(group, out):
+            return lambda: self.backbone.forward_features(group, out=out, **kwargs)
+        thunks = [job(g, o) for g, o in jobs]
+        if self.concurrent_groups and len(thunks) > 1 and feats.is_cuda:
+            run_concurrent(thunks, feats.device)      # the resolution groups are independent
+        else:
+            for fn in thunks:
+                fn()
         return self.head(feats)

@@ -69,6 +69,23 @@ def test_gemm_bias_gelu(dtype, M, N, K, gemm_variant):
             check(back(out), f(ref), dtype, "gemm epi=%d f32out=%d" % (epi, out_f32))
 
 
+def test_gelu_epilogue_accuracy():
+    """The fused GELU (A&S 7.1.26 erf) against scipy's erf elementwise on x in [-10, 10]:
+    an fp32 identity GEMM passes x through exactly, so the epilogue alone is measured."""
+    from dsvt import ops
+    from dsvt._lib import EPI_BIAS_GELU
+    x = np.concatenate([np.linspace(-10, 10, 64 * 500), [0.0, 1e-6, -1e-6, 1e-3, -1e-3, 30.0, -30.0]])
+    x = np.resize(x, (len(x) + 63) // 64 * 64).astype(np.float32).reshape(-1, 64)
+    A = to(x, torch.float32)
+    W = torch.eye(64, device=dev(), dtype=torch.float32)
+    out = torch.empty_like(A)
+    ops.gemm(A, W, torch.zeros(64, device=dev()), out, epilogue=EPI_BIAS_GELU)
+    torch.cuda.synchronize()
+    got, ref = back(out), O.gelu(x.astype(np.float64))
+    err = np.abs(got - ref) / np.maximum(1.0, np.abs(x))
+    assert err.max() < 3e-7, err.max()
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8)])
 def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):

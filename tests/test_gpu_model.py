@@ -172,6 +172,33 @@ def test_e2e_cfg1_multicrop_head_loss(tiny_sd, dtype, tol):
     assert rel(loss_fn.center.cpu(), f["center"]) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_concurrent_streams_bitwise_equal_serial(tiny_sd, dtype):
+    """MultiCropWrapper's concurrent resolution groups and dino_forward's concurrent teacher /
+    student (side HIP streams) give bit-identical outputs to the serial order, repeatably."""
+    from dsvt.utils import MultiCropWrapper, dino_forward
+    from dsvt.vision_transformer import DINOHead
+
+    def net(seed):
+        bb = tsf(tiny_sd, dtype, embed_dim=192, num_heads=3, img_size=112, num_frames=4)
+        hd = DINOHead(192, 4096)
+        hd.load_state_dict({k: torch.from_numpy(v) for k, v in P.dino_head_state(seed, 192, 4096).items()})
+        hd = hd.cuda()
+        hd.dsvt_dtype = dtype
+        return MultiCropWrapper(bb, hd)
+    student, teacher = net(6), net(7)
+    crops = [cu(P.clip(1101 + i, (2, 3, 4, 112, 112))) for i in range(2)] + \
+            [cu(P.clip(1103 + i, (2, 3, 4, 64, 64))) for i in range(4)]
+    with torch.no_grad():
+        student.concurrent_groups = teacher.concurrent_groups = False
+        s_ser, t_ser = dino_forward(student, teacher, crops, concurrent=False)
+        student.concurrent_groups = teacher.concurrent_groups = True
+        for _ in range(3):
+            s_con, t_con = dino_forward(student, teacher, crops)
+            torch.cuda.synchronize()
+            assert torch.equal(s_con, s_ser) and torch.equal(t_con, t_ser)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
 def test_frame_scores_vs_oracle(dtype, tol):
     """Per-frame importance scores (dino_similarity.py:66-93) on a 14-frame video, local 3 /
