@@ -8,9 +8,13 @@
 //   holds 16 scores of ONE query: the row max / sum are in-register + 2 cross-lane xors,
 //   and the probabilities feed O^T = V^T.P^T directly as the B operand (k order permuted
 //   to match); V^T fragments come from ds_read_b64_tr_b16 transposed LDS reads.
+//   Used for sequences longer than 256 keys (joint space-time attention).
+// attn_short_bf16 (L <= 256: spatial 1+N per frame, 2-D ViT): one workgroup per (sequence,
+//   head) with the whole K/V sequence staged in LDS once, 16-query tiles per wave, 16-key
+//   tiles, exact two-pass softmax in registers.
 // attn_seq_f32 (parity mode): same decomposition on the fp32 VALU, one query per lane.
-// attn_temporal (K5): T <= 64 tokens per sequence, all heads of a group staged in LDS,
-//   16 lanes per (head, query), online softmax; HBM-bound.
+// attn_temporal_reg (K5, bf16, T <= 8): register-only, 16 lanes per (patch, head), butterfly
+//   reduce-scatter of Q.K^T; HBM-bound.  attn_temporal_kernel: LDS-staged general-T fallback.
 #include <math.h>
 
 #include "common.h"
@@ -103,13 +107,13 @@ __global__ __launch_bounds__(256) void attn_seq_bf16(AttnParams p) {
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);          // args <= 0 (-inf -> 0)
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float e = exp2f(s[kt][j] - mn);
+        const float e = __builtin_amdgcn_exp2f(s[kt][j] - mn);
         s[kt][j] = e;
         rs += e;
       }
@@ -213,7 +217,164 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------- short sequences (L <= 16*NKT)
+// One workgroup per (sequence, head): K and V of the WHOLE sequence are gathered into LDS once
+// (rows past L zero-filled), then the 4 waves take the 16-query tiles round-robin.  Keys are
+// handled in 16-key tiles (197 -> 13 tiles = 208 slots instead of 4 x 64 = 256), and with
+// every score of a query row in registers the softmax is exact two-pass (no rescaling).  Same
+// MFMA decomposition as attn_seq_bf16: S^T = K.Q^T (lane = one query, 4 keys per tile) and
+// O^T = V^T.P^T with the k-slot permutation and ds_read_b64_tr_b16 V^T fragments.
+template <int NKT>
+__global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
+  constexpr int LP = NKT * 16;
+  __shared__ __attribute__((aligned(16))) bf16_t kv[2][LP * KV_ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.x;
+  const int64_t seq = blockIdx.y, b = seq / p.tin, t = seq % p.tin;
+  const bf16_t* qkv = (const bf16_t*)p.qkv;
+  const int64_t C = p.C;
+  const int L = (int)p.seqlen;
+  const int nkt = (L + 15) >> 4;
+  const int rows = ((nkt + 1) >> 1) * 32;   // staged rows: whole 32-key PV steps
+  const int nqt = nkt;
+
+  // Issue EVERY global load up front (this wave's Q fragments for all its query tiles, and
+  // the thread's <= 8 K/V pieces), then one wait, then the LDS writes: a load -> ds_write
+  // loop would serialize one HBM round trip per iteration.
+  constexpr int QT_W = (NKT + 3) / 4;        // query tiles per wave
+  sv8 qa[QT_W], qb[QT_W];
+#pragma unroll
+  for (int w = 0; w < QT_W; ++w) {
+    int qi = (wave + 4 * w) * 16 + r16;
+    if (qi > L - 1) qi = L - 1;
+    const bf16_t* qrow = qkv + tok_row(p, b, t, qi) * p.ld_qkv + h * 64;
+    qa[w] = *reinterpret_cast<const sv8*>(qrow + g * 8);
+    qb[w] = *reinterpret_cast<const sv8*>(qrow + 32 + g * 8);
+  }
+  constexpr int PCS = (LP * 8 + 255) / 256;  // K/V 16-B pieces per thread
+  uint4 kq[PCS], vq[PCS];
+#pragma unroll
+  for (int i = 0; i < PCS; ++i) {
+    const int pc = tid + 256 * i, r = pc >> 3, ch = pc & 7;
+    kq[i] = make_uint4(0, 0, 0, 0);
+    vq[i] = kq[i];
+    if (r < L) {
+      const bf16_t* src = qkv + tok_row(p, b, t, r) * p.ld_qkv + C + h * 64 + ch * 8;
+      kq[i] = *reinterpret_cast<const uint4*>(src);
+      vq[i] = *reinterpret_cast<const uint4*>(src + C);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PCS; ++i) {
+    const int pc = tid + 256 * i, r = pc >> 3, ch = pc & 7;
+    if (r < rows) {
+      *reinterpret_cast<uint4*>(&kv[0][r * KV_ROW + ch * 8]) = kq[i];
+      *reinterpret_cast<uint4*>(&kv[1][r * KV_ROW + ch * 8]) = vq[i];
+    }
+  }
+  __syncthreads();
+  const bf16_t* Ks = kv[0];
+  const bf16_t* Vs = kv[1];
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+#pragma unroll
+  for (int w = 0; w < QT_W; ++w) {
+    const int qt = wave + 4 * w;
+    if (qt >= nqt) break;
+    const sv8 qf0 = qa[w], qf1 = qb[w];
+    // scores: s[kt][j] = raw score(query qt*16 + r16, key kt*16 + 4g + j); the row max is taken
+    // on raw scores (scale > 0) and the scale folded into the exponent: exp2(s*c - max*c)
+    fv4 s[NKT];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+        const bf16_t* kr = Ks + (kt * 16 + r16) * KV_ROW + g * 8;
+        const sv8 k0 = *reinterpret_cast<const sv8*>(kr);
+        const sv8 k1 = *reinterpret_cast<const sv8*>(kr + 32);
+        fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
+        if (kt * 16 + 16 > L) {                      // the one partial key tile: mask
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kt * 16 + 4 * g + j >= L) s[kt][j] = -INFINITY;
+        }
+        mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mxs = mx * sl2;
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));   // args <= 0
+          s[kt][j] = e;
+          rs += e;
+        }
+      } else {
+        s[kt] = fv4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    // O^T += V^T . P^T over 32-key steps; k-slot (g, jj): jj<4 -> key tile 2kp, jj>=4 -> 2kp+1
+    fv4 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = fv4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kp = 0; kp < NKT / 2; ++kp) {
+      if (2 * kp >= nkt) break;
+      sv8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[2 * kp][j]);
+        pb[4 + j] = (short)f2bf(s[2 * kp + 1][j]);
+      }
+      const int vr0 = kp * 32 + 4 * g + (r16 >> 2);
+      const int vr1 = vr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr0 * KV_ROW + col));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr1 * KV_ROW + col));
+        const sv8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+      }
+    }
+    // lane holds O[query qt*16 + r16][d = dt*16 + 4g + 0..3]
+    const int qo = qt * 16 + r16;
+    if (qo < L) {
+      const float inv = 1.0f / rs;
+      if (qo == 0 && p.cls_aux) {
+        float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+      } else {
+        bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+      }
+    }
+  }
+}
+
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
+  if (dtype == 0 && p.seqlen <= 256) {
+    dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
+    if (p.seqlen <= 64) attn_short_bf16<4><<<grid, 256, 0, s>>>(p);
+    else attn_short_bf16<16><<<grid, 256, 0, s>>>(p);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)(p.nb * p.tin));
   if (dtype == 0) attn_seq_bf16<<<grid, 256, 0, s>>>(p);
   else attn_seq_f32<<<grid, 64, 0, s>>>(p);

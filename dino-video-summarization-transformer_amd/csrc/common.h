@@ -42,6 +42,26 @@ __device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
 }
 __device__ __forceinline__ int pair_off(int g) { return ((g & 1) << 4) | ((g >> 1) << 3); }
 
+// Bias of a wave's 64 output columns cbase .. cbase+63 (cbase wave-uniform) as the lane's
+// 4 x float4 (fragment j, columns cbase + 16j + 4g .. +3).  Read through the constant address
+// space, i.e. SCALAR loads counted on lgkmcnt: a vector load here would sit on vmcnt behind
+// the GEMM's in-flight LDS-DMA prefetches and stores, and its wait would drain them all.
+__device__ __forceinline__ void bias_frag4(const float* bias, int64_t cbase, int g, float4 (&out)[4]) {
+  if (!bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  typedef __attribute__((address_space(4))) const fv4* CF4;
+  const CF4 bp = (CF4)(bias + cbase);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const fv4 v0 = bp[4 * j], v1 = bp[4 * j + 1], v2 = bp[4 * j + 2], v3 = bp[4 * j + 3];
+    const fv4 v = g == 0 ? v0 : g == 1 ? v1 : g == 2 ? v2 : v3;
+    out[j] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // Generic element <-> float conversion for the two storage types.
 template <typename T> struct Elem;
 template <> struct Elem<bf16_t> {

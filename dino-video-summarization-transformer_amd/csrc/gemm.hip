@@ -99,10 +99,82 @@ template <> struct TileMMA<float> {
   }
 };
 
+template <typename T, int EPI, bool OUT_F32, bool CHECK>
+__device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][4], int64_t m0, int64_t n0, int wm,
+                                             int wn, int lane) {
+  const int r16 = lane & 15, g = lane >> 4;
+  int64_t orow[4];
+  bool vrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + wm * 64 + i * 16 + r16;
+    vrow[i] = !CHECK || m < p.M;
+    orow[i] = map_row(vrow[i] ? m : p.M - 1, p.rpg, p.gstride, p.goff);
+  }
+  float4 bias4[4];
+  if (!CHECK || n0 + wn * 64 + 64 <= p.N) {
+    bias_frag4(p.bias, n0 + wn * 64, g, bias4);         // scalar loads (lgkmcnt)
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
+      bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  float4 add[4][4];                    // residual / embedding addend per fragment
+  if constexpr (EPI == EPI_RESID || EPI == EPI_PATCH) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = m0 + wm * 64 + i * 16 + r16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
+        add[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (CHECK && (!vrow[i] || n >= p.N)) continue;
+        if constexpr (EPI == EPI_RESID) {
+          add[i][j] = *reinterpret_cast<const float4*>((const float*)p.out + orow[i] * p.ldo + n);
+        } else {
+          const int64_t rr = m % p.rpg;
+          const int64_t np = rr / p.T, t = rr % p.T;
+          float4 o = *reinterpret_cast<const float4*>(p.pos + (1 + (int64_t)p.pidx[np]) * p.N + n);
+          if (p.temb) {
+            const float4 te = *reinterpret_cast<const float4*>(p.temb + (int64_t)p.tidx[t] * p.N + n);
+            o.x += te.x; o.y += te.y; o.z += te.z; o.w += te.w;
+          }
+          add[i][j] = o;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (CHECK && !vrow[i]) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
+      if (CHECK && n >= p.N) continue;
+      const float4 bb = bias4[j];
+      float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y, v2 = acc[i][j][2] + bb.z, v3 = acc[i][j][3] + bb.w;
+      if constexpr (EPI == EPI_GELU) {
+        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+      }
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
+        if constexpr (OUT_F32)
+          store4((float*)p.out + orow[i] * p.ldo + n, v0, v1, v2, v3);
+        else
+          store4((T*)p.out + orow[i] * p.ldo + n, v0, v1, v2, v3);
+      } else {  // EPI_RESID / EPI_PATCH: fp32 token rows
+        const float4 a = add[i][j];
+        store4((float*)p.out + orow[i] * p.ldo + n, v0 + a.x, v1 + a.y, v2 + a.z, v3 + a.w);
+      }
+    }
+  }
+}
+
 template <typename T, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
   // XCD-aware bijective remap: consecutive workgroup ids of one XCD walk the N-tiles of
@@ -142,47 +214,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   }
 
   // ---- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + 0..3]
-  const int r16 = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + wm * 64 + i * 16 + r16;
-    if (m >= p.M) continue;
-    const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
-      if (n >= p.N) continue;
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      if (p.bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-        v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
-      }
-      if constexpr (EPI == EPI_GELU) {
-        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-      }
-      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
-        if constexpr (OUT_F32)
-          store4((float*)p.out + orow * p.ldo + n, v0, v1, v2, v3);
-        else
-          store4((T*)p.out + orow * p.ldo + n, v0, v1, v2, v3);
-      } else if constexpr (EPI == EPI_RESID) {
-        float4* xo = reinterpret_cast<float4*>((float*)p.out + orow * p.ldo + n);
-        float4 x = *xo;
-        x.x += v0; x.y += v1; x.z += v2; x.w += v3;
-        *xo = x;
-      } else {  // EPI_PATCH
-        const int64_t rr = m % p.rpg;
-        const int64_t np = rr / p.T, t = rr % p.T;
-        const float4 pe = *reinterpret_cast<const float4*>(p.pos + (1 + (int64_t)p.pidx[np]) * p.N + n);
-        v0 += pe.x; v1 += pe.y; v2 += pe.z; v3 += pe.w;
-        if (p.temb) {
-          const float4 te = *reinterpret_cast<const float4*>(p.temb + (int64_t)p.tidx[t] * p.N + n);
-          v0 += te.x; v1 += te.y; v2 += te.z; v3 += te.w;
-        }
-        store4((float*)p.out + orow * p.ldo + n, v0, v1, v2, v3);
-      }
-    }
-  }
+  // Every global load of the epilogue (bias, residual X, pos/time embeddings) is issued
+  // before the first store: stores to the row-mapped X may alias later loads as far as the
+  // compiler knows, so a load/add/store loop would pay one HBM round trip per fragment.
+  // Full tiles (uniform per workgroup) take a branch-free path: no per-lane bounds branches,
+  // so the compiler's vmcnt waits stay exact instead of draining after every store.
+  if (m0 + BM <= p.M && n0 + BN <= p.N) epilogue_128<T, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
+  else epilogue_128<T, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
 }
 
 template <typename T>
@@ -210,15 +248,15 @@ static int g_gemm_variant = 0;  // 0 = auto; otherwise forced (tools/gemm_bench.
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
 // Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, >= 2: gemm_big.hip variants).
-// Measured on MI355X (tools/gemm_bench.py): wide bf16 outputs (qkv N=2304, fc1 N=3072) ->
-// persistent staggered 256x128 (v10: 2 WGs/CU, the store tail overlaps the next tile's
-// prologue); N <= 1024 (proj, temporal_fc, fc2), small M (DINO head) and the patch GEMM ->
-// 128x128 (finer tiles, better fill of 256 CUs).
+// Measured on MI355X (tools/gemm_bench.py): every big bf16 projection with K <= 1024 (qkv
+// N=2304, fc1 N=3072, proj / folded temporal fc N=768) -> persistent staggered 256x128 (v10:
+// 2 WGs/CU, the epilogue of one overlaps the MFMA loop of the other, the next tile's loads fly
+// under the store tail); K = 3072 (fc2), small M (DINO head) and the patch GEMM -> 128x128.
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
   if (g_gemm_variant) return g_gemm_variant;
-  return (p.M >= 2048 && p.N >= 2048 && p.N % 128 == 0) ? 10 : 1;
+  return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {

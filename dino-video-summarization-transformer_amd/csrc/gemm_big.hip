@@ -45,16 +45,79 @@ template <int MI, int NJ, int EPI, bool OUT_F32>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
+  // bias: scalar loads for a full 64-column wave slab (no vmcnt wait behind the in-flight
+  // prefetch of the next tile); per-lane vector loads only at a ragged N edge
+  float4 bias4[NJ];
+  if (NJ == 4 && cbase + 64 <= p.N) {
+    float4 b4[4];
+    bias_frag4(p.bias, cbase, g, b4);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bias4[j] = b4[j & 3];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t n = cbase + j * 16 + 4 * g;
+      bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // full wave tile (uniform): branch-free bias / GELU / 16-B stores, so the compiler's vmcnt
+  // waits stay exact (a per-lane bounds branch around each store makes it drain every time)
+  if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0) {
+    if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int64_t orow = map_row(rbase + i * 16 + r16, p.rpg, p.gstride, p.goff);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const float4 bb = bias4[j];
+          acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
+          if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; j += 2)
+          store_pair_bf16((bf16_t*)p.out + orow * p.ldo + cbase + j * 16, acc[i][j], acc[i][j + 1], g);
+      }
+      return;
+    }
+  }
+  // full wave tile, fp32 residual add into X: the X fragments of two rows are loaded before
+  // their stores (one HBM round trip per row pair instead of per fragment), branch-free
+  if constexpr (EPI == EPI_RESID && MI % 2 == 0) {
+    if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
+#pragma unroll
+      for (int i = 0; i < MI; i += 2) {
+        float* xr[2];
+        float4 x[2][NJ];
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          xr[ii] = (float*)p.out + map_row(rbase + (i + ii) * 16 + r16, p.rpg, p.gstride, p.goff) * p.ldo + cbase + 4 * g;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) x[ii][j] = *reinterpret_cast<const float4*>(xr[ii] + j * 16);
+        }
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const float4 bb = bias4[j];
+            const fv4 a = acc[i + ii][j];
+            *reinterpret_cast<float4*>(xr[ii] + j * 16) =
+                make_float4(x[ii][j].x + a[0] + bb.x, x[ii][j].y + a[1] + bb.y, x[ii][j].z + a[2] + bb.z,
+                            x[ii][j].w + a[3] + bb.w);
+          }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int64_t m = rbase + i * 16 + r16;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int64_t n = cbase + j * 16 + 4 * g;
-      if (p.bias && n < p.N) {
-        const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-        acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
-      }
+      const float4 bb = bias4[j];
+      acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
       if constexpr (EPI == EPI_GELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
@@ -120,7 +183,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_big_kernel(GemmParams p)
   static_assert((NST - 2) * PER_STAGE < 16, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[NST * ST_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int r16 = lane & 15, g = lane >> 4;
 
@@ -360,7 +423,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
   static_assert(NST >= 3 && NST <= 5 && (NST - 2) * PER_STAGE < 16, "ring depth");
   __shared__ __attribute__((aligned(16))) char smem[NST * ST_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int r16 = lane & 15, g = lane >> 4;
   const int tilesN = (int)((p.N + BN - 1) / BN);

@@ -189,8 +189,10 @@ def test_attn_spatial_cls_mean(dtype, B, T, N, heads):
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("nb,L,heads", [(2, 5, 3), (1, 65, 12), (2, 197, 3), (1, 300, 2), (1, 1569, 1)])
+@pytest.mark.parametrize("nb,L,heads", [(2, 5, 3), (1, 16, 2), (1, 17, 2), (1, 64, 2), (1, 65, 12), (2, 197, 3),
+                                        (1, 256, 2), (1, 257, 2), (1, 300, 2), (1, 1569, 1)])
 def test_attn_joint(dtype, nb, L, heads):
+    """L <= 256: whole-sequence LDS kernel (attn_short_bf16 in bf16); longer: flash kernel."""
     from dsvt import ops
     C = heads * 64
     qkv = rnd((nb * L, 3 * C), 13, 1.5)
@@ -208,13 +210,15 @@ def test_attn_joint(dtype, nb, L, heads):
     check(back(out), ref, dtype, "joint")
 
 
-def test_attn_softmax_spike():
-    """Force the online-softmax rescale branch: one key far above the rest in a LATE chunk."""
+@pytest.mark.parametrize("L,hot", [(200, 190), (400, 390)])
+def test_attn_softmax_spike(L, hot):
+    """One key far above the rest in a LATE chunk: the online-softmax rescale branch of the
+    flash kernel (L=400) and the two-pass softmax of the short kernel (L=200)."""
     from dsvt import ops
-    nb, L, heads = 1, 200, 1
+    nb, heads = 1, 1
     qkv = rnd((L, 192), 14, 0.5)
     qkv[:, :64] = 1.0
-    qkv[190, 64:128] = 40.0        # key 190 (chunk 3) dominates every query
+    qkv[hot, 64:128] = 40.0        # key `hot` dominates every query
     for dtype in DT:
         Q = to(qkv, dtype)
         out = torch.empty(L, 64, device=dev(), dtype=dtype)
