@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
     ap.add_argument("--serial", action="store_true",
                     help="run the backbone calls one after another (no stream overlap)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every kernel eagerly instead of replaying the captured HIP graph")
     args = ap.parse_args()
 
     from dsvt import dist as ddist
@@ -188,19 +190,58 @@ def main():
     from dsvt.utils import dino_forward
     student.concurrent_groups = teacher.concurrent_groups = not args.serial
 
-    def step():
+    dino_loss.defer_center_update = True   # center all-reduce + EMA outside the graph
+
+    def forward_loss(concurrent=not args.serial):
+        student.concurrent_groups = teacher.concurrent_groups = concurrent
         with torch.no_grad():
             # student: 2 backbone calls (224 / 96 groups) + head on (2+6)*clips rows; teacher:
             # 1 backbone call + head on 2*clips rows -- three independent calls, overlapped
-            s_out, t_out = dino_forward(student, teacher, crops, concurrent=not args.serial)
-            return dino_loss(s_out, t_out, 0)  # loss + center (RCCL all-reduce when N > 1)
+            s_out, t_out = dino_forward(student, teacher, crops, concurrent=concurrent)
+            return dino_loss(s_out, t_out, 0)
+
+    def center_update():
+        colsum, rows = dino_loss.last_colsum
+        dino_loss.update_center(colsum, rows)   # RCCL all-reduce of the teacher column sum when N > 1
+
+    def step(concurrent=not args.serial):
+        loss = forward_loss(concurrent)
+        center_update()
+        return loss
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
+    # ---- per-kernel measurement pass: eager, SERIAL launches (the probe brackets each launch
+    # with HIP events on its stream; kernels sharing the chip with another stream would read
+    # long), so the roofline is each kernel's own time -- same command as the rocprof summary
+    probe = None
     if not args.no_probe:
         ops.probe_enable(PROBE_GEMM, 1 << 16)
+        for _ in range(min(args.steps, 5)):
+            step(concurrent=False)
+        torch.cuda.synchronize()
+        probe = ops.probe_read(1 << 16)
+        ops.probe_disable()
+
+    # ---- the timed run: the whole forward + loss of a step as ONE captured HIP graph (every
+    # kernel of every step still runs; the graph only removes per-launch CPU work and gaps)
+    graph = None
+    if not args.no_graph:
+        graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph):
+            g_loss = forward_loss()
+        torch.cuda.synchronize()
+
+        def step(concurrent=None):  # noqa: F811
+            graph.replay()
+            center_update()
+            return g_loss
+        step()                                  # one replay before timing
+        torch.cuda.synchronize()
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -214,9 +255,8 @@ def main():
     loss_val = float(loss.item())
 
     roofline = None
-    if not args.no_probe:
-        ms, work, fam, tag = ops.probe_read(1 << 16)
-        ops.probe_disable()
+    if probe is not None:
+        ms, work, fam, tag = probe
         if len(ms):
             by_tag = {}
             for t, m_, w_ in zip(tag, ms, work):
@@ -235,7 +275,8 @@ def main():
                         "kernel": kname, "launches": n,
                         "avg_launch_us": round(tms / n * 1e3, 2),
                         "flops_per_launch": tfl / n,
-                        "gemm_share_of_step": round(all_ms / (elapsed * 1e3), 3),
+                        "gemm_kernel_ms_per_step": round(all_ms / min(args.steps, 5), 3),
+                        "measured": "HIP events around each launch, serial eager pass of the same step",
                         "all_gemm_tflops": round(float(np.sum(work)) / (all_ms * 1e-3) / 1e12, 1)}
 
     value = world * args.clips * args.steps / elapsed
@@ -252,7 +293,9 @@ def main():
                       "gflop_per_clip": round(clip_flops() / 1e9, 1),
                       "executed_gflop_per_clip": round(clip_flops(folded=folded) / 1e9, 1),
                       "parallelism": "dp%d" % world,
-                      "weights": "random init (torch seed 0)"},
+                      "weights": "random init (torch seed 0)",
+                      "launch": "eager" if graph is None else "hip_graph (forward+loss captured; center all-reduce eager)",
+                      "streams": "serial" if args.serial else "3 backbone calls on concurrent HIP streams"},
            "step_roofline": {"achieved": round(step_tflops / world, 1), "peak": PEAK_TFLOPS[args.dtype],
                              "unit": "TFLOP/s per GPU", "flops": "executed",
                              "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4),

@@ -224,9 +224,11 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
 // every score of a query row in registers the softmax is exact two-pass (no rescaling).  Same
 // MFMA decomposition as attn_seq_bf16: S^T = K.Q^T (lane = one query, 4 keys per tile) and
 // O^T = V^T.P^T with the k-slot permutation and ds_read_b64_tr_b16 V^T fragments.
-template <int NKT>
-__global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
-  constexpr int LP = NKT * 16;
+template <int NKT, int NW>
+__global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(AttnParams p) {
+  constexpr int NKP = (NKT + 1) / 2;         // 32-key PV steps
+  constexpr int SN = 2 * NKP;                // score tiles held (the last one of an odd NKT is 0)
+  constexpr int LP = NKP * 32;               // LDS rows: whole PV steps
   __shared__ __attribute__((aligned(16))) bf16_t kv[2][LP * KV_ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
@@ -242,21 +244,22 @@ __global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
   // Issue EVERY global load up front (this wave's Q fragments for all its query tiles, and
   // the thread's <= 8 K/V pieces), then one wait, then the LDS writes: a load -> ds_write
   // loop would serialize one HBM round trip per iteration.
-  constexpr int QT_W = (NKT + 3) / 4;        // query tiles per wave
+  constexpr int QT_W = (NKT + NW - 1) / NW;  // query tiles per wave
   sv8 qa[QT_W], qb[QT_W];
 #pragma unroll
   for (int w = 0; w < QT_W; ++w) {
-    int qi = (wave + 4 * w) * 16 + r16;
+    int qi = (wave + NW * w) * 16 + r16;
     if (qi > L - 1) qi = L - 1;
     const bf16_t* qrow = qkv + tok_row(p, b, t, qi) * p.ld_qkv + h * 64;
     qa[w] = *reinterpret_cast<const sv8*>(qrow + g * 8);
     qb[w] = *reinterpret_cast<const sv8*>(qrow + 32 + g * 8);
   }
-  constexpr int PCS = (LP * 8 + 255) / 256;  // K/V 16-B pieces per thread
+  constexpr int NT = 64 * NW;
+  constexpr int PCS = (LP * 8 + NT - 1) / NT;  // K/V 16-B pieces per thread
   uint4 kq[PCS], vq[PCS];
 #pragma unroll
   for (int i = 0; i < PCS; ++i) {
-    const int pc = tid + 256 * i, r = pc >> 3, ch = pc & 7;
+    const int pc = tid + NT * i, r = pc >> 3, ch = pc & 7;
     kq[i] = make_uint4(0, 0, 0, 0);
     vq[i] = kq[i];
     if (r < L) {
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
   }
 #pragma unroll
   for (int i = 0; i < PCS; ++i) {
-    const int pc = tid + 256 * i, r = pc >> 3, ch = pc & 7;
+    const int pc = tid + NT * i, r = pc >> 3, ch = pc & 7;
     if (r < rows) {
       *reinterpret_cast<uint4*>(&kv[0][r * KV_ROW + ch * 8]) = kq[i];
       *reinterpret_cast<uint4*>(&kv[1][r * KV_ROW + ch * 8]) = vq[i];
@@ -280,15 +283,15 @@ __global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
 
 #pragma unroll
   for (int w = 0; w < QT_W; ++w) {
-    const int qt = wave + 4 * w;
+    const int qt = wave + NW * w;
     if (qt >= nqt) break;
     const sv8 qf0 = qa[w], qf1 = qb[w];
     // scores: s[kt][j] = raw score(query qt*16 + r16, key kt*16 + 4g + j); the row max is taken
     // on raw scores (scale > 0) and the scale folded into the exponent: exp2(s*c - max*c)
-    fv4 s[NKT];
+    fv4 s[SN];
     float mx = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
+    for (int kt = 0; kt < SN; ++kt) {
       if (kt < nkt) {
         const bf16_t* kr = Ks + (kt * 16 + r16) * KV_ROW + g * 8;
         const sv8 k0 = *reinterpret_cast<const sv8*>(kr);
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
     const float mxs = mx * sl2;
     float rs = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
+    for (int kt = 0; kt < SN; ++kt) {
       if (kt < nkt) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[d] = fv4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kp = 0; kp < NKT / 2; ++kp) {
+    for (int kp = 0; kp < NKP; ++kp) {
       if (2 * kp >= nkt) break;
       sv8 pb;
 #pragma unroll
@@ -371,8 +374,9 @@ __global__ __launch_bounds__(256) void attn_short_bf16(AttnParams p) {
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
   if (dtype == 0 && p.seqlen <= 256) {
     dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
-    if (p.seqlen <= 64) attn_short_bf16<4><<<grid, 256, 0, s>>>(p);
-    else attn_short_bf16<16><<<grid, 256, 0, s>>>(p);
+    if (p.seqlen <= 64) attn_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
+    else if (p.seqlen <= 208) attn_short_bf16<13, 8><<<grid, 512, 0, s>>>(p);   // 1 + 196 patches
+    else attn_short_bf16<16, 4><<<grid, 256, 0, s>>>(p);
     return hipGetLastError();
   }
   dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)(p.nb * p.tin));

@@ -568,18 +568,15 @@ static hipError_t launch_big_t(const GemmParams& p, int epi, int out_f32, hipStr
   return hipGetLastError();
 }
 
-// variant: 2 = 256x256 / 8 waves / 4 stages (1 WG per CU); 3 = 256x128 / 8 waves / 4 stages;
+// variant: 3 = 256x128 / 8 waves / 4 stages (fragment double-buffered);
 // 4 = 256x128 / 4 waves (wave tile 128x64) / 3 stages = 72 KB LDS -> 2 WGs per CU, the
 // epilogue of one overlaps the MFMA loop of the other; 5 = 128x256 / 4 waves / 3 stages.
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s) {
   switch (variant) {
-    case 2: return launch_big_t<256, 256, 2, 4, 4, true, true>(p, epi, out_f32, s);
     case 3: return launch_big_t<256, 128, 4, 2, 4, true, true>(p, epi, out_f32, s);
     case 4: return launch_big_t<256, 128, 2, 2, 3, false, false>(p, epi, out_f32, s);
     case 5: return launch_big_t<128, 256, 1, 4, 3, false, false>(p, epi, out_f32, s);
     case 6: return launch_big_t<256, 128, 2, 2, 3, true, false>(p, epi, out_f32, s);
-    case 7: return launch_big_t<256, 128, 2, 2, 3, false, true>(p, epi, out_f32, s);
-    case 8: return launch_big_t<128, 256, 1, 4, 3, false, true>(p, epi, out_f32, s);
     case 9: return launch_persist_t<256, 128, 2, 2, false>(p, epi, out_f32, s);
     case 10: return launch_persist_t<256, 128, 2, 2, true>(p, epi, out_f32, s);
     case 11: return launch_persist_t<128, 256, 1, 4, true>(p, epi, out_f32, s);

@@ -33,6 +33,11 @@ class DINOLoss(nn.Module):
         self.global_crops = global_crops
         self.two_token = two_token
         self.register_buffer("center", torch.zeros(1, out_dim))
+        # When True, forward() leaves the center update to the caller: the teacher column sum
+        # and row count are kept in `last_colsum` for update_center().  Lets a HIP graph hold
+        # the forward while the RCCL all-reduce of the center runs outside it.
+        self.defer_center_update = False
+        self.last_colsum = None
         # train_ssl.py:627-631
         self.teacher_temp_schedule = np.concatenate((
             np.linspace(warmup_teacher_temp, teacher_temp, warmup_teacher_temp_epochs),
@@ -52,7 +57,9 @@ class DINOLoss(nn.Module):
             raise ValueError("student rows %d != ncrops %d x batch %d" % (s.shape[0], self.n_crops, B))
         temp = float(self.teacher_temp_schedule[epoch])
         loss, colsum = ops.dino_loss(s, t, self.center, B, self.n_crops, self.global_crops, self.student_temp, temp)
-        self.update_center(colsum, t.shape[0])
+        self.last_colsum = (colsum, t.shape[0])
+        if not self.defer_center_update:
+            self.update_center(colsum, t.shape[0])
         return loss.reshape(())
 
     @torch.no_grad()

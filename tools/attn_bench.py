@@ -34,7 +34,27 @@ def run(B, T, N, heads, reps):
           flush=True)
 
 
+def run_joint(nb, L, heads, reps):
+    """Same per-sequence work with the sequence's rows CONTIGUOUS (layout comparison)."""
+    C = heads * 64
+    dev = torch.device("cuda")
+    qkv = (torch.randn(nb * L, 3 * C, device=dev) * 1.5).to(torch.bfloat16)
+    out = torch.empty(nb * L, C, device=dev, dtype=torch.bfloat16)
+    ops.attn_joint(qkv, out, nb, L, heads, 0.125)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ops.attn_joint(qkv, out, nb, L, heads, 0.125)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    print("joint nb=%d L=%d: %.1f us  %.2f TB/s (qkv+out)" % (nb, L, us, nb * L * 4 * C * 2 / us / 1e6), flush=True)
+
+
 if __name__ == "__main__":
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     run(16, 8, 196, 12, reps)
     run(48, 8, 36, 12, reps)
+    run_joint(128, 197, 12, reps)
+    run_joint(384, 37, 12, reps)
