@@ -208,6 +208,25 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
       m = mn;
     }
   }
+  if (p.probs) {                            // get_attn: exp(s - m) / l, second pass over the keys
+    float* prow = p.probs + ((seq * p.heads + h) * p.seqlen + qc) * p.seqlen;
+    for (int c = 0; c < nchunks; ++c) {
+      __syncthreads();
+      int64_t ki = (int64_t)c * 64 + lane;
+      if (ki > p.seqlen - 1) ki = p.seqlen - 1;
+      const float* base = qkv + tok_row(p, b, t, ki) * p.ld_qkv + h * 64;
+      for (int d = 0; d < 64; ++d) ks[lane][d] = base[C + d];
+      __syncthreads();
+      const int64_t rem = p.seqlen - (int64_t)c * 64;
+      const int nk = rem < 64 ? (int)rem : 64;
+      for (int j = 0; j < nk; ++j) {
+        float sdot = 0.f;
+#pragma unroll
+        for (int d = 0; d < 64; ++d) sdot = fmaf(q[d], ks[j][d], sdot);
+        if (qi < p.seqlen) prow[(int64_t)c * 64 + j] = expf(sdot * p.scale - m) / l;
+      }
+    }
+  }
   if (qi < p.seqlen) {
     const float inv = 1.0f / l;
     float* dst = (qi == 0 && p.cls_aux) ? p.cls_aux + seq * C + h * 64
@@ -354,6 +373,20 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
     }
     // lane holds O[query qt*16 + r16][d = dt*16 + 4g + 0..3]
     const int qo = qt * 16 + r16;
+    if (p.probs && qo < L) {                 // get_attn: normalized probabilities, fp32
+      const float inv = 1.0f / rs;
+      float* prow = p.probs + ((seq * p.heads + h) * (int64_t)L + qo) * L;
+#pragma unroll
+      for (int kt = 0; kt < SN; ++kt) {
+        if (kt < nkt) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int key = kt * 16 + 4 * g + j;
+            if (key < L) prow[key] = s[kt][j] * inv;
+          }
+        }
+      }
+    }
     if (qo < L) {
       const float inv = 1.0f / rs;
       if (qo == 0 && p.cls_aux) {

@@ -235,6 +235,26 @@ int dsvt_attn_spatial_fwd(int dtype, const void* qkv, void* out, int64_t B, int6
   return 0;
 }
 
+int dsvt_attn_spatial_probs_fwd(int dtype, const void* qkv, void* out, float* probs, int64_t B, int64_t T, int64_t L,
+                                int64_t heads, int64_t head_dim, float scale, void* workspace, int64_t workspace_bytes,
+                                void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial_probs: bad dtype");
+  REQUIRE(qkv && out && probs && aligned16(qkv) && aligned16(out), "attn_spatial_probs: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_spatial_probs: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_probs: need (L-1) %% T == 0");
+  const int64_t C = heads * 64, seqlen = 1 + (L - 1) / T;
+  REQUIRE(dtype == DSVT_F32 || seqlen <= 256, "attn_spatial_probs: bf16 export supports 1+N <= 256 (got %lld)",
+          (long long)seqlen);
+  REQUIRE(workspace && aligned16(workspace) &&
+              workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_SPATIAL, dtype, B * T, C, 0),
+          "attn_spatial_probs: workspace too small");
+  AttnParams p{qkv, 3 * C, out, C, (float*)workspace, B, T, L, T, seqlen, heads, C, scale, probs};
+  hipStream_t s = (hipStream_t)stream;
+  if (hipError_t e = launch_attn_seq(dtype, p, s)) return hip_fail(e, "attn_spatial_probs");
+  if (hipError_t e = launch_cls_mean(dtype, (const float*)workspace, out, B, T, L, C, s)) return hip_fail(e, "cls_mean");
+  return 0;
+}
+
 int dsvt_attn_joint_fwd(int dtype, const void* qkv, void* out, int64_t nb, int64_t L, int64_t heads, int64_t head_dim,
                         float scale, void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_joint: bad dtype");

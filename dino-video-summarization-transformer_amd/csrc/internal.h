@@ -52,6 +52,7 @@ struct AttnParams {
   float* cls_aux;          // when non-null, position 0's output goes to cls_aux[(b*tin+t)*C + ...]
   int64_t nb, tin, L, tok_stride, seqlen, heads, C;
   float scale;
+  float* probs;            // optional: softmax probabilities [nb*tin][heads][seqlen][seqlen] (get_attn)
 };
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s);
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T,

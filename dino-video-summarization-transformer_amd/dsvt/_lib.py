@@ -31,6 +31,7 @@ SIGNATURES = {
     "dsvt_pos_bicubic_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _p]),
     "dsvt_attn_temporal_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_attn_spatial_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
+    "dsvt_attn_spatial_probs_fwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
     "dsvt_attn_joint_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_frame_mean_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
     "dsvt_cast_fwd": (_i32, [_i32, _p, _p, _i64, _p]),

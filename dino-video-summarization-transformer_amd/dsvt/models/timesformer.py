@@ -98,8 +98,10 @@ class Block(nn.Module):
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
 
     # -------------------------------------------------------------- HIP forward
-    def run(self, X, ctx):
-        """One block on the fp32 token tensor X (in place).  ctx: per-forward buffers."""
+    def run(self, X, ctx, probs=None):
+        """One block on the fp32 token tensor X (in place).  ctx: per-forward buffers.
+        probs (divided only): stop after the spatial softmax and write it there -- the
+        return_attn path of timesformer.py:155-157 (X is then left mid-block)."""
         w = ctx.w
         C, heads = ctx.C, self.attn.num_heads
         eps1, eps2 = self.norm1.eps, self.norm2.eps
@@ -122,6 +124,9 @@ class Block(nn.Module):
             # spatial with CLS replicate/mean (:139-181)
             ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, eps1, w(self.attn.qkv.weight),
                         self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            if probs is not None:
+                ops.attn_spatial_probs(ctx.qkv, ctx.o, probs, B, T, L, heads, self.attn.scale, ctx.cls_ws)
+                return
             ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
         else:
             nb, L = ctx.nb, ctx.L
@@ -277,8 +282,6 @@ class VisionTransformer(nn.Module):
         return self._forward_sources([(frames, frame_index, B)], B, T, H, W, Cin, get_all, False, out)
 
     def _forward_sources(self, srcs, B, T, H, W, Cin, get_all, get_attn, out):
-        if get_attn:
-            raise NotImplementedError("get_attn (attention-probability export) is not on the hot path yet")
         for src, _, _ in srcs:
             self._check_supported(src)
         mode = self.dsvt_dtype
@@ -319,6 +322,18 @@ class VisionTransformer(nn.Module):
                 ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
             nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
             ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+        if get_attn:            # timesformer.py:325-331: the last block's attention instead of features
+            for blk in self.blocks[:-1]:
+                blk.run(X, ctx)
+            if self.attention_type == 'divided_space_time':
+                heads = self.blocks[-1].attn.num_heads
+                probs = torch.empty(B * T, heads, 1 + Np, 1 + Np, device=dev, dtype=torch.float32)
+                self.blocks[-1].run(X, ctx, probs=probs)
+                return probs
+            # space-only / joint: the reference Block has no return_attn branch and returns its
+            # output tokens (un-normed)
+            self.blocks[-1].run(X, ctx)
+            return X.view(ctx.nb, ctx.L, C)
         for blk in self.blocks:
             blk.run(X, ctx)
         L = ctx.L

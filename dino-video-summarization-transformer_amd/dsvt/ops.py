@@ -111,6 +111,14 @@ def attn_spatial(qkv, out, B, T, L, heads, scale, ws):
     return out
 
 
+def attn_spatial_probs(qkv, out, probs, B, T, L, heads, scale, ws):
+    """attn_spatial that also writes the softmax probabilities [B*T, heads, 1+N, 1+N] fp32."""
+    _check(probs, torch.float32, "probs")
+    call("dsvt_attn_spatial_probs_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), _ptr(probs), B, T, L, heads, 64,
+         float(scale), _ptr(ws), ws.numel() * ws.element_size(), _stream())
+    return probs
+
+
 def attn_joint(qkv, out, nb, L, heads, scale):
     call("dsvt_attn_joint_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), nb, L, heads, 64, float(scale), _stream())
     return out

@@ -129,6 +129,13 @@ int dsvt_attn_temporal_fwd(int dtype, const void *qkv, void *out, int64_t nseq, 
 int dsvt_attn_spatial_fwd(int dtype, const void *qkv, void *out, int64_t B, int64_t T, int64_t L,
                           int64_t heads, int64_t head_dim, float scale, void *workspace,
                           int64_t workspace_bytes, void *stream);
+/* Same as dsvt_attn_spatial_fwd, and also writes the softmax probabilities of every frame
+ * sequence (CLS + N patches) to probs [B*T][heads][1+N][1+N] fp32 -- the last-block
+ * attention map of VisionTransformer.forward_features(get_attn=True), models/timesformer.py:
+ * 77-78, 155-157, 325-331.  bf16 mode: 1+N <= 256. */
+int dsvt_attn_spatial_probs_fwd(int dtype, const void *qkv, void *out, float *probs, int64_t B, int64_t T,
+                                int64_t L, int64_t heads, int64_t head_dim, float scale, void *workspace,
+                                int64_t workspace_bytes, void *stream);
 
 /* K10: plain (joint space-time / space-only / 2-D ViT) attention over each of nb
  * contiguous sequences of L rows (models/timesformer.py:120-123, vision_transformer.py:80-92). */

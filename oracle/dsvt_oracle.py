@@ -106,9 +106,10 @@ def resized_time_embed(temb, T):
     return temb[0][nearest_index(T, temb.shape[1])]
 
 
-def block_divided(x, sd, i, B, T, W, num_heads):
+def block_divided(x, sd, i, B, T, W, num_heads, return_attn=False):
     """Block.forward divided_space_time  models/timesformer.py:116-185 (drop_path = id, eval).
-    x [B, 1+N*T, C], token 1+n*T+t = patch n of frame t."""
+    x [B, 1+N*T, C], token 1+n*T+t = patch n of frame t.  return_attn (:155-157): the spatial
+    softmax [B*T, heads, 1+N, 1+N] of this block instead of its output."""
     p = "blocks.%d." % i
     _, L, C = x.shape
     N = (L - 1) // T
@@ -122,7 +123,9 @@ def block_divided(x, sd, i, B, T, W, num_heads):
     cls0 = x[:, :1]
     xs = xt.reshape(B, N, T, C).transpose(0, 2, 1, 3).reshape(B * T, N, C)
     xs = np.concatenate([np.repeat(cls0, T, axis=1).reshape(B * T, 1, C), xs], 1)
-    rs, _ = attention(layer_norm(xs, sd[p + "norm1.weight"], sd[p + "norm1.bias"]), sd, p + "attn", num_heads)
+    rs, attn = attention(layer_norm(xs, sd[p + "norm1.weight"], sd[p + "norm1.bias"]), sd, p + "attn", num_heads)
+    if return_attn:
+        return attn.astype(np.float32)
     # CLS: mean over frames (162-164); patches back to (h w t) order (172-175)
     cls = rs[:, 0].reshape(B, T, C).mean(1, keepdims=True)
     res = rs[:, 1:].reshape(B, T, N, C).transpose(0, 2, 1, 3).reshape(B, N * T, C)
@@ -156,18 +159,24 @@ def embed_tokens(sd, x, attention_type="divided_space_time"):
     return np.concatenate([np.broadcast_to(cls, (B, 1, C)), tok], 1).astype(np.float32), T, Wp
 
 
-def forward_features(sd, x, num_heads, attention_type="divided_space_time", get_all=False, depth=None):
+def forward_features(sd, x, num_heads, attention_type="divided_space_time", get_all=False, depth=None,
+                     get_attn=False):
     """VisionTransformer.forward_features  models/timesformer.py:285-345 (eval mode).
-    Returns the normed CLS [B, C] (or all tokens when get_all)."""
+    Returns the normed CLS [B, C] (or all tokens when get_all).  get_attn (:325-331): the last
+    block's spatial softmax (divided); for space-only / joint models the reference's Block has
+    no return_attn branch, so it is the last block's (un-normed) output tokens."""
     B = x.shape[0]
     h, T, W = embed_tokens(sd, x, attention_type)
     if depth is None:
         depth = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("blocks."))
     for i in range(depth):
+        last = get_attn and i == depth - 1
         if attention_type == "divided_space_time":
-            h = block_divided(h, sd, i, B, T, W, num_heads)
+            h = block_divided(h, sd, i, B, T, W, num_heads, return_attn=last)
         else:
             h = block_plain(h, sd, i, num_heads)
+        if last:
+            return h
     if attention_type == "space_only":                              # 338-340
         h = h.reshape(B, T, h.shape[1], h.shape[2]).mean(1)
     h = layer_norm(h, sd["norm.weight"], sd["norm.bias"])

@@ -92,7 +92,8 @@ def main():
     xl = P.clip(102, (2, 3, 4, 64, 64))
     xt3 = P.clip(103, (1, 3, 3, 112, 112))
     out["tiny_div"] = dict(cls_g=run(tiny, xg), all_g=run(tiny, xg, get_all=True),
-                           cls_l=run(tiny, xl), cls_t3=run(tiny, xt3))
+                           cls_l=run(tiny, xl), cls_t3=run(tiny, xt3),
+                           attn_g=run(tiny, xg, get_attn=True))     # last-block spatial softmax
     # block-level probe: tokens entering block 0 and leaving block 0
     cap = {}
     h0 = tiny.blocks[0].register_forward_hook(lambda mod, i, o: cap.update(inp=i[0].numpy().copy(), out=o.numpy().copy()))
@@ -107,13 +108,18 @@ def main():
     for name, shape, seed in [("cls_224", (1, 3, 8, 224, 224), 202), ("cls_96", (1, 3, 8, 96, 96), 203),
                               ("cls_t3", (1, 3, 3, 224, 224), 204), ("cls_t30", (1, 3, 30, 224, 224), 205)]:
         d[name] = run(base, P.clip(seed, shape))
+    d["attn_64"] = run(base, P.clip(206, (1, 3, 8, 64, 64)), get_attn=True)
     out["base_div"] = d
 
     # ---- 3. joint space-time + space-only variants (config 4 family, small shapes) ----
     joint = tsf_model(3, attention_type="joint_space_time")
-    out["base_joint"] = dict(cls_small=run(joint, P.clip(301, (1, 3, 4, 64, 64))))
+    # get_attn on a non-divided model: the reference's Block.forward has no return_attn branch
+    # for these types, so forward_features returns the LAST BLOCK'S OUTPUT tokens
+    out["base_joint"] = dict(cls_small=run(joint, P.clip(301, (1, 3, 4, 64, 64))),
+                             attn_small=run(joint, P.clip(301, (1, 3, 4, 64, 64)), get_attn=True))
     sonly = tsf_model(4, attention_type="space_only")
-    out["base_sonly"] = dict(cls_small=run(sonly, P.clip(401, (2, 3, 4, 64, 64))))
+    out["base_sonly"] = dict(cls_small=run(sonly, P.clip(401, (2, 3, 4, 64, 64))),
+                             attn_small=run(sonly, P.clip(401, (2, 3, 4, 64, 64)), get_attn=True))
 
     # ---- 4. 2-D ViT (vision_transformer.py vit_tiny), incl. bicubic pos interp ----
     v2 = ref_vit.vit_tiny(patch_size=16, img_size=[64])

@@ -112,6 +112,27 @@ def test_base_divided_unfolded_golden(base_sd, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
+def test_get_attn_golden(tiny_sd, base_sd, dtype, tol):
+    """forward_features(get_attn=True) (timesformer.py:325-331): last-block spatial softmax
+    [B*T, heads, 1+N, 1+N] for divided models; last-block tokens for joint / space-only."""
+    with torch.no_grad():
+        m = tsf(tiny_sd, dtype, embed_dim=192, num_heads=3, img_size=112, num_frames=4)
+        a = m.forward_features(cu(P.clip(101, (2, 3, 4, 112, 112))), get_attn=True)
+        assert tuple(a.shape) == (8, 3, 50, 50)
+        assert rel(a.cpu(), g("tiny_div")["attn_g"]) < tol
+        assert (a.sum(-1) - 1).abs().max().item() < 1e-3
+        m = tsf(base_sd, dtype)
+        assert rel(m.forward_features(cu(P.clip(206, (1, 3, 8, 64, 64))), get_attn=True).cpu(),
+                   g("base_div")["attn_64"]) < tol
+        mj = tsf(P.timesformer_state(3, attention_type="joint_space_time"), dtype, attention_type="joint_space_time")
+        assert rel(mj.forward_features(cu(P.clip(301, (1, 3, 4, 64, 64))), get_attn=True).cpu(),
+                   g("base_joint")["attn_small"]) < tol
+        ms = tsf(P.timesformer_state(4, attention_type="space_only"), dtype, attention_type="space_only")
+        assert rel(ms.forward_features(cu(P.clip(401, (2, 3, 4, 64, 64))), get_attn=True).cpu(),
+                   g("base_sonly")["attn_small"]) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
 def test_joint_and_space_only_golden(dtype, tol):
     with torch.no_grad():
         mj = tsf(P.timesformer_state(3, attention_type="joint_space_time"), dtype, attention_type="joint_space_time")

@@ -114,3 +114,21 @@ def test_e2e_cfg1(tiny_sd):
     loss, c = O.dino_loss(s_out, t_out, np.zeros((1, 4096), np.float32), 2, 0.04, global_crops=1)
     close(loss, f["loss"], 1e-5)
     close(c, f["center"], 1e-6)
+
+
+def test_oracle_get_attn_matches_reference():
+    """forward_features(get_attn=True): last-block spatial softmax (divided) and the last
+    block's output tokens (joint / space-only quirk), against the reference's own outputs."""
+    f = np.load(os.path.join(GOLDEN, "tiny_div.npz"))
+    sd = P.timesformer_state(1, embed_dim=192, num_heads=3, img_size=112, num_frames=4)
+    got = O.forward_features(sd, P.clip(101, (2, 3, 4, 112, 112)), 3, get_attn=True)
+    np.testing.assert_allclose(got, f["attn_g"], rtol=1e-4, atol=1e-5)
+    f = np.load(os.path.join(GOLDEN, "base_div.npz"))
+    got = O.forward_features(P.timesformer_state(2), P.clip(206, (1, 3, 8, 64, 64)), 12, get_attn=True)
+    np.testing.assert_allclose(got, f["attn_64"], rtol=1e-4, atol=1e-5)
+    for name, seed, att, shape in (("base_joint", 3, "joint_space_time", (1, 3, 4, 64, 64)),
+                                   ("base_sonly", 4, "space_only", (2, 3, 4, 64, 64))):
+        f = np.load(os.path.join(GOLDEN, name + ".npz"))
+        got = O.forward_features(P.timesformer_state(seed, attention_type=att), P.clip(301 if seed == 3 else 401, shape),
+                                 12, attention_type=att, get_attn=True)
+        np.testing.assert_allclose(got, f["attn_small"], rtol=1e-4, atol=1e-4)
