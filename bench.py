@@ -253,6 +253,8 @@ def main():
         dist.barrier()
     elapsed = ddist.max_over_ranks(time.perf_counter() - t0, device)
     loss_val = float(loss.item())
+    if not np.isfinite(loss_val):
+        raise SystemExit("bench: non-finite DINO loss %r -- the measured step is not valid" % loss_val)
 
     roofline = None
     if probe is not None:

@@ -152,6 +152,7 @@ __global__ __launch_bounds__(256) void attn_seq_bf16(AttnParams p) {
 
 #undef DSVT_LOAD_CHUNK
 #undef DSVT_STORE_CHUNK
+  mfma_result_fence();   // accumulators read below, after the loop exit branch
   // lane holds O[query q0 + r16][d = dt*16 + 4g + 0..3]
   const int64_t qo = q0 + r16;
   if (qo < p.seqlen) {
@@ -243,8 +244,10 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
 // every score of a query row in registers the softmax is exact two-pass (no rescaling).  Same
 // MFMA decomposition as attn_seq_bf16: S^T = K.Q^T (lane = one query, 4 keys per tile) and
 // O^T = V^T.P^T with the k-slot permutation and ds_read_b64_tr_b16 V^T fragments.
-template <int NKT, int NW>
-__global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(AttnParams p) {
+// DBG (diagnostic builds only): 1 = drain lgkmcnt before every P.V MFMA, 2 = V^T fragments by
+// scalar LDS reads instead of ds_read_b64_tr_b16.
+template <int NKT, int NW, int DBG = 0>
+__global__ __launch_bounds__(64 * NW, 2) void attn_short_bf16(AttnParams p) {
   constexpr int NKP = (NKT + 1) / 2;         // 32-key PV steps
   constexpr int SN = 2 * NKP;                // score tiles held (the last one of an odd NKT is 0)
   constexpr int LP = NKP * 32;               // LDS rows: whole PV steps
@@ -257,7 +260,6 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
   const int64_t C = p.C;
   const int L = (int)p.seqlen;
   const int nkt = (L + 15) >> 4;
-  const int rows = ((nkt + 1) >> 1) * 32;   // staged rows: whole 32-key PV steps
   const int nqt = nkt;
 
   // Issue EVERY global load up front (this wave's Q fragments for all its query tiles, and
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
 #pragma unroll
   for (int i = 0; i < PCS; ++i) {
     const int pc = tid + NT * i, r = pc >> 3, ch = pc & 7;
-    if (r < rows) {
+    if (r < LP) {
       *reinterpret_cast<uint4*>(&kv[0][r * KV_ROW + ch * 8]) = kq[i];
       *reinterpret_cast<uint4*>(&kv[1][r * KV_ROW + ch * 8]) = vq[i];
     }
@@ -307,24 +309,27 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
     const sv8 qf0 = qa[w], qf1 = qb[w];
     // scores: s[kt][j] = raw score(query qt*16 + r16, key kt*16 + 4g + j); the row max is taken
     // on raw scores (scale > 0) and the scale folded into the exponent: exp2(s*c - max*c)
+    // Every tile of the compile-time extent is computed (rows past the sequence are staged
+    // zeros; their scores are masked by a select): the score -> max -> exp -> P.V chain is
+    // straight-line code.  A runtime branch between an MFMA and the VALU reading its result
+    // made the ROCm 7.2 hazard recognizer under-insert wait states on the taken path (stale
+    // scores in the row max: ~1-ulp nondeterminism at 4 waves, NaN at 8).
     fv4 s[SN];
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+      const bf16_t* kr = Ks + (kt * 16 + r16) * KV_ROW + g * 8;
+      const sv8 k0 = *reinterpret_cast<const sv8*>(kr);
+      const sv8 k1 = *reinterpret_cast<const sv8*>(kr + 32);
+      fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < SN; ++kt) {
-      if (kt < nkt) {
-        const bf16_t* kr = Ks + (kt * 16 + r16) * KV_ROW + g * 8;
-        const sv8 k0 = *reinterpret_cast<const sv8*>(kr);
-        const sv8 k1 = *reinterpret_cast<const sv8*>(kr + 32);
-        fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
-        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
-        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
-        if (kt * 16 + 16 > L) {                      // the one partial key tile: mask
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (kt * 16 + 4 * g + j >= L) s[kt][j] = -INFINITY;
-        }
-        mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
-      }
+      for (int j = 0; j < 4; ++j) s[kt][j] = (kt * 16 + 4 * g + j < L) ? s[kt][j] : -INFINITY;
+      mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -332,15 +337,11 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < SN; ++kt) {
-      if (kt < nkt) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));   // args <= 0
-          s[kt][j] = e;
-          rs += e;
-        }
-      } else {
-        s[kt] = fv4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));   // args <= 0; masked -> 0
+        s[kt][j] = e;
+        rs += e;
       }
     }
     rs += __shfl_xor(rs, 16, 64);
@@ -351,7 +352,6 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
     for (int d = 0; d < 4; ++d) o[d] = fv4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kp = 0; kp < NKP; ++kp) {
-      if (2 * kp >= nkt) break;
       sv8 pb;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -363,14 +363,25 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int col = dt * 16 + 4 * (r16 & 3);
-        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) sv4*)(Vs + vr0 * KV_ROW + col));
-        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) sv4*)(Vs + vr1 * KV_ROW + col));
-        const sv8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        sv8 vf;
+        if constexpr (DBG == 2) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            vf[jj] = (short)Vs[(kp * 32 + 4 * g + jj) * KV_ROW + dt * 16 + r16];
+            vf[4 + jj] = (short)Vs[(kp * 32 + 16 + 4 * g + jj) * KV_ROW + dt * 16 + r16];
+          }
+        } else {
+          const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) sv4*)(Vs + vr0 * KV_ROW + col));
+          const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) sv4*)(Vs + vr1 * KV_ROW + col));
+          vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        if constexpr (DBG == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
       }
     }
+    mfma_result_fence();     // the stores below are under per-lane branches
     // lane holds O[query qt*16 + r16][d = dt*16 + 4g + 0..3]
     const int qo = qt * 16 + r16;
     if (p.probs && qo < L) {                 // get_attn: normalized probabilities, fp32
@@ -404,11 +415,21 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 4 : 2)) void attn_short_bf16(At
   }
 }
 
+static int g_attn_variant = 0;  // 0 = auto; otherwise forced (tools/attn_check.py, tests)
+void set_attn_variant(int v) { g_attn_variant = v; }
+
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
-  if (dtype == 0 && p.seqlen <= 256) {
+  const int v = g_attn_variant;
+  if (dtype == 0 && p.seqlen <= 256 && v != 4) {
     dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
-    if (p.seqlen <= 64) attn_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
-    else if (p.seqlen <= 208) attn_short_bf16<13, 8><<<grid, 512, 0, s>>>(p);   // 1 + 196 patches
+    // measured at 1 + 196 keys x 8 frames x 16 clips (tools/attn_bench.py): <13, 4> 60 us,
+    // <16, 4> 63 us, <13, 8> 66 us, streaming flash kernel 77 us
+    if (v == 1) attn_short_bf16<16, 4><<<grid, 256, 0, s>>>(p);
+    else if (v == 2 && p.seqlen <= 208) attn_short_bf16<13, 8><<<grid, 512, 0, s>>>(p);
+    else if (v == 5 && p.seqlen <= 208) attn_short_bf16<13, 4, 1><<<grid, 256, 0, s>>>(p);
+    else if (v == 6 && p.seqlen <= 208) attn_short_bf16<13, 4, 2><<<grid, 256, 0, s>>>(p);
+    else if (p.seqlen <= 64 && v == 0) attn_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
+    else if (p.seqlen <= 208) attn_short_bf16<13, 4><<<grid, 256, 0, s>>>(p);   // 1 + 196 patches
     else attn_short_bf16<16, 4><<<grid, 256, 0, s>>>(p);
     return hipGetLastError();
   }

@@ -357,6 +357,12 @@ int dsvt_set_gemm_variant(int variant) {
   return 0;
 }
 
+int dsvt_set_attn_variant(int variant) {
+  REQUIRE(variant >= 0 && variant <= 6, "attention variant must be 0-6");
+  set_attn_variant(variant);
+  return 0;
+}
+
 int dsvt_probe_enable(int mask, int capacity) {
   g_probe.clear();
   REQUIRE(capacity > 0 && capacity <= (1 << 20), "probe: bad capacity");

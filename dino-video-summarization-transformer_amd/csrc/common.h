@@ -95,6 +95,15 @@ __device__ __forceinline__ void load4(const float* p, float* v) {
   v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
 }
 
+// Wait states covering the longest MFMA result latency before code that reads accumulators
+// under control flow: the compiler's hazard recognizer has been seen to under-insert them on
+// a branch target right after an MFMA (attention.hip, attn_short_bf16).  s_nop n = n+1 states.
+__device__ __forceinline__ void mfma_result_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -219,6 +219,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   // compiler knows, so a load/add/store loop would pay one HBM round trip per fragment.
   // Full tiles (uniform per workgroup) take a branch-free path: no per-lane bounds branches,
   // so the compiler's vmcnt waits stay exact instead of draining after every store.
+  mfma_result_fence();   // acc is read under the branches below
   if (m0 + BM <= p.M && n0 + BN <= p.N) epilogue_128<T, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
   else epilogue_128<T, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
 }

@@ -318,6 +318,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_big_kernel(GemmParams p)
 #undef DSVT_READ
 #undef DSVT_ISSUE
 
+  mfma_result_fence();   // acc is read under the branches below
   // ---- epilogue.  Lane holds C[m = .. + r16][n = .. + 4g + 0..3] per (i, j) subtile.
   // Bias / GELU are applied on the way to LDS; the tile is staged through LDS in row chunks
   // (padded rows: conflict-free 8-/16-B writes), then written back as WHOLE rows with 16 B
@@ -524,6 +525,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
       DSVT_PROLOGUE();
     }
     // ---- direct epilogue of tile (cm0, cn0)
+    mfma_result_fence();
     epilogue_direct<MI, NJ, EPI, OUT_F32>(p, acc, cm0 + wm * WTM, cn0 + wn * WTN, r16, g);
     if (tn >= t_end) break;
     t = tn;

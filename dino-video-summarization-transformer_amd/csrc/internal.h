@@ -55,6 +55,7 @@ struct AttnParams {
   float* probs;            // optional: softmax probabilities [nb*tin][heads][seqlen][seqlen] (get_attn)
 };
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s);
+void set_attn_variant(int v);
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T,
                                 int64_t heads, int64_t C, float scale, hipStream_t s);
 

@@ -41,6 +41,7 @@ SIGNATURES = {
     "dsvt_dino_pair_loss_fwd": (_i32, [_p, _p, _p, _i64, _i64, _f32, _f32, _p, _p, _i64, _p]),
     "dsvt_center_ema": (_i32, [_p, _p, _i64, _f32, _f32, _p]),
     "dsvt_set_gemm_variant": (_i32, [_i32]),
+    "dsvt_set_attn_variant": (_i32, [_i32]),
     "dsvt_probe_enable": (_i32, [_i32, _i32]),
     "dsvt_probe_disable": (_i32, []),
     "dsvt_probe_read": (_i32, [_p, _p, _p, _p, _i32]),

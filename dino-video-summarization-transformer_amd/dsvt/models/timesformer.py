@@ -161,6 +161,8 @@ class _Ctx:
 class VisionTransformer(nn.Module):
     """models/timesformer.py:212-364."""
 
+    takes_clip_lists = True     # forward_features accepts a list of clip tensors (MultiCropWrapper)
+
     def __init__(self, img_size=224, patch_size=16, in_chans=3, num_classes=1000, embed_dim=768, depth=12,
                  num_heads=12, mlp_ratio=4., qkv_bias=False, qk_scale=None, drop_rate=0., attn_drop_rate=0.,
                  drop_path_rate=0.1, hybrid_backbone=None, norm_layer=nn.LayerNorm, num_frames=8,
@@ -232,6 +234,25 @@ class VisionTransformer(nn.Module):
         self.head = nn.Linear(self.embed_dim, num_classes) if num_classes > 0 else nn.Identity()
 
     # -------------------------------------------------------------- helpers
+    def prepare_weights(self):
+        """Make every storage-dtype weight copy (and the folded temporal proj/fc) current on the
+        CURRENT stream, before a caller forks backbone calls onto side streams."""
+        if not self.pos_embed.is_cuda:
+            return
+        mode = self.dsvt_dtype
+        w = self._wcache.getter(mode)
+        w(self.patch_embed.proj.weight, flat=True)
+        for blk in self.blocks:
+            lins = [blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2]
+            if blk.attention_type == 'divided_space_time':
+                lins += [blk.temporal_attn.qkv]
+                if self.fold_temporal_fc:
+                    self._wcache.folded(mode, blk.temporal_fc, blk.temporal_attn.proj)
+                else:
+                    lins += [blk.temporal_attn.proj, blk.temporal_fc]
+            for lin in lins:
+                w(lin.weight)
+
     def _indices(self, Hp, Wp, T, device):
         key = (Hp, Wp, T, device)
         if key not in self._index_cache:

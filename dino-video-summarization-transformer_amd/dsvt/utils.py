@@ -41,11 +41,22 @@ def run_concurrent(thunks, device, slot0=0):
     return results
 
 
+def prepare_weights(module):
+    """Call prepare_weights() on every dsvt sub-module (storage-dtype weight copies produced
+    on the current stream before work forks onto side streams)."""
+    for m in module.modules():
+        fn = getattr(m, "prepare_weights", None)
+        if callable(fn):
+            fn()
+
+
 def dino_forward(student, teacher, images, n_global=2, concurrent=True):
     """train_ssl.py:523-527: teacher on the `n_global` global views, student on all views.
     The two networks are independent, so their backbone calls run concurrently."""
     if not concurrent:
         return student(images), teacher(images[:n_global])
+    for net in (student, teacher):
+        prepare_weights(net)
     s_out, t_out = run_concurrent([lambda: student(images), lambda: teacher(images[:n_global])],
                                   images[0].device, slot0=8)
     return s_out, t_out
@@ -92,10 +103,15 @@ class MultiCropWrapper(nn.Module):
             row += n
             start = end
 
+        list_input = getattr(self.backbone, "takes_clip_lists", False)
+
         def job(group, out):
-            return lambda: self.backbone.forward_features(group, out=out, **kwargs)
+            if list_input:   # dsvt TimeSformer: the group's clips go in as a list (no cat copy)
+                return lambda: self.backbone.forward_features(group, out=out, **kwargs)
+            return lambda: out.copy_(self.backbone(torch.cat(group), **kwargs))   # utils.py:601
         thunks = [job(g, o) for g, o in jobs]
         if self.concurrent_groups and len(thunks) > 1 and feats.is_cuda:
+            prepare_weights(self.backbone)            # weight copies made before the fork
             run_concurrent(thunks, feats.device)      # the resolution groups are independent
         else:
             for fn in thunks:

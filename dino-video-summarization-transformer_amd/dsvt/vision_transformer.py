@@ -91,6 +91,16 @@ class VisionTransformer(nn.Module):
             self._pos_cache[key] = tab
         return tab, idx
 
+    def prepare_weights(self):
+        """Storage-dtype weight copies made current on the current stream (see weights.py)."""
+        if not self.pos_embed.is_cuda:
+            return
+        w = self._wcache.getter(self.dsvt_dtype)
+        w(self.patch_embed.proj.weight, flat=True)
+        for blk in self.blocks:
+            for lin in (blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2):
+                w(lin.weight)
+
     def _run(self, x, keep_last=0):
         if not x.is_cuda or not self.pos_embed.is_cuda:
             raise DsvtError("dsvt runs only on the GPU (no CPU fallback)")
@@ -199,6 +209,15 @@ class DINOHead(nn.Module):
             trunc_normal_(m.weight, std=.02)
             if m.bias is not None:
                 nn.init.constant_(m.bias, 0)
+
+    def prepare_weights(self):
+        """Storage-dtype copies of the MLP weights made current on the current stream."""
+        if not self.last_layer.weight_v.is_cuda:
+            return
+        w = self._wcache.getter(self.dsvt_dtype)
+        for m in ([self.mlp] if isinstance(self.mlp, nn.Linear) else self.mlp):
+            if isinstance(m, nn.Linear):
+                w(m.weight)
 
     def forward(self, x):
         """x [R, in_dim] fp32 -> logits [R, out_dim] fp32 (GELU MLP, L2 normalize, weight-normed

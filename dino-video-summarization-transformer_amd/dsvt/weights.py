@@ -3,15 +3,48 @@
 bf16 mode: each weight is cast ONCE by the dsvt cast kernel and cached until the parameter
 changes (tracked by its autograd version counter + storage pointer, so optimizer steps,
 EMA updates, load_state_dict and .to() all invalidate it).  fp32 mode: the parameter
-itself (no copy)."""
+itself (no copy).
+
+Stream safety: a cached copy is produced on whatever stream was current at the cache miss.
+Every entry records an event after its producer; the first use from any OTHER stream waits on
+that event (once per stream).  Callers that fan work out over side streams (MultiCropWrapper,
+dino_forward) additionally call `prepare()` on the launching stream first, so all copies exist
+before the side streams fork from it."""
 import torch
 
 from . import ops
+from ._lib import DsvtError
 
 
 class WeightCache:
     def __init__(self):
         self._c = {}
+
+    @staticmethod
+    def _sync(ent):
+        """Order the current stream after the entry's producer (no-op on the producing stream)."""
+        ev, waited = ent[-2], ent[-1]
+        if ev is None:
+            return
+        sid = torch.cuda.current_stream().cuda_stream
+        if sid in waited:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            # cross-capture waits are illegal; a copy made before the capture must be finished
+            if not ev.query():
+                raise DsvtError("weight cache entry still in flight at HIP-graph capture: run one eager "
+                                "forward (and synchronize) before capturing")
+        else:
+            torch.cuda.current_stream().wait_event(ev)
+        waited.add(sid)
+
+    @staticmethod
+    def _event():
+        if torch.cuda.is_current_stream_capturing():
+            return None, set()
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev, {torch.cuda.current_stream().cuda_stream}
 
     def getter(self, mode):
         def get(p, flat=False):
@@ -25,10 +58,11 @@ class WeightCache:
             key = (id(p), flat)
             ent = self._c.get(key)
             if ent is not None and ent[0] == p._version and ent[1] == p.data_ptr():
+                self._sync(ent)
                 return ent[2]
             out = torch.empty(t.shape, device=t.device, dtype=mode)
             ops.cast(t.contiguous(), out)
-            self._c[key] = (p._version, p.data_ptr(), out)
+            self._c[key] = (p._version, p.data_ptr(), out) + self._event()
             return out
         return get
 
@@ -42,6 +76,7 @@ class WeightCache:
         key = ("fold", id(outer), id(inner), mode)
         ent = self._c.get(key)
         if ent is not None and ent[0] == stamp:
+            self._sync(ent)
             return ent[1]
         wo, bo, wi, bi = (p.detach().float().contiguous() for p in params)
         dev = wo.device
@@ -56,7 +91,7 @@ class WeightCache:
         else:
             w = torch.empty(w32.shape, device=dev, dtype=mode)
             ops.cast(w32, w)
-        self._c[key] = (stamp, (w, b32))
+        self._c[key] = (stamp, (w, b32)) + self._event()
         return w, b32
 
     def clear(self):

@@ -178,6 +178,11 @@ int dsvt_center_ema(float *center, const float *colsum, int64_t D, float momentu
 /* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
  * 1 = 128x128 / 4-wave kernel, 2 = 256x256 / 8-wave, 3 = 256x128 / 8-wave.  Process-global. */
 int dsvt_set_gemm_variant(int variant);
+/* Tuning knob (benchmarking / tests only): bf16 short-sequence attention kernel. 0 = automatic,
+ * 1 = 16-key-tile x 4 waves, 2 = 13 x 8 waves, 3 = 13 x 4 waves, 4 = streaming flash kernel
+ * (5, 6: diagnostic builds of 3).
+ * Process-global. */
+int dsvt_set_attn_variant(int variant);
 
 /* Measurement probe: when enabled, every launch of a family in `mask` is bracketed by a
  * pair of hipEvents on its own stream (diagnostic; not thread-safe). */

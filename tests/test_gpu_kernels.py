@@ -188,6 +188,35 @@ def test_attn_spatial_cls_mean(dtype, B, T, N, heads):
     check(back(out), spatial_ref(back(Q), B, T, L, heads, 0.125), dtype, "spatial")
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_attn_spatial_variants_repeatable(variant):
+    """Every bf16 short-sequence kernel at a multi-clip global shape (B=4, 8x196 patches, 12 heads,
+    N(0,1) q/k/v): finite, within tolerance of the float64 reference, and bitwise identical over
+    repeated launches.  (Before the score/P.V chain was made branch-free, the compiler left too
+    few wait states between an MFMA and the VALU reading it on one branch path: ~1-ulp
+    nondeterminism with 4 waves, NaN with 8, while single-clip shapes passed.)"""
+    from dsvt import _lib, ops
+    from dsvt._lib import WS_ATTN_SPATIAL
+    B, T, N, heads = 4, 8, 196, 12
+    C, L = heads * 64, 1 + N * T
+    Q = to(rnd((B * L, 3 * C), 21, 1.0), torch.bfloat16)
+    ws = torch.empty(ops.workspace_bytes(WS_ATTN_SPATIAL, torch.bfloat16, B * T, C, 0) // 4, device=dev())
+    _lib.call("dsvt_set_attn_variant", variant)
+    try:
+        outs = []
+        for _ in range(3):
+            out = torch.full((B * L, C), 7.0, device=dev(), dtype=torch.bfloat16)
+            ops.attn_spatial(Q, out, B, T, L, heads, 0.125, ws)
+            outs.append(out)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("dsvt_set_attn_variant", 0)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "repeat launches differ"
+    ref = spatial_ref(back(Q)[:2 * L], 2, T, L, heads, 0.125)     # first 2 clips vs float64
+    check(back(outs[0])[:2 * L], ref, torch.bfloat16, "spatial variant %d" % variant)
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("nb,L,heads", [(2, 5, 3), (1, 16, 2), (1, 17, 2), (1, 64, 2), (1, 65, 12), (2, 197, 3),
                                         (1, 208, 2), (1, 209, 2), (1, 256, 2), (1, 257, 2), (1, 300, 2),

@@ -254,3 +254,18 @@ def test_bf16_vs_fp32_full_size(base_sd):
     with torch.no_grad():
         c = tsf(base_sd, torch.float32)(x[2:3]).cpu()
     assert rel(c, a[2:3]) < 1e-5
+
+
+def test_bench_shape_repeatable_and_finite(base_sd):
+    """The bench's global group (16 clips x 8x224^2, bf16): repeated forwards are bitwise
+    identical and finite, and the per-clip result does not depend on the batch it rides in
+    (the multi-clip grids are where a kernel hazard once showed up)."""
+    x = cu(P.clip(43, (16, 3, 8, 224, 224)))
+    m = tsf(base_sd, torch.bfloat16)
+    with torch.no_grad():
+        outs = [m(x) for _ in range(3)]
+        one = m(x[5:6])
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
+    assert rel(one.cpu(), outs[0][5:6].cpu()) < BF16_TOL

@@ -109,6 +109,7 @@ def test_multicrop_grouping():
 
     class FakeBackbone(nn.Module):
         embed_dim = 4
+        takes_clip_lists = True
 
         def __init__(self):
             super().__init__()

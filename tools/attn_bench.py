@@ -1,6 +1,6 @@
 """Spatial-attention micro-benchmark on the bench's global shape (B=16 clips, T=8, N=196,
 12 heads) and local shape (B=48, T=8, N=36): average launch time of ops.attn_spatial.
-usage: python tools/attn_bench.py [reps]"""
+usage: python tools/attn_bench.py [reps [variant ...]]"""
 import os
 import sys
 
@@ -54,6 +54,13 @@ def run_joint(nb, L, heads, reps):
 
 if __name__ == "__main__":
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    from dsvt import _lib
+    for v in [int(a) for a in sys.argv[2:]]:     # forced short-attention variants (dsvt_set_attn_variant)
+        _lib.call("dsvt_set_attn_variant", v)
+        print("variant", v)
+        run(16, 8, 196, 12, reps)
+        run(48, 8, 36, 12, reps)
+    _lib.call("dsvt_set_attn_variant", 0)
     run(16, 8, 196, 12, reps)
     run(48, 8, 36, 12, reps)
     run_joint(128, 197, 12, reps)
