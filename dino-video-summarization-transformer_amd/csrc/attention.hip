@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void attn_seq_bf16(AttnParams p) {
   // lane holds O[query q0 + r16][d = dt*16 + 4g + 0..3]
   const int64_t qo = q0 + r16;
   if (qo < p.seqlen) {
-    const float inv = 1.0f / l;
+    const float inv = (p.seq_scale ? p.seq_scale[seq] : 1.0f) / l;
     if (qo == 0 && p.cls_aux) {
       float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
 #pragma unroll
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
     }
   }
   if (qi < p.seqlen) {
-    const float inv = 1.0f / l;
+    const float inv = (p.seq_scale ? p.seq_scale[seq] : 1.0f) / l;
     float* dst = (qi == 0 && p.cls_aux) ? p.cls_aux + seq * C + h * 64
                                         : (float*)p.out + tok_row(p, b, t, qi) * p.ld_out + h * 64;
 #pragma unroll
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_short_bf16(AttnParams p) {
       }
     }
     if (qo < L) {
-      const float inv = 1.0f / rs;
+      const float inv = (p.seq_scale ? p.seq_scale[seq] : 1.0f) / rs;
       if (qo == 0 && p.cls_aux) {
         float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
 #pragma unroll

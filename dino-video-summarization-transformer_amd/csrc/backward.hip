@@ -1,0 +1,768 @@
+// Backward kernels of the DINO-SVT student: what autograd
+// runs for loss.backward() at train_ssl.py:538/545 through the divided block
+// (models/timesformer.py:116-185), the DINO head (vision_transformer.py:278-282) and the
+// DINO loss (train_ssl.py:653-669).  The weight-gradient GEMMs (dW = dY^T . X) are plain
+// library GEMMs (hipBLASLt via torch); everything else of the backward is here or in the
+// dsvt GEMM with its backward epilogues (gemm.hip / gemm_big.hip: DGELU).
+//
+//   ln_bwd_kernel          LayerNorm input gradient, ADDED into the fp32 residual gradient dX
+//                          through a row map (the residual branch of every pre-LN sub-layer),
+//                          plus per-block dgamma / dbeta partial sums (deterministic: no atomics)
+//   colsum_partial_kernel  bias gradients (column sums) through a row map, per-block partials
+//   reduce_partials_kernel fixed-order sum of the partials (optionally accumulated into .grad)
+//   attn_temporal_bwd      per (patch, head) sequence of T frames, LDS-resident, VALU
+//   attn_rows_bwd /        generic (spatial-with-CLS / joint) attention backward, two passes:
+//   attn_cols_bwd            per query (lse, D = sum P dP, dQ), then per key (dK, dV); VALU,
+//                            K/V/Q/dO read through L2 -- parity mode and the fallback
+//   cls_sum_kernel         the CLS row is shared by the T frame sequences: its dq/dk/dv are the
+//                          sum over frames (timesformer.py:140-146 repeat -> gradient sum)
+//   dino_loss_bwd_kernel   d loss / d student logits
+//   l2norm_bwd / weightnorm_bwd   F.normalize and the weight-normed last layer
+//   cast_rows / cast_transpose    layout helpers (row-mapped gather-cast, W^T in storage dtype)
+//   embed_grad kernels     dpos / dtime / dcls sums of the token gradient
+//   ema / sumsq / scale    multi-tensor teacher EMA (train_ssl.py:555-558) and per-tensor
+//                          gradient norm clipping (utils/utils.py:102-111)
+#include <math.h>
+
+#include "common.h"
+
+namespace dsvt {
+
+// ================================================================ LayerNorm backward
+// x: fp32 rows through the row map (the saved residual stream), dy: compact rows [rows, C]
+// (storage dtype or fp32), dx: fp32 with x's layout (the residual gradient) -- dx[row] += dLN.
+// One wave per row (grid-stride), lane owns columns c = i*64 + lane; dgamma / dbeta are
+// accumulated in registers, reduced over the 4 waves in LDS and written per block.
+template <typename DyT>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
+                                                     const float* __restrict__ gamma, float* __restrict__ dx,
+                                                     int64_t rows, int C, int64_t rpg, int64_t gstride, int64_t goff,
+                                                     float eps, float* __restrict__ partial) {
+  __shared__ float red[4][2][1024];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = C >> 6;
+  float dg[16], db[16], g[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    dg[i] = 0.f; db[i] = 0.f;
+    g[i] = i < n ? gamma[i * 64 + lane] : 0.f;
+  }
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
+    const int64_t xr = map_row(r, rpg, gstride, goff) * C;
+    float v[16], d[16];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) {
+        v[i] = x[xr + i * 64 + lane];
+        d[i] = Elem<DyT>::to_f(dy[r * C + i * 64 + lane]);
+        s += v[i];
+      }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) { v[i] -= mean; q += v[i] * v[i]; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) {
+        const float xh = v[i] * rstd, gd = g[i] * d[i];
+        v[i] = xh;
+        s1 += gd;
+        s2 += gd * xh;
+        dg[i] += d[i] * xh;
+        db[i] += d[i];
+      }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < n) dx[xr + i * 64 + lane] += rstd * (g[i] * d[i] - s1 - v[i] * s2);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < n) { red[wave][0][i * 64 + lane] = dg[i]; red[wave][1][i * 64 + lane] = db[i]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    partial[(int64_t)blockIdx.x * 2 * C + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    partial[(int64_t)blockIdx.x * 2 * C + C + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+  }
+}
+
+int ln_bwd_blocks(int64_t rows) {
+  int64_t b = (rows + 31) / 32;   // >= 8 rows per wave
+  return (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
+}
+
+hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
+                         int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* partial,
+                         hipStream_t s) {
+  const int nb = ln_bwd_blocks(rows);
+  if (dy_dtype == 0)
+    ln_bwd_kernel<bf16_t><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, (int)C, rpg, gstride, goff, eps,
+                                             partial);
+  else
+    ln_bwd_kernel<float><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, (int)C, rpg, gstride, goff, eps,
+                                            partial);
+  return hipGetLastError();
+}
+
+// ================================================================ column sums (bias grads)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ y, int64_t rows, int64_t C,
+                                                             int64_t ld, int64_t rpg, int64_t gstride, int64_t goff,
+                                                             const float* __restrict__ row_scale, int64_t chunk,
+                                                             float* __restrict__ partial) {
+  const int64_t r0 = (int64_t)blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a0 = 0.f, a1 = 0.f;
+  int64_t r = r0;
+  for (; r + 1 < r1; r += 2) {
+    float v0 = Elem<T>::to_f(y[map_row(r, rpg, gstride, goff) * ld + c]);
+    float v1 = Elem<T>::to_f(y[map_row(r + 1, rpg, gstride, goff) * ld + c]);
+    if (row_scale) { v0 *= row_scale[r]; v1 *= row_scale[r + 1]; }
+    a0 += v0;
+    a1 += v1;
+  }
+  if (r < r1) a0 += Elem<T>::to_f(y[map_row(r, rpg, gstride, goff) * ld + c]) * (row_scale ? row_scale[r] : 1.0f);
+  partial[(int64_t)blockIdx.y * C + c] = a0 + a1;
+}
+
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ partial, int64_t nparts,
+                                                              int64_t width, int64_t stride, float* __restrict__ out,
+                                                              int accumulate) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= width) return;
+  float a = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) a += partial[p * stride + c];
+  out[c] = accumulate ? out[c] + a : a;
+}
+
+int64_t colsum_parts(int64_t rows) {
+  int64_t p = (rows + 127) / 128;
+  return p < 1 ? 1 : (p > 256 ? 256 : p);
+}
+
+hipError_t launch_colsum_rows(int dtype, const void* y, int64_t rows, int64_t C, int64_t ld, int64_t rpg,
+                              int64_t gstride, int64_t goff, const float* row_scale, float* partial, float* out,
+                              int accumulate, hipStream_t s) {
+  const int64_t parts = colsum_parts(rows), chunk = (rows + parts - 1) / parts;
+  dim3 grid((unsigned)((C + 255) / 256), (unsigned)parts);
+  if (dtype == 0)
+    colsum_partial_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)y, rows, C, ld, rpg, gstride, goff, row_scale,
+                                                       chunk, partial);
+  else
+    colsum_partial_kernel<float><<<grid, 256, 0, s>>>((const float*)y, rows, C, ld, rpg, gstride, goff, row_scale,
+                                                      chunk, partial);
+  if (hipError_t e = hipGetLastError()) return e;
+  reduce_partials_kernel<<<(unsigned)((C + 255) / 256), 256, 0, s>>>(partial, parts, C, C, out, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_partials(const float* partial, int64_t nparts, int64_t width, int64_t stride, float* out,
+                                  int accumulate, hipStream_t s) {
+  reduce_partials_kernel<<<(unsigned)((width + 255) / 256), 256, 0, s>>>(partial, nparts, width, stride, out,
+                                                                         accumulate);
+  return hipGetLastError();
+}
+
+// ================================================================ temporal attention backward
+// grid (nseq, ceil(heads/G)); LDS per head: q, k, v, dO [T][64] fp32 and P, dS [T][T].
+// Phase 1, item (head hh, query i), 16 lanes x 4 dims: scores, softmax, dP = dO_i.v_j,
+// D_i = sum_j P dP, dS = P (dP - D), dq_i = scale sum_j dS_ij k_j.  Phase 2, item (hh, key j):
+// dk_j = scale sum_i dS_ij q_i, dv_j = sum_i P_ij dO_i.
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_temporal_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                                T* __restrict__ dqkv, int Tf, int heads, int G,
+                                                                int64_t C, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char dyn_smem[];
+  float* sm = reinterpret_cast<float*>(dyn_smem);
+  const int tid = threadIdx.x;
+  const int64_t sq = blockIdx.x;
+  const int h0 = blockIdx.y * G;
+  const int gh = (heads - h0) < G ? (heads - h0) : G;
+  const int per_head = 4 * Tf * 64 + 2 * Tf * Tf;
+  // stage q, k, v, dO of the group's heads as fp32
+  for (int e = tid; e < gh * Tf * 64 * 4; e += 256) {
+    const int d = e & 63, rest = e >> 6;
+    const int which = rest % 4, tt = (rest / 4) % Tf, hh = rest / (4 * Tf);
+    const int64_t row = sq * Tf + tt;
+    const int64_t col = (int64_t)(h0 + hh) * 64 + d;
+    const float v = which < 3 ? Elem<T>::to_f(qkv[row * 3 * C + which * C + col]) : Elem<T>::to_f(dout[row * C + col]);
+    sm[hh * per_head + (which * Tf + tt) * 64 + d] = v;
+  }
+  __syncthreads();
+  const int sub = tid & 15, d0 = sub * 4;
+  for (int it = tid >> 4; it < gh * Tf; it += 16) {
+    const int hh = it % gh, i = it / gh;
+    float* H = sm + hh * per_head;
+    const float* q = H + i * 64 + d0;
+    const float* dO = H + (3 * Tf + i) * 64 + d0;
+    float* P = H + 4 * Tf * 64;
+    float* dS = P + Tf * Tf;
+    float m = -INFINITY;
+    for (int j = 0; j < Tf; ++j) {
+      const float* k = H + (Tf + j) * 64 + d0;
+      const float s = sum16(q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3]) * scale;
+      if (sub == 0) P[i * Tf + j] = s;
+      m = fmaxf(m, s);
+    }
+    __builtin_amdgcn_wave_barrier();
+    float l = 0.f;
+    for (int j = 0; j < Tf; ++j) l += expf(P[i * Tf + j] - m);
+    const float inv = 1.0f / l;
+    float D = 0.f;
+    for (int j = 0; j < Tf; ++j) {
+      const float* v = H + (2 * Tf + j) * 64 + d0;
+      const float dp = sum16(dO[0] * v[0] + dO[1] * v[1] + dO[2] * v[2] + dO[3] * v[3]);
+      const float p = expf(P[i * Tf + j] - m) * inv;
+      D += p * dp;
+      if (sub == 0) dS[i * Tf + j] = dp;
+    }
+    __builtin_amdgcn_wave_barrier();
+    float dq[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < Tf; ++j) {
+      const float p = expf(P[i * Tf + j] - m) * inv;
+      const float ds = p * (dS[i * Tf + j] - D);
+      const float* k = H + (Tf + j) * 64 + d0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dq[e] = fmaf(ds, k[e], dq[e]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (sub == 0)
+      for (int j = 0; j < Tf; ++j) {
+        const float p = expf(P[i * Tf + j] - m) * inv;
+        dS[i * Tf + j] = p * (dS[i * Tf + j] - D);
+        P[i * Tf + j] = p;
+      }
+    store4(dqkv + (sq * Tf + i) * 3 * C + (int64_t)(h0 + hh) * 64 + d0, dq[0] * scale, dq[1] * scale, dq[2] * scale,
+           dq[3] * scale);
+  }
+  __syncthreads();
+  for (int it = tid >> 4; it < gh * Tf; it += 16) {
+    const int hh = it % gh, j = it / gh;
+    const float* H = sm + hh * per_head;
+    const float* P = H + 4 * Tf * 64;
+    const float* dS = P + Tf * Tf;
+    float dk[4] = {0.f, 0.f, 0.f, 0.f}, dv[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < Tf; ++i) {
+      const float* q = H + i * 64 + d0;
+      const float* dO = H + (3 * Tf + i) * 64 + d0;
+      const float ds = dS[i * Tf + j], p = P[i * Tf + j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { dk[e] = fmaf(ds, q[e], dk[e]); dv[e] = fmaf(p, dO[e], dv[e]); }
+    }
+    T* o = dqkv + (sq * Tf + j) * 3 * C + (int64_t)(h0 + hh) * 64 + d0;
+    store4(o + C, dk[0] * scale, dk[1] * scale, dk[2] * scale, dk[3] * scale);
+    store4(o + 2 * C, dv[0], dv[1], dv[2], dv[3]);
+  }
+}
+
+hipError_t launch_attn_temporal_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nseq, int64_t T,
+                                    int64_t heads, int64_t C, float scale, hipStream_t s) {
+  const int64_t per_head = (4 * T * 64 + 2 * T * T) * 4;
+  int64_t G = (48 * 1024) / per_head;
+  if (G < 1) G = 1;
+  if (G > heads) G = heads;
+  dim3 grid((unsigned)nseq, (unsigned)((heads + G - 1) / G));
+  const size_t smem = (size_t)(per_head * G);
+  if (dtype == 0)
+    attn_temporal_bwd_kernel<bf16_t><<<grid, 256, smem, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, (bf16_t*)dqkv,
+                                                            (int)T, (int)heads, (int)G, C, scale);
+  else
+    attn_temporal_bwd_kernel<float><<<grid, 256, smem, s>>>((const float*)qkv, (const float*)dout, (float*)dqkv,
+                                                           (int)T, (int)heads, (int)G, C, scale);
+  return hipGetLastError();
+}
+
+// ================================================================ generic attention backward
+// Sequence (b, t) position i -> token row b*L + (i == 0 ? 0 : 1 + (i-1)*tok_stride + t)
+// (spatial: CLS + every T-th patch row; joint / 2-D: tok_stride = 1, tin = 1, contiguous).
+__device__ __forceinline__ int64_t brow(const AttnBwdParams& p, int64_t b, int64_t t, int64_t i) {
+  return b * p.L + (i == 0 ? 0 : 1 + (i - 1) * p.tok_stride + t);
+}
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float* v) { load4(p, v); }
+
+// pass 1: 16 lanes per (seq, head, query): lse, D = sum_j P_ij dP_ij, dq
+template <typename T>
+__global__ __launch_bounds__(256) void attn_rows_bwd(AttnBwdParams p) {
+  const int64_t item = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15, d0 = sub * 4;
+  const int64_t total = p.nb * p.tin * p.heads * p.seqlen;
+  if (item >= total) return;
+  const int64_t i = item % p.seqlen;
+  const int h = (int)((item / p.seqlen) % p.heads);
+  const int64_t seq = item / (p.seqlen * p.heads), b = seq / p.tin, t = seq % p.tin;
+  const T* qkv = (const T*)p.qkv;
+  const T* dout = (const T*)p.dout;
+  const int64_t C = p.C;
+  float q[4], dO[4];
+  ld4(qkv + brow(p, b, t, i) * p.ld_qkv + h * 64 + d0, q);
+  ld4(dout + brow(p, b, t, i) * p.ld_dout + h * 64 + d0, dO);
+  {
+    const float sc = (i == 0 && p.cls_aux ? p.cls_scale : 1.0f) * (p.seq_scale ? p.seq_scale[seq] : 1.0f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dO[e] *= sc;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int64_t j = 0; j < p.seqlen; ++j) {
+    float k[4];
+    ld4(qkv + brow(p, b, t, j) * p.ld_qkv + C + h * 64 + d0, k);
+    const float s = sum16(q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3]) * p.scale;
+    const float mn = fmaxf(m, s);
+    l = l * expf(m - mn) + expf(s - mn);
+    m = mn;
+  }
+  const float lse = m + logf(l);
+  float D = 0.f;
+  for (int64_t j = 0; j < p.seqlen; ++j) {
+    float k[4], v[4];
+    const T* r = qkv + brow(p, b, t, j) * p.ld_qkv + h * 64 + d0;
+    ld4(r + C, k);
+    ld4(r + 2 * C, v);
+    const float s = sum16(q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3]) * p.scale;
+    const float dp = sum16(dO[0] * v[0] + dO[1] * v[1] + dO[2] * v[2] + dO[3] * v[3]);
+    D += expf(s - lse) * dp;
+  }
+  float dq[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t j = 0; j < p.seqlen; ++j) {
+    float k[4], v[4];
+    const T* r = qkv + brow(p, b, t, j) * p.ld_qkv + h * 64 + d0;
+    ld4(r + C, k);
+    ld4(r + 2 * C, v);
+    const float s = sum16(q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3]) * p.scale;
+    const float dp = sum16(dO[0] * v[0] + dO[1] * v[1] + dO[2] * v[2] + dO[3] * v[3]);
+    const float ds = expf(s - lse) * (dp - D);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dq[e] = fmaf(ds, k[e], dq[e]);
+  }
+  if (sub == 0) {
+    p.stats[2 * item] = lse;
+    p.stats[2 * item + 1] = D;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dq[e] *= p.scale;
+  if (i == 0 && p.cls_aux)
+    store4(p.cls_aux + seq * 3 * C + h * 64 + d0, dq[0], dq[1], dq[2], dq[3]);
+  else
+    store4((T*)p.dqkv + brow(p, b, t, i) * p.ld_dqkv + h * 64 + d0, dq[0], dq[1], dq[2], dq[3]);
+}
+
+// pass 2: 16 lanes per (seq, head, key): dk, dv
+template <typename T>
+__global__ __launch_bounds__(256) void attn_cols_bwd(AttnBwdParams p) {
+  const int64_t item = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15, d0 = sub * 4;
+  const int64_t total = p.nb * p.tin * p.heads * p.seqlen;
+  if (item >= total) return;
+  const int64_t j = item % p.seqlen;
+  const int h = (int)((item / p.seqlen) % p.heads);
+  const int64_t seq = item / (p.seqlen * p.heads), b = seq / p.tin, t = seq % p.tin;
+  const T* qkv = (const T*)p.qkv;
+  const T* dout = (const T*)p.dout;
+  const int64_t C = p.C;
+  float k[4], v[4];
+  const T* kr = qkv + brow(p, b, t, j) * p.ld_qkv + h * 64 + d0;
+  ld4(kr + C, k);
+  ld4(kr + 2 * C, v);
+  const float* st = p.stats + 2 * (seq * p.heads + h) * p.seqlen;
+  float dk[4] = {0.f, 0.f, 0.f, 0.f}, dv[4] = {0.f, 0.f, 0.f, 0.f};
+  const float ssc = p.seq_scale ? p.seq_scale[seq] : 1.0f;
+  for (int64_t i = 0; i < p.seqlen; ++i) {
+    float q[4], dO[4];
+    ld4(qkv + brow(p, b, t, i) * p.ld_qkv + h * 64 + d0, q);
+    ld4(dout + brow(p, b, t, i) * p.ld_dout + h * 64 + d0, dO);
+    {
+      const float sc = (i == 0 && p.cls_aux ? p.cls_scale : 1.0f) * ssc;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dO[e] *= sc;
+    }
+    const float s = sum16(q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3]) * p.scale;
+    const float dp = sum16(dO[0] * v[0] + dO[1] * v[1] + dO[2] * v[2] + dO[3] * v[3]);
+    const float P = expf(s - st[2 * i]);
+    const float ds = P * (dp - st[2 * i + 1]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { dk[e] = fmaf(ds, q[e], dk[e]); dv[e] = fmaf(P, dO[e], dv[e]); }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dk[e] *= p.scale;
+  if (j == 0 && p.cls_aux) {
+    float* o = p.cls_aux + seq * 3 * C + h * 64 + d0;
+    store4(o + C, dk[0], dk[1], dk[2], dk[3]);
+    store4(o + 2 * C, dv[0], dv[1], dv[2], dv[3]);
+  } else {
+    T* o = (T*)p.dqkv + brow(p, b, t, j) * p.ld_dqkv + h * 64 + d0;
+    store4(o + C, dk[0], dk[1], dk[2], dk[3]);
+    store4(o + 2 * C, dv[0], dv[1], dv[2], dv[3]);
+  }
+}
+
+// dqkv[b*L][:] = sum_t cls_aux[b*tin + t][:]   (3C wide)
+template <typename T>
+__global__ __launch_bounds__(256) void cls_sum_kernel(const float* __restrict__ aux, T* __restrict__ dqkv, int tin,
+                                                      int64_t L, int64_t width, int64_t ld) {
+  const int64_t b = blockIdx.y;
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= width) return;
+  float a = 0.f;
+  for (int t = 0; t < tin; ++t) a += aux[(b * tin + t) * width + c];
+  dqkv[b * L * ld + c] = Elem<T>::from_f(a);
+}
+
+hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s) {
+  const int64_t items = p.nb * p.tin * p.heads * p.seqlen;
+  const unsigned blocks = (unsigned)((items * 16 + 255) / 256);
+  if (dtype == 0) {
+    attn_rows_bwd<bf16_t><<<blocks, 256, 0, s>>>(p);
+    attn_cols_bwd<bf16_t><<<blocks, 256, 0, s>>>(p);
+  } else {
+    attn_rows_bwd<float><<<blocks, 256, 0, s>>>(p);
+    attn_cols_bwd<float><<<blocks, 256, 0, s>>>(p);
+  }
+  if (hipError_t e = hipGetLastError()) return e;
+  if (p.cls_aux) {
+    dim3 grid((unsigned)((3 * p.C + 255) / 256), (unsigned)p.nb);
+    if (dtype == 0)
+      cls_sum_kernel<bf16_t><<<grid, 256, 0, s>>>(p.cls_aux, (bf16_t*)p.dqkv, (int)p.tin, p.L, 3 * p.C, p.ld_dqkv);
+    else
+      cls_sum_kernel<float><<<grid, 256, 0, s>>>(p.cls_aux, (float*)p.dqkv, (int)p.tin, p.L, 3 * p.C, p.ld_dqkv);
+  }
+  return hipGetLastError();
+}
+
+// ================================================================ DINO loss backward
+// d loss / d s[v*B + b][j] = coef * (n_v * softmax(s/ts)[j] - sum_{iq != v, iq < gc} q_iq[b][j])
+// with q = softmax((t - center)/tt) (teacher, detached), coef = dloss / (npairs * B * ts),
+// n_v = #global crops other than v (train_ssl.py:653-669).  One block per student row; the row
+// statistics (max, sum of exp) are passed in (softmax_stats_kernel of the forward).
+__global__ __launch_bounds__(256) void dino_loss_bwd_kernel(const float* __restrict__ student,
+                                                            const float* __restrict__ teacher,
+                                                            const float* __restrict__ center, int64_t B, int64_t gc,
+                                                            int64_t D, float inv_ts, float inv_tt,
+                                                            const float* __restrict__ t_m, const float* __restrict__ t_z,
+                                                            const float* __restrict__ s_m, const float* __restrict__ s_z,
+                                                            const float* __restrict__ dloss, float coef,
+                                                            float* __restrict__ grad) {
+  const int64_t row = blockIdx.x;           // student row v*B + b
+  const int64_t v = row / B, b = row % B;
+  const float g = coef * dloss[0];
+  const float sm = s_m[row], sz = 1.0f / s_z[row];
+  int nv = 0;
+  for (int64_t iq = 0; iq < gc; ++iq) nv += (iq != v);
+  for (int64_t j = (int64_t)threadIdx.x * 4; j < D; j += 1024) {
+    const float4 sv = *reinterpret_cast<const float4*>(student + row * D + j);
+    const float4 cv = center ? *reinterpret_cast<const float4*>(center + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float a[4] = {nv * expf(sv.x * inv_ts - sm) * sz, nv * expf(sv.y * inv_ts - sm) * sz,
+                  nv * expf(sv.z * inv_ts - sm) * sz, nv * expf(sv.w * inv_ts - sm) * sz};
+    for (int64_t iq = 0; iq < gc; ++iq) {
+      if (iq == v) continue;
+      const int64_t tr = iq * B + b;
+      const float4 tv = *reinterpret_cast<const float4*>(teacher + tr * D + j);
+      const float tm = t_m[tr], tz = 1.0f / t_z[tr];
+      a[0] -= expf((tv.x - cv.x) * inv_tt - tm) * tz;
+      a[1] -= expf((tv.y - cv.y) * inv_tt - tm) * tz;
+      a[2] -= expf((tv.z - cv.z) * inv_tt - tm) * tz;
+      a[3] -= expf((tv.w - cv.w) * inv_tt - tm) * tz;
+    }
+    *reinterpret_cast<float4*>(grad + row * D + j) = make_float4(g * a[0], g * a[1], g * a[2], g * a[3]);
+  }
+}
+
+hipError_t launch_dino_loss_bwd(const float* student, const float* teacher, const float* center, int64_t B,
+                                int64_t ncrops, int64_t gc, int64_t D, float inv_ts, float inv_tt, const float* t_m,
+                                const float* t_z, const float* s_m, const float* s_z, const float* dloss, float coef,
+                                float* grad, hipStream_t s) {
+  dino_loss_bwd_kernel<<<(unsigned)(ncrops * B), 256, 0, s>>>(student, teacher, center, B, gc, D, inv_ts, inv_tt, t_m,
+                                                              t_z, s_m, s_z, dloss, coef, grad);
+  return hipGetLastError();
+}
+
+// ================================================================ F.normalize / weight-norm backward
+// z = x / max(||x||, eps):  dx = (dz - z (z.dz)) / ||x||   (||x|| > eps),  dz / eps otherwise
+__global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+                                                         float* __restrict__ dx, int64_t rows, int D, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* xr = x + r * D;
+  const float* gr = dz + r * D;
+  float ss = 0.f, xd = 0.f;
+  for (int c = lane; c < D; c += 64) { ss += xr[c] * xr[c]; xd += xr[c] * gr[c]; }
+  ss = wave_sum(ss);
+  xd = wave_sum(xd);
+  const float nrm = sqrtf(ss);
+  if (nrm > eps) {
+    const float inv = 1.0f / nrm, k = xd * inv * inv * inv;
+    for (int c = lane; c < D; c += 64) dx[r * D + c] = gr[c] * inv - xr[c] * k;
+  } else {
+    for (int c = lane; c < D; c += 64) dx[r * D + c] = gr[c] / eps;
+  }
+}
+
+// w = g v / ||v|| per row: dv = (g/||v||)(dW - w_hat (w_hat.dW)), dg = w_hat.dW (accumulated)
+__global__ __launch_bounds__(256) void weightnorm_bwd_kernel(const float* __restrict__ v, const float* __restrict__ g,
+                                                             const float* __restrict__ dw, float* __restrict__ dv,
+                                                             float* __restrict__ dg, int64_t rows, int D,
+                                                             int accumulate) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* vr = v + r * D;
+  const float* gr = dw + r * D;
+  float ss = 0.f, vd = 0.f;
+  for (int c = lane; c < D; c += 64) { ss += vr[c] * vr[c]; vd += vr[c] * gr[c]; }
+  ss = wave_sum(ss);
+  vd = wave_sum(vd);
+  const float nrm = sqrtf(ss), inv = 1.0f / nrm;
+  const float gg = g[r], dot = vd * inv;   // w_hat . dW
+  for (int c = lane; c < D; c += 64) {
+    const float val = gg * inv * (gr[c] - vr[c] * inv * dot);
+    dv[r * D + c] = accumulate ? dv[r * D + c] + val : val;
+  }
+  if (dg && lane == 0) dg[r] = accumulate ? dg[r] + dot : dot;
+}
+
+hipError_t launch_l2norm_bwd(const float* x, const float* dz, float* dx, int64_t rows, int64_t D, float eps,
+                             hipStream_t s) {
+  l2norm_bwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, dz, dx, rows, (int)D, eps);
+  return hipGetLastError();
+}
+
+hipError_t launch_weightnorm_bwd(const float* v, const float* g, const float* dw, float* dv, float* dg, int64_t rows,
+                                 int64_t D, int accumulate, hipStream_t s) {
+  weightnorm_bwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(v, g, dw, dv, dg, rows, (int)D, accumulate);
+  return hipGetLastError();
+}
+
+// ================================================================ layout helpers
+// y[m] = cast(x[row(m)]) for compact rows m < rows (C % 4 == 0)
+// y[m] = cast(x[row(m)] * row_scale[m / group]) (row_scale nullable)
+template <typename OutT>
+__global__ __launch_bounds__(256) void cast_rows_kernel(const float* __restrict__ x, OutT* __restrict__ y,
+                                                        int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
+                                                        int64_t goff, const float* __restrict__ row_scale,
+                                                        int64_t group) {
+  const int64_t c4 = C / 4, total = rows * c4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / c4, c = (i % c4) * 4;
+    const float4 f = *reinterpret_cast<const float4*>(x + map_row(m, rpg, gstride, goff) * C + c);
+    const float sc = row_scale ? row_scale[m / group] : 1.0f;
+    store4(y + m * C + c, f.x * sc, f.y * sc, f.z * sc, f.w * sc);
+  }
+}
+
+static unsigned grid_for(int64_t work) {
+  int64_t blocks = (work + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
+hipError_t launch_cast_rows(int dtype, const float* x, void* y, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
+                            int64_t goff, const float* row_scale, int64_t group, hipStream_t s) {
+  const unsigned blocks = grid_for(rows * C / 4);
+  if (dtype == 0)
+    cast_rows_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, (bf16_t*)y, rows, C, rpg, gstride, goff, row_scale, group);
+  else
+    cast_rows_kernel<float><<<blocks, 256, 0, s>>>(x, (float*)y, rows, C, rpg, gstride, goff, row_scale, group);
+  return hipGetLastError();
+}
+
+// in place: y[m][c] *= row_scale[m / group]  (DropPath of a compact branch activation)
+template <typename T>
+__global__ __launch_bounds__(256) void row_scale_kernel(T* __restrict__ y, int64_t rows, int64_t C, int64_t ld,
+                                                        const float* __restrict__ row_scale, int64_t group) {
+  const int64_t c4 = C / 4, total = rows * c4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / c4, c = (i % c4) * 4;
+    float v[4];
+    load4(y + m * ld + c, v);
+    const float sc = row_scale[m / group];
+    store4(y + m * ld + c, v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
+  }
+}
+
+hipError_t launch_row_scale(int dtype, void* y, int64_t rows, int64_t C, int64_t ld, const float* row_scale,
+                            int64_t group, hipStream_t s) {
+  const unsigned blocks = grid_for(rows * C / 4);
+  if (dtype == 0) row_scale_kernel<bf16_t><<<blocks, 256, 0, s>>>((bf16_t*)y, rows, C, ld, row_scale, group);
+  else row_scale_kernel<float><<<blocks, 256, 0, s>>>((float*)y, rows, C, ld, row_scale, group);
+  return hipGetLastError();
+}
+
+// X[m][c] += row_scale[m] * bias[c]  (the DropPath-scaled bias of a residual branch)
+__global__ __launch_bounds__(256) void rowscale_bias_kernel(float* __restrict__ X, int64_t rows, int64_t C,
+                                                            const float* __restrict__ row_scale,
+                                                            const float* __restrict__ bias) {
+  const int64_t c4 = C / 4, total = rows * c4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / c4, c = (i % c4) * 4;
+    const float sc = row_scale[m];
+    float4 x = *reinterpret_cast<float4*>(X + m * C + c);
+    const float4 b = *reinterpret_cast<const float4*>(bias + c);
+    x.x += sc * b.x; x.y += sc * b.y; x.z += sc * b.z; x.w += sc * b.w;
+    *reinterpret_cast<float4*>(X + m * C + c) = x;
+  }
+}
+
+hipError_t launch_rowscale_bias_add(float* X, int64_t rows, int64_t C, const float* row_scale, const float* bias,
+                                    hipStream_t s) {
+  rowscale_bias_kernel<<<grid_for(rows * C / 4), 256, 0, s>>>(X, rows, C, row_scale, bias);
+  return hipGetLastError();
+}
+
+// y[c][r] = cast(x[r][c]), x [R, C] fp32: 64x64 tiles through LDS (coalesced both ways)
+template <typename OutT>
+__global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ x, OutT* __restrict__ y,
+                                                             int64_t R, int64_t C) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? x[r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) y[c * R + r] = Elem<OutT>::from_f(tile[tx][i]);
+  }
+}
+
+hipError_t launch_cast_transpose(int dtype, const float* x, void* y, int64_t R, int64_t C, hipStream_t s) {
+  dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+  if (dtype == 0) cast_transpose_kernel<bf16_t><<<grid, 256, 0, s>>>(x, (bf16_t*)y, R, C);
+  else cast_transpose_kernel<float><<<grid, 256, 0, s>>>(x, (float*)y, R, C);
+  return hipGetLastError();
+}
+
+// ================================================================ token-embedding gradients
+// Token gradient dX [B, L = 1 + Np*T, C] (NT order).  gn[n][c] = sum_{b,t} dX[b][1 + n*T + t][c],
+// gt[t][c] = sum_{b,n} dX[b][1 + n*T + t][c], gc[c] = sum_b dX[b][0][c].
+__global__ __launch_bounds__(256) void embed_sums_kernel(const float* __restrict__ dX, int64_t B, int64_t Np,
+                                                         int64_t T, int64_t C, float* __restrict__ gn,
+                                                         float* __restrict__ gt, float* __restrict__ gcls) {
+  const int64_t L = 1 + Np * T;
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int64_t which = blockIdx.y;      // 0..Np-1 -> gn, Np..Np+T-1 -> gt, Np+T -> cls
+  float a = 0.f;
+  if (which < Np) {
+    for (int64_t b = 0; b < B; ++b)
+      for (int64_t t = 0; t < T; ++t) a += dX[(b * L + 1 + which * T + t) * C + c];
+    gn[which * C + c] = a;
+  } else if (which < Np + T) {
+    const int64_t t = which - Np;
+    for (int64_t b = 0; b < B; ++b)
+      for (int64_t n = 0; n < Np; ++n) a += dX[(b * L + 1 + n * T + t) * C + c];
+    gt[t * C + c] = a;
+  } else {
+    for (int64_t b = 0; b < B; ++b) a += dX[b * L * C + c];
+    gcls[c] = a;
+  }
+}
+
+// out[dst[i]][c] += src[i][c] for i < n (sequential over i: duplicates in dst are summed
+// deterministically) -- the nearest-resize index maps of pos_embed / time_embed
+__global__ __launch_bounds__(256) void index_accum_kernel(const float* __restrict__ src, const int32_t* __restrict__ dst,
+                                                          int64_t n, int64_t C, int64_t dst_off,
+                                                          float* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  for (int64_t i = 0; i < n; ++i) out[((int64_t)dst[i] + dst_off) * C + c] += src[i * C + c];
+}
+
+hipError_t launch_embed_grads(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C, float* gn, float* gt,
+                              float* gcls, hipStream_t s) {
+  dim3 grid((unsigned)((C + 255) / 256), (unsigned)(Np + T + 1));
+  embed_sums_kernel<<<grid, 256, 0, s>>>(dX, B, Np, T, C, gn, gt, gcls);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_accum(const float* src, const int32_t* dst, int64_t n, int64_t C, int64_t dst_off, float* out,
+                              hipStream_t s) {
+  index_accum_kernel<<<(unsigned)((C + 255) / 256), 256, 0, s>>>(src, dst, n, C, dst_off, out);
+  return hipGetLastError();
+}
+
+// ================================================================ multi-tensor EMA / grad clipping
+// Tensor list: ptrs[i] (fp32), sizes[i]; work items are (tensor, 4096-element chunk) pairs
+// listed in chunk_tensor / chunk_start (built once on the host per parameter list).
+__global__ __launch_bounds__(256) void ema_kernel(float* const* __restrict__ teacher, const float* const* __restrict__ student,
+                                                  const int64_t* __restrict__ sizes, const int32_t* __restrict__ ctensor,
+                                                  const int64_t* __restrict__ cstart, float m) {
+  const int ti = ctensor[blockIdx.x];
+  const int64_t s0 = cstart[blockIdx.x], n = sizes[ti];
+  float* t = teacher[ti];
+  const float* q = student[ti];
+  for (int64_t i = s0 + threadIdx.x; i < s0 + 4096 && i < n; i += 256) t[i] = t[i] * m + (1.0f - m) * q[i];
+}
+
+// per-chunk sum of squares of grads -> partial[chunk]
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* const* __restrict__ x, const int64_t* __restrict__ sizes,
+                                                    const int32_t* __restrict__ ctensor, const int64_t* __restrict__ cstart,
+                                                    float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int ti = ctensor[blockIdx.x];
+  const int64_t s0 = cstart[blockIdx.x], n = sizes[ti];
+  const float* p = x[ti];
+  float a = 0.f;
+  for (int64_t i = s0 + threadIdx.x; i < s0 + 4096 && i < n; i += 256) a += p[i] * p[i];
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// norms[i] = sqrt(sum of the tensor's chunk partials) (chunks of one tensor are contiguous)
+__global__ void chunk_norms_kernel(const float* __restrict__ partial, const int32_t* __restrict__ first_chunk,
+                                   int ntensors, float* __restrict__ norms) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ntensors) return;
+  float a = 0.f;
+  for (int c = first_chunk[i]; c < first_chunk[i + 1]; ++c) a += partial[c];
+  norms[i] = sqrtf(a);
+}
+
+// utils/utils.py:102-111: clip_coef = clip / (norm + 1e-6); grad *= clip_coef if < 1
+__global__ __launch_bounds__(256) void clip_scale_kernel(float* const* __restrict__ x, const int64_t* __restrict__ sizes,
+                                                         const int32_t* __restrict__ ctensor,
+                                                         const int64_t* __restrict__ cstart,
+                                                         const float* __restrict__ norms, float clip) {
+  const int ti = ctensor[blockIdx.x];
+  const float coef = clip / (norms[ti] + 1e-6f);
+  if (coef >= 1.0f) return;
+  const int64_t s0 = cstart[blockIdx.x], n = sizes[ti];
+  float* p = x[ti];
+  for (int64_t i = s0 + threadIdx.x; i < s0 + 4096 && i < n; i += 256) p[i] *= coef;
+}
+
+hipError_t launch_ema(float* const* teacher, const float* const* student, const int64_t* sizes, const int32_t* ctensor,
+                      const int64_t* cstart, int64_t nchunks, float m, hipStream_t s) {
+  ema_kernel<<<(unsigned)nchunks, 256, 0, s>>>(teacher, student, sizes, ctensor, cstart, m);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_grads(float* const* grads, const int64_t* sizes, const int32_t* ctensor, const int64_t* cstart,
+                             const int32_t* first_chunk, int64_t nchunks, int64_t ntensors, float clip, float* partial,
+                             float* norms, hipStream_t s) {
+  sumsq_kernel<<<(unsigned)nchunks, 256, 0, s>>>(grads, sizes, ctensor, cstart, partial);
+  chunk_norms_kernel<<<(unsigned)((ntensors + 255) / 256), 256, 0, s>>>(partial, first_chunk, (int)ntensors, norms);
+  if (clip > 0.f) clip_scale_kernel<<<(unsigned)nchunks, 256, 0, s>>>(grads, sizes, ctensor, cstart, norms, clip);
+  return hipGetLastError();
+}
+
+}  // namespace dsvt

@@ -84,7 +84,7 @@ void norm_map(int64_t& rpg, int64_t& gstride, int64_t& goff) {
 int check_gemm(int dtype, int epi, const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                const void* out, int64_t ldo, int64_t M, int64_t N, int64_t K) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "gemm: bad dtype %d", dtype);
-  REQUIRE(epi >= 0 && epi <= 3, "gemm: bad epilogue %d", epi);
+  REQUIRE(epi >= 0 && epi <= 5, "gemm: bad epilogue %d", epi);
   REQUIRE(A && W && out, "gemm: null pointer");
   REQUIRE(M > 0 && N > 0 && K > 0, "gemm: empty problem M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
   REQUIRE((K * esize(dtype)) % 128 == 0, "gemm: K=%lld must be a multiple of %d", (long long)K, dtype == DSVT_BF16 ? 64 : 32);
@@ -116,6 +116,10 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
       return up((2 * rt + 2 * rs + np) * 4);
     }
     case DSVT_WS_PAIR_LOSS: return up(4 * M * 4);
+    case DSVT_WS_LN_BWD: return up((int64_t)ln_bwd_blocks(M) * 2 * K * 4);          // M = rows, K = C
+    case DSVT_WS_COLSUM: return up(colsum_parts(M) * N * 4);                        // M = rows, N = C
+    case DSVT_WS_ATTN_BWD: return up(M * 3 * N * 4 + M * (N / 64) * K * 2 * 4);     // M = nb*tin, N = C, K = seqlen
+    case DSVT_WS_EMBED_BWD: return up((M + N + 1) * K * 4);                         // M = Np, N = T, K = C
     default: return -1;
   }
 }
@@ -124,7 +128,8 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t l
                   const float* bias, void* out, int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg,
                   int64_t gstride, int64_t goff, void* stream) {
   if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
-  REQUIRE(epilogue != 3, "gemm: the patch epilogue is reachable only through dsvt_patch_embed_fwd");
+  REQUIRE(epilogue <= 2, "gemm: epilogue %d is reachable only through dsvt_patch_embed_fwd / dsvt_gemm_aux_fwd",
+          epilogue);
   norm_map(rpg, gstride, goff);
   GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
@@ -230,6 +235,26 @@ int dsvt_attn_spatial_fwd(int dtype, const void* qkv, void* out, int64_t B, int6
   hipStream_t s = (hipStream_t)stream;
   const double flops = 4.0 * B * T * heads * (double)p.seqlen * p.seqlen * 64;
   int rc = probed(DSVT_PROBE_ATTN_SPATIAL, flops, s, "dsvt_attn_spatial_fwd", [&] { return launch_attn_seq(dtype, p, s); });
+  if (rc) return rc;
+  if (hipError_t e = launch_cls_mean(dtype, (const float*)workspace, out, B, T, L, C, s)) return hip_fail(e, "cls_mean");
+  return 0;
+}
+
+int dsvt_attn_spatial_scaled_fwd(int dtype, const void* qkv, void* out, const float* seq_scale, int64_t B, int64_t T,
+                                 int64_t L, int64_t heads, int64_t head_dim, float scale, void* workspace,
+                                 int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial_scaled: bad dtype");
+  REQUIRE(qkv && out && seq_scale && aligned16(qkv) && aligned16(out), "attn_spatial_scaled: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_spatial_scaled: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_scaled: need (L-1) %% T == 0");
+  const int64_t C = heads * 64;
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_SPATIAL, dtype, B * T, C, 0),
+          "attn_spatial_scaled: workspace too small");
+  AttnParams p{qkv, 3 * C, out, C, (float*)workspace, B, T, L, T, 1 + (L - 1) / T, heads, C, scale, nullptr, seq_scale};
+  hipStream_t s = (hipStream_t)stream;
+  const double flops = 4.0 * B * T * heads * (double)p.seqlen * p.seqlen * 64;
+  int rc = probed(DSVT_PROBE_ATTN_SPATIAL, flops, s, "dsvt_attn_spatial_scaled_fwd",
+                  [&] { return launch_attn_seq(dtype, p, s); });
   if (rc) return rc;
   if (hipError_t e = launch_cls_mean(dtype, (const float*)workspace, out, B, T, L, C, s)) return hip_fail(e, "cls_mean");
   return 0;
@@ -401,6 +426,212 @@ int dsvt_probe_read(float* ms, double* work, int32_t* family, int32_t* tag, int 
   }
   g_probe.count = 0;
   return n;
+}
+
+// ================================================================ backward / training (backward.hip)
+int dsvt_gemm_aux_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, const void* W, int64_t ldw,
+                      const float* bias, void* out, int64_t ldo, void* aux, int64_t ld_aux, int64_t M, int64_t N,
+                      int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void* stream) {
+  if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
+  REQUIRE(epilogue == DSVT_EPI_GELU_SAVE || epilogue == DSVT_EPI_DGELU, "gemm_aux: epilogue must be GELU_SAVE/DGELU");
+  REQUIRE(aux && ld_aux >= N && ld_aux % 4 == 0 && ((uintptr_t)aux & 7) == 0, "gemm_aux: bad aux operand");
+  REQUIRE(epilogue != DSVT_EPI_GELU_SAVE || !out_f32, "gemm_aux: GELU_SAVE writes the storage dtype");
+  norm_map(rpg, gstride, goff);
+  GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1,
+               aux, ld_aux};
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_aux_fwd",
+                [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
+                gemm_tag(p, dtype, epilogue, out_f32));
+}
+
+int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
+                       int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* dgamma, float* dbeta,
+                       int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(dy_dtype == DSVT_BF16 || dy_dtype == DSVT_F32, "layernorm_bwd: bad dy dtype");
+  REQUIRE(x && dy && gamma && dx && dgamma && dbeta, "layernorm_bwd: null pointer");
+  REQUIRE(rows > 0 && C % 64 == 0 && C > 0 && C <= 1024, "layernorm_bwd: need 0 < C <= 1024, C %% 64 == 0");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, 1, rows, 0, C),
+          "layernorm_bwd: workspace too small");
+  norm_map(rpg, gstride, goff);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const int nb = ln_bwd_blocks(rows);
+  return probed(DSVT_PROBE_NORM, (double)rows * C * (12 + esize(dy_dtype)), s, "dsvt_layernorm_bwd",
+                [&]() -> hipError_t {
+                  hipError_t e;
+                  if ((e = launch_ln_bwd(dy_dtype, x, dy, gamma, dx, rows, C, rpg, gstride, goff, eps, part, s)))
+                    return e;
+                  if ((e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s))) return e;
+                  return launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
+                });
+}
+
+int dsvt_colsum_bwd(int dtype, const void* y, int64_t rows, int64_t C, int64_t ld, int64_t rpg, int64_t gstride,
+                    int64_t goff, const float* row_scale, float* out, int accumulate, void* workspace,
+                    int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "colsum: bad dtype");
+  REQUIRE(y && out && rows > 0 && C > 0 && ld >= C, "colsum: bad args");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_COLSUM, 1, rows, C, 0), "colsum: workspace too small");
+  norm_map(rpg, gstride, goff);
+  hipError_t e = launch_colsum_rows(dtype, y, rows, C, ld, rpg, gstride, goff, row_scale, (float*)workspace, out,
+                                    accumulate, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "colsum");
+}
+
+int dsvt_attn_temporal_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nseq, int64_t T,
+                           int64_t heads, int64_t head_dim, float scale, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_temporal_bwd: bad dtype");
+  REQUIRE(qkv && dout && dqkv && aligned16(qkv) && aligned16(dout) && aligned16(dqkv), "attn_temporal_bwd: bad pointer");
+  REQUIRE(head_dim == 64 && nseq > 0 && T >= 1 && T <= 64 && heads >= 1, "attn_temporal_bwd: bad shape");
+  const double flops = 10.0 * nseq * heads * T * T * 64;
+  return probed(DSVT_PROBE_ATTN_TEMPORAL, flops, (hipStream_t)stream, "dsvt_attn_temporal_bwd", [&] {
+    return launch_attn_temporal_bwd(dtype, qkv, dout, dqkv, nseq, T, heads, heads * 64, scale, (hipStream_t)stream);
+  });
+}
+
+static int attn_bwd_common(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nb, int64_t tin,
+                           int64_t L, int64_t tok_stride, int64_t seqlen, int64_t heads, float scale, bool cls,
+                           const float* seq_scale, void* workspace, int64_t workspace_bytes, void* stream,
+                           const char* name) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "%s: bad dtype", name);
+  REQUIRE(qkv && dout && dqkv && aligned16(qkv) && aligned16(dout) && aligned16(dqkv), "%s: bad pointer", name);
+  const int64_t C = heads * 64;
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_BWD, dtype, nb * tin, C, seqlen),
+          "%s: workspace too small", name);
+  float* ws = (float*)workspace;
+  AttnBwdParams p{qkv, 3 * C, dout, C, dqkv, 3 * C, cls ? ws : nullptr, ws + (cls ? nb * tin * 3 * C : 0),
+                  nb, tin, L, tok_stride, seqlen, heads, C, scale, 1.0f / (float)tin, seq_scale};
+  const double flops = 10.0 * nb * tin * heads * (double)seqlen * seqlen * 64;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, name,
+                [&] { return launch_attn_bwd_generic(dtype, p, (hipStream_t)stream); });
+}
+
+int dsvt_attn_spatial_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, const float* seq_scale,
+                          int64_t B, int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(head_dim == 64, "attn_spatial_bwd: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_bwd: need (L-1) %% T == 0");
+  return attn_bwd_common(dtype, qkv, dout, dqkv, B, T, L, T, 1 + (L - 1) / T, heads, scale, true, seq_scale,
+                         workspace, workspace_bytes, stream, "dsvt_attn_spatial_bwd");
+}
+
+int dsvt_attn_joint_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nb, int64_t L, int64_t heads,
+                        int64_t head_dim, float scale, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(head_dim == 64 && nb > 0 && L > 0, "attn_joint_bwd: bad shape");
+  return attn_bwd_common(dtype, qkv, dout, dqkv, nb, 1, L, 1, L, heads, scale, false, nullptr, workspace,
+                         workspace_bytes, stream, "dsvt_attn_joint_bwd");
+}
+
+int dsvt_dino_loss_bwd(const float* student, const float* teacher, const float* center, int64_t B, int64_t ncrops,
+                       int64_t global_crops, int64_t D, float student_temp, float teacher_temp, const float* dloss,
+                       float* dstudent, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(student && teacher && center && dloss && dstudent, "dino_loss_bwd: null pointer");
+  REQUIRE(aligned16(student) && aligned16(teacher) && aligned16(center) && aligned16(dstudent),
+          "dino_loss_bwd: pointers must be 16-byte aligned");
+  REQUIRE(B > 0 && D > 0 && D % 4 == 0 && global_crops >= 1 && ncrops >= global_crops && ncrops >= 2,
+          "dino_loss_bwd: bad shape");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_DINO_LOSS, 1, B, ncrops, global_crops),
+          "dino_loss_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rt = global_crops * B, rs = ncrops * B;
+  float* ws = (float*)workspace;
+  float *t_m = ws, *t_z = ws + rt, *s_m = ws + 2 * rt, *s_z = ws + 2 * rt + rs;
+  const double n_terms = (double)global_crops * (ncrops - 1);
+  const float coef = (float)(1.0 / (n_terms * B * student_temp));
+  return probed(DSVT_PROBE_LOSS, 4.0 * D * (rs * 2 + rt), s, "dsvt_dino_loss_bwd", [&]() -> hipError_t {
+    hipError_t e;
+    if ((e = launch_softmax_stats(teacher, center, 1.0f / teacher_temp, rt, D, t_m, t_z, s))) return e;
+    if ((e = launch_softmax_stats(student, nullptr, 1.0f / student_temp, rs, D, s_m, s_z, s))) return e;
+    return launch_dino_loss_bwd(student, teacher, center, B, ncrops, global_crops, D, 1.0f / student_temp,
+                                1.0f / teacher_temp, t_m, t_z, s_m, s_z, dloss, coef, dstudent, s);
+  });
+}
+
+int dsvt_dino_head_norm_bwd(const float* x, const float* dz, float* dx, int64_t rows, int64_t D, float eps,
+                            void* stream) {
+  REQUIRE(x && dz && dx && rows > 0 && D > 0, "head_norm_bwd: bad args");
+  hipError_t e = launch_l2norm_bwd(x, dz, dx, rows, D, eps, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "head_norm_bwd");
+}
+
+int dsvt_weight_norm_bwd(const float* v, const float* g, const float* dw, float* dv, float* dg, int64_t rows, int64_t D,
+                         int accumulate, void* stream) {
+  REQUIRE(v && g && dw && dv && rows > 0 && D > 0, "weight_norm_bwd: bad args");
+  hipError_t e = launch_weightnorm_bwd(v, g, dw, dv, dg, rows, D, accumulate, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "weight_norm_bwd");
+}
+
+int dsvt_cast_rows(int dtype, const float* x, void* y, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
+                   int64_t goff, const float* row_scale, int64_t group, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "cast_rows: bad dtype");
+  REQUIRE(x && y && aligned16(x) && ((uintptr_t)y & 7) == 0 && rows > 0 && C > 0 && C % 4 == 0, "cast_rows: bad args");
+  REQUIRE(!row_scale || group > 0, "cast_rows: row_scale needs group > 0");
+  norm_map(rpg, gstride, goff);
+  hipError_t e = launch_cast_rows(dtype, x, y, rows, C, rpg, gstride, goff, row_scale, group, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "cast_rows");
+}
+
+int dsvt_row_scale(int dtype, void* y, int64_t rows, int64_t C, int64_t ld, const float* row_scale, int64_t group,
+                   void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "row_scale: bad dtype");
+  REQUIRE(y && row_scale && rows > 0 && C > 0 && C % 4 == 0 && ld >= C && ld % 4 == 0 && group > 0,
+          "row_scale: bad args");
+  hipError_t e = launch_row_scale(dtype, y, rows, C, ld, row_scale, group, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "row_scale");
+}
+
+int dsvt_rowscale_bias_add(float* X, int64_t rows, int64_t C, const float* row_scale, const float* bias,
+                           void* stream) {
+  REQUIRE(X && row_scale && bias && aligned16(X) && aligned16(bias) && rows > 0 && C % 4 == 0,
+          "rowscale_bias_add: bad args");
+  hipError_t e = launch_rowscale_bias_add(X, rows, C, row_scale, bias, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "rowscale_bias_add");
+}
+
+int dsvt_cast_transpose(int dtype, const float* x, void* y, int64_t R, int64_t C, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "cast_transpose: bad dtype");
+  REQUIRE(x && y && R > 0 && C > 0, "cast_transpose: bad args");
+  hipError_t e = launch_cast_transpose(dtype, x, y, R, C, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "cast_transpose");
+}
+
+int dsvt_embed_bwd(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C, const int32_t* pos_index,
+                   const int32_t* time_index, float* dpos, float* dtime, float* dcls, void* workspace,
+                   int64_t workspace_bytes, void* stream) {
+  REQUIRE(dX && pos_index && dpos && dcls && B > 0 && Np > 0 && T > 0 && C > 0, "embed_bwd: bad args");
+  REQUIRE(!dtime == !time_index, "embed_bwd: time_embed grad needs time_index");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_EMBED_BWD, 1, Np, T, C),
+          "embed_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* gn = (float*)workspace;
+  float* gt = gn + Np * C;
+  float* gc = gt + T * C;
+  hipError_t e;
+  if ((e = launch_embed_grads(dX, B, Np, T, C, gn, gt, gc, s))) return hip_fail(e, "embed_grads");
+  if ((e = launch_index_accum(gn, pos_index, Np, C, 1, dpos, s))) return hip_fail(e, "embed pos");
+  if (dtime && (e = launch_index_accum(gt, time_index, T, C, 0, dtime, s))) return hip_fail(e, "embed time");
+  // CLS token row = cls_token + pos_embed[0] (timesformer.py:288-290)
+  if ((e = launch_reduce_partials(gc, 1, C, C, dcls, 1, s))) return hip_fail(e, "embed cls");
+  if ((e = launch_reduce_partials(gc, 1, C, C, dpos, 1, s))) return hip_fail(e, "embed cls pos");
+  return 0;
+}
+
+int dsvt_ema(float* const* teacher, const float* const* student, const int64_t* sizes, const int32_t* chunk_tensor,
+             const int64_t* chunk_start, int64_t nchunks, float momentum, void* stream) {
+  REQUIRE(teacher && student && sizes && chunk_tensor && chunk_start && nchunks > 0, "ema: bad args");
+  hipError_t e = launch_ema(teacher, student, sizes, chunk_tensor, chunk_start, nchunks, momentum, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "ema");
+}
+
+int dsvt_clip_grads(float* const* grads, const int64_t* sizes, const int32_t* chunk_tensor, const int64_t* chunk_start,
+                    const int32_t* first_chunk, int64_t nchunks, int64_t ntensors, float clip, float* norms,
+                    void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(grads && sizes && chunk_tensor && chunk_start && first_chunk && norms && nchunks > 0 && ntensors > 0,
+          "clip_grads: bad args");
+  REQUIRE(workspace && workspace_bytes >= nchunks * 4, "clip_grads: workspace too small");
+  hipError_t e = launch_clip_grads(grads, sizes, chunk_tensor, chunk_start, first_chunk, nchunks, ntensors, clip,
+                                   (float*)workspace, norms, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "clip_grads");
 }
 
 }  // extern "C"

@@ -132,6 +132,20 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * one_plus_erf;
 }
 
+// d GELU / dx = Phi(x) + x phi(x) (same A&S 7.1.26 erf as gelu_erf): the Mlp.fc1 backward.
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);   // exp(-x^2/2)
+  const float tail = p * t * e;                                            // 1 - erf(z)
+  const float cdf = 0.5f * (x >= 0.f ? 2.0f - tail : tail);
+  return cdf + x * e * 0.3989422804014327f;
+}
+
 // Output-row map used by every kernel that writes into the [B, L, C] token tensor:
 //   row(m) = (m / rpg) * gstride + goff + (m % rpg)
 // identity: rpg = huge, gstride = 0, goff = 0.

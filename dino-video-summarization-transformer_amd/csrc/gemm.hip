@@ -155,10 +155,19 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
       if (CHECK && n >= p.N) continue;
       const float4 bb = bias4[j];
       float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y, v2 = acc[i][j][2] + bb.z, v3 = acc[i][j][3] + bb.w;
-      if constexpr (EPI == EPI_GELU) {
+      if constexpr (EPI == EPI_GELU_SAVE) {
+        store4((T*)p.aux + orow[i] * p.ld_aux + n, v0, v1, v2, v3);
+      }
+      if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE) {
         v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
       }
-      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
+      if constexpr (EPI == EPI_DGELU) {
+        float pre[4];
+        load4((const T*)p.aux + orow[i] * p.ld_aux + n, pre);
+        v0 = acc[i][j][0] * gelu_erf_grad(pre[0]); v1 = acc[i][j][1] * gelu_erf_grad(pre[1]);
+        v2 = acc[i][j][2] * gelu_erf_grad(pre[2]); v3 = acc[i][j][3] * gelu_erf_grad(pre[3]);
+      }
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU || EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
         if constexpr (OUT_F32)
           store4((float*)p.out + orow[i] * p.ldo + n, v0, v1, v2, v3);
         else
@@ -239,6 +248,11 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
       break;
     case EPI_RESID: gemm_kernel<T, EPI_RESID, true><<<grid, block, 0, s>>>(p); break;
     case EPI_PATCH: gemm_kernel<T, EPI_PATCH, true><<<grid, block, 0, s>>>(p); break;
+    case EPI_GELU_SAVE: gemm_kernel<T, EPI_GELU_SAVE, false><<<grid, block, 0, s>>>(p); break;
+    case EPI_DGELU:
+      if (out_f32) gemm_kernel<T, EPI_DGELU, true><<<grid, block, 0, s>>>(p);
+      else gemm_kernel<T, EPI_DGELU, false><<<grid, block, 0, s>>>(p);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -256,6 +270,10 @@ void set_gemm_variant(int v) { g_gemm_variant = v; }
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
+  if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
+    if (g_gemm_variant == 1 || g_gemm_variant == 9 || g_gemm_variant == 10) return g_gemm_variant;
+    return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
+  }
   if (g_gemm_variant) return g_gemm_variant;
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }

@@ -60,6 +60,36 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
       bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  // training epilogues (per-element, bf16 aux operand): GELU with the pre-activation saved,
+  // and GELU backward
+  if constexpr (EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = rbase + i * 16 + r16;
+      if (m >= p.M) continue;
+      const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int64_t n = cbase + j * 16 + 4 * g;
+        if (n >= p.N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == EPI_GELU_SAVE) {
+          const float4 bb = bias4[j];
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+          store4((bf16_t*)p.aux + orow * p.ld_aux + n, v[0], v[1], v[2], v[3]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+        } else {
+          float pre[4];
+          load4((const bf16_t*)p.aux + orow * p.ld_aux + n, pre);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= gelu_erf_grad(pre[e]);
+        }
+        store4(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n, v[0], v[1], v[2], v[3]);
+      }
+    }
+    return;
+  }
   // full wave tile (uniform): branch-free bias / GELU / 16-B stores, so the compiler's vmcnt
   // waits stay exact (a per-lane bounds branch around each store makes it drain every time)
   if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0) {
@@ -548,6 +578,8 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
     case EPI_GELU: if (out_f32) DSVT_K(EPI_GELU, true); else DSVT_K(EPI_GELU, false); break;
     case EPI_RESID: DSVT_K(EPI_RESID, true); break;
     case EPI_PATCH: DSVT_K(EPI_PATCH, true); break;
+    case EPI_GELU_SAVE: DSVT_K(EPI_GELU_SAVE, false); break;
+    case EPI_DGELU: if (out_f32) DSVT_K(EPI_DGELU, true); else DSVT_K(EPI_DGELU, false); break;
     default: return hipErrorInvalidValue;
   }
 #undef DSVT_K

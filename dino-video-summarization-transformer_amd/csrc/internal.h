@@ -15,9 +15,13 @@ struct GemmParams {
   // patch-embed epilogue (X = acc + bias + pos[1 + pidx[n]] + temb[tidx[t]])
   const float* pos; const int32_t* pidx; const float* temb; const int32_t* tidx;
   int64_t T;  // frames per patch group (1 for the frame-major order)
+  // backward / training epilogues: second operand in the storage dtype, row-major, ld_aux
+  void* aux; int64_t ld_aux;
 };
 
-enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_PATCH = 3 };
+// EPI_GELU_SAVE: out = GELU(acc + bias), aux = acc + bias (the pre-activation, for the backward)
+// EPI_DGELU:     out = acc * GELU'(aux)   (Mlp.fc1 backward through nn.GELU, bias ignored)
+enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_PATCH = 3, EPI_GELU_SAVE = 4, EPI_DGELU = 5 };
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s);
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // the kernel launch_gemm dispatches
@@ -53,11 +57,63 @@ struct AttnParams {
   int64_t nb, tin, L, tok_stride, seqlen, heads, C;
   float scale;
   float* probs;            // optional: softmax probabilities [nb*tin][heads][seqlen][seqlen] (get_attn)
+  const float* seq_scale;  // optional: per-sequence output scale (training DropPath over (b, t), timesformer.py:159)
 };
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s);
 void set_attn_variant(int v);
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T,
                                 int64_t heads, int64_t C, float scale, hipStream_t s);
+
+// Backward (backward.hip).  Attention backward: sequence layout as AttnParams; the
+// dO of position 0 is scaled by cls_scale and its dq/dk/dv go to cls_aux [nb*tin, 3C] fp32
+// (then summed over t into the CLS row) when cls_aux is non-null; stats = [nb*tin*heads*seqlen][2].
+struct AttnBwdParams {
+  const void* qkv; int64_t ld_qkv;
+  const void* dout; int64_t ld_dout;
+  void* dqkv; int64_t ld_dqkv;
+  float* cls_aux;
+  float* stats;
+  int64_t nb, tin, L, tok_stride, seqlen, heads, C;
+  float scale, cls_scale;
+  const float* seq_scale;  // optional: dO of sequence seq scaled (the forward's DropPath scale)
+};
+int ln_bwd_blocks(int64_t rows);
+int64_t colsum_parts(int64_t rows);
+hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
+                         int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* partial,
+                         hipStream_t s);
+hipError_t launch_reduce_partials(const float* partial, int64_t nparts, int64_t width, int64_t stride, float* out,
+                                  int accumulate, hipStream_t s);
+hipError_t launch_colsum_rows(int dtype, const void* y, int64_t rows, int64_t C, int64_t ld, int64_t rpg,
+                              int64_t gstride, int64_t goff, const float* row_scale, float* partial, float* out,
+                              int accumulate, hipStream_t s);
+hipError_t launch_attn_temporal_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nseq, int64_t T,
+                                    int64_t heads, int64_t C, float scale, hipStream_t s);
+hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s);
+hipError_t launch_dino_loss_bwd(const float* student, const float* teacher, const float* center, int64_t B,
+                                int64_t ncrops, int64_t gc, int64_t D, float inv_ts, float inv_tt, const float* t_m,
+                                const float* t_z, const float* s_m, const float* s_z, const float* dloss, float coef,
+                                float* grad, hipStream_t s);
+hipError_t launch_l2norm_bwd(const float* x, const float* dz, float* dx, int64_t rows, int64_t D, float eps,
+                             hipStream_t s);
+hipError_t launch_weightnorm_bwd(const float* v, const float* g, const float* dw, float* dv, float* dg, int64_t rows,
+                                 int64_t D, int accumulate, hipStream_t s);
+hipError_t launch_cast_rows(int dtype, const float* x, void* y, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
+                            int64_t goff, const float* row_scale, int64_t group, hipStream_t s);
+hipError_t launch_row_scale(int dtype, void* y, int64_t rows, int64_t C, int64_t ld, const float* row_scale,
+                            int64_t group, hipStream_t s);
+hipError_t launch_rowscale_bias_add(float* X, int64_t rows, int64_t C, const float* row_scale, const float* bias,
+                                    hipStream_t s);
+hipError_t launch_cast_transpose(int dtype, const float* x, void* y, int64_t R, int64_t C, hipStream_t s);
+hipError_t launch_embed_grads(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C, float* gn, float* gt,
+                              float* gcls, hipStream_t s);
+hipError_t launch_index_accum(const float* src, const int32_t* dst, int64_t n, int64_t C, int64_t dst_off, float* out,
+                              hipStream_t s);
+hipError_t launch_ema(float* const* teacher, const float* const* student, const int64_t* sizes, const int32_t* ctensor,
+                      const int64_t* cstart, int64_t nchunks, float m, hipStream_t s);
+hipError_t launch_clip_grads(float* const* grads, const int64_t* sizes, const int32_t* ctensor, const int64_t* cstart,
+                             const int32_t* first_chunk, int64_t nchunks, int64_t ntensors, float clip, float* partial,
+                             float* norms, hipStream_t s);
 
 hipError_t launch_softmax_stats(const float* x, const float* center, float inv_temp, int64_t rows,
                                 int64_t D, float* m_out, float* z_out, hipStream_t s);

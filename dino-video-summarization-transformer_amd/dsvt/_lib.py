@@ -10,9 +10,11 @@ LIB_PATH = os.environ.get("DSVT_LIB", os.path.join(_HERE, "libdsvt.so"))
 
 BF16, F32 = 0, 1
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID = 0, 1, 2
+EPI_GELU_SAVE, EPI_DGELU = 4, 5
 TOKENS_NT, TOKENS_FRAME = 0, 1
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
 WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
+WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
 
 _i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -40,6 +42,26 @@ SIGNATURES = {
     "dsvt_dino_loss_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _f32, _f32, _p, _p, _p, _i64, _p]),
     "dsvt_dino_pair_loss_fwd": (_i32, [_p, _p, _p, _i64, _i64, _f32, _f32, _p, _p, _i64, _p]),
     "dsvt_center_ema": (_i32, [_p, _p, _i64, _f32, _f32, _p]),
+    "dsvt_attn_spatial_scaled_fwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
+    # backward / training
+    "dsvt_gemm_aux_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64,
+                                 _i64, _i64, _i64, _p]),
+    "dsvt_layernorm_bwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _p, _i32, _p, _i64,
+                                  _p]),
+    "dsvt_colsum_bwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _i32, _p, _i64, _p]),
+    "dsvt_attn_temporal_bwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_attn_spatial_bwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
+    "dsvt_attn_joint_bwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
+    "dsvt_dino_loss_bwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _f32, _f32, _p, _p, _p, _i64, _p]),
+    "dsvt_dino_head_norm_bwd": (_i32, [_p, _p, _p, _i64, _i64, _f32, _p]),
+    "dsvt_weight_norm_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _p]),
+    "dsvt_cast_rows": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
+    "dsvt_row_scale": (_i32, [_i32, _p, _i64, _i64, _i64, _p, _i64, _p]),
+    "dsvt_rowscale_bias_add": (_i32, [_p, _i64, _i64, _p, _p, _p]),
+    "dsvt_cast_transpose": (_i32, [_i32, _p, _p, _i64, _i64, _p]),
+    "dsvt_embed_bwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
+    "dsvt_ema": (_i32, [_p, _p, _p, _p, _p, _i64, _f32, _p]),
+    "dsvt_clip_grads": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _f32, _p, _p, _i64, _p]),
     "dsvt_set_gemm_variant": (_i32, [_i32]),
     "dsvt_set_attn_variant": (_i32, [_i32]),
     "dsvt_probe_enable": (_i32, [_i32, _i32]),

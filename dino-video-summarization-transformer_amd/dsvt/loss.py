@@ -46,7 +46,7 @@ class DINOLoss(nn.Module):
     def forward(self, student_output, teacher_output, epoch):
         """Returns the 0-d loss tensor (device); updates `center` (train_ssl.py:633-671)."""
         if torch.is_grad_enabled() and student_output.requires_grad:
-            raise NotImplementedError("dsvt DINOLoss backward is not implemented yet (SURVEY §8(f) rank 1)")
+            return self._forward_train(student_output, teacher_output, epoch)
         s = _fp32(student_output, "student_output")
         t = _fp32(teacher_output, "teacher_output")
         if t.shape[0] % self.global_crops:
@@ -61,6 +61,28 @@ class DINOLoss(nn.Module):
         if not self.defer_center_update:
             self.update_center(colsum, t.shape[0])
         return loss.reshape(())
+
+    def _forward_train(self, student_output, teacher_output, epoch):
+        """Differentiable w.r.t. the student logits (dsvt.training.LossFn); the teacher is
+        detached as in train_ssl.py:651."""
+        from .training import LossFn
+        if not student_output.is_cuda:
+            raise DsvtError("student_output must be on the GPU (no CPU fallback)")
+        s = student_output.float()
+        s = s if s.is_contiguous() else s.contiguous()
+        t = _fp32(teacher_output, "teacher_output")
+        B = t.shape[0] // self.global_crops
+        if t.shape[0] % self.global_crops or s.shape[0] != self.n_crops * B:
+            raise ValueError("student rows %d / teacher rows %d do not match ncrops %d, global_crops %d" %
+                             (s.shape[0], t.shape[0], self.n_crops, self.global_crops))
+        temp = float(self.teacher_temp_schedule[epoch])
+        if self.center.dtype != torch.float32 or not self.center.is_contiguous():
+            self.center = self.center.float().contiguous()
+        loss, colsum = LossFn.apply(s, t, self.center, B, self.n_crops, self.global_crops, self.student_temp, temp)
+        self.last_colsum = (colsum, t.shape[0])
+        if not self.defer_center_update:
+            self.update_center(colsum, t.shape[0])
+        return loss
 
     @torch.no_grad()
     def update_center(self, colsum, rows):

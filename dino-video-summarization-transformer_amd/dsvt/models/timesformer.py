@@ -272,15 +272,25 @@ class VisionTransformer(nn.Module):
         if not getattr(x, "is_cuda", False) or not self.pos_embed.is_cuda:
             raise DsvtError("dsvt VisionTransformer runs only on the GPU (no CPU fallback): move model and input "
                             "to cuda")
+        divided = self.attention_type == 'divided_space_time'
         if self.training:
-            if any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0 for b in self.blocks):
-                raise NotImplementedError("training-mode stochastic depth (DropPath) is not implemented in the "
-                                          "dsvt forward yet; call .eval() (SURVEY §8(f))")
             if any(r > 0 for r in self._drop_rates):
-                raise NotImplementedError("dropout > 0 is not supported by the dsvt forward")
+                raise NotImplementedError("dropout > 0 is not supported by the dsvt forward (the reference's "
+                                          "drop_rate / attn_drop_rate are 0)")
+            if not divided and any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0
+                                   for b in self.blocks):
+                raise NotImplementedError("training-mode DropPath is implemented for divided space-time "
+                                          "attention only; call .eval() for %s" % self.attention_type)
+        if self._grad_path() and not divided:
+            raise NotImplementedError("dsvt backward is implemented for divided space-time attention only")
+
+    def _grad_path(self):
+        """Training path: autograd through dsvt.training.BackboneFn (saved activations +
+        HIP backward).  Also taken in train mode with DropPath so the masks are applied."""
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("dsvt backward is not implemented yet (SURVEY §8(f) rank 1): run the "
-                                      "forward under torch.no_grad() or freeze the parameters")
+            return True
+        return self.training and any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0
+                                     for b in self.blocks)
 
     # -------------------------------------------------------------- forward
     def forward_features(self, x, get_all=False, get_attn=False, out=None):
@@ -305,6 +315,15 @@ class VisionTransformer(nn.Module):
     def _forward_sources(self, srcs, B, T, H, W, Cin, get_all, get_attn, out):
         for src, _, _ in srcs:
             self._check_supported(src)
+        if self._grad_path():
+            if get_all or get_attn:
+                raise NotImplementedError("get_all / get_attn are inference exports (no backward)")
+            from ..training import BackboneFn
+            feats = BackboneFn.apply(self, srcs, B, T, H, W, Cin, *self.parameters())
+            if out is not None:
+                with torch.no_grad():
+                    out.copy_(feats)
+            return feats
         mode = self.dsvt_dtype
         w = self._wcache.getter(mode)
         Hp, Wp = H // 16, W // 16

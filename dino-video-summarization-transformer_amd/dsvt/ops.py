@@ -182,6 +182,132 @@ def center_ema(center, colsum, momentum, inv_count):
     return center
 
 
+def attn_spatial_scaled(qkv, out, seq_scale, B, T, L, heads, scale, ws):
+    """attn_spatial with the output of sequence (b,t) scaled by seq_scale[b*T+t] (DropPath)."""
+    _check(seq_scale, torch.float32, "seq_scale")
+    call("dsvt_attn_spatial_scaled_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), _ptr(seq_scale), B, T, L, heads, 64,
+         float(scale), _ptr(ws), ws.numel() * ws.element_size(), _stream())
+    return out
+
+
+# ---------------------------------------------------------------- backward / training
+def _ws(op, mode, M, N, K, device):
+    nbytes = workspace_bytes(op, mode, M, N, K)
+    return torch.empty(max(nbytes, 4) // 4, device=device, dtype=torch.float32)
+
+
+def gemm_aux(a, w, bias, out, aux, epilogue, out_f32=False, rowmap=None, M=None):
+    """GELU_SAVE: out = GELU(a.w^T + b), aux = a.w^T + b; DGELU: out = (a.w^T) * GELU'(aux)."""
+    mode = w.dtype
+    _check(a, mode, "A")
+    _check(w, mode, "W")
+    _check(aux, mode, "aux")
+    M = a.shape[0] if M is None else M
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    call("dsvt_gemm_aux_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), a.shape[-1], _ptr(w), w.shape[1],
+         _ptr(bias), _ptr(out), out.shape[-1], _ptr(aux), aux.shape[-1], M, w.shape[0], a.shape[-1], rpg, gs, go,
+         _stream())
+    return out
+
+
+def layernorm_bwd(x, dy, gamma, eps, dx, rows, dgamma, dbeta, rowmap=None, accumulate=True):
+    """dx[row(m)] += dLN(x[row(m)], dy[m]); dgamma / dbeta (+)= the affine-parameter grads."""
+    C = x.shape[-1]
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    ws = _ws(_lib.WS_LN_BWD, torch.float32, rows, 0, C, x.device)
+    call("dsvt_layernorm_bwd", _dt(dy.dtype), _ptr(x), _ptr(dy), _ptr(gamma), _ptr(dx), rows, C, rpg, gs, go,
+         float(eps), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ptr(ws), ws.numel() * 4, _stream())
+    return dx
+
+
+def colsum(y, out, rows=None, rowmap=None, row_scale=None, accumulate=True):
+    """out (+)= sum over rows of y (rows through rowmap, optionally scaled per row)."""
+    rows = y.shape[0] if rows is None else rows
+    C = out.numel()
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    ws = _ws(_lib.WS_COLSUM, torch.float32, rows, C, 0, y.device)
+    call("dsvt_colsum_bwd", _dt(y.dtype), _ptr(y), rows, C, y.shape[-1], rpg, gs, go, _ptr(row_scale), _ptr(out),
+         int(accumulate), _ptr(ws), ws.numel() * 4, _stream())
+    return out
+
+
+def attn_temporal_bwd(qkv, dout, dqkv, nseq, T, heads, scale):
+    call("dsvt_attn_temporal_bwd", _dt(qkv.dtype), _ptr(qkv), _ptr(dout), _ptr(dqkv), nseq, T, heads, 64,
+         float(scale), _stream())
+    return dqkv
+
+
+def attn_spatial_bwd(qkv, dout, dqkv, B, T, L, heads, scale, seq_scale=None):
+    C = heads * 64
+    ws = _ws(_lib.WS_ATTN_BWD, qkv.dtype, B * T, C, 1 + (L - 1) // T, qkv.device)
+    call("dsvt_attn_spatial_bwd", _dt(qkv.dtype), _ptr(qkv), _ptr(dout), _ptr(dqkv), _ptr(seq_scale), B, T, L, heads,
+         64, float(scale), _ptr(ws), ws.numel() * 4, _stream())
+    return dqkv
+
+
+def attn_joint_bwd(qkv, dout, dqkv, nb, L, heads, scale):
+    ws = _ws(_lib.WS_ATTN_BWD, qkv.dtype, nb, heads * 64, L, qkv.device)
+    call("dsvt_attn_joint_bwd", _dt(qkv.dtype), _ptr(qkv), _ptr(dout), _ptr(dqkv), nb, L, heads, 64, float(scale),
+         _ptr(ws), ws.numel() * 4, _stream())
+    return dqkv
+
+
+def dino_loss_bwd(student, teacher, center, B, ncrops, global_crops, student_temp, teacher_temp, dloss):
+    _check(student, torch.float32, "student_output")
+    _check(teacher, torch.float32, "teacher_output")
+    D = student.shape[-1]
+    ds = torch.empty_like(student)
+    ws = _ws(_lib.WS_DINO_LOSS, torch.float32, B, ncrops, global_crops, student.device)
+    call("dsvt_dino_loss_bwd", _ptr(student), _ptr(teacher), _ptr(center.reshape(-1).contiguous()), B, ncrops,
+         global_crops, D, float(student_temp), float(teacher_temp), _ptr(dloss.reshape(-1).float().contiguous()),
+         _ptr(ds), _ptr(ws), ws.numel() * 4, _stream())
+    return ds
+
+
+def head_norm_bwd(x, dz, eps=1e-12):
+    dx = torch.empty_like(x)
+    call("dsvt_dino_head_norm_bwd", _ptr(x), _ptr(dz), _ptr(dx), x.shape[0], x.shape[1], float(eps), _stream())
+    return dx
+
+
+def weight_norm_bwd(v, g, dw, dv, dg, accumulate=True):
+    call("dsvt_weight_norm_bwd", _ptr(v), _ptr(g), _ptr(dw), _ptr(dv), _ptr(dg), v.shape[0], v.shape[1],
+         int(accumulate), _stream())
+    return dv
+
+
+def cast_rows(x, out, rows, rowmap=None, row_scale=None, group=1):
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    call("dsvt_cast_rows", _dt(out.dtype), _ptr(x), _ptr(out), rows, x.shape[-1], rpg, gs, go, _ptr(row_scale),
+         int(group), _stream())
+    return out
+
+
+def row_scale(y, row_scale_, group, rows=None):
+    rows = y.shape[0] if rows is None else rows
+    call("dsvt_row_scale", _dt(y.dtype), _ptr(y), rows, y.shape[-1], y.shape[-1], _ptr(row_scale_), int(group),
+         _stream())
+    return y
+
+
+def rowscale_bias_add(X, row_scale_, bias):
+    call("dsvt_rowscale_bias_add", _ptr(X), X.shape[0], X.shape[-1], _ptr(row_scale_), _ptr(bias), _stream())
+    return X
+
+
+def cast_transpose(x, out):
+    _check(x, torch.float32, "x")
+    call("dsvt_cast_transpose", _dt(out.dtype), _ptr(x), _ptr(out), x.shape[0], x.shape[1], _stream())
+    return out
+
+
+def embed_bwd(dX, B, Np, T, pos_index, time_index, dpos, dtime, dcls):
+    C = dX.shape[-1]
+    ws = _ws(_lib.WS_EMBED_BWD, torch.float32, Np, T, C, dX.device)
+    call("dsvt_embed_bwd", _ptr(dX), B, Np, T, C, _ptr(pos_index), _ptr(time_index), _ptr(dpos), _ptr(dtime),
+         _ptr(dcls), _ptr(ws), ws.numel() * 4, _stream())
+
+
 # ---------------------------------------------------------------- measurement probe
 def probe_enable(mask, capacity=65536):
     call("dsvt_probe_enable", mask, capacity)

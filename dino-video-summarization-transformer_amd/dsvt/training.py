@@ -1,0 +1,429 @@
+"""Training (backward) path of the DINO-SVT student: autograd Functions over libdsvt.so.
+
+What loss.backward() runs at train_ssl.py:538/545 in the reference, rebuilt on the gfx950
+kernels:
+
+  BackboneFn   TimeSformer divided-ST backbone (models/timesformer.py:116-185, 285-345): a
+               training forward that keeps the activations each backward GEMM needs, and the
+               block-by-block backward -- LayerNorm / attention / GELU / embedding gradients
+               in HIP (backward.hip), input-gradient GEMMs on the dsvt MFMA GEMM (cached W^T,
+               fused GELU' epilogue), weight-gradient GEMMs dW = dY^T.X on hipBLASLt (plain
+               library GEMMs via torch.mm), fp32 gradient accumulation.
+  HeadFn       DINOHead (vision_transformer.py:278-282): GELU MLP, F.normalize, weight-norm.
+  LossFn       DINOLoss.forward (train_ssl.py:633-671); the teacher branch is detached.
+
+Training-mode stochastic depth (DropPath, models/vit_utils.py:152-167) follows the
+reference's sample axes: per (b, patch) for the temporal branch (xt is [(B*N), T, C]), per
+(b, frame) for the spatial branch ([(B*T), 1+N, C]; the CLS output is the mean over frames of
+the DROPPED per-frame outputs) and per clip for the MLP, each scaled by 1/keep_prob.  The
+masks come from torch.rand on the device in that order, block by block.
+
+The gradients of every parameter are returned from Function.backward, so autograd's
+accumulation -- and DDP's bucketed all-reduce hooks -- see them like the reference's.
+"""
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SPATIAL, WS_PATCH_EMBED, TOKENS_NT, \
+    DsvtError
+
+
+def wgrad(dy, x, out):
+    """out [N, K] (fp32) += dy^T [N, M] . x [M, K]: a plain library GEMM (hipBLASLt)."""
+    out.add_(torch.mm(dy.t(), x))
+
+
+class _Grads:
+    """fp32 zero-initialised gradient buffers, one per parameter (returned by backward)."""
+
+    def __init__(self):
+        self.g = {}
+
+    def __call__(self, p):
+        buf = self.g.get(id(p))
+        if buf is None:
+            buf = self.g[id(p)] = torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+        return buf
+
+    def get(self, p):
+        return self.g.get(id(p))
+
+
+def _keep_scale(n, p, device):
+    """DropPath per-sample scale floor(keep + U[0,1)) / keep (models/vit_utils.py:152-167)."""
+    keep = 1.0 - p
+    return (torch.floor(keep + torch.rand(n, device=device, dtype=torch.float32)) / keep).contiguous()
+
+
+class _S:
+    """Saved activations of one block."""
+
+
+# ================================================================================ backbone
+class BackboneFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, srcs, B, T, H, W, Cin, *params):
+        feats, state = _backbone_forward(model, srcs, B, T, H, W, Cin)
+        ctx.model, ctx.state, ctx.params = model, state, params
+        return feats
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        grads = _backbone_backward(ctx.model, ctx.state, dfeat.float().contiguous())
+        ctx.state = None
+        out = [None] * 7
+        for p in ctx.params:
+            g = grads.get(p)
+            out.append(g if (g is not None and p.requires_grad) else None)
+        return tuple(out)
+
+
+def _masks(model, nblk, B, Np, T, L, device):
+    """DropPath scales for each block (None when inactive): temporal [B*Np], spatial [B*T]
+    (+ per-X-row bias scale [B*L]), MLP [B] (+ [B*L])."""
+    out = []
+    for blk in model.blocks[:nblk]:
+        dp = getattr(blk.drop_path, "drop_prob", 0.0)
+        if not model.training or dp <= 0.0:
+            out.append(None)
+            continue
+        m = _S()
+        m.t = _keep_scale(B * Np, dp, device)
+        m.s = _keep_scale(B * T, dp, device)
+        m.m = _keep_scale(B, dp, device)
+        st = m.s.view(B, T)
+        rows_s = torch.empty(B, L, device=device, dtype=torch.float32)
+        rows_s[:, 0] = st.mean(1)
+        rows_s[:, 1:] = st.unsqueeze(1).expand(B, Np, T).reshape(B, Np * T)
+        m.s_rows = rows_s.reshape(-1).contiguous()
+        m.m_rows = m.m.view(B, 1).expand(B, L).reshape(-1).contiguous()
+        out.append(m)
+    return out
+
+
+def _backbone_forward(model, srcs, B, T, H, W, Cin):
+    if model.attention_type != 'divided_space_time':
+        raise NotImplementedError("dsvt backward is implemented for divided space-time attention (the DINO-SVT "
+                                  "path); got %s" % model.attention_type)
+    mode = model.dsvt_dtype
+    w = model._wcache.getter(mode)
+    Hp, Wp = H // 16, W // 16
+    Np, C = Hp * Wp, model.embed_dim
+    L = 1 + Np * T
+    rows, R = B * L, B * Np * T
+    dev = srcs[0][0].device
+    pidx, tidx = model._indices(Hp, Wp, T, dev)
+    st = _S()
+    st.mode, st.B, st.T, st.Np, st.L, st.C, st.pidx, st.tidx = mode, B, T, Np, L, C, pidx, tidx
+    X = torch.empty(rows, C, device=dev, dtype=torch.float32)
+    st.im2col = []
+    row0 = 0
+    for src, fidx, nb in srcs:        # K1+K2; keep each source's im2col matrix for dW_conv
+        K = Cin * 256
+        ws = torch.empty(ops.workspace_bytes(WS_PATCH_EMBED, mode, nb * T * Np, C, K) // 2, device=dev,
+                         dtype=torch.bfloat16)
+        ops.patch_embed(src.float().contiguous(), w(model.patch_embed.proj.weight, flat=True),
+                        model.patch_embed.proj.bias, model.cls_token, model.pos_embed, pidx, model.time_embed, tidx,
+                        X[row0 * L:(row0 + nb) * L], ws, TOKENS_NT, frame_index=fidx, clip_shape=(nb, T))
+        a = ws.view(mode)[:nb * T * Np * K].view(nb * T * Np, K)
+        st.im2col.append((row0, nb, a))
+        row0 += nb
+    masks = _masks(model, len(model.blocks), B, Np, T, L, dev)
+    st.masks = masks
+    cls_ws = torch.empty(ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0) // 4, device=dev)
+    patch_map = (Np * T, L, 1)
+    st.blocks = []
+    for blk, mk in zip(model.blocks, masks):
+        S = _S()
+        heads = blk.attn.num_heads
+        ta = blk.temporal_attn
+        # ---- temporal (timesformer.py:127-137)
+        S.X0 = X.clone()
+        S.a_t = torch.empty(R, C, device=dev, dtype=mode)
+        ops.layernorm(X, R, C, blk.temporal_norm1.weight, blk.temporal_norm1.bias, blk.temporal_norm1.eps, S.a_t,
+                      rowmap=patch_map, out_f32=False)
+        S.qkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
+        ops.gemm(S.a_t, w(ta.qkv.weight), ta.qkv.bias, S.qkv_t)
+        S.o_t = torch.empty(R, C, device=dev, dtype=mode)
+        ops.attn_temporal(S.qkv_t, S.o_t, B * Np, T, heads, ta.scale)
+        S.u = torch.empty(R, C, device=dev, dtype=mode)          # temporal_attn.proj output
+        ops.gemm(S.o_t, w(ta.proj.weight), ta.proj.bias, S.u)
+        if mk is not None:
+            ops.row_scale(S.u, mk.t, T)                           # drop_path before temporal_fc
+        ops.gemm(S.u, w(blk.temporal_fc.weight), blk.temporal_fc.bias, X, epilogue=EPI_BIAS_RESID,
+                 rowmap=patch_map, M=R)
+        # ---- spatial with CLS replicate / mean (:139-181)
+        S.X1 = X.clone()
+        S.a_s = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.layernorm(X, rows, C, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, S.a_s, out_f32=False)
+        S.qkv_s = torch.empty(rows, 3 * C, device=dev, dtype=mode)
+        ops.gemm(S.a_s, w(blk.attn.qkv.weight), blk.attn.qkv.bias, S.qkv_s)
+        S.o_s = torch.empty(rows, C, device=dev, dtype=mode)
+        if mk is None:
+            ops.attn_spatial(S.qkv_s, S.o_s, B, T, L, heads, blk.attn.scale, cls_ws)
+            ops.gemm(S.o_s, w(blk.attn.proj.weight), blk.attn.proj.bias, X, epilogue=EPI_BIAS_RESID)
+        else:
+            ops.attn_spatial_scaled(S.qkv_s, S.o_s, mk.s, B, T, L, heads, blk.attn.scale, cls_ws)
+            ops.gemm(S.o_s, w(blk.attn.proj.weight), None, X, epilogue=EPI_BIAS_RESID)
+            ops.rowscale_bias_add(X, mk.s_rows, blk.attn.proj.bias)
+        # ---- MLP (:184)
+        S.X2 = X.clone()
+        S.a_m = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.layernorm(X, rows, C, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, S.a_m, out_f32=False)
+        hid = blk.mlp.fc1.out_features
+        S.pre = torch.empty(rows, hid, device=dev, dtype=mode)
+        S.h = torch.empty(rows, hid, device=dev, dtype=mode)
+        ops.gemm_aux(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, S.pre, EPI_GELU_SAVE)
+        if mk is None:
+            ops.gemm(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID)
+        else:
+            ops.row_scale(S.h, mk.m, L)
+            ops.gemm(S.h, w(blk.mlp.fc2.weight), None, X, epilogue=EPI_BIAS_RESID)
+            ops.rowscale_bias_add(X, mk.m_rows, blk.mlp.fc2.bias)
+        st.blocks.append(S)
+    st.X = X
+    feats = torch.empty(B, C, device=dev, dtype=torch.float32)
+    ops.layernorm(X, B, C, model.norm.weight, model.norm.bias, model.norm.eps, feats, rowmap=(1, L, 0))
+    return feats, st
+
+
+def _backbone_backward(model, st, dfeat):
+    mode, B, T, Np, L, C = st.mode, st.B, st.T, st.Np, st.L, st.C
+    rows, R = B * L, B * Np * T
+    dev = dfeat.device
+    wt = model._wcache.transposed(mode)
+    G = _Grads()
+    patch_map = (Np * T, L, 1)
+    # final norm on the CLS rows (timesformer.py:342-345)
+    dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
+    ops.layernorm_bwd(st.X, dfeat, model.norm.weight, model.norm.eps, dX, B, G(model.norm.weight),
+                      G(model.norm.bias), rowmap=(1, L, 0))
+    for blk, S, mk in zip(reversed(model.blocks), reversed(st.blocks), reversed(st.masks)):
+        heads = blk.attn.num_heads
+        ta = blk.temporal_attn
+        # ---- MLP
+        fc1, fc2 = blk.mlp.fc1, blk.mlp.fc2
+        dXb = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.cast_rows(dX, dXb, rows)
+        if mk is None:
+            dXs = dXb
+            ops.colsum(dX, G(fc2.bias))
+        else:
+            dXs = torch.empty(rows, C, device=dev, dtype=mode)
+            ops.cast_rows(dX, dXs, rows, row_scale=mk.m, group=L)
+            ops.colsum(dX, G(fc2.bias), row_scale=mk.m_rows)
+        wgrad(dXb, S.h, G(fc2.weight))
+        dpre = torch.empty(rows, fc1.out_features, device=dev, dtype=mode)
+        ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
+        wgrad(dpre, S.a_m, G(fc1.weight))
+        ops.colsum(dpre, G(fc1.bias))
+        da = torch.empty(rows, C, device=dev, dtype=torch.float32)
+        ops.gemm(dpre, wt(fc1.weight), None, da, out_f32=True)
+        del dpre
+        ops.layernorm_bwd(S.X2, da, blk.norm2.weight, blk.norm2.eps, dX, rows, G(blk.norm2.weight),
+                          G(blk.norm2.bias))
+        # ---- spatial
+        ops.cast_rows(dX, dXb, rows)
+        wgrad(dXb, S.o_s, G(blk.attn.proj.weight))
+        ops.colsum(dX, G(blk.attn.proj.bias), row_scale=None if mk is None else mk.s_rows)
+        do = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)
+        dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
+        ops.attn_spatial_bwd(S.qkv_s, do, dqkv, B, T, L, heads, blk.attn.scale,
+                             seq_scale=None if mk is None else mk.s)
+        wgrad(dqkv, S.a_s, G(blk.attn.qkv.weight))
+        ops.colsum(dqkv, G(blk.attn.qkv.bias))
+        ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da, out_f32=True)
+        del dqkv, do
+        ops.layernorm_bwd(S.X1, da, blk.norm1.weight, blk.norm1.eps, dX, rows, G(blk.norm1.weight),
+                          G(blk.norm1.bias))
+        # ---- temporal (patch rows of X only)
+        dY = torch.empty(R, C, device=dev, dtype=mode)
+        ops.cast_rows(dX, dY, R, rowmap=patch_map)
+        wgrad(dY, S.u, G(blk.temporal_fc.weight))
+        ops.colsum(dY, G(blk.temporal_fc.bias))
+        du = torch.empty(R, C, device=dev, dtype=mode)
+        ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
+        if mk is not None:
+            ops.row_scale(du, mk.t, T)
+        wgrad(du, S.o_t, G(ta.proj.weight))
+        ops.colsum(du, G(ta.proj.bias))
+        do_t = torch.empty(R, C, device=dev, dtype=mode)
+        ops.gemm(du, wt(ta.proj.weight), None, do_t)
+        dqkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
+        ops.attn_temporal_bwd(S.qkv_t, do_t, dqkv_t, B * Np, T, heads, ta.scale)
+        wgrad(dqkv_t, S.a_t, G(ta.qkv.weight))
+        ops.colsum(dqkv_t, G(ta.qkv.bias))
+        da_t = torch.empty(R, C, device=dev, dtype=torch.float32)
+        ops.gemm(dqkv_t, wt(ta.qkv.weight), None, da_t, out_f32=True)
+        ops.layernorm_bwd(S.X0, da_t, blk.temporal_norm1.weight, blk.temporal_norm1.eps, dX, R,
+                          G(blk.temporal_norm1.weight), G(blk.temporal_norm1.bias), rowmap=patch_map)
+        for k in list(vars(S)):
+            setattr(S, k, None)        # free this block's activations as soon as it is done
+    # ---- patch embedding + token embeddings (timesformer.py:201-209, 288-323)
+    dP = torch.empty(R, C, device=dev, dtype=mode)
+    ops.cast_rows(dX, dP, R, rowmap=patch_map)
+    conv = model.patch_embed.proj
+    dWc = G(conv.weight).view(C, -1)
+    for row0, nb, a in st.im2col:
+        r0 = row0 * Np * T
+        wgrad(dP[r0:r0 + nb * Np * T], a, dWc)
+    ops.colsum(dP, G(conv.bias))
+    ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G(model.pos_embed), G(model.time_embed), G(model.cls_token))
+    return G
+
+
+# ================================================================================ DINO head
+class HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, head, x, *params):
+        logits, st = _head_forward(head, x)
+        ctx.head, ctx.state, ctx.params = head, st, params
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        G, dx = _head_backward(ctx.head, ctx.state, dlogits.float().contiguous())
+        ctx.state = None
+        out = [None, dx]
+        for p in ctx.params:
+            g = G.get(p)
+            out.append(g if (g is not None and p.requires_grad) else None)
+        return tuple(out)
+
+
+def _head_linears(head):
+    import torch.nn as nn
+    return [head.mlp] if isinstance(head.mlp, nn.Linear) else [m for m in head.mlp if isinstance(m, nn.Linear)]
+
+
+def _head_forward(head, x):
+    mode = head.dsvt_dtype
+    w = head._wcache.getter(mode)
+    x = x.detach().float().contiguous()
+    R, dev = x.shape[0], x.device
+    st = _S()
+    st.mode = mode
+    h = torch.empty(R, x.shape[1], device=dev, dtype=mode)
+    ops.cast(x, h)
+    lins = _head_linears(head)
+    st.a, st.pre = [], []
+    for i, lin in enumerate(lins):
+        st.a.append(h)
+        if i == len(lins) - 1:
+            y = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32)
+            ops.gemm(h, w(lin.weight), lin.bias, y, out_f32=True)
+            st.pre.append(None)
+        else:
+            nxt = torch.empty(R, lin.out_features, device=dev, dtype=mode)
+            pre = torch.empty(R, lin.out_features, device=dev, dtype=mode)
+            ops.gemm_aux(h, w(lin.weight), lin.bias, nxt, pre, EPI_GELU_SAVE)
+            st.pre.append(pre)
+            h = nxt
+    st.y = y
+    st.z = torch.empty(R, y.shape[1], device=dev, dtype=mode)
+    ops.head_norm(y, st.z)
+    ll = head.last_layer
+    st.wn = torch.empty(ll.out_features, ll.in_features, device=dev, dtype=mode)
+    ops.weight_norm(ll.weight_v.detach(), ll.weight_g.detach(), st.wn)
+    logits = torch.empty(R, ll.out_features, device=dev, dtype=torch.float32)
+    ops.gemm(st.z, st.wn, None, logits, out_f32=True)
+    return logits, st
+
+
+def _head_backward(head, st, dlogits):
+    mode = st.mode
+    wt = head._wcache.transposed(mode)
+    G = _Grads()
+    R, dev = dlogits.shape[0], dlogits.device
+    ll = head.last_layer
+    dl = torch.empty(R, dlogits.shape[1], device=dev, dtype=mode)
+    ops.cast(dlogits, dl)
+    dW = torch.mm(dl.t(), st.z).float()                       # d(effective weight) [out, bottleneck]
+    ops.weight_norm_bwd(ll.weight_v.detach(), ll.weight_g.detach(), dW, G(ll.weight_v),
+                        G(ll.weight_g).view(-1) if ll.weight_g.requires_grad else None)
+    dz = torch.mm(dl, st.wn).float()                          # [R, bottleneck]
+    dy = ops.head_norm_bwd(st.y, dz.contiguous())
+    lins = _head_linears(head)
+    g = dy                                                    # gradient w.r.t. the current linear's output
+    dx = None
+    for i in range(len(lins) - 1, -1, -1):
+        lin = lins[i]
+        gb = g if g.dtype == mode else torch.empty(R, g.shape[1], device=dev, dtype=mode)
+        if gb is not g:
+            ops.cast(g.contiguous(), gb)
+        wgrad(gb, st.a[i], G(lin.weight))
+        ops.colsum(g, G(lin.bias))
+        if i > 0:
+            nxt = torch.empty(R, lin.in_features, device=dev, dtype=mode)
+            ops.gemm_aux(gb, wt(lin.weight), None, nxt, st.pre[i - 1], EPI_DGELU)
+            g = nxt
+        else:
+            dx = torch.empty(R, lin.in_features, device=dev, dtype=torch.float32)
+            ops.gemm(gb, wt(lin.weight), None, dx, out_f32=True)
+    return G, dx
+
+
+# ================================================================================ DINO loss
+class LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, student, teacher, center, B, ncrops, global_crops, student_temp, teacher_temp):
+        loss, colsum = ops.dino_loss(student, teacher, center, B, ncrops, global_crops, student_temp, teacher_temp)
+        ctx.save_for_backward(student, teacher, center.clone())
+        ctx.cfg = (B, ncrops, global_crops, student_temp, teacher_temp)
+        ctx.mark_non_differentiable(colsum)
+        return loss.reshape(()), colsum
+
+    @staticmethod
+    def backward(ctx, dloss, dcolsum):
+        student, teacher, center = ctx.saved_tensors
+        B, ncrops, gc, ts, tt = ctx.cfg
+        ds = ops.dino_loss_bwd(student, teacher, center, B, ncrops, gc, ts, tt, dloss.reshape(1).contiguous())
+        return ds, None, None, None, None, None, None, None
+
+
+# ================================================================================ step helpers
+class TensorList:
+    """Device-side pointer / size / 4096-element chunk tables of a tensor list (built once; the
+    multi-tensor EMA and gradient-clip kernels walk them)."""
+
+    CHUNK = 4096
+
+    def __init__(self, tensors, device):
+        self.tensors = list(tensors)
+        sizes = [t.numel() for t in self.tensors]
+        ct, cs, first = [], [], [0]
+        for i, n in enumerate(sizes):
+            for s0 in range(0, n, self.CHUNK):
+                ct.append(i)
+                cs.append(s0)
+            first.append(len(ct))
+        self.nchunks = len(ct)
+        self.sizes = torch.tensor(sizes, dtype=torch.int64, device=device)
+        self.ctensor = torch.tensor(ct, dtype=torch.int32, device=device)
+        self.cstart = torch.tensor(cs, dtype=torch.int64, device=device)
+        self.first = torch.tensor(first, dtype=torch.int32, device=device)
+
+    @staticmethod
+    def ptrs(tensors, device):
+        return torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=device)
+
+
+def check_fp32_contiguous(tensors, what):
+    for t in tensors:
+        if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+            raise DsvtError("%s: dsvt multi-tensor kernels need contiguous fp32 GPU tensors" % what)
+
+
+def np_cosine_scheduler(base_value, final_value, epochs, niter_per_ep, warmup_epochs=0, start_warmup_value=0):
+    """utils/utils.py:157-168 (host-side schedule)."""
+    warmup_schedule = np.array([])
+    warmup_iters = warmup_epochs * niter_per_ep
+    if warmup_epochs > 0:
+        warmup_schedule = np.linspace(start_warmup_value, base_value, warmup_iters)
+    iters = np.arange(epochs * niter_per_ep - warmup_iters)
+    schedule = final_value + 0.5 * (base_value - final_value) * (1 + np.cos(np.pi * iters / len(iters)))
+    schedule = np.concatenate((warmup_schedule, schedule))
+    assert len(schedule) == epochs * niter_per_ep
+    return schedule

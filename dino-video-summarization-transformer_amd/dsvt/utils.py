@@ -93,6 +93,17 @@ class MultiCropWrapper(nn.Module):
             for i in range(1, len(sizes) + 1):
                 if i == len(sizes) or sizes[i] != sizes[i - 1]:
                     idx_crops.append(i)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            # training: autograd-tracked backbone calls, one per resolution group, in order
+            outs, start = [], 0
+            for end in idx_crops:
+                group = x[start:end]
+                if getattr(self.backbone, "takes_clip_lists", False):
+                    outs.append(self.backbone.forward_features(group, **kwargs))
+                else:
+                    outs.append(self.backbone(torch.cat(group), **kwargs))
+                start = end
+            return self.head(torch.cat(outs) if len(outs) > 1 else outs[0])
         total = sum(inp.shape[0] for inp in x)
         feats = torch.empty(total, self.backbone.embed_dim, device=x[0].device, dtype=torch.float32)
         jobs, start, row = [], 0, 0
@@ -117,3 +128,84 @@ class MultiCropWrapper(nn.Module):
             for fn in thunks:
                 fn()
         return self.head(feats)
+
+
+# ---------------------------------------------------------------- training-step utilities
+_TLISTS = {}
+
+
+def _tensor_list(tensors):
+    """Cached device tables (pointers, sizes, chunks) for a list of fp32 GPU tensors."""
+    from .training import TensorList, check_fp32_contiguous
+    check_fp32_contiguous(tensors, "multi-tensor op")
+    key = tuple((t.data_ptr(), t.numel()) for t in tensors)
+    ent = _TLISTS.get(key)
+    if ent is None:
+        dev = tensors[0].device
+        tl = TensorList(tensors, dev)
+        ent = _TLISTS[key] = (tl, TensorList.ptrs(tensors, dev))
+        if len(_TLISTS) > 64:
+            _TLISTS.pop(next(iter(_TLISTS)))
+    return ent
+
+
+def ema_update_(teacher_tensors, student_tensors, momentum):
+    """teacher = m * teacher + (1 - m) * student over whole tensor lists in ONE launch
+    (train_ssl.py:555-558 loops param by param)."""
+    from . import ops
+    from ._lib import call
+    tl, tptr = _tensor_list(list(teacher_tensors))
+    _, sptr = _tensor_list(list(student_tensors))
+    call("dsvt_ema", tptr.data_ptr(), sptr.data_ptr(), tl.sizes.data_ptr(), tl.ctensor.data_ptr(),
+         tl.cstart.data_ptr(), tl.nchunks, float(momentum), ops._stream())
+
+
+def clip_gradients_(grads, clip):
+    """utils/utils.py:102-111 per-tensor clipping (clip_coef = clip / (norm + 1e-6), applied when
+    < 1) over a gradient list in three launches, no host sync; returns the norms (device)."""
+    from . import ops
+    from ._lib import call
+    tl, gptr = _tensor_list(list(grads))
+    norms = torch.empty(len(tl.tensors), device=tl.sizes.device, dtype=torch.float32)
+    ws = torch.empty(tl.nchunks, device=tl.sizes.device, dtype=torch.float32)
+    call("dsvt_clip_grads", gptr.data_ptr(), tl.sizes.data_ptr(), tl.ctensor.data_ptr(), tl.cstart.data_ptr(),
+         tl.first.data_ptr(), tl.nchunks, len(tl.tensors), float(clip), norms.data_ptr(), ws.data_ptr(),
+         ws.numel() * 4, ops._stream())
+    return norms
+
+
+def clip_gradients(model, clip):
+    """utils/utils.py:102-111: returns the per-parameter gradient norms (a device tensor here;
+    the reference returns a list of Python floats after one .item() sync per parameter)."""
+    grads = [p.grad for p in model.parameters() if p.grad is not None]
+    if not grads:
+        return []
+    return clip_gradients_(grads, clip)
+
+
+def cancel_gradients_last_layer(epoch, model, freeze_last_layer):
+    """utils/utils.py:114-119."""
+    if epoch >= freeze_last_layer:
+        return
+    for n, p in model.named_parameters():
+        if "last_layer" in n:
+            p.grad = None
+
+
+def get_params_groups(model):
+    """utils/utils.py:612-623: no weight decay on biases and norm parameters."""
+    regularized, not_regularized = [], []
+    for name, param in model.named_parameters():
+        if not param.requires_grad:
+            continue
+        if name.endswith(".bias") or len(param.shape) == 1:
+            not_regularized.append(param)
+        else:
+            regularized.append(param)
+    return [{'params': regularized}, {'params': not_regularized, 'weight_decay': 0.}]
+
+
+def cosine_scheduler(base_value, final_value, epochs, niter_per_ep, warmup_epochs=0, start_warmup_value=0):
+    """utils/utils.py:157-168."""
+    from .training import np_cosine_scheduler
+    return np_cosine_scheduler(base_value, final_value, epochs, niter_per_ep, warmup_epochs, start_warmup_value)

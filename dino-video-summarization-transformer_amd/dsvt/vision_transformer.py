@@ -222,10 +222,11 @@ class DINOHead(nn.Module):
     def forward(self, x):
         """x [R, in_dim] fp32 -> logits [R, out_dim] fp32 (GELU MLP, L2 normalize, weight-normed
         last layer; vision_transformer.py:278-282)."""
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("dsvt backward is not implemented yet: use torch.no_grad()")
         if not x.is_cuda:
             raise DsvtError("dsvt runs only on the GPU (no CPU fallback)")
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            from .training import HeadFn                      # training: saved activations + HIP backward
+            return HeadFn.apply(self, x, *self.parameters())
         mode = self.dsvt_dtype
         w = self._wcache.getter(mode)
         x = x.float().contiguous()

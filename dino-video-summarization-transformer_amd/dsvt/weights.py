@@ -66,6 +66,24 @@ class WeightCache:
             return out
         return get
 
+    def transposed(self, mode):
+        """W^T [in, out] in the storage dtype (dsvt cast-transpose kernel), cached like the
+        casts: the B operand of the backward's input-gradient GEMMs dX = dY . W."""
+        def get(p):
+            t = p.detach()
+            if t.dtype != torch.float32 or t.dim() != 2:
+                raise TypeError("dsvt expects 2-D fp32 master weights, got %s %s" % (t.dtype, tuple(t.shape)))
+            key = (id(p), "T", mode)
+            ent = self._c.get(key)
+            if ent is not None and ent[0] == p._version and ent[1] == p.data_ptr():
+                self._sync(ent)
+                return ent[2]
+            out = torch.empty(t.shape[1], t.shape[0], device=t.device, dtype=mode)
+            ops.cast_transpose(t.contiguous(), out)
+            self._c[key] = (p._version, p.data_ptr(), out) + self._event()
+            return out
+        return get
+
     def folded(self, mode, outer, inner):
         """outer(inner(x)) for two nn.Linear with nothing between them, as ONE Linear:
         W = Wo.Wi, b = Wo.bi + bo, formed in fp32 on the dsvt GEMM (then cast to `mode`) and

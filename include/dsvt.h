@@ -37,6 +37,8 @@ extern "C" {
 #define DSVT_EPI_BIAS 0       /* out[row(m)] = acc + bias                  (Linear)          */
 #define DSVT_EPI_BIAS_GELU 1  /* out[row(m)] = GELU_erf(acc + bias)        (Mlp.fc1 + act)   */
 #define DSVT_EPI_BIAS_RESID 2 /* X[row(m)]  += acc + bias   (fp32 X)       (residual adds)   */
+#define DSVT_EPI_GELU_SAVE 4  /* out = GELU_erf(acc + bias), aux = acc + bias (training fc1)   */
+#define DSVT_EPI_DGELU 5      /* out = acc * GELU_erf'(aux)               (fc1 backward)    */
 
 /* token orders for patch embedding */
 #define DSVT_TOKENS_NT 0      /* divided / joint: X[b][1 + n*T + t]   (timesformer.py:312-323)  */
@@ -55,6 +57,10 @@ extern "C" {
 #define DSVT_WS_ATTN_SPATIAL 3
 #define DSVT_WS_DINO_LOSS 4
 #define DSVT_WS_PAIR_LOSS 5
+#define DSVT_WS_LN_BWD 6
+#define DSVT_WS_COLSUM 7
+#define DSVT_WS_ATTN_BWD 8
+#define DSVT_WS_EMBED_BWD 9
 
 int dsvt_version(void);
 const char *dsvt_last_error(void);
@@ -129,6 +135,12 @@ int dsvt_attn_temporal_fwd(int dtype, const void *qkv, void *out, int64_t nseq, 
 int dsvt_attn_spatial_fwd(int dtype, const void *qkv, void *out, int64_t B, int64_t T, int64_t L,
                           int64_t heads, int64_t head_dim, float scale, void *workspace,
                           int64_t workspace_bytes, void *stream);
+/* dsvt_attn_spatial_fwd with the output of sequence (b,t) scaled by seq_scale[b*T + t] before the
+ * CLS mean: training-mode DropPath of the spatial branch, whose mask is per (b,t) sequence
+ * (timesformer.py:159 drop_path over the [(B*T), 1+N, C] batch). */
+int dsvt_attn_spatial_scaled_fwd(int dtype, const void *qkv, void *out, const float *seq_scale, int64_t B,
+                                 int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                                 void *workspace, int64_t workspace_bytes, void *stream);
 /* Same as dsvt_attn_spatial_fwd, and also writes the softmax probabilities of every frame
  * sequence (CLS + N patches) to probs [B*T][heads][1+N][1+N] fp32 -- the last-block
  * attention map of VisionTransformer.forward_features(get_attn=True), models/timesformer.py:
@@ -174,6 +186,86 @@ int dsvt_dino_pair_loss_fwd(const float *student, const float *teacher, const fl
  * after the caller's all-reduce of colsum). */
 int dsvt_center_ema(float *center, const float *colsum, int64_t D, float momentum,
                     float inv_count, void *stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Backward / training step (loss.backward() at train_ssl.py:538/545).
+ * Gradients are fp32 and ACCUMULATED where `accumulate` != 0 (param.grad semantics).  The
+ * weight-gradient GEMMs dW = dY^T . X are plain library GEMMs on the host side; these entry
+ * points are the rest of the backward.
+ * ------------------------------------------------------------------------------------------ */
+
+/* dsvt_gemm_fwd with a second storage-dtype operand aux [M, ld_aux] (rows through the output
+ * row map): DSVT_EPI_GELU_SAVE (Mlp.fc1 + nn.GELU saving the pre-activation, timesformer.py:
+ * 46-47) or DSVT_EPI_DGELU (dX of fc1 through GELU: out = (dY . W2) * GELU'(pre)). */
+int dsvt_gemm_aux_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
+                      int64_t ldw, const float *bias, void *out, int64_t ldo, void *aux, int64_t ld_aux,
+                      int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
+                      void *stream);
+/* nn.LayerNorm backward: dx[row(m)] += dLN(x[row(m)], dy[m]) (dx has x's layout: the residual
+ * gradient of the pre-LN sub-layer), dgamma/dbeta (+)= column sums.  dy_dtype: storage dtype of
+ * dy (DSVT_BF16 or DSVT_F32).  workspace >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, ., rows, 0, C). */
+int dsvt_layernorm_bwd(int dy_dtype, const float *x, const void *dy, const float *gamma, float *dx,
+                       int64_t rows, int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps,
+                       float *dgamma, float *dbeta, int accumulate, void *workspace,
+                       int64_t workspace_bytes, void *stream);
+/* bias gradient: out[c] (+)= sum_m row_scale[m] * y[row(m)][c]  (y in dtype, row stride ld;
+ * row_scale nullable = 1). */
+int dsvt_colsum_bwd(int dtype, const void *y, int64_t rows, int64_t C, int64_t ld, int64_t rpg,
+                    int64_t gstride, int64_t goff, const float *row_scale, float *out, int accumulate,
+                    void *workspace, int64_t workspace_bytes, void *stream);
+/* Attention backward: dqkv [rows, 3C] (same layout as qkv) from qkv and dout [rows, C].
+ * temporal: as dsvt_attn_temporal_fwd; spatial: as dsvt_attn_spatial_fwd (the CLS row's dout is
+ * the gradient of the frame MEAN, its dq/dk/dv are summed over frames); joint: contiguous
+ * sequences.  seq_scale (nullable): the forward's per-(b,t) DropPath scale, applied to dout.
+ * workspace >= dsvt_workspace_bytes(DSVT_WS_ATTN_BWD, ., B*T (or nb), C, seqlen). */
+int dsvt_attn_temporal_bwd(int dtype, const void *qkv, const void *dout, void *dqkv, int64_t nseq,
+                           int64_t T, int64_t heads, int64_t head_dim, float scale, void *stream);
+int dsvt_attn_spatial_bwd(int dtype, const void *qkv, const void *dout, void *dqkv, const float *seq_scale,
+                          int64_t B, int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                          void *workspace, int64_t workspace_bytes, void *stream);
+int dsvt_attn_joint_bwd(int dtype, const void *qkv, const void *dout, void *dqkv, int64_t nb, int64_t L,
+                        int64_t heads, int64_t head_dim, float scale, void *workspace,
+                        int64_t workspace_bytes, void *stream);
+/* DINOLoss backward (train_ssl.py:653-669): dstudent = dloss[0] * d loss / d student_output
+ * (the teacher branch is detached).  Same workspace as dsvt_dino_loss_fwd. */
+int dsvt_dino_loss_bwd(const float *student, const float *teacher, const float *center, int64_t B,
+                       int64_t ncrops, int64_t global_crops, int64_t D, float student_temp,
+                       float teacher_temp, const float *dloss, float *dstudent, void *workspace,
+                       int64_t workspace_bytes, void *stream);
+/* F.normalize backward (vision_transformer.py:280) and weight-norm backward (dv, dg). */
+int dsvt_dino_head_norm_bwd(const float *x, const float *dz, float *dx, int64_t rows, int64_t D,
+                            float eps, void *stream);
+int dsvt_weight_norm_bwd(const float *v, const float *g, const float *dw, float *dv, float *dg,
+                         int64_t rows, int64_t D, int accumulate, void *stream);
+/* y[m] = cast(x[row(m)] * row_scale[m / group]) (compact gather of row-mapped fp32 rows,
+ * row_scale nullable); y = cast(x)^T for x [R, C]. */
+int dsvt_cast_rows(int dtype, const float *x, void *y, int64_t rows, int64_t C, int64_t rpg,
+                   int64_t gstride, int64_t goff, const float *row_scale, int64_t group, void *stream);
+/* Training DropPath (models/vit_utils.py:152-167) on a residual branch: y[m] *= row_scale[m/group]
+ * in place (ld = row stride), and X[m] += row_scale[m] * bias (a branch bias under DropPath). */
+int dsvt_row_scale(int dtype, void *y, int64_t rows, int64_t C, int64_t ld, const float *row_scale,
+                   int64_t group, void *stream);
+int dsvt_rowscale_bias_add(float *X, int64_t rows, int64_t C, const float *row_scale, const float *bias,
+                           void *stream);
+int dsvt_cast_transpose(int dtype, const float *x, void *y, int64_t R, int64_t C, void *stream);
+/* Token-embedding gradients from dX [B, 1 + Np*T, C] (NT order): dpos[1 + pos_index[n]] +=,
+ * dtime[time_index[t]] += (time_index may be NULL with dtime NULL), dcls += and dpos[0] +=
+ * the CLS rows (timesformer.py:288-323). */
+int dsvt_embed_bwd(const float *dX, int64_t B, int64_t Np, int64_t T, int64_t C, const int32_t *pos_index,
+                   const int32_t *time_index, float *dpos, float *dtime, float *dcls, void *workspace,
+                   int64_t workspace_bytes, void *stream);
+/* Multi-tensor ops over fp32 tensor lists (device arrays of pointers / sizes, work split in
+ * 4096-element chunks: chunk i covers tensor chunk_tensor[i] from chunk_start[i]).
+ * EMA: teacher = m*teacher + (1-m)*student (train_ssl.py:555-558).  clip: per-tensor L2 norms
+ * (norms[ntensors]), grads *= clip/(norm+1e-6) where that is < 1 (utils/utils.py:102-111;
+ * clip <= 0: norms only); first_chunk[ntensors+1] = chunk ranges; workspace >= nchunks*4 B. */
+int dsvt_ema(float *const *teacher, const float *const *student, const int64_t *sizes,
+             const int32_t *chunk_tensor, const int64_t *chunk_start, int64_t nchunks, float momentum,
+             void *stream);
+int dsvt_clip_grads(float *const *grads, const int64_t *sizes, const int32_t *chunk_tensor,
+                    const int64_t *chunk_start, const int32_t *first_chunk, int64_t nchunks,
+                    int64_t ntensors, float clip, float *norms, void *workspace, int64_t workspace_bytes,
+                    void *stream);
 
 /* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
  * 1 = 128x128 / 4-wave kernel, 2 = 256x256 / 8-wave, 3 = 256x128 / 8-wave.  Process-global. */

@@ -77,6 +77,62 @@ def tsf_model(seed, **kw):
     return m.eval()
 
 
+TRAIN_CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
+
+
+def train_grads(TL):
+    import models.vit_utils as ref_vu
+    res = {}
+    for tag, dpr in (("eval", 0.0), ("drop", 0.5)):
+        bb = ref_tsf.VisionTransformer(img_size=64, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1,
+                                       mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                                       drop_rate=0., attn_drop_rate=0., drop_path_rate=dpr, num_frames=4,
+                                       attention_type="divided_space_time")
+        _load(bb, P.timesformer_state(1201, **TRAIN_CFG))
+        hd = ref_vit.DINOHead(64, 512, hidden_dim=128, bottleneck_dim=64)
+        _load(hd, P.dino_head_state(1202, 64, 512, hidden_dim=128, bottleneck_dim=64))
+        masks = []
+        gen = torch.Generator().manual_seed(1203)
+        orig = ref_vu.DropPath.forward
+
+        def dp_forward(self, x):
+            if self.drop_prob == 0. or not self.training:
+                return x
+            keep = 1 - self.drop_prob
+            r = torch.floor(keep + torch.rand((x.shape[0],), generator=gen, dtype=x.dtype))
+            masks.append((r / keep).numpy().astype(np.float32))
+            return x.div(keep) * r.view((x.shape[0],) + (1,) * (x.ndim - 1))
+        ref_vu.DropPath.forward = dp_forward
+        try:
+            if tag == "eval":
+                bb.eval()
+            else:
+                bb.train()
+            hd.train()
+            g_in = [torch.from_numpy(P.clip(1210 + i, (2, 3, 4, 64, 64))) for i in range(2)]
+            l_in = [torch.from_numpy(P.clip(1220 + i, (2, 3, 4, 32, 32))) for i in range(2)]
+            s_out = hd(torch.cat([bb(torch.cat(g_in)), bb(torch.cat(l_in))]))
+            with torch.no_grad():
+                t_out = torch.from_numpy(P.uniform(1230, (4, 512)))
+            lf = TL(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2)
+            loss = lf(s_out, t_out, 0)
+            loss.backward()
+        finally:
+            ref_vu.DropPath.forward = orig
+        res[tag + "_loss"] = np.float32(loss.item())
+        res[tag + "_student"] = s_out.detach().numpy()
+        res[tag + "_teacher"] = t_out.numpy()
+        for k, p in bb.named_parameters():
+            res[tag + "_bb." + k] = p.grad.numpy().copy()
+        for k, p in hd.named_parameters():
+            if p.grad is not None:
+                res[tag + "_hd." + k] = p.grad.numpy().copy()
+        if masks:
+            res[tag + "_masks"] = np.concatenate(masks)
+            res[tag + "_mask_sizes"] = np.array([len(m) for m in masks], np.int32)
+    return res
+
+
 def run(m, x, **kw):
     with torch.no_grad():
         return m.forward_features(torch.from_numpy(x), **kw).numpy()
@@ -190,6 +246,13 @@ def main():
     e2e_loss = l3(s_out, t_out, 0).item()
     out["e2e_cfg1"] = dict(student=s_out.numpy(), teacher=t_out.numpy(), loss=np.float32(e2e_loss),
                            center=l3.center.numpy().copy())
+
+    # ---- 8. training step: student gradients of the DINO loss (loss.backward(), train_ssl.py:538)
+    # tiny divided student (C=64, 1 head, depth 2, 64^2 globals / 32^2 locals, T=4), DINOHead
+    # (64 -> 128 -> 128 -> 64 -> 512), DINOLoss(ncrops=4, global_crops=2), B=2.  Two runs: eval
+    # mode (no DropPath), and train mode with drop_path_rate 0.5 where every DropPath draws its
+    # mask from a seeded CPU generator (recorded, in call order, for the dsvt test to replay).
+    out["train_grads"] = train_grads(TL)
     dist.destroy_process_group()
 
     for name, arrays in out.items():

@@ -1,0 +1,290 @@
+"""Training-path parity on the GPU: student gradients of
+the DINO loss through libdsvt.so against the reference's own loss.backward()
+(tests/golden/train_grads.npz, produced by tests/golden/make_golden.py from /root/reference),
+plus kernel-level backward checks against torch fp32 autograd of the same op.
+
+Tolerances: fp32 parity mode 1e-3 relative to max|ref| per tensor (the north-star bar);
+bf16 perf mode 6e-2 (bf16 storage of activations and of dY in the weight-gradient GEMMs)."""
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from oracle import params as P
+
+pytestmark = pytest.mark.gpu
+TOL = {torch.float32: 1e-3, torch.bfloat16: 6e-2}
+CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-12)
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return dict(np.load("tests/golden/train_grads.npz"))
+
+
+def _student(dtype, drop):
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+    bb = VisionTransformer(img_size=64, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
+                           qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                           drop_path_rate=0.5 if drop else 0.0, num_frames=4, attention_type="divided_space_time")
+    bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(1201, **CFG).items()})
+    hd = DINOHead(64, 512, hidden_dim=128, bottleneck_dim=64)
+    hd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                        P.dino_head_state(1202, 64, 512, hidden_dim=128, bottleneck_dim=64).items()})
+    bb.dsvt_dtype = hd.dsvt_dtype = dtype
+    net = MultiCropWrapper(bb, hd).cuda()
+    net.train()
+    if not drop:
+        bb.eval()
+    return net
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tag", ["eval", "drop"])
+def test_student_grads_match_reference(gold, dtype, tag, monkeypatch):
+    """loss.backward() through MultiCropWrapper(TimeSformer divided, DINOHead) + DINOLoss: loss,
+    student logits and EVERY student parameter gradient vs the reference.  'drop': training-mode
+    DropPath (rate 0.5) replaying the reference's masks in its call order (per (b, patch)
+    temporal, per (b, frame) spatial, per clip MLP)."""
+    from dsvt import training
+    from dsvt.loss import DINOLoss
+    if tag == "drop":
+        masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
+        state = {"off": 0, "i": 0}
+
+        def replay(n, p, device):
+            assert n == sizes[state["i"]], (n, sizes[state["i"]])
+            m = masks[state["off"]:state["off"] + n]
+            state["off"] += n
+            state["i"] += 1
+            return torch.from_numpy(m.copy()).to(device)
+        monkeypatch.setattr(training, "_keep_scale", replay)
+    net = _student(dtype, tag == "drop")
+    crops = [torch.from_numpy(P.clip(1210 + i, (2, 3, 4, 64, 64))).cuda() for i in range(2)] + \
+            [torch.from_numpy(P.clip(1220 + i, (2, 3, 4, 32, 32))).cuda() for i in range(2)]
+    s_out = net(crops)
+    t_out = torch.from_numpy(gold[tag + "_teacher"]).cuda()
+    loss_fn = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    loss = loss_fn(s_out, t_out, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert abs(loss.item() - float(gold[tag + "_loss"])) < tol * abs(float(gold[tag + "_loss"]))
+    assert rel(s_out.detach().cpu().numpy(), gold[tag + "_student"]) < tol
+    named = [("bb." + k, p) for k, p in net.backbone.named_parameters()] + \
+            [("hd." + k, p) for k, p in net.head.named_parameters()]
+    checked = 0
+    for k, p in named:
+        key = tag + "_" + k
+        if key not in gold:
+            assert p.grad is None or not p.requires_grad, k
+            continue
+        assert p.grad is not None, k
+        err = rel(p.grad.cpu().numpy(), gold[key])
+        assert err < tol, "%s grad rel err %.3g" % (k, err)
+        checked += 1
+    assert checked >= 40
+
+
+def _ref_spatial(qkv, B, T, Np, H, scale, seq_scale=None):
+    """torch fp32 restatement of the spatial branch attention with CLS replicate / mean."""
+    C = qkv.shape[1] // 3
+    L = 1 + Np * T
+    x = qkv.view(B, L, 3, H, 64)
+    cls = x[:, :1]
+    pat = x[:, 1:].view(B, Np, T, 3, H, 64).permute(0, 2, 1, 3, 4, 5)
+    seq = torch.cat([cls.unsqueeze(1).expand(B, T, 1, 3, H, 64), pat], dim=2)
+    q, k, v = seq[:, :, :, 0], seq[:, :, :, 1], seq[:, :, :, 2]
+    a = torch.einsum("btihd,btjhd->bthij", q, k) * scale
+    o = torch.einsum("bthij,btjhd->btihd", a.softmax(-1), v)
+    if seq_scale is not None:
+        o = o * seq_scale.view(B, T, 1, 1, 1)
+    out = torch.cat([o[:, :, :1].mean(1), o[:, :, 1:].permute(0, 2, 1, 3, 4).reshape(B, Np * T, H, 64)], dim=1)
+    return out.reshape(B * L, C)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("B,T,Np,H,scaled", [(2, 3, 5, 2, False), (1, 4, 49, 3, True), (2, 8, 16, 1, True)])
+def test_attn_spatial_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled):
+    from dsvt import ops
+    C, L = H * 64, 1 + Np * T
+    g = torch.Generator(device="cuda").manual_seed(7)
+    qkv = torch.randn(B * L, 3 * C, device="cuda", generator=g).to(dtype)
+    dout = torch.randn(B * L, C, device="cuda", generator=g).to(dtype)
+    ss = (torch.rand(B * T, device="cuda", generator=g) + 0.5) if scaled else None
+    q32 = qkv.float().requires_grad_(True)
+    _ref_spatial(q32, B, T, Np, H, 0.125, ss).backward(dout.float())
+    dq = torch.empty_like(qkv)
+    ops.attn_spatial_bwd(qkv, dout, dq, B, T, L, H, 0.125, seq_scale=ss)
+    torch.cuda.synchronize()
+    assert rel(dq.float().cpu(), q32.grad.cpu()) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("T,H", [(4, 2), (8, 12), (30, 1)])
+def test_attn_temporal_bwd_vs_autograd(dtype, tol, T, H):
+    from dsvt import ops
+    nseq, C = 6, H * 64
+    g = torch.Generator(device="cuda").manual_seed(8)
+    qkv = torch.randn(nseq * T, 3 * C, device="cuda", generator=g).to(dtype)
+    dout = torch.randn(nseq * T, C, device="cuda", generator=g).to(dtype)
+    q32 = qkv.float().requires_grad_(True)
+    x = q32.view(nseq, T, 3, H, 64)
+    o = F.scaled_dot_product_attention(x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2),
+                                       x[:, :, 2].transpose(1, 2), scale=0.125)
+    o.transpose(1, 2).reshape(nseq * T, C).backward(dout.float())
+    dq = torch.empty_like(qkv)
+    ops.attn_temporal_bwd(qkv, dout, dq, nseq, T, H, 0.125)
+    torch.cuda.synchronize()
+    assert rel(dq.float().cpu(), q32.grad.cpu()) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+def test_attn_joint_bwd_vs_autograd(dtype, tol):
+    from dsvt import ops
+    nb, L, H = 2, 37, 2
+    C = H * 64
+    g = torch.Generator(device="cuda").manual_seed(9)
+    qkv = torch.randn(nb * L, 3 * C, device="cuda", generator=g).to(dtype)
+    dout = torch.randn(nb * L, C, device="cuda", generator=g).to(dtype)
+    q32 = qkv.float().requires_grad_(True)
+    x = q32.view(nb, L, 3, H, 64)
+    o = F.scaled_dot_product_attention(x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2),
+                                       x[:, :, 2].transpose(1, 2), scale=0.125)
+    o.transpose(1, 2).reshape(nb * L, C).backward(dout.float())
+    dq = torch.empty_like(qkv)
+    ops.attn_joint_bwd(qkv, dout, dq, nb, L, H, 0.125)
+    torch.cuda.synchronize()
+    assert rel(dq.float().cpu(), q32.grad.cpu()) < tol
+
+
+@pytest.mark.parametrize("C,dy_dtype", [(64, torch.float32), (768, torch.float32), (768, torch.bfloat16)])
+def test_layernorm_bwd_rowmap_vs_autograd(C, dy_dtype):
+    """dX[row(m)] += dLN for the patch rows of a [B, 1 + Np*T, C] token tensor; dgamma/dbeta."""
+    from dsvt import ops
+    B, Np, T = 3, 5, 4
+    L, R = 1 + Np * T, B * Np * T
+    g = torch.Generator(device="cuda").manual_seed(10)
+    X = torch.randn(B * L, C, device="cuda", generator=g) * 2 + 0.3
+    gamma = torch.randn(C, device="cuda", generator=g)
+    beta = torch.randn(C, device="cuda", generator=g)
+    dy = torch.randn(R, C, device="cuda", generator=g).to(dy_dtype)
+    rows = (torch.arange(R, device="cuda") // (Np * T)) * L + 1 + torch.arange(R, device="cuda") % (Np * T)
+    x32 = X[rows].clone().requires_grad_(True)
+    g32, b32 = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    F.layer_norm(x32, (C,), g32, b32, 1e-6).backward(dy.float())
+    dX0 = torch.randn(B * L, C, device="cuda", generator=g)
+    dX = dX0.clone()
+    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    ops.layernorm_bwd(X, dy, gamma, 1e-6, dX, R, dg, db, rowmap=(Np * T, L, 1))
+    torch.cuda.synchronize()
+    exp = dX0.clone()
+    exp[rows] += x32.grad
+    tol = 2e-5 if dy_dtype == torch.float32 else 1e-5
+    assert rel(dX.cpu(), exp.cpu()) < tol
+    assert rel(dg.cpu(), g32.grad.cpu()) < 1e-4 and rel(db.cpu(), b32.grad.cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+def test_gelu_save_and_dgelu_epilogues(dtype, tol):
+    """fc1 forward saving the pre-activation, and (dY.W2) * GELU'(pre) -- vs torch autograd."""
+    from dsvt import ops
+    from dsvt._lib import EPI_DGELU, EPI_GELU_SAVE
+    M, K, N = 300, 128, 256
+    g = torch.Generator(device="cuda").manual_seed(11)
+    a = torch.randn(M, K, device="cuda", generator=g).to(dtype)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.1).to(dtype)
+    b = torch.randn(N, device="cuda", generator=g)
+    h = torch.empty(M, N, device="cuda", dtype=dtype)
+    pre = torch.empty(M, N, device="cuda", dtype=dtype)
+    ops.gemm_aux(a, w, b, h, pre, EPI_GELU_SAVE)
+    pre_ref = a.float() @ w.float().t() + b
+    assert rel(pre.float().cpu(), pre_ref.cpu()) < tol
+    assert rel(h.float().cpu(), F.gelu(pre_ref).cpu()) < tol
+    w2 = (torch.randn(K, N, device="cuda", generator=g) * 0.1).to(dtype)      # fc2 weight [out=K, in=N]
+    dy = torch.randn(M, K, device="cuda", generator=g).to(dtype)
+    w2t = w2.float().t().contiguous().to(dtype)                                # W2^T [N, K]
+    dpre = torch.empty(M, N, device="cuda", dtype=dtype)
+    ops.gemm_aux(dy, w2t, None, dpre, pre, EPI_DGELU)
+    x = pre.float().requires_grad_(True)
+    F.gelu(x).backward(dy.float() @ w2.float())
+    torch.cuda.synchronize()
+    assert rel(dpre.float().cpu(), x.grad.cpu()) < tol
+
+
+def test_head_norm_and_weight_norm_bwd():
+    from dsvt import ops
+    g = torch.Generator(device="cuda").manual_seed(12)
+    x = torch.randn(7, 256, device="cuda", generator=g)
+    dz = torch.randn(7, 256, device="cuda", generator=g)
+    x32 = x.clone().requires_grad_(True)
+    F.normalize(x32, dim=-1, p=2).backward(dz)
+    dx = ops.head_norm_bwd(x, dz)
+    v = torch.randn(300, 64, device="cuda", generator=g)
+    gg = torch.rand(300, 1, device="cuda", generator=g) + 0.5
+    dw = torch.randn(300, 64, device="cuda", generator=g)
+    v32, g32 = v.clone().requires_grad_(True), gg.clone().requires_grad_(True)
+    (g32 * v32 / v32.norm(dim=1, keepdim=True)).backward(dw)
+    dv, dgb = torch.zeros_like(v), torch.zeros(300, device="cuda")
+    ops.weight_norm_bwd(v, gg, dw, dv, dgb)
+    torch.cuda.synchronize()
+    assert rel(dx.cpu(), x32.grad.cpu()) < 1e-5
+    assert rel(dv.cpu(), v32.grad.cpu()) < 1e-5 and rel(dgb.cpu(), g32.grad.view(-1).cpu()) < 1e-5
+
+
+def test_dino_loss_bwd_vs_autograd():
+    """train_ssl.py:653-669 restated in torch (fp32 autograd) vs dsvt_dino_loss_bwd."""
+    from dsvt import ops
+    g = torch.Generator(device="cuda").manual_seed(13)
+    B, ncrops, gc, D = 3, 5, 2, 1024
+    s = torch.randn(ncrops * B, D, device="cuda", generator=g)
+    t = torch.randn(gc * B, D, device="cuda", generator=g)
+    c = torch.randn(1, D, device="cuda", generator=g) * 0.1
+    s32 = s.clone().requires_grad_(True)
+    so = (s32 / 0.1).chunk(ncrops)
+    to = F.softmax((t - c) / 0.04, dim=-1).chunk(gc)
+    tot, n = 0, 0
+    for iq, q in enumerate(to):
+        for v in range(ncrops):
+            if v == iq:
+                continue
+            tot = tot + torch.sum(-q * F.log_softmax(so[v], dim=-1), dim=-1).mean()
+            n += 1
+    (tot / n * 1.7).backward()
+    ds = ops.dino_loss_bwd(s, t, c, B, ncrops, gc, 0.1, 0.04, torch.tensor([1.7], device="cuda"))
+    torch.cuda.synchronize()
+    assert rel(ds.cpu(), s32.grad.cpu()) < 1e-4
+
+
+def test_ema_and_clip_multi_tensor():
+    """train_ssl.py:555-558 EMA and utils/utils.py:102-111 per-parameter clipping."""
+    from dsvt.utils import clip_gradients_, ema_update_
+    g = torch.Generator(device="cuda").manual_seed(14)
+    shapes = [(5000,), (3, 7), (64, 64), (1,), (4097,)]
+    st = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    te = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    ref = [0.996 * b + 0.004 * a for a, b in zip(st, te)]
+    ema_update_(te, st, 0.996)
+    for a, b in zip(te, ref):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
+    grads = [torch.randn(s, device="cuda", generator=g) * (3.0 if i % 2 else 0.01) for i, s in enumerate(shapes)]
+    exp = []
+    for x in grads:
+        nrm = x.norm(2)
+        coef = 3.0 / (nrm + 1e-6)
+        exp.append(x * coef if coef < 1 else x.clone())
+    norms = clip_gradients_(grads, 3.0)
+    torch.cuda.synchronize()
+    for a, b in zip(grads, exp):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-7)
+    assert norms.shape == (len(shapes),)
