@@ -158,6 +158,57 @@ def synthetic_crops(clips, device, seed):
     return [crop(224) for _ in range(2)] + [crop(96) for _ in range(6)]
 
 
+# ----------------------------------------------------------------- config 3: SSL training step
+def train_bench(args, device, rank, world, steps, warmup):
+    """Config 3: the full DINO SSL step of train_ssl.py:466-573 per GPU --
+    teacher fwd (2 global crops) + student fwd (2 global + 6 local, DropPath 0.1 active) + DINO
+    loss with the RCCL center all-reduce + student backward on libdsvt with the DDP bucketed
+    RCCL gradient all-reduce (world > 1) + per-parameter clipping + AdamW + teacher EMA.
+    Weak scaling: `--clips` per GPU; value = all ranks' clips / max-over-ranks time."""
+    from dsvt import dist as ddist
+    from dsvt.trainer import DINOTrainer
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    student, teacher, dino_loss = build(dtype, device, seed=0)
+    for p in student.parameters():
+        p.requires_grad_(True)
+    student.train()
+    teacher.eval()          # the reference never sets eval on the teacher (SURVEY §5 defect 2); dsvt does
+    ddp = None
+    if world > 1:
+        ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[device.index],
+                                                        gradient_as_bucket_view=True, broadcast_buffers=False)
+    trainer = DINOTrainer(student, teacher, dino_loss, ddp=ddp, niter_per_ep=1000, epochs=100)
+    crops = synthetic_crops(args.clips, device, seed=4321 + rank)
+    for i in range(warmup):
+        trainer.step(crops, 2000 + i)       # past warm-up / first epoch: the last layer trains too
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = trainer.step(crops, 2000 + warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = ddist.max_over_ranks(time.perf_counter() - t0, device)
+    loss_val = float(loss.item())
+    if not np.isfinite(loss_val):
+        raise SystemExit("bench: non-finite training loss %r" % loss_val)
+    g, l = vit_fwd_flops(8, 224), vit_fwd_flops(8, 96)
+    fwd_s = 2 * g + 6 * l + 8 * head_flops()
+    clip_gf = (2 * g + 2 * head_flops() + 3 * fwd_s) / 1e9      # teacher fwd + student fwd + 2x-fwd backward
+    value = world * args.clips * steps / elapsed
+    del trainer, student, teacher
+    return {"metric": "clips/sec (DINO SSL train step: teacher fwd + student fwd/bwd + RCCL grad/center "
+                      "all-reduce + AdamW + EMA)",
+            "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "gflop_per_clip": round(clip_gf, 1),
+            "tflops_per_gpu": round(value * clip_gf / 1e3 / world, 1), "loss": round(loss_val, 5),
+            "parallelism": "dp%d (DDP, RCCL bucketed all-reduce)" % world if world > 1 else "dp1",
+            "drop_path": 0.1, "teacher_mode": "eval"}
+
+
 # ----------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -172,6 +223,8 @@ def main():
                     help="run the backbone calls one after another (no stream overlap)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
+    ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
+    ap.add_argument("--train-steps", type=int, default=5)
     args = ap.parse_args()
 
     from dsvt import dist as ddist
@@ -304,6 +357,10 @@ def main():
                              "frac_reference_flops": round(value * clip_flops() / 1e12 / world
                                                            / PEAK_TFLOPS[args.dtype], 4)},
            "roofline": roofline, "loss": round(loss_val, 5)}
+    if not args.no_train:
+        graph = None                        # release the captured forward's memory pool
+        torch.cuda.empty_cache()
+        out["train_step"] = train_bench(args, device, rank, world, args.train_steps, 2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -31,59 +31,85 @@ namespace dsvt {
 // ================================================================ LayerNorm backward
 // x: fp32 rows through the row map (the saved residual stream), dy: compact rows [rows, C]
 // (storage dtype or fp32), dx: fp32 with x's layout (the residual gradient) -- dx[row] += dLN.
-// One wave per row (grid-stride), lane owns columns c = i*64 + lane; dgamma / dbeta are
-// accumulated in registers, reduced over the 4 waves in LDS and written per block.
-template <typename DyT>
+// One wave per row (grid-stride).  VEC (C % 256 == 0): lane owns columns i*256 + 4*lane + e
+// (16-B x / dx accesses); else columns i*64 + lane.  dgamma / dbeta are accumulated in
+// registers, reduced over the 4 waves in LDS and written per block.
+template <typename DyT, bool VEC>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
                                                      const float* __restrict__ gamma, float* __restrict__ dx,
                                                      int64_t rows, int C, int64_t rpg, int64_t gstride, int64_t goff,
                                                      float eps, float* __restrict__ partial) {
   __shared__ float red[4][2][1024];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n = C >> 6;
+  const int n = VEC ? 4 * (C >> 8) : (C >> 6);                 // slots in use (<= 16)
+  auto col = [&](int k) { return VEC ? (k >> 2) * 256 + lane * 4 + (k & 3) : k * 64 + lane; };
   float dg[16], db[16], g[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    dg[i] = 0.f; db[i] = 0.f;
-    g[i] = i < n ? gamma[i * 64 + lane] : 0.f;
+  for (int k = 0; k < 16; ++k) {
+    dg[k] = 0.f; db[k] = 0.f;
+    g[k] = k < n ? gamma[col(k)] : 0.f;
   }
   for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
     const int64_t xr = map_row(r, rpg, gstride, goff) * C;
     float v[16], d[16];
     float s = 0.f;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < n) {
-        v[i] = x[xr + i * 64 + lane];
-        d[i] = Elem<DyT>::to_f(dy[r * C + i * 64 + lane]);
-        s += v[i];
-      }
+      for (int i = 0; i < 4; ++i)
+        if (4 * i < n) {
+          load4(x + xr + i * 256 + lane * 4, v + 4 * i);
+          load4(dy + r * C + i * 256 + lane * 4, d + 4 * i);
+          s += (v[4 * i] + v[4 * i + 1]) + (v[4 * i + 2] + v[4 * i + 3]);
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < n) {
+          v[k] = x[xr + col(k)];
+          d[k] = Elem<DyT>::to_f(dy[r * C + col(k)]);
+          s += v[k];
+        }
+    }
     const float mean = wave_sum(s) / C;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < n) { v[i] -= mean; q += v[i] * v[i]; }
+    for (int k = 0; k < 16; ++k)
+      if (k < n) { v[k] -= mean; q += v[k] * v[k]; }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < n) {
-        const float xh = v[i] * rstd, gd = g[i] * d[i];
-        v[i] = xh;
+    for (int k = 0; k < 16; ++k)
+      if (k < n) {
+        const float xh = v[k] * rstd, gd = g[k] * d[k];
+        v[k] = xh;
         s1 += gd;
         s2 += gd * xh;
-        dg[i] += d[i] * xh;
-        db[i] += d[i];
+        dg[k] += d[k] * xh;
+        db[k] += d[k];
       }
     s1 = wave_sum(s1) / C;
     s2 = wave_sum(s2) / C;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < n) dx[xr + i * 64 + lane] += rstd * (g[i] * d[i] - s1 - v[i] * s2);
+      for (int i = 0; i < 4; ++i)
+        if (4 * i < n) {
+          float4* p = reinterpret_cast<float4*>(dx + xr + i * 256 + lane * 4);
+          float4 o = *p;
+          o.x += rstd * (g[4 * i] * d[4 * i] - s1 - v[4 * i] * s2);
+          o.y += rstd * (g[4 * i + 1] * d[4 * i + 1] - s1 - v[4 * i + 1] * s2);
+          o.z += rstd * (g[4 * i + 2] * d[4 * i + 2] - s1 - v[4 * i + 2] * s2);
+          o.w += rstd * (g[4 * i + 3] * d[4 * i + 3] - s1 - v[4 * i + 3] * s2);
+          *p = o;
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < n) dx[xr + col(k)] += rstd * (g[k] * d[k] - s1 - v[k] * s2);
+    }
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (i < n) { red[wave][0][i * 64 + lane] = dg[i]; red[wave][1][i * 64 + lane] = db[i]; }
+  for (int k = 0; k < 16; ++k)
+    if (k < n) { red[wave][0][col(k)] = dg[k]; red[wave][1][col(k)] = db[k]; }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
     partial[(int64_t)blockIdx.x * 2 * C + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
@@ -100,51 +126,75 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
                          int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* partial,
                          hipStream_t s) {
   const int nb = ln_bwd_blocks(rows);
-  if (dy_dtype == 0)
-    ln_bwd_kernel<bf16_t><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, (int)C, rpg, gstride, goff, eps,
-                                             partial);
-  else
-    ln_bwd_kernel<float><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, (int)C, rpg, gstride, goff, eps,
-                                            partial);
+#define DSVT_LNB(T, V) ln_bwd_kernel<T, V><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, gstride, \
+                                                             goff, eps, partial)
+  if (C % 256 == 0) {
+    if (dy_dtype == 0) DSVT_LNB(bf16_t, true); else DSVT_LNB(float, true);
+  } else {
+    if (dy_dtype == 0) DSVT_LNB(bf16_t, false); else DSVT_LNB(float, false);
+  }
+#undef DSVT_LNB
   return hipGetLastError();
 }
 
 // ================================================================ column sums (bias grads)
+// Block = 64 column groups of 4 (256 columns, 8-/16-B loads) x 4 row lanes; grid.y = row chunks.
+// Each thread sums its 4 columns over the chunk's rows r = lane_row (mod 4); the 4 row lanes are
+// combined in LDS and the block writes one partial row.  C % 4 == 0.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ y, int64_t rows, int64_t C,
                                                              int64_t ld, int64_t rpg, int64_t gstride, int64_t goff,
                                                              const float* __restrict__ row_scale, int64_t chunk,
                                                              float* __restrict__ partial) {
+  __shared__ float4 red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.y * chunk;
   const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float a0 = 0.f, a1 = 0.f;
-  int64_t r = r0;
-  for (; r + 1 < r1; r += 2) {
-    float v0 = Elem<T>::to_f(y[map_row(r, rpg, gstride, goff) * ld + c]);
-    float v1 = Elem<T>::to_f(y[map_row(r + 1, rpg, gstride, goff) * ld + c]);
-    if (row_scale) { v0 *= row_scale[r]; v1 *= row_scale[r + 1]; }
-    a0 += v0;
-    a1 += v1;
+  const int64_t c = ((int64_t)blockIdx.x * 64 + tx) * 4;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    for (int64_t r = r0 + ty; r < r1; r += 4) {
+      float v[4];
+      load4(y + map_row(r, rpg, gstride, goff) * ld + c, v);
+      const float sc = row_scale ? row_scale[r] : 1.0f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = fmaf(v[e], sc, a[e]);
+    }
   }
-  if (r < r1) a0 += Elem<T>::to_f(y[map_row(r, rpg, gstride, goff) * ld + c]) * (row_scale ? row_scale[r] : 1.0f);
-  partial[(int64_t)blockIdx.y * C + c] = a0 + a1;
+  red[ty][tx] = make_float4(a[0], a[1], a[2], a[3]);
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    const float4 p0 = red[0][tx], p1 = red[1][tx], p2 = red[2][tx], p3 = red[3][tx];
+    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.y * C + c) =
+        make_float4((p0.x + p1.x) + (p2.x + p3.x), (p0.y + p1.y) + (p2.y + p3.y), (p0.z + p1.z) + (p2.z + p3.z),
+                    (p0.w + p1.w) + (p2.w + p3.w));
+  }
 }
 
+// out[c] (+)= sum_p partial[p*stride + c]: block = 32 columns x 8 part lanes, LDS combine
+// (fixed order -> deterministic)
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ partial, int64_t nparts,
                                                               int64_t width, int64_t stride, float* __restrict__ out,
                                                               int accumulate) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= width) return;
+  __shared__ float red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t c = (int64_t)blockIdx.x * 32 + tx;
   float a = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) a += partial[p * stride + c];
-  out[c] = accumulate ? out[c] + a : a;
+  if (c < width)
+    for (int64_t p = ty; p < nparts; p += 8) a += partial[p * stride + c];
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < width) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += red[k][tx];
+    out[c] = accumulate ? out[c] + s : s;
+  }
 }
 
 int64_t colsum_parts(int64_t rows) {
-  int64_t p = (rows + 127) / 128;
-  return p < 1 ? 1 : (p > 256 ? 256 : p);
+  int64_t p = (rows + 63) / 64;
+  return p < 1 ? 1 : (p > 128 ? 128 : p);
 }
 
 hipError_t launch_colsum_rows(int dtype, const void* y, int64_t rows, int64_t C, int64_t ld, int64_t rpg,
@@ -159,14 +209,14 @@ hipError_t launch_colsum_rows(int dtype, const void* y, int64_t rows, int64_t C,
     colsum_partial_kernel<float><<<grid, 256, 0, s>>>((const float*)y, rows, C, ld, rpg, gstride, goff, row_scale,
                                                       chunk, partial);
   if (hipError_t e = hipGetLastError()) return e;
-  reduce_partials_kernel<<<(unsigned)((C + 255) / 256), 256, 0, s>>>(partial, parts, C, C, out, accumulate);
+  reduce_partials_kernel<<<(unsigned)((C + 31) / 32), 256, 0, s>>>(partial, parts, C, C, out, accumulate);
   return hipGetLastError();
 }
 
 hipError_t launch_reduce_partials(const float* partial, int64_t nparts, int64_t width, int64_t stride, float* out,
                                   int accumulate, hipStream_t s) {
-  reduce_partials_kernel<<<(unsigned)((width + 255) / 256), 256, 0, s>>>(partial, nparts, width, stride, out,
-                                                                         accumulate);
+  reduce_partials_kernel<<<(unsigned)((width + 31) / 32), 256, 0, s>>>(partial, nparts, width, stride, out,
+                                                                       accumulate);
   return hipGetLastError();
 }
 
@@ -423,10 +473,256 @@ __global__ __launch_bounds__(256) void cls_sum_kernel(const float* __restrict__ 
   dqkv[b * L * ld + c] = Elem<T>::from_f(a);
 }
 
+// ---------------------------------------------------------------- bf16 MFMA, whole sequence in LDS
+// One workgroup per (sequence, head) with Q, K, V and dO of the whole sequence (<= 16*NKT rows)
+// staged in LDS (bf16, 72-element rows; rows past the sequence are zero).  Same MFMA
+// decomposition as the forward attn_short_bf16 (attention.hip): 16x16x32 bf16 tiles,
+// ds_read_b64_tr_b16 for the transposed operands, the k-slot permutation for P-like B operands.
+//   phase 1 (wave per 16-query tile): S^T = K.Q^T and dP^T = V.dO^T (lane = query, 4 keys per
+//     tile), P = softmax, D = sum_k P dP, dS = P (dP - D), dQ^T = K^T.dS^T; the row statistic
+//     M2 = max*c + log2(sum) and D go to LDS;
+//   phase 2 (wave per 16-key tile): S = Q.K^T and dP = dO.V^T (lane = key, 4 queries per tile),
+//     P = exp2(S c - M2[q]), dS = P (dP - D[q]); dV^T += dO^T.P and dK^T += Q^T.dS over 32-query
+//     steps.
+// Every tile loop is straight-line code (see attn_short_bf16 on MFMA result hazards under
+// branches); per-lane stores are fenced.
+constexpr int BKV = 72;   // bf16 per LDS row
+
+template <int NKT, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_short_bf16(AttnBwdParams p) {
+  constexpr int NKP = (NKT + 1) / 2, SN = 2 * NKP, LP = NKP * 32;
+  constexpr int NT = 64 * NW, PCS = (LP * 8 + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) bf16_t sm[4][LP * BKV];   // Q, K, V, dO
+  __shared__ float m2s[LP], dds[LP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.x;
+  const int64_t seq = blockIdx.y, b = seq / p.tin, t = seq % p.tin;
+  const int L = (int)p.seqlen;
+  const bf16_t* qkv = (const bf16_t*)p.qkv;
+  const bf16_t* dout = (const bf16_t*)p.dout;
+  const int64_t C = p.C;
+  const float ssc = p.seq_scale ? p.seq_scale[seq] : 1.0f;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  // ---- stage Q, K, V, dO (dO scaled by the DropPath scale and, for the CLS row, 1/T)
+#pragma unroll
+  for (int i = 0; i < PCS; ++i) {
+    const int pc = tid + NT * i, r = pc >> 3, ch = pc & 7;
+    if (r < LP) {
+      uint4 vq = make_uint4(0, 0, 0, 0), vk = vq, vv = vq, vd = vq;
+      if (r < L) {
+        const int64_t row = brow(p, b, t, r);
+        const bf16_t* src = qkv + row * p.ld_qkv + h * 64 + ch * 8;
+        vq = *reinterpret_cast<const uint4*>(src);
+        vk = *reinterpret_cast<const uint4*>(src + C);
+        vv = *reinterpret_cast<const uint4*>(src + 2 * C);
+        vd = *reinterpret_cast<const uint4*>(dout + row * p.ld_dout + h * 64 + ch * 8);
+        const float sc = ssc * ((r == 0 && p.cls_aux) ? p.cls_scale : 1.0f);
+        if (sc != 1.0f) {
+          unsigned* u = reinterpret_cast<unsigned*>(&vd);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = pack_bf16x2(bf16_lo(u[e]) * sc, bf16_hi(u[e]) * sc);
+        }
+      }
+      *reinterpret_cast<uint4*>(&sm[0][r * BKV + ch * 8]) = vq;
+      *reinterpret_cast<uint4*>(&sm[1][r * BKV + ch * 8]) = vk;
+      *reinterpret_cast<uint4*>(&sm[2][r * BKV + ch * 8]) = vv;
+      *reinterpret_cast<uint4*>(&sm[3][r * BKV + ch * 8]) = vd;
+    }
+  }
+  __syncthreads();
+  const bf16_t* Qs = sm[0];
+  const bf16_t* Ks = sm[1];
+  const bf16_t* Vs = sm[2];
+  const bf16_t* Ds = sm[3];
+  const int nkt = (L + 15) >> 4;
+  typedef __attribute__((address_space(3))) sv4* LDS4;
+
+  // ================= phase 1: dQ, row statistics
+  for (int qt = wave; qt < nkt; qt += NW) {
+    const bf16_t* qr = Qs + (qt * 16 + r16) * BKV + g * 8;
+    const bf16_t* dr = Ds + (qt * 16 + r16) * BKV + g * 8;
+    const sv8 qf0 = *reinterpret_cast<const sv8*>(qr), qf1 = *reinterpret_cast<const sv8*>(qr + 32);
+    const sv8 df0 = *reinterpret_cast<const sv8*>(dr), df1 = *reinterpret_cast<const sv8*>(dr + 32);
+    fv4 s[SN], dp[SN];
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+      const bf16_t* kr = Ks + (kt * 16 + r16) * BKV + g * 8;
+      const bf16_t* vr = Vs + (kt * 16 + r16) * BKV + g * 8;
+      fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(kr), qf0, z, 0, 0, 0);
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(kr + 32), qf1, z, 0, 0, 0);
+      fv4 y = fv4{0.f, 0.f, 0.f, 0.f};
+      y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(vr), df0, y, 0, 0, 0);
+      dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(vr + 32), df1, y, 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[kt][j] = (kt * 16 + 4 * g + j < L) ? s[kt][j] : -INFINITY;
+      mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mxs = mx * sl2;
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[kt][j] = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));
+        rs += s[kt][j];
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    const float inv = 1.0f / rs;
+    float D = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[kt][j] *= inv;                    // P
+        D = fmaf(s[kt][j], dp[kt][j], D);
+      }
+    D += __shfl_xor(D, 16, 64);
+    D += __shfl_xor(D, 32, 64);
+    // dQ^T = K^T . dS^T (K^T fragments by transposed LDS reads; dS in the P.V k-slot order)
+    fv4 dq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dq[d] = fv4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kp = 0; kp < NKP; ++kp) {
+      sv8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[2 * kp][j] * (dp[2 * kp][j] - D));
+        pb[4 + j] = (short)f2bf(s[2 * kp + 1][j] * (dp[2 * kp + 1][j] - D));
+      }
+      const int kr0 = kp * 32 + 4 * g + (r16 >> 2), kr1 = kr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ks + kr0 * BKV + col));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ks + kr1 * BKV + col));
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                                         pb, dq[dt], 0, 0, 0);
+      }
+    }
+    mfma_result_fence();
+    const int qo = qt * 16 + r16;
+    if (g == 0) {
+      m2s[qo] = qo < L ? mxs + __log2f(rs) : INFINITY;
+      dds[qo] = qo < L ? D : 0.f;
+    }
+    if (qo < L) {
+      if (qo == 0 && p.cls_aux) {
+        float* dst = p.cls_aux + seq * 3 * C + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          store4(dst + dt * 16, dq[dt][0] * p.scale, dq[dt][1] * p.scale, dq[dt][2] * p.scale, dq[dt][3] * p.scale);
+      } else {
+        bf16_t* dst = (bf16_t*)p.dqkv + brow(p, b, t, qo) * p.ld_dqkv + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          store4(dst + dt * 16, dq[dt][0] * p.scale, dq[dt][1] * p.scale, dq[dt][2] * p.scale, dq[dt][3] * p.scale);
+      }
+    }
+  }
+  // query rows of tiles past the sequence (whole 32-row PV steps): P = 0
+  for (int q = nkt * 16 + tid; q < LP; q += NT) { m2s[q] = INFINITY; dds[q] = 0.f; }
+  __syncthreads();
+
+  // ================= phase 2: dK, dV
+  for (int kt = wave; kt < nkt; kt += NW) {
+    const bf16_t* kr = Ks + (kt * 16 + r16) * BKV + g * 8;
+    const bf16_t* vr = Vs + (kt * 16 + r16) * BKV + g * 8;
+    const sv8 kf0 = *reinterpret_cast<const sv8*>(kr), kf1 = *reinterpret_cast<const sv8*>(kr + 32);
+    const sv8 vf0 = *reinterpret_cast<const sv8*>(vr), vf1 = *reinterpret_cast<const sv8*>(vr + 32);
+    fv4 dk[4], dv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) { dk[d] = fv4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+#pragma unroll
+    for (int qp = 0; qp < NKP; ++qp) {
+      fv4 P[2], dS[2];
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        const int q0 = (2 * qp + hq) * 16;
+        const bf16_t* qr = Qs + (q0 + r16) * BKV + g * 8;
+        const bf16_t* dr = Ds + (q0 + r16) * BKV + g * 8;
+        fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(qr), kf0, z, 0, 0, 0);
+        const fv4 sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(qr + 32), kf1, z, 0, 0, 0);
+        fv4 y = fv4{0.f, 0.f, 0.f, 0.f};
+        y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(dr), vf0, y, 0, 0, 0);
+        const fv4 dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(dr + 32), vf1, y, 0, 0, 0);
+        // lane (key r16) holds queries q0 + 4g + j
+        const float4 m2 = *reinterpret_cast<const float4*>(&m2s[q0 + 4 * g]);
+        const float4 dd = *reinterpret_cast<const float4*>(&dds[q0 + 4 * g]);
+        const float mm[4] = {m2.x, m2.y, m2.z, m2.w}, D4[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          P[hq][j] = __builtin_amdgcn_exp2f(fmaf(sc[j], sl2, -mm[j]));
+          dS[hq][j] = P[hq][j] * (dpv[j] - D4[j]);
+        }
+      }
+      sv8 pb, sb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(P[0][j]);
+        pb[4 + j] = (short)f2bf(P[1][j]);
+        sb[j] = (short)f2bf(dS[0][j]);
+        sb[4 + j] = (short)f2bf(dS[1][j]);
+      }
+      const int qr0 = qp * 32 + 4 * g + (r16 >> 2), qr1 = qr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 dlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ds + qr0 * BKV + col));
+        const sv4 dhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ds + qr1 * BKV + col));
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(dlo, dhi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                                         pb, dv[dt], 0, 0, 0);
+        const sv4 qlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Qs + qr0 * BKV + col));
+        const sv4 qhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Qs + qr1 * BKV + col));
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(qlo, qhi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                                         sb, dk[dt], 0, 0, 0);
+      }
+    }
+    mfma_result_fence();
+    const int ko = kt * 16 + r16;
+    if (ko < L) {
+      if (ko == 0 && p.cls_aux) {
+        float* dst = p.cls_aux + seq * 3 * C + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          store4(dst + C + dt * 16, dk[dt][0] * p.scale, dk[dt][1] * p.scale, dk[dt][2] * p.scale, dk[dt][3] * p.scale);
+          store4(dst + 2 * C + dt * 16, dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+        }
+      } else {
+        bf16_t* dst = (bf16_t*)p.dqkv + brow(p, b, t, ko) * p.ld_dqkv + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          store4(dst + C + dt * 16, dk[dt][0] * p.scale, dk[dt][1] * p.scale, dk[dt][2] * p.scale, dk[dt][3] * p.scale);
+          store4(dst + 2 * C + dt * 16, dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+        }
+      }
+    }
+  }
+}
+
+static int g_attn_bwd_variant = 0;   // 0 = auto, 1 = force the generic VALU kernels (tests / tools)
+void set_attn_bwd_variant(int v) { g_attn_bwd_variant = v; }
+
 hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s) {
   const int64_t items = p.nb * p.tin * p.heads * p.seqlen;
   const unsigned blocks = (unsigned)((items * 16 + 255) / 256);
-  if (dtype == 0) {
+  if (dtype == 0 && p.seqlen <= 256 && g_attn_bwd_variant == 0) {
+    dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
+    if (p.seqlen <= 64) attn_bwd_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
+    else if (p.seqlen <= 208) attn_bwd_short_bf16<13, 8><<<grid, 512, 0, s>>>(p);
+    else attn_bwd_short_bf16<16, 8><<<grid, 512, 0, s>>>(p);
+  } else if (dtype == 0) {
     attn_rows_bwd<bf16_t><<<blocks, 256, 0, s>>>(p);
     attn_cols_bwd<bf16_t><<<blocks, 256, 0, s>>>(p);
   } else {

@@ -388,6 +388,12 @@ int dsvt_set_attn_variant(int variant) {
   return 0;
 }
 
+int dsvt_set_attn_bwd_variant(int variant) {
+  REQUIRE(variant == 0 || variant == 1, "attention backward variant must be 0 (auto) or 1 (generic VALU)");
+  set_attn_bwd_variant(variant);
+  return 0;
+}
+
 int dsvt_probe_enable(int mask, int capacity) {
   g_probe.clear();
   REQUIRE(capacity > 0 && capacity <= (1 << 20), "probe: bad capacity");
@@ -470,7 +476,8 @@ int dsvt_colsum_bwd(int dtype, const void* y, int64_t rows, int64_t C, int64_t l
                     int64_t goff, const float* row_scale, float* out, int accumulate, void* workspace,
                     int64_t workspace_bytes, void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "colsum: bad dtype");
-  REQUIRE(y && out && rows > 0 && C > 0 && ld >= C, "colsum: bad args");
+  REQUIRE(y && out && rows > 0 && C > 0 && ld >= C && C % 4 == 0 && ld % 4 == 0 && aligned16(out),
+          "colsum: bad args (C, ld multiples of 4)");
   REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_COLSUM, 1, rows, C, 0), "colsum: workspace too small");
   norm_map(rpg, gstride, goff);
   hipError_t e = launch_colsum_rows(dtype, y, rows, C, ld, rpg, gstride, goff, row_scale, (float*)workspace, out,

@@ -90,6 +90,7 @@ hipError_t launch_colsum_rows(int dtype, const void* y, int64_t rows, int64_t C,
 hipError_t launch_attn_temporal_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nseq, int64_t T,
                                     int64_t heads, int64_t C, float scale, hipStream_t s);
 hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s);
+void set_attn_bwd_variant(int v);
 hipError_t launch_dino_loss_bwd(const float* student, const float* teacher, const float* center, int64_t B,
                                 int64_t ncrops, int64_t gc, int64_t D, float inv_ts, float inv_tt, const float* t_m,
                                 const float* t_z, const float* s_m, const float* s_z, const float* dloss, float coef,

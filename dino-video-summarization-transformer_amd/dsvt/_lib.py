@@ -64,6 +64,7 @@ SIGNATURES = {
     "dsvt_clip_grads": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _f32, _p, _p, _i64, _p]),
     "dsvt_set_gemm_variant": (_i32, [_i32]),
     "dsvt_set_attn_variant": (_i32, [_i32]),
+    "dsvt_set_attn_bwd_variant": (_i32, [_i32]),
     "dsvt_probe_enable": (_i32, [_i32, _i32]),
     "dsvt_probe_disable": (_i32, []),
     "dsvt_probe_read": (_i32, [_p, _p, _p, _p, _i32]),

@@ -1,0 +1,68 @@
+"""One DINO-SVT SSL training step (train_ssl.py:466-573, `train_one_epoch` body) on dsvt:
+
+  student(all crops) [DDP] -> teacher(global crops) [no grad] -> DINOLoss (center all-reduce)
+  -> backward (DDP bucketed all-reduce of the student gradients over RCCL)
+  -> per-parameter gradient clipping -> cancel last-layer grads in the first epoch(s)
+  -> AdamW with the lr / wd schedules -> teacher EMA (one multi-tensor launch)
+
+Differences from the reference loop, all deliberate and documented:
+  * no fp16 GradScaler: dsvt computes in bf16 storage / fp32 accumulate with fp32 master
+    weights and fp32 gradients (no loss scaling needed);
+  * the non-finite-loss check reads the loss once per step like the reference (optional,
+    `check_finite`), but clipping returns device-side norms instead of 254 .item() syncs.
+"""
+import math
+
+import torch
+
+from .training import np_cosine_scheduler
+from .utils import cancel_gradients_last_layer, clip_gradients, ema_update_, get_params_groups
+
+
+class DINOTrainer:
+    def __init__(self, student, teacher, dino_loss, lr=5e-4, min_lr=1e-6, weight_decay=0.04, weight_decay_end=0.4,
+                 momentum_teacher=0.996, clip_grad=3.0, freeze_last_layer=1, epochs=100, niter_per_ep=1000,
+                 warmup_epochs=10, n_global=2, ddp=None):
+        self.student = student                      # MultiCropWrapper (possibly DDP-wrapped: ddp)
+        self.model = ddp if ddp is not None else student
+        self.teacher = teacher
+        self.dino_loss = dino_loss
+        self.clip_grad = clip_grad
+        self.freeze_last_layer = freeze_last_layer
+        self.n_global = n_global
+        self.niter_per_ep = niter_per_ep
+        # train_ssl.py:367-407: schedules
+        self.lr_schedule = np_cosine_scheduler(lr, min_lr, epochs, niter_per_ep, warmup_epochs=warmup_epochs)
+        self.wd_schedule = np_cosine_scheduler(weight_decay, weight_decay_end, epochs, niter_per_ep)
+        self.momentum_schedule = np_cosine_scheduler(momentum_teacher, 1, epochs, niter_per_ep)
+        groups = get_params_groups(student)
+        try:
+            self.optimizer = torch.optim.AdamW(groups, fused=True)
+        except (RuntimeError, TypeError):  # pragma: no cover
+            self.optimizer = torch.optim.AdamW(groups, foreach=True)
+        for p in teacher.parameters():
+            p.requires_grad_(False)
+        self._s_params = [p for p in student.parameters()]
+        self._t_params = [p for p in teacher.parameters()]
+
+    def step(self, images, it, check_finite=False):
+        epoch = it // self.niter_per_ep
+        for i, pg in enumerate(self.optimizer.param_groups):       # train_ssl.py:486-490
+            pg["lr"] = float(self.lr_schedule[it])
+            if i == 0:
+                pg["weight_decay"] = float(self.wd_schedule[it])
+        with torch.no_grad():
+            t_out = self.teacher(images[:self.n_global])           # :527 (teacher on global views)
+        s_out = self.model(images)                                 # :528
+        loss = self.dino_loss(s_out, t_out, epoch)
+        if check_finite and not math.isfinite(loss.item()):        # :530-532
+            raise FloatingPointError("Loss is %s, stopping training" % loss.item())
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.clip_grad:
+            clip_gradients(self.student, self.clip_grad)           # :547-548
+        cancel_gradients_last_layer(epoch, self.student, self.freeze_last_layer)
+        self.optimizer.step()
+        with torch.no_grad():                                      # :555-558 EMA
+            ema_update_(self._t_params, self._s_params, float(self.momentum_schedule[it]))
+        return loss

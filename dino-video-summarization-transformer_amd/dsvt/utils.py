@@ -154,10 +154,13 @@ def ema_update_(teacher_tensors, student_tensors, momentum):
     (train_ssl.py:555-558 loops param by param)."""
     from . import ops
     from ._lib import call
-    tl, tptr = _tensor_list(list(teacher_tensors))
+    teacher_tensors = list(teacher_tensors)
+    tl, tptr = _tensor_list(teacher_tensors)
     _, sptr = _tensor_list(list(student_tensors))
     call("dsvt_ema", tptr.data_ptr(), sptr.data_ptr(), tl.sizes.data_ptr(), tl.ctensor.data_ptr(),
          tl.cstart.data_ptr(), tl.nchunks, float(momentum), ops._stream())
+    for t in teacher_tensors:   # written behind autograd's back: bump the version counters so the
+        torch.autograd.graph.increment_version(t)   # storage-dtype weight caches refresh
 
 
 def clip_gradients_(grads, clip):
@@ -165,7 +168,8 @@ def clip_gradients_(grads, clip):
     < 1) over a gradient list in three launches, no host sync; returns the norms (device)."""
     from . import ops
     from ._lib import call
-    tl, gptr = _tensor_list(list(grads))
+    grads = list(grads)
+    tl, gptr = _tensor_list(grads)
     norms = torch.empty(len(tl.tensors), device=tl.sizes.device, dtype=torch.float32)
     ws = torch.empty(tl.nchunks, device=tl.sizes.device, dtype=torch.float32)
     call("dsvt_clip_grads", gptr.data_ptr(), tl.sizes.data_ptr(), tl.ctensor.data_ptr(), tl.cstart.data_ptr(),

@@ -275,6 +275,9 @@ int dsvt_set_gemm_variant(int variant);
  * (5, 6: diagnostic builds of 3).
  * Process-global. */
 int dsvt_set_attn_variant(int variant);
+/* Tuning knob (tests only): attention backward, 0 = automatic (bf16 MFMA kernel for sequences
+ * <= 256), 1 = the generic two-pass VALU kernels.  Process-global. */
+int dsvt_set_attn_bwd_variant(int variant);
 
 /* Measurement probe: when enabled, every launch of a family in `mask` is bracketed by a
  * pair of hipEvents on its own stream (diagnostic; not thread-safe). */

@@ -113,10 +113,22 @@ def _ref_spatial(qkv, B, T, Np, H, scale, seq_scale=None):
     return out.reshape(B * L, C)
 
 
+@pytest.fixture(params=[0, 1], ids=["auto", "generic"])
+def attn_bwd_variant(request):
+    """bf16: the MFMA whole-sequence kernel (auto, L <= 256) and the generic VALU kernels."""
+    from dsvt import _lib
+    _lib.call("dsvt_set_attn_bwd_variant", request.param)
+    yield request.param
+    _lib.call("dsvt_set_attn_bwd_variant", 0)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
-@pytest.mark.parametrize("B,T,Np,H,scaled", [(2, 3, 5, 2, False), (1, 4, 49, 3, True), (2, 8, 16, 1, True)])
-def test_attn_spatial_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled):
+@pytest.mark.parametrize("B,T,Np,H,scaled", [(2, 3, 5, 2, False), (1, 4, 49, 3, True), (2, 8, 16, 1, True),
+                                              (2, 8, 196, 2, True), (1, 1, 224, 1, False)])
+def test_attn_spatial_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled, attn_bwd_variant):
     from dsvt import ops
+    if dtype == torch.float32 and attn_bwd_variant:
+        pytest.skip("fp32 has one (generic) kernel")
     C, L = H * 64, 1 + Np * T
     g = torch.Generator(device="cuda").manual_seed(7)
     qkv = torch.randn(B * L, 3 * C, device="cuda", generator=g).to(dtype)
@@ -124,10 +136,14 @@ def test_attn_spatial_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled):
     ss = (torch.rand(B * T, device="cuda", generator=g) + 0.5) if scaled else None
     q32 = qkv.float().requires_grad_(True)
     _ref_spatial(q32, B, T, Np, H, 0.125, ss).backward(dout.float())
-    dq = torch.empty_like(qkv)
-    ops.attn_spatial_bwd(qkv, dout, dq, B, T, L, H, 0.125, seq_scale=ss)
+    outs = []
+    for _ in range(2):
+        dq = torch.full_like(qkv, 7.0)
+        ops.attn_spatial_bwd(qkv, dout, dq, B, T, L, H, 0.125, seq_scale=ss)
+        outs.append(dq)
     torch.cuda.synchronize()
-    assert rel(dq.float().cpu(), q32.grad.cpu()) < tol
+    assert torch.equal(outs[0], outs[1]), "repeat launches differ"
+    assert rel(outs[0].float().cpu(), q32.grad.cpu()) < tol
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
@@ -150,9 +166,12 @@ def test_attn_temporal_bwd_vs_autograd(dtype, tol, T, H):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
-def test_attn_joint_bwd_vs_autograd(dtype, tol):
+@pytest.mark.parametrize("L", [37, 200, 250, 300])
+def test_attn_joint_bwd_vs_autograd(dtype, tol, L, attn_bwd_variant):
     from dsvt import ops
-    nb, L, H = 2, 37, 2
+    if dtype == torch.float32 and attn_bwd_variant:
+        pytest.skip("fp32 has one (generic) kernel")
+    nb, H = 2, 2
     C = H * 64
     g = torch.Generator(device="cuda").manual_seed(9)
     qkv = torch.randn(nb * L, 3 * C, device="cuda", generator=g).to(dtype)
