@@ -118,8 +118,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
 }
 
 int ln_bwd_blocks(int64_t rows) {
-  int64_t b = (rows + 31) / 32;   // >= 8 rows per wave
-  return (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
+  int64_t b = (rows + 15) / 16;   // >= 4 rows per wave
+  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
 }
 
 hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
@@ -948,26 +948,34 @@ hipError_t launch_cast_transpose(int dtype, const float* x, void* y, int64_t R, 
 // ================================================================ token-embedding gradients
 // Token gradient dX [B, L = 1 + Np*T, C] (NT order).  gn[n][c] = sum_{b,t} dX[b][1 + n*T + t][c],
 // gt[t][c] = sum_{b,n} dX[b][1 + n*T + t][c], gc[c] = sum_b dX[b][0][c].
-__global__ __launch_bounds__(256) void embed_sums_kernel(const float* __restrict__ dX, int64_t B, int64_t Np,
-                                                         int64_t T, int64_t C, float* __restrict__ gn,
-                                                         float* __restrict__ gt, float* __restrict__ gcls) {
-  const int64_t L = 1 + Np * T;
+// stage 1: S[i][c] = sum_b dX[b][i][c] for every token position i in [0, L) (clip-sum)
+__global__ __launch_bounds__(256) void embed_bsum_kernel(const float* __restrict__ dX, int64_t B, int64_t L, int64_t C,
+                                                         float* __restrict__ S) {
+  const int64_t i = blockIdx.y;
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f;
+  for (int64_t b = 0; b < B; ++b) a += dX[(b * L + i) * C + c];
+  S[i * C + c] = a;
+}
+
+// stage 2: gn[n] = sum_t S[1 + n*T + t], gt[t] = sum_n S[1 + n*T + t], gcls = S[0]
+__global__ __launch_bounds__(256) void embed_sums_kernel(const float* __restrict__ S, int64_t Np, int64_t T, int64_t C,
+                                                         float* __restrict__ gn, float* __restrict__ gt,
+                                                         float* __restrict__ gcls) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const int64_t which = blockIdx.y;      // 0..Np-1 -> gn, Np..Np+T-1 -> gt, Np+T -> cls
   float a = 0.f;
   if (which < Np) {
-    for (int64_t b = 0; b < B; ++b)
-      for (int64_t t = 0; t < T; ++t) a += dX[(b * L + 1 + which * T + t) * C + c];
+    for (int64_t t = 0; t < T; ++t) a += S[(1 + which * T + t) * C + c];
     gn[which * C + c] = a;
   } else if (which < Np + T) {
     const int64_t t = which - Np;
-    for (int64_t b = 0; b < B; ++b)
-      for (int64_t n = 0; n < Np; ++n) a += dX[(b * L + 1 + n * T + t) * C + c];
+    for (int64_t n = 0; n < Np; ++n) a += S[(1 + n * T + t) * C + c];
     gt[t * C + c] = a;
   } else {
-    for (int64_t b = 0; b < B; ++b) a += dX[b * L * C + c];
-    gcls[c] = a;
+    gcls[c] = S[c];
   }
 }
 
@@ -982,9 +990,11 @@ __global__ __launch_bounds__(256) void index_accum_kernel(const float* __restric
 }
 
 hipError_t launch_embed_grads(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C, float* gn, float* gt,
-                              float* gcls, hipStream_t s) {
-  dim3 grid((unsigned)((C + 255) / 256), (unsigned)(Np + T + 1));
-  embed_sums_kernel<<<grid, 256, 0, s>>>(dX, B, Np, T, C, gn, gt, gcls);
+                              float* gcls, float* S, hipStream_t s) {
+  const int64_t L = 1 + Np * T;
+  embed_bsum_kernel<<<dim3((unsigned)((C + 255) / 256), (unsigned)L), 256, 0, s>>>(dX, B, L, C, S);
+  embed_sums_kernel<<<dim3((unsigned)((C + 255) / 256), (unsigned)(Np + T + 1)), 256, 0, s>>>(S, Np, T, C, gn, gt,
+                                                                                            gcls);
   return hipGetLastError();
 }
 

@@ -119,7 +119,7 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_LN_BWD: return up((int64_t)ln_bwd_blocks(M) * 2 * K * 4);          // M = rows, K = C
     case DSVT_WS_COLSUM: return up(colsum_parts(M) * N * 4);                        // M = rows, N = C
     case DSVT_WS_ATTN_BWD: return up(M * 3 * N * 4 + M * (N / 64) * K * 2 * 4);     // M = nb*tin, N = C, K = seqlen
-    case DSVT_WS_EMBED_BWD: return up((M + N + 1) * K * 4);                         // M = Np, N = T, K = C
+    case DSVT_WS_EMBED_BWD: return up((M + N + 2 + M * N) * K * 4);                 // M = Np, N = T, K = C
     default: return -1;
   }
 }
@@ -614,7 +614,7 @@ int dsvt_embed_bwd(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C,
   float* gt = gn + Np * C;
   float* gc = gt + T * C;
   hipError_t e;
-  if ((e = launch_embed_grads(dX, B, Np, T, C, gn, gt, gc, s))) return hip_fail(e, "embed_grads");
+  if ((e = launch_embed_grads(dX, B, Np, T, C, gn, gt, gc, gc + C, s))) return hip_fail(e, "embed_grads");
   if ((e = launch_index_accum(gn, pos_index, Np, C, 1, dpos, s))) return hip_fail(e, "embed pos");
   if (dtime && (e = launch_index_accum(gt, time_index, T, C, 0, dtime, s))) return hip_fail(e, "embed time");
   // CLS token row = cls_token + pos_embed[0] (timesformer.py:288-290)

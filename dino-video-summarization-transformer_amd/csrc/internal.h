@@ -107,7 +107,7 @@ hipError_t launch_rowscale_bias_add(float* X, int64_t rows, int64_t C, const flo
                                     hipStream_t s);
 hipError_t launch_cast_transpose(int dtype, const float* x, void* y, int64_t R, int64_t C, hipStream_t s);
 hipError_t launch_embed_grads(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C, float* gn, float* gt,
-                              float* gcls, hipStream_t s);
+                              float* gcls, float* S, hipStream_t s);
 hipError_t launch_index_accum(const float* src, const int32_t* dst, int64_t n, int64_t C, int64_t dst_off, float* out,
                               hipStream_t s);
 hipError_t launch_ema(float* const* teacher, const float* const* student, const int64_t* sizes, const int32_t* ctensor,

@@ -29,25 +29,54 @@ from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SP
     DsvtError
 
 
-def wgrad(dy, x, out):
-    """out [N, K] (fp32) += dy^T [N, M] . x [M, K]: a plain library GEMM (hipBLASLt)."""
-    out.add_(torch.mm(dy.t(), x))
+def wgrad(dy, x, G, p, view=None):
+    """grad(p) (+)= dy^T [N, M] . x [M, K]: a plain library GEMM (hipBLASLt); the first write
+    of a gradient buffer is a copy (no zero fill)."""
+    buf, acc = G.acc(p)
+    if view is not None:
+        buf = buf.view(view)
+    r = torch.mm(dy.t(), x)
+    if acc:
+        buf.add_(r)
+    else:
+        buf.copy_(r)
 
 
 class _Grads:
-    """fp32 zero-initialised gradient buffers, one per parameter (returned by backward)."""
+    """fp32 gradient buffers, one per parameter (returned by backward).  `acc(p)` hands out the
+    buffer and whether it already holds a partial sum (False on the first write: the kernels
+    then overwrite instead of accumulating, so no zero fill is needed)."""
 
     def __init__(self):
         self.g = {}
 
-    def __call__(self, p):
+    def acc(self, p):
         buf = self.g.get(id(p))
         if buf is None:
-            buf = self.g[id(p)] = torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+            buf = self.g[id(p)] = torch.empty(p.shape, device=p.device, dtype=torch.float32)
+            return buf, False
+        return buf, True
+
+    def zeros(self, p):
+        buf, acc = self.acc(p)
+        if not acc:
+            buf.zero_()
         return buf
 
     def get(self, p):
         return self.g.get(id(p))
+
+
+def _colsum(y, G, p, **kw):
+    buf, acc = G.acc(p)
+    ops.colsum(y, buf, accumulate=acc, **kw)
+
+
+def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None):
+    dg, acc = G.acc(ln.weight)
+    db, acc2 = G.acc(ln.bias)
+    assert acc == acc2
+    ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
 
 
 def _keep_scale(n, p, device):
@@ -197,8 +226,7 @@ def _backbone_backward(model, st, dfeat):
     patch_map = (Np * T, L, 1)
     # final norm on the CLS rows (timesformer.py:342-345)
     dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
-    ops.layernorm_bwd(st.X, dfeat, model.norm.weight, model.norm.eps, dX, B, G(model.norm.weight),
-                      G(model.norm.bias), rowmap=(1, L, 0))
+    _ln_bwd(st.X, dfeat, model.norm, dX, B, G, rowmap=(1, L, 0))
     for blk, S, mk in zip(reversed(model.blocks), reversed(st.blocks), reversed(st.masks)):
         heads = blk.attn.num_heads
         ta = blk.temporal_attn
@@ -208,69 +236,66 @@ def _backbone_backward(model, st, dfeat):
         ops.cast_rows(dX, dXb, rows)
         if mk is None:
             dXs = dXb
-            ops.colsum(dX, G(fc2.bias))
+            _colsum(dX, G, fc2.bias)
         else:
             dXs = torch.empty(rows, C, device=dev, dtype=mode)
             ops.cast_rows(dX, dXs, rows, row_scale=mk.m, group=L)
-            ops.colsum(dX, G(fc2.bias), row_scale=mk.m_rows)
-        wgrad(dXb, S.h, G(fc2.weight))
+            _colsum(dX, G, fc2.bias, row_scale=mk.m_rows)
+        wgrad(dXb, S.h, G, fc2.weight)
         dpre = torch.empty(rows, fc1.out_features, device=dev, dtype=mode)
         ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
-        wgrad(dpre, S.a_m, G(fc1.weight))
-        ops.colsum(dpre, G(fc1.bias))
-        da = torch.empty(rows, C, device=dev, dtype=torch.float32)
-        ops.gemm(dpre, wt(fc1.weight), None, da, out_f32=True)
+        wgrad(dpre, S.a_m, G, fc1.weight)
+        _colsum(dpre, G, fc1.bias)
+        da = torch.empty(rows, C, device=dev, dtype=mode)       # LN input gradient (storage dtype)
+        ops.gemm(dpre, wt(fc1.weight), None, da)
         del dpre
-        ops.layernorm_bwd(S.X2, da, blk.norm2.weight, blk.norm2.eps, dX, rows, G(blk.norm2.weight),
-                          G(blk.norm2.bias))
+        _ln_bwd(S.X2, da, blk.norm2, dX, rows, G)
         # ---- spatial
         ops.cast_rows(dX, dXb, rows)
-        wgrad(dXb, S.o_s, G(blk.attn.proj.weight))
-        ops.colsum(dX, G(blk.attn.proj.bias), row_scale=None if mk is None else mk.s_rows)
+        wgrad(dXb, S.o_s, G, blk.attn.proj.weight)
+        _colsum(dX, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_rows)
         do = torch.empty(rows, C, device=dev, dtype=mode)
         ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)
         dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
         ops.attn_spatial_bwd(S.qkv_s, do, dqkv, B, T, L, heads, blk.attn.scale,
                              seq_scale=None if mk is None else mk.s)
-        wgrad(dqkv, S.a_s, G(blk.attn.qkv.weight))
-        ops.colsum(dqkv, G(blk.attn.qkv.bias))
-        ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da, out_f32=True)
+        wgrad(dqkv, S.a_s, G, blk.attn.qkv.weight)
+        _colsum(dqkv, G, blk.attn.qkv.bias)
+        ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da)
         del dqkv, do
-        ops.layernorm_bwd(S.X1, da, blk.norm1.weight, blk.norm1.eps, dX, rows, G(blk.norm1.weight),
-                          G(blk.norm1.bias))
+        _ln_bwd(S.X1, da, blk.norm1, dX, rows, G)
         # ---- temporal (patch rows of X only)
         dY = torch.empty(R, C, device=dev, dtype=mode)
         ops.cast_rows(dX, dY, R, rowmap=patch_map)
-        wgrad(dY, S.u, G(blk.temporal_fc.weight))
-        ops.colsum(dY, G(blk.temporal_fc.bias))
+        wgrad(dY, S.u, G, blk.temporal_fc.weight)
+        _colsum(dY, G, blk.temporal_fc.bias)
         du = torch.empty(R, C, device=dev, dtype=mode)
         ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
         if mk is not None:
             ops.row_scale(du, mk.t, T)
-        wgrad(du, S.o_t, G(ta.proj.weight))
-        ops.colsum(du, G(ta.proj.bias))
+        wgrad(du, S.o_t, G, ta.proj.weight)
+        _colsum(du, G, ta.proj.bias)
         do_t = torch.empty(R, C, device=dev, dtype=mode)
         ops.gemm(du, wt(ta.proj.weight), None, do_t)
         dqkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
         ops.attn_temporal_bwd(S.qkv_t, do_t, dqkv_t, B * Np, T, heads, ta.scale)
-        wgrad(dqkv_t, S.a_t, G(ta.qkv.weight))
-        ops.colsum(dqkv_t, G(ta.qkv.bias))
-        da_t = torch.empty(R, C, device=dev, dtype=torch.float32)
-        ops.gemm(dqkv_t, wt(ta.qkv.weight), None, da_t, out_f32=True)
-        ops.layernorm_bwd(S.X0, da_t, blk.temporal_norm1.weight, blk.temporal_norm1.eps, dX, R,
-                          G(blk.temporal_norm1.weight), G(blk.temporal_norm1.bias), rowmap=patch_map)
+        wgrad(dqkv_t, S.a_t, G, ta.qkv.weight)
+        _colsum(dqkv_t, G, ta.qkv.bias)
+        da_t = torch.empty(R, C, device=dev, dtype=mode)
+        ops.gemm(dqkv_t, wt(ta.qkv.weight), None, da_t)
+        _ln_bwd(S.X0, da_t, blk.temporal_norm1, dX, R, G, rowmap=patch_map)
         for k in list(vars(S)):
             setattr(S, k, None)        # free this block's activations as soon as it is done
     # ---- patch embedding + token embeddings (timesformer.py:201-209, 288-323)
     dP = torch.empty(R, C, device=dev, dtype=mode)
     ops.cast_rows(dX, dP, R, rowmap=patch_map)
     conv = model.patch_embed.proj
-    dWc = G(conv.weight).view(C, -1)
     for row0, nb, a in st.im2col:
         r0 = row0 * Np * T
-        wgrad(dP[r0:r0 + nb * Np * T], a, dWc)
-    ops.colsum(dP, G(conv.bias))
-    ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G(model.pos_embed), G(model.time_embed), G(model.cls_token))
+        wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1))
+    _colsum(dP, G, conv.bias)
+    ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
+                  G.zeros(model.cls_token))
     return G
 
 
@@ -341,8 +366,8 @@ def _head_backward(head, st, dlogits):
     dl = torch.empty(R, dlogits.shape[1], device=dev, dtype=mode)
     ops.cast(dlogits, dl)
     dW = torch.mm(dl.t(), st.z).float()                       # d(effective weight) [out, bottleneck]
-    ops.weight_norm_bwd(ll.weight_v.detach(), ll.weight_g.detach(), dW, G(ll.weight_v),
-                        G(ll.weight_g).view(-1) if ll.weight_g.requires_grad else None)
+    ops.weight_norm_bwd(ll.weight_v.detach(), ll.weight_g.detach(), dW, G.acc(ll.weight_v)[0],
+                        G.acc(ll.weight_g)[0].view(-1) if ll.weight_g.requires_grad else None, accumulate=False)
     dz = torch.mm(dl, st.wn).float()                          # [R, bottleneck]
     dy = ops.head_norm_bwd(st.y, dz.contiguous())
     lins = _head_linears(head)
@@ -353,8 +378,8 @@ def _head_backward(head, st, dlogits):
         gb = g if g.dtype == mode else torch.empty(R, g.shape[1], device=dev, dtype=mode)
         if gb is not g:
             ops.cast(g.contiguous(), gb)
-        wgrad(gb, st.a[i], G(lin.weight))
-        ops.colsum(g, G(lin.bias))
+        wgrad(gb, st.a[i], G, lin.weight)
+        _colsum(g, G, lin.bias)
         if i > 0:
             nxt = torch.empty(R, lin.in_features, device=dev, dtype=mode)
             ops.gemm_aux(gb, wt(lin.weight), None, nxt, st.pre[i - 1], EPI_DGELU)
