@@ -641,4 +641,75 @@ int dsvt_clip_grads(float* const* grads, const int64_t* sizes, const int32_t* ch
   return e == hipSuccess ? 0 : hip_fail(e, "clip_grads");
 }
 
+// ================================================================ Video Swin (swin.hip)
+int dsvt_swin_patch_embed_fwd(int dtype, const float* x, int64_t B, int64_t Cin, int64_t D, int64_t H, int64_t W,
+                              int64_t pd, int64_t ph, int64_t pw, const void* w, int64_t ldk, const float* bias,
+                              int64_t C, float* X, void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "swin_patch_embed: bad dtype");
+  REQUIRE(x && w && X && B > 0 && Cin > 0 && D > 0 && H > 0 && W > 0 && pd > 0 && ph > 0 && pw > 0 && C > 0,
+          "swin_patch_embed: bad args");
+  REQUIRE(ldk >= Cin * pd * ph * pw, "swin_patch_embed: ldk < Cin*pd*ph*pw");
+  const int64_t M = B * ((D + pd - 1) / pd) * ((H + ph - 1) / ph) * ((W + pw - 1) / pw);
+  REQUIRE(workspace && workspace_bytes >= M * ldk * esize(dtype), "swin_patch_embed: workspace too small");
+  if (int e = check_gemm(dtype, EPI_BIAS, workspace, ldk, w, ldk, bias, X, C, M, C, ldk)) return e;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipError_t e = launch_im2col3d(dtype, x, workspace, B, Cin, D, H, W, (int)pd, (int)ph, (int)pw, ldk, s))
+    return hip_fail(e, "im2col3d");
+  return dsvt_gemm_fwd(dtype, EPI_BIAS, 1, workspace, ldk, w, ldk, bias, X, C, M, C, ldk, 0, 0, 0, stream);
+}
+
+int dsvt_swin_ln_rows_fwd(int dtype, const float* x, const int32_t* idx, const float* gamma, const float* beta,
+                          void* out, int64_t rows, int64_t C, int64_t ldo, float eps, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "swin_ln_rows: bad dtype");
+  REQUIRE(x && gamma && beta && out && rows > 0 && C > 0 && C <= 2048 && ldo >= C && ldo <= 2048,
+          "swin_ln_rows: bad args (C, ldo <= 2048)");
+  hipError_t e = launch_swin_ln_rows(dtype, x, idx, gamma, beta, out, rows, C, ldo, eps, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "swin_ln_rows");
+}
+
+int dsvt_swin_merge_ln_fwd(int dtype, const float* x, const float* gamma, const float* beta, void* out, int64_t B,
+                           int64_t D, int64_t H, int64_t W, int64_t C, float eps, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "swin_merge_ln: bad dtype");
+  REQUIRE(x && gamma && beta && out && B > 0 && D > 0 && H > 0 && W > 0 && C > 0 && 4 * C <= 2048,
+          "swin_merge_ln: bad args (4C <= 2048)");
+  hipError_t e = launch_swin_merge_ln(dtype, x, gamma, beta, out, B, D, H, W, C, eps, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "swin_merge_ln");
+}
+
+int dsvt_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C, void* stream) {
+  REQUIRE(X && y && idx && aligned16(X) && aligned16(y) && rows > 0 && C > 0 && C % 4 == 0,
+          "window_scatter_add: bad args");
+  hipError_t e = launch_window_scatter_add(X, y, idx, rows, C, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "window_scatter_add");
+}
+
+int dsvt_relpos_bias_fwd(const float* table, const int64_t* index, int64_t nmax, int64_t N, int64_t heads, float* out,
+                         void* stream) {
+  REQUIRE(table && index && out && N > 0 && N <= nmax && heads > 0, "relpos_bias: bad args");
+  hipError_t e = launch_relpos_bias(table, index, nmax, N, heads, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "relpos_bias");
+}
+
+int dsvt_attn_window_fwd(int dtype, const void* qkv, void* out, int64_t ldo, const float* bias, const int32_t* region,
+                         int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t head_dim, float scale,
+                         void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_window: bad dtype");
+  REQUIRE(qkv && out && bias && region && aligned16(qkv) && aligned16(out), "attn_window: bad pointer");
+  REQUIRE(head_dim == 32, "attn_window: head_dim must be 32 (Video Swin)");
+  REQUIRE(nwin > 0 && nwc > 0 && N > 0 && N <= 128 && heads > 0, "attn_window: need 0 < N <= 128");
+  REQUIRE(ldo >= heads * 32 && (ldo * esize(dtype)) % 16 == 0, "attn_window: bad ldo");
+  const double flops = 4.0 * nwin * heads * (double)N * N * 32;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, "dsvt_attn_window_fwd", [&] {
+    return launch_attn_window(dtype, qkv, out, ldo, bias, region, nwin, nwc, N, heads, heads * 32, scale,
+                              (hipStream_t)stream);
+  });
+}
+
+int dsvt_cast_pad_fwd(int dtype, const float* x, void* y, int64_t N, int64_t K, int64_t ldk, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "cast_pad: bad dtype");
+  REQUIRE(x && y && N > 0 && K > 0 && ldk >= K, "cast_pad: bad args");
+  hipError_t e = launch_cast_pad(dtype, x, y, N, K, ldk, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "cast_pad");
+}
+
 }  // extern "C"

@@ -116,6 +116,22 @@ hipError_t launch_clip_grads(float* const* grads, const int64_t* sizes, const in
                              const int32_t* first_chunk, int64_t nchunks, int64_t ntensors, float clip, float* partial,
                              float* norms, hipStream_t s);
 
+// Video Swin (swin.hip)
+hipError_t launch_im2col3d(int dtype, const float* x, void* a, int64_t B, int64_t Cin, int64_t D, int64_t H,
+                           int64_t W, int pd, int ph, int pw, int64_t ldk, hipStream_t s);
+hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, const float* gamma, const float* beta,
+                               void* out, int64_t rows, int64_t C, int64_t ldo, float eps, hipStream_t s);
+hipError_t launch_swin_merge_ln(int dtype, const float* x, const float* gamma, const float* beta, void* out, int64_t B,
+                                int64_t D, int64_t H, int64_t W, int64_t C, float eps, hipStream_t s);
+hipError_t launch_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C,
+                                     hipStream_t s);
+hipError_t launch_relpos_bias(const float* table, const int64_t* index, int64_t nmax, int64_t N, int64_t heads,
+                              float* out, hipStream_t s);
+hipError_t launch_attn_window(int dtype, const void* qkv, void* out, int64_t ldo, const float* bias,
+                              const int32_t* region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C,
+                              float scale, hipStream_t s);
+hipError_t launch_cast_pad(int dtype, const float* x, void* y, int64_t N, int64_t K, int64_t ldk, hipStream_t s);
+
 hipError_t launch_softmax_stats(const float* x, const float* center, float inv_temp, int64_t rows,
                                 int64_t D, float* m_out, float* z_out, hipStream_t s);
 hipError_t launch_pair_ce(const float* student, const float* teacher, const float* center,

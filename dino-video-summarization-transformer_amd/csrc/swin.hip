@@ -1,0 +1,398 @@
+// Video Swin Transformer (config 5): the pieces of models/swin_transformer.py
+// that are not plain GEMMs (those run on the dsvt GEMM).  Token layout: fp32 X [B, D, H, W, C]
+// (channels last, row = ((b*D + d)*H + h)*W + w), the residual stream of a stage.
+//
+//   im2col3d_kernel        PatchEmbed3D Conv3d(k = s = patch) as an im2col GEMM operand (:419-460)
+//   swin_ln_rows_kernel    norm1 / norm2 (+ the window partition: rows gathered through an index
+//                          that encodes the cyclic shift and the zero padding, :221-237), written
+//                          with zero-padded K columns for the MFMA GEMM (C = 96 -> K = 128)
+//   swin_merge_ln_kernel   PatchMerging 2x2 gather + norm over 4C (:293-315)
+//   window_scatter_add     window_reverse + reverse shift + crop + residual add (:241-251, :269)
+//   relpos_bias_kernel     relative_position_bias_table[relative_position_index[:N, :N]] (:152-156)
+//   attn_window_bf16       W-MSA / SW-MSA (:139-171): per (window, head) MFMA attention, head_dim
+//                          32, scores + relative-position bias + shift mask (-100 across regions)
+//   attn_window_f32        the same on the fp32 VALU (parity mode)
+#include <math.h>
+
+#include "common.h"
+
+namespace dsvt {
+
+// ---------------------------------------------------------------- patch embedding (Conv3d)
+// a[m][k], m = ((b*Do + od)*Ho + oh)*Wo + ow, k = ((c*pd + kd)*ph + kh)*pw + kw (Conv3d weight
+// flatten order); taps past the input are the reference's zero padding (F.pad, :446-451).
+template <typename T>
+__global__ __launch_bounds__(256) void im2col3d_kernel(const float* __restrict__ x, T* __restrict__ a, int64_t total,
+                                                       int Cin, int D, int H, int W, int pd, int ph, int pw, int Do,
+                                                       int Ho, int Wo, int ldk) {
+  const int K = Cin * pd * ph * pw;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / ldk;
+    const int k = (int)(i % ldk);
+    float v = 0.f;
+    if (k < K) {
+      const int kw = k % pw, kh = (k / pw) % ph, kd = (k / (pw * ph)) % pd, c = k / (pw * ph * pd);
+      const int ow = (int)(m % Wo), oh = (int)((m / Wo) % Ho), od = (int)((m / ((int64_t)Wo * Ho)) % Do);
+      const int64_t b = m / ((int64_t)Wo * Ho * Do);
+      const int z = od * pd + kd, y = oh * ph + kh, xx = ow * pw + kw;
+      if (z < D && y < H && xx < W) v = x[(((b * Cin + c) * D + z) * (int64_t)H + y) * W + xx];
+    }
+    a[i] = Elem<T>::from_f(v);
+  }
+}
+
+hipError_t launch_im2col3d(int dtype, const float* x, void* a, int64_t B, int64_t Cin, int64_t D, int64_t H,
+                           int64_t W, int pd, int ph, int pw, int64_t ldk, hipStream_t s) {
+  const int64_t Do = (D + pd - 1) / pd, Ho = (H + ph - 1) / ph, Wo = (W + pw - 1) / pw;
+  const int64_t total = B * Do * Ho * Wo * ldk;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (dtype == 0)
+    im2col3d_kernel<bf16_t><<<(unsigned)blocks, 256, 0, s>>>(x, (bf16_t*)a, total, (int)Cin, (int)D, (int)H, (int)W, pd,
+                                                            ph, pw, (int)Do, (int)Ho, (int)Wo, (int)ldk);
+  else
+    im2col3d_kernel<float><<<(unsigned)blocks, 256, 0, s>>>(x, (float*)a, total, (int)Cin, (int)D, (int)H, (int)W, pd,
+                                                           ph, pw, (int)Do, (int)Ho, (int)Wo, (int)ldk);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- LayerNorm with row gather
+// out[m][0:C] = LN(x[idx[m]]) (idx nullable = identity; idx[m] < 0 -> a zero row: the padding
+// that the reference adds AFTER norm1), out[m][C:ldo] = 0.  One wave per row, C <= 2048.
+template <typename T>
+__global__ __launch_bounds__(256) void swin_ln_rows_kernel(const float* __restrict__ x, const int32_t* __restrict__ idx,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, T* __restrict__ out,
+                                                           int64_t rows, int C, int ldo, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + wave;
+  if (m >= rows) return;
+  const int64_t src = idx ? (int64_t)idx[m] : m;
+  T* o = out + m * ldo;
+  if (src < 0) {
+    for (int c = lane; c < ldo; c += 64) o[c] = Elem<T>::from_f(0.f);
+    return;
+  }
+  const float* xr = x + src * C;
+  float v[32];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int c = i * 64 + lane;
+    v[i] = c < C ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int c = i * 64 + lane;
+    if (c < C) { v[i] -= mean; q += v[i] * v[i]; }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int c = i * 64 + lane;
+    if (c < C) o[c] = Elem<T>::from_f(v[i] * rstd * gamma[c] + beta[c]);
+    else if (c < ldo) o[c] = Elem<T>::from_f(0.f);
+  }
+}
+
+hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, const float* gamma, const float* beta,
+                               void* out, int64_t rows, int64_t C, int64_t ldo, float eps, hipStream_t s) {
+  const unsigned blocks = (unsigned)((rows + 3) / 4);
+  if (dtype == 0)
+    swin_ln_rows_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, idx, gamma, beta, (bf16_t*)out, rows, (int)C, (int)ldo, eps);
+  else
+    swin_ln_rows_kernel<float><<<blocks, 256, 0, s>>>(x, idx, gamma, beta, (float*)out, rows, (int)C, (int)ldo, eps);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- PatchMerging 2x2 + LN(4C)
+// out row (b, d, h2, w2) = LN([x(2h2, 2w2), x(2h2+1, 2w2), x(2h2, 2w2+1), x(2h2+1, 2w2+1)]) with
+// zero taps past odd H / W (the reference's F.pad, :302-310).  4C <= 2048.
+template <typename T>
+__global__ __launch_bounds__(256) void swin_merge_ln_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, T* __restrict__ out,
+                                                            int64_t B, int D, int H, int W, int C, float eps) {
+  const int H2 = (H + 1) / 2, W2 = (W + 1) / 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + wave;
+  if (m >= B * D * H2 * W2) return;
+  const int w2 = (int)(m % W2), h2 = (int)((m / W2) % H2);
+  const int64_t bd = m / ((int64_t)W2 * H2);                 // b*D + d
+  const int C4 = 4 * C;
+  float v[32];                                               // slot part*8 + i <-> column part*C + i*64 + lane
+  float s = 0.f;
+#pragma unroll
+  for (int part = 0; part < 4; ++part) {                     // x0, x1, x2, x3
+    const int hh = 2 * h2 + (part & 1), ww = 2 * w2 + (part >> 1);
+    const bool in = hh < H && ww < W;
+    const float* xr = x + ((bd * H + (in ? hh : 0)) * W + (in ? ww : 0)) * C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cc = i * 64 + lane;
+      v[part * 8 + i] = (in && cc < C) ? xr[cc] : 0.f;
+      s += v[part * 8 + i];
+    }
+  }
+  const float mean = wave_sum(s) / C4;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if ((k & 7) * 64 + lane < C) { v[k] -= mean; q += v[k] * v[k]; }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / C4 + eps);
+  T* o = out + m * C4;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const int cc = (k & 7) * 64 + lane;
+    if (cc < C) {
+      const int c = (k >> 3) * C + cc;
+      o[c] = Elem<T>::from_f(v[k] * rstd * gamma[c] + beta[c]);
+    }
+  }
+}
+
+hipError_t launch_swin_merge_ln(int dtype, const float* x, const float* gamma, const float* beta, void* out, int64_t B,
+                                int64_t D, int64_t H, int64_t W, int64_t C, float eps, hipStream_t s) {
+  const int64_t rows = B * D * ((H + 1) / 2) * ((W + 1) / 2);
+  const unsigned blocks = (unsigned)((rows + 3) / 4);
+  if (dtype == 0)
+    swin_merge_ln_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, gamma, beta, (bf16_t*)out, B, (int)D, (int)H, (int)W,
+                                                        (int)C, eps);
+  else
+    swin_merge_ln_kernel<float><<<blocks, 256, 0, s>>>(x, gamma, beta, (float*)out, B, (int)D, (int)H, (int)W, (int)C,
+                                                       eps);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- window reverse + residual
+// X[idx[m]] += y[m] for idx[m] >= 0 (window rows -> token rows; every token row has exactly one
+// window row, so the adds never collide).  C % 4 == 0.
+__global__ __launch_bounds__(256) void window_scatter_add_kernel(float* __restrict__ X, const float* __restrict__ y,
+                                                                 const int32_t* __restrict__ idx, int64_t rows, int C) {
+  const int c4 = C / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows * c4; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / c4;
+    const int c = (int)(i % c4) * 4;
+    const int32_t dst = idx[m];
+    if (dst < 0) continue;
+    const float4 v = *reinterpret_cast<const float4*>(y + m * C + c);
+    float4* xo = reinterpret_cast<float4*>(X + (int64_t)dst * C + c);
+    float4 xv = *xo;
+    xv.x += v.x; xv.y += v.y; xv.z += v.z; xv.w += v.w;
+    *xo = xv;
+  }
+}
+
+hipError_t launch_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C,
+                                     hipStream_t s) {
+  int64_t blocks = (rows * C / 4 + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  window_scatter_add_kernel<<<(unsigned)(blocks < 1 ? 1 : blocks), 256, 0, s>>>(X, y, idx, rows, (int)C);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- relative position bias
+// out[h][i][j] = table[index[i][j]][h] for i, j < N (index of the module's full window, ld nmax)
+__global__ __launch_bounds__(256) void relpos_bias_kernel(const float* __restrict__ table,
+                                                          const int64_t* __restrict__ index, int nmax, int N,
+                                                          int heads, float* __restrict__ out) {
+  const int64_t total = (int64_t)heads * N * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int j = (int)(e % N), i = (int)((e / N) % N), h = (int)(e / ((int64_t)N * N));
+    out[e] = table[index[(int64_t)i * nmax + j] * heads + h];
+  }
+}
+
+hipError_t launch_relpos_bias(const float* table, const int64_t* index, int64_t nmax, int64_t N, int64_t heads,
+                              float* out, hipStream_t s) {
+  int64_t blocks = (heads * N * N + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  relpos_bias_kernel<<<(unsigned)blocks, 256, 0, s>>>(table, index, (int)nmax, (int)N, (int)heads, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- window attention
+// qkv [nwin*N, 3C] (window-ordered rows), out [nwin*N, C]; bias [heads][N][N]; region
+// [nwc][N] (nullable: no shift mask) with window w using region row w % nwc; mask = -100
+// between tokens of different regions (compute_mask, :318-332).  head_dim 32.
+struct WinAttnParams {
+  const void* qkv; void* out;
+  const float* bias; const int32_t* region;
+  int64_t nwin, nwc, N, heads, C;
+  float scale;
+  int64_t ldo;   // out row stride (>= C: the proj GEMM's zero-padded K)
+};
+
+// bf16 MFMA: one workgroup (4 waves) per (window, head); K/V of the window in LDS (rows past N
+// zero); wave per 16-query tile; S^T = K.Q^T is ONE 16x16x32 MFMA per key tile (head_dim 32);
+// O^T = V^T.P^T over 32-key steps with ds_read_b64_tr_b16 V^T fragments.  N <= 128.  region is
+// required (all zeros without a shift) so the score chain stays branch-free after the MFMAs.
+constexpr int WROW = 40;   // bf16 per LDS row: 32 + 8 pad
+__global__ __launch_bounds__(256) void attn_window_bf16(WinAttnParams p) {
+  constexpr int SN = 8, LPW = 128;
+  __shared__ __attribute__((aligned(16))) bf16_t kv[2][LPW * WROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.x;
+  const int64_t win = blockIdx.y;
+  const int N = (int)p.N;
+  const int64_t C = p.C;
+  const bf16_t* qkv = (const bf16_t*)p.qkv + win * N * 3 * C;
+  // stage K, V: 128 rows x 4 pieces of 16 B each
+  for (int pc = tid; pc < LPW * 4; pc += 256) {
+    const int r = pc >> 2, ch = pc & 3;
+    uint4 k4 = make_uint4(0, 0, 0, 0), v4 = k4;
+    if (r < N) {
+      const bf16_t* src = qkv + (int64_t)r * 3 * C + C + h * 32 + ch * 8;
+      k4 = *reinterpret_cast<const uint4*>(src);
+      v4 = *reinterpret_cast<const uint4*>(src + C);
+    }
+    *reinterpret_cast<uint4*>(&kv[0][r * WROW + ch * 8]) = k4;
+    *reinterpret_cast<uint4*>(&kv[1][r * WROW + ch * 8]) = v4;
+  }
+  __syncthreads();
+  const bf16_t* Ks = kv[0];
+  const bf16_t* Vs = kv[1];
+  const float* bias = p.bias + (int64_t)h * N * N;
+  const int32_t* reg = p.region + (win % p.nwc) * N;    // never null here (all-zero: no shift mask)
+  const float l2e = 1.4426950408889634f;
+  const int nqt = (N + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    int qi = qt * 16 + r16;
+    const int qc = qi < N ? qi : N - 1;
+    const sv8 qf = *reinterpret_cast<const sv8*>(qkv + (int64_t)qc * 3 * C + h * 32 + g * 8);
+    fv4 s[SN];
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+      const sv8 kf = *reinterpret_cast<const sv8*>(Ks + (kt * 16 + r16) * WROW + g * 8);
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, fv4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    const int rq = reg[qc];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kt * 16 + 4 * g + j;
+        const int kc = key < N ? key : N - 1;
+        float v = s[kt][j] * p.scale + bias[(int64_t)qc * N + kc] + ((reg[kc] != rq) ? -100.0f : 0.0f);
+        v = key < N ? v * l2e : -INFINITY;
+        s[kt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[kt][j] = __builtin_amdgcn_exp2f(s[kt][j] - mx);
+        rs += s[kt][j];
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    fv4 o[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kp = 0; kp < SN / 2; ++kp) {
+      sv8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[2 * kp][j]);
+        pb[4 + j] = (short)f2bf(s[2 * kp + 1][j]);
+      }
+      const int vr0 = kp * 32 + 4 * g + (r16 >> 2), vr1 = vr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr0 * WROW + col));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr1 * WROW + col));
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), pb,
+                                                        o[dt], 0, 0, 0);
+      }
+    }
+    mfma_result_fence();
+    if (qi < N) {
+      const float inv = 1.0f / rs;
+      bf16_t* dst = (bf16_t*)p.out + (win * N + qi) * p.ldo + h * 32 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    }
+  }
+}
+
+// fp32 VALU: one thread per (window, head, query), K/V rows read through L2
+__global__ __launch_bounds__(256) void attn_window_f32(WinAttnParams p) {
+  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t N = p.N, C = p.C;
+  if (item >= p.nwin * p.heads * N) return;
+  const int64_t i = item % N;
+  const int h = (int)((item / N) % p.heads);
+  const int64_t win = item / (N * p.heads);
+  const float* qkv = (const float*)p.qkv + win * N * 3 * C;
+  const float* q = qkv + i * 3 * C + h * 32;
+  const float* bias = p.bias + ((int64_t)h * N + i) * N;
+  const int32_t* reg = p.region ? p.region + (win % p.nwc) * N : nullptr;
+  float qv[32], o[32];
+#pragma unroll
+  for (int d = 0; d < 32; ++d) { qv[d] = q[d] * p.scale; o[d] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  for (int64_t j = 0; j < N; ++j) {
+    const float* k = qkv + j * 3 * C + C + h * 32;
+    float sdot = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) sdot = fmaf(qv[d], k[d], sdot);
+    sdot += bias[j];
+    if (reg) sdot += (reg[j] != reg[i]) ? -100.0f : 0.0f;
+    const float mn = fmaxf(m, sdot);
+    const float corr = expf(m - mn), pe = expf(sdot - mn);
+    l = l * corr + pe;
+    const float* v = k + C;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] = fmaf(pe, v[d], o[d] * corr);
+    m = mn;
+  }
+  float* dst = (float*)p.out + (win * N + i) * p.ldo + h * 32;
+  const float inv = 1.0f / l;
+#pragma unroll
+  for (int d = 0; d < 32; ++d) dst[d] = o[d] * inv;
+}
+
+hipError_t launch_attn_window(int dtype, const void* qkv, void* out, int64_t ldo, const float* bias,
+                              const int32_t* region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C,
+                              float scale, hipStream_t s) {
+  WinAttnParams p{qkv, out, bias, region, nwin, nwc, N, heads, C, scale, ldo};
+  if (dtype == 0) {
+    attn_window_bf16<<<dim3((unsigned)heads, (unsigned)nwin), 256, 0, s>>>(p);
+  } else {
+    const int64_t items = nwin * heads * N;
+    attn_window_f32<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(p);
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- zero-padded weight cast
+// y[n][k] = k < K ? x[n][k] : 0, y [N, ldk] in the storage dtype (K = 96 -> 128 for bf16 MFMA)
+template <typename T>
+__global__ __launch_bounds__(256) void cast_pad_kernel(const float* __restrict__ x, T* __restrict__ y, int64_t N,
+                                                       int64_t K, int64_t ldk) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N * ldk; i += (int64_t)gridDim.x * 256) {
+    const int64_t n = i / ldk, k = i % ldk;
+    y[i] = Elem<T>::from_f(k < K ? x[n * K + k] : 0.f);
+  }
+}
+
+hipError_t launch_cast_pad(int dtype, const float* x, void* y, int64_t N, int64_t K, int64_t ldk, hipStream_t s) {
+  int64_t blocks = (N * ldk + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (dtype == 0) cast_pad_kernel<bf16_t><<<(unsigned)blocks, 256, 0, s>>>(x, (bf16_t*)y, N, K, ldk);
+  else cast_pad_kernel<float><<<(unsigned)blocks, 256, 0, s>>>(x, (float*)y, N, K, ldk);
+  return hipGetLastError();
+}
+
+}  // namespace dsvt

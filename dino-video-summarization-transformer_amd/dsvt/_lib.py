@@ -62,6 +62,15 @@ SIGNATURES = {
     "dsvt_embed_bwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "dsvt_ema": (_i32, [_p, _p, _p, _p, _p, _i64, _f32, _p]),
     "dsvt_clip_grads": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _f32, _p, _p, _i64, _p]),
+    # Video Swin
+    "dsvt_swin_patch_embed_fwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p,
+                                         _i64, _p, _p, _i64, _p]),
+    "dsvt_swin_ln_rows_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_swin_merge_ln_fwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_window_scatter_add": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "dsvt_relpos_bias_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p]),
+    "dsvt_attn_window_fwd": (_i32, [_i32, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_cast_pad_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _p]),
     "dsvt_set_gemm_variant": (_i32, [_i32]),
     "dsvt_set_attn_variant": (_i32, [_i32]),
     "dsvt_set_attn_bwd_variant": (_i32, [_i32]),

@@ -1,0 +1,415 @@
+"""Video Swin Transformer backbone (config 5) on libdsvt.so -- drop-in for
+models/swin_transformer.py of the reference (`SwinTransformer3D` :463-687 and its parts), with
+the same constructor signatures and state_dict keys (incl. the `relative_position_index`
+buffers), so checkpoints load unchanged.  Inference forward only (training DropPath / backward
+are implemented for the TimeSformer hot path).
+
+Layout: the residual stream of a stage is fp32 X [B, D, H, W, C] (channels last).  Each block:
+  norm1 + zero pad + cyclic roll + window_partition   -> ONE gather-LayerNorm kernel through an
+                                                         int32 window->token index map
+  qkv / proj / fc1 / fc2 / reduction Linear           -> dsvt MFMA GEMM (K zero-padded: 96 -> 128)
+  W-MSA / SW-MSA + relative position bias + mask      -> dsvt_attn_window_fwd (head_dim 32)
+  window_reverse + roll back + crop + residual        -> one scatter-add through the same map
+PatchMerging is a 2x2 gather + LayerNorm(4C) kernel and the reduction GEMM; the head is the
+final LayerNorm and the average pool over (D, H, W).
+"""
+from functools import lru_cache, reduce
+from operator import mul
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .._lib import EPI_BIAS_GELU, EPI_BIAS_RESID, DsvtError
+from ..weights import WeightCache
+from .timesformer import _DEFAULT_DTYPE
+from .vit_utils import DropPath, trunc_normal_
+
+
+def get_window_size(x_size, window_size, shift_size=None):
+    """swin_transformer.py:71-84."""
+    use_window_size = list(window_size)
+    if shift_size is not None:
+        use_shift_size = list(shift_size)
+    for i in range(len(x_size)):
+        if x_size[i] <= window_size[i]:
+            use_window_size[i] = x_size[i]
+            if shift_size is not None:
+                use_shift_size[i] = 0
+    if shift_size is None:
+        return tuple(use_window_size)
+    return tuple(use_window_size), tuple(use_shift_size)
+
+
+@lru_cache(maxsize=64)
+def window_maps(B, D, H, W, window_size, shift_size):
+    """(win2tok [B*nW*N] int32, region [nW, N] int32, nW, N): window row -> token row of
+    X [B, D, H, W] (-1 = zero padding) for norm1 -> F.pad -> torch.roll(-shift) ->
+    window_partition (:221-237), and the shift-mask regions of compute_mask (:318-332; all
+    zero when there is no shift)."""
+    ws, ss = window_size, shift_size
+    Dp, Hp, Wp = [int(np.ceil(n / w)) * w for n, w in zip((D, H, W), ws)]
+    # token index on the padded grid (-1 in the padding)
+    tok = -np.ones((B, Dp, Hp, Wp), np.int64)
+    tok[:, :D, :H, :W] = np.arange(B * D * H * W).reshape(B, D, H, W)
+    shifted = np.roll(tok, shift=(-ss[0], -ss[1], -ss[2]), axis=(1, 2, 3))
+    nd, nh, nw = Dp // ws[0], Hp // ws[1], Wp // ws[2]
+    win = shifted.reshape(B, nd, ws[0], nh, ws[1], nw, ws[2]).transpose(0, 1, 3, 5, 2, 4, 6).reshape(-1)
+    N = reduce(mul, ws)
+    nW = nd * nh * nw
+    region = np.zeros((Dp, Hp, Wp), np.int64)
+    if any(s > 0 for s in ss):
+        cnt = 0
+        for d in (slice(-ws[0]), slice(-ws[0], -ss[0]), slice(-ss[0], None)):
+            for h in (slice(-ws[1]), slice(-ws[1], -ss[1]), slice(-ss[1], None)):
+                for w in (slice(-ws[2]), slice(-ws[2], -ss[2]), slice(-ss[2], None)):
+                    region[d, h, w] = cnt
+                    cnt += 1
+    reg = region.reshape(nd, ws[0], nh, ws[1], nw, ws[2]).transpose(0, 2, 4, 1, 3, 5).reshape(nW, N)
+    return win.astype(np.int32), reg.astype(np.int32), nW, N
+
+
+def window_partition(x, window_size):
+    """swin_transformer.py:38-51 (host-side helper, kept for API parity)."""
+    B, D, H, W, C = x.shape
+    x = x.view(B, D // window_size[0], window_size[0], H // window_size[1], window_size[1], W // window_size[2],
+               window_size[2], C)
+    return x.permute(0, 1, 3, 5, 2, 4, 6, 7).contiguous().view(-1, reduce(mul, window_size), C)
+
+
+def window_reverse(windows, window_size, B, D, H, W):
+    """swin_transformer.py:54-68 (host-side helper, kept for API parity)."""
+    x = windows.view(B, D // window_size[0], H // window_size[1], W // window_size[2], window_size[0], window_size[1],
+                     window_size[2], -1)
+    return x.permute(0, 1, 4, 2, 5, 3, 6, 7).contiguous().view(B, D, H, W, -1)
+
+
+class Mlp(nn.Module):
+    """swin_transformer.py:17-35 (parameter container)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+
+class WindowAttention3D(nn.Module):
+    """swin_transformer.py:87-171 (parameters + relative position index buffer)."""
+
+    def __init__(self, dim, window_size, num_heads, qkv_bias=False, qk_scale=None, attn_drop=0., proj_drop=0.):
+        super().__init__()
+        self.dim = dim
+        self.window_size = window_size
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        if head_dim != 32:
+            raise NotImplementedError("dsvt window attention is specialised for head_dim 32 (Swin-T/S/B); got %d"
+                                      % head_dim)
+        self.scale = qk_scale or head_dim ** -0.5
+        self.relative_position_bias_table = nn.Parameter(
+            torch.zeros((2 * window_size[0] - 1) * (2 * window_size[1] - 1) * (2 * window_size[2] - 1), num_heads))
+        coords = torch.stack(torch.meshgrid(torch.arange(window_size[0]), torch.arange(window_size[1]),
+                                            torch.arange(window_size[2]), indexing="ij"))
+        coords_flatten = torch.flatten(coords, 1)
+        rel = (coords_flatten[:, :, None] - coords_flatten[:, None, :]).permute(1, 2, 0).contiguous()
+        rel[:, :, 0] += window_size[0] - 1
+        rel[:, :, 1] += window_size[1] - 1
+        rel[:, :, 2] += window_size[2] - 1
+        rel[:, :, 0] *= (2 * window_size[1] - 1) * (2 * window_size[2] - 1)
+        rel[:, :, 1] *= (2 * window_size[2] - 1)
+        self.register_buffer("relative_position_index", rel.sum(-1))
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        trunc_normal_(self.relative_position_bias_table, std=.02)
+        self.softmax = nn.Softmax(dim=-1)
+
+
+class SwinTransformerBlock3D(nn.Module):
+    """swin_transformer.py:174-276."""
+
+    def __init__(self, dim, num_heads, window_size=(2, 7, 7), shift_size=(0, 0, 0), mlp_ratio=4., qkv_bias=True,
+                 qk_scale=None, drop=0., attn_drop=0., drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm,
+                 use_checkpoint=False):
+        super().__init__()
+        self.dim = dim
+        self.num_heads = num_heads
+        self.window_size = window_size
+        self.shift_size = shift_size
+        self.mlp_ratio = mlp_ratio
+        self.use_checkpoint = use_checkpoint
+        assert 0 <= self.shift_size[0] < self.window_size[0], "shift_size must in 0-window_size"
+        assert 0 <= self.shift_size[1] < self.window_size[1], "shift_size must in 0-window_size"
+        assert 0 <= self.shift_size[2] < self.window_size[2], "shift_size must in 0-window_size"
+        self.norm1 = norm_layer(dim)
+        self.attn = WindowAttention3D(dim, window_size=self.window_size, num_heads=num_heads, qkv_bias=qkv_bias,
+                                      qk_scale=qk_scale, attn_drop=attn_drop, proj_drop=drop)
+        self.drop_path = DropPath(drop_path) if drop_path > 0. else nn.Identity()
+        self.norm2 = norm_layer(dim)
+        self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+
+    def run(self, X, B, D, H, W, ctx):
+        """X [B*D*H*W, C] fp32 in place: X += W-MSA(norm1(X)); X += MLP(norm2(X))."""
+        C = self.dim
+        dev = X.device
+        window_size, shift_size = get_window_size((D, H, W), self.window_size, self.shift_size)
+        win, reg, nW, N = ctx.maps(B, D, H, W, window_size, shift_size)
+        rows_w = win.shape[0]
+        mode, wp = ctx.mode, ctx.wp
+        wq, ldk = wp(self.attn.qkv.weight)
+        a = torch.empty(rows_w, ldk, device=dev, dtype=mode)
+        ops.swin_ln_rows(X, win, self.norm1, a, rows_w)
+        qkv = torch.empty(rows_w, 3 * C, device=dev, dtype=mode)
+        ops.gemm(a, wq, self.attn.qkv.bias, qkv)
+        o = ctx.zeros((rows_w, ldk), mode)                     # pad columns stay zero (proj K)
+        ops.attn_window(qkv, o, ctx.bias(self.attn, N), reg, rows_w // N, nW, N, self.num_heads, self.attn.scale)
+        wpj, _ = wp(self.attn.proj.weight)
+        y = torch.empty(rows_w, C, device=dev, dtype=torch.float32)
+        ops.gemm(o, wpj, self.attn.proj.bias, y, out_f32=True)
+        ops.window_scatter_add(X, y, win)
+        rows = X.shape[0]
+        w1, ldk1 = wp(self.mlp.fc1.weight)
+        a2 = torch.empty(rows, ldk1, device=dev, dtype=mode)
+        ops.swin_ln_rows(X, None, self.norm2, a2, rows)
+        h = torch.empty(rows, self.mlp.fc1.out_features, device=dev, dtype=mode)
+        ops.gemm(a2, w1, self.mlp.fc1.bias, h, epilogue=EPI_BIAS_GELU)
+        w2, ldk2 = wp(self.mlp.fc2.weight)
+        if ldk2 != h.shape[1]:
+            raise DsvtError("mlp hidden width %d must be a multiple of the GEMM K tile" % h.shape[1])
+        ops.gemm(h, w2, self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID)
+
+
+class PatchMerging(nn.Module):
+    """swin_transformer.py:279-315."""
+
+    def __init__(self, dim, norm_layer=nn.LayerNorm):
+        super().__init__()
+        self.dim = dim
+        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+        self.norm = norm_layer(4 * dim)
+
+    def run(self, X, B, D, H, W, ctx):
+        H2, W2 = (H + 1) // 2, (W + 1) // 2
+        rows = B * D * H2 * W2
+        wr, ldk = ctx.wp(self.reduction.weight)
+        if ldk != 4 * self.dim:
+            raise DsvtError("PatchMerging width 4C=%d must be a multiple of the GEMM K tile" % (4 * self.dim))
+        m = torch.empty(rows, 4 * self.dim, device=X.device, dtype=ctx.mode)
+        ops.swin_merge_ln(X, self.norm, m, B, D, H, W)
+        out = torch.empty(rows, 2 * self.dim, device=X.device, dtype=torch.float32)
+        ops.gemm(m, wr, None, out, out_f32=True)
+        return out, H2, W2
+
+
+class BasicLayer(nn.Module):
+    """swin_transformer.py:335-416."""
+
+    def __init__(self, dim, depth, num_heads, window_size=(1, 7, 7), mlp_ratio=4., qkv_bias=False, qk_scale=None,
+                 drop=0., attn_drop=0., drop_path=0., norm_layer=nn.LayerNorm, downsample=None, use_checkpoint=False):
+        super().__init__()
+        self.window_size = window_size
+        self.shift_size = tuple(i // 2 for i in window_size)
+        self.depth = depth
+        self.use_checkpoint = use_checkpoint
+        self.blocks = nn.ModuleList([
+            SwinTransformerBlock3D(dim=dim, num_heads=num_heads, window_size=window_size,
+                                   shift_size=(0, 0, 0) if (i % 2 == 0) else self.shift_size, mlp_ratio=mlp_ratio,
+                                   qkv_bias=qkv_bias, qk_scale=qk_scale, drop=drop, attn_drop=attn_drop,
+                                   drop_path=drop_path[i] if isinstance(drop_path, list) else drop_path,
+                                   norm_layer=norm_layer, use_checkpoint=use_checkpoint)
+            for i in range(depth)])
+        self.downsample = downsample
+        if self.downsample is not None:
+            self.downsample = downsample(dim=dim, norm_layer=norm_layer)
+
+    def run(self, X, B, D, H, W, ctx):
+        for blk in self.blocks:
+            blk.run(X, B, D, H, W, ctx)
+        if self.downsample is not None:
+            X, H, W = self.downsample.run(X, B, D, H, W, ctx)
+        return X, H, W
+
+
+class PatchEmbed3D(nn.Module):
+    """swin_transformer.py:419-460."""
+
+    def __init__(self, patch_size=(2, 4, 4), in_chans=3, embed_dim=96, norm_layer=None):
+        super().__init__()
+        self.patch_size = patch_size
+        self.in_chans = in_chans
+        self.embed_dim = embed_dim
+        self.proj = nn.Conv3d(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size)
+        self.norm = norm_layer(embed_dim) if norm_layer is not None else None
+
+
+class _SwinCtx:
+    def __init__(self, model, mode, device):
+        self.model, self.mode, self.device = model, mode, device
+        self.wp = model._wcache.padded(mode)
+
+    def maps(self, B, D, H, W, ws, ss):
+        key = ("maps", B, D, H, W, ws, ss, self.device)
+        ent = self.model._aux.get(key)
+        if ent is None:
+            win, reg, nW, N = window_maps(B, D, H, W, tuple(ws), tuple(ss))
+            ent = (torch.from_numpy(win).to(self.device), torch.from_numpy(reg).to(self.device), nW, N)
+            self.model._aux[key] = ent
+        return ent
+
+    def bias(self, attn, N):
+        t = attn.relative_position_bias_table
+        key = ("bias", id(attn), N, t._version, t.data_ptr())
+        ent = self.model._aux.get(key)
+        if ent is None:
+            ent = torch.empty(attn.num_heads, N, N, device=self.device, dtype=torch.float32)
+            ops.relpos_bias(t.detach().contiguous(), attn.relative_position_index.contiguous(), N, ent)
+            self.model._aux[key] = ent
+        return ent
+
+    def zeros(self, shape, dtype):
+        return torch.zeros(shape, device=self.device, dtype=dtype)
+
+
+class SwinTransformer3D(nn.Module):
+    """swin_transformer.py:463-687 (defaults = Swin-T: patch (4,4,4), C 96, depths 2-2-6-2,
+    heads 3-6-12-24, window (2,7,7))."""
+
+    def __init__(self, pretrained=None, pretrained2d=True, patch_size=(4, 4, 4), in_chans=3, embed_dim=96,
+                 depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24], window_size=(2, 7, 7), mlp_ratio=4., qkv_bias=True,
+                 qk_scale=None, drop_rate=0., attn_drop_rate=0., drop_path_rate=0.2, norm_layer=nn.LayerNorm,
+                 patch_norm=False, frozen_stages=-1, use_checkpoint=False):
+        super().__init__()
+        self.pretrained = pretrained
+        self.pretrained2d = pretrained2d
+        self.num_layers = len(depths)
+        self.embed_dim = embed_dim
+        self.patch_norm = patch_norm
+        self.frozen_stages = frozen_stages
+        self.window_size = window_size
+        self.patch_size = patch_size
+        self.patch_embed = PatchEmbed3D(patch_size=patch_size, in_chans=in_chans, embed_dim=embed_dim,
+                                        norm_layer=norm_layer if self.patch_norm else None)
+        self.pos_drop = nn.Dropout(p=drop_rate)
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
+        self.layers = nn.ModuleList()
+        for i_layer in range(self.num_layers):
+            self.layers.append(BasicLayer(
+                dim=int(embed_dim * 2 ** i_layer), depth=depths[i_layer], num_heads=num_heads[i_layer],
+                window_size=window_size, mlp_ratio=mlp_ratio, qkv_bias=qkv_bias, qk_scale=qk_scale, drop=drop_rate,
+                attn_drop=attn_drop_rate, drop_path=dpr[sum(depths[:i_layer]):sum(depths[:i_layer + 1])],
+                norm_layer=norm_layer, downsample=PatchMerging if i_layer < self.num_layers - 1 else None,
+                use_checkpoint=use_checkpoint))
+        self.num_features = int(embed_dim * 2 ** (self.num_layers - 1))
+        self.norm = norm_layer(self.num_features)
+        self.avg_pool = torch.nn.AdaptiveAvgPool3d((1, 1, 1))
+        self._freeze_stages()
+        self.dsvt_dtype = _DEFAULT_DTYPE[0]
+        self._wcache = WeightCache()
+        self._aux = {}
+        self._drop = (drop_rate, attn_drop_rate, drop_path_rate)
+
+    def _freeze_stages(self):
+        """swin_transformer.py:555-567."""
+        if self.frozen_stages >= 0:
+            self.patch_embed.eval()
+            for param in self.patch_embed.parameters():
+                param.requires_grad = False
+        if self.frozen_stages >= 1:
+            self.pos_drop.eval()
+            for i in range(0, self.frozen_stages):
+                m = self.layers[i]
+                m.eval()
+                for param in m.parameters():
+                    param.requires_grad = False
+
+    def init_weights(self, pretrained=None):
+        """swin_transformer.py:632-666 (local checkpoints only)."""
+        def _init_weights(m):
+            if isinstance(m, nn.Linear):
+                trunc_normal_(m.weight, std=.02)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+            elif isinstance(m, nn.LayerNorm):
+                nn.init.constant_(m.bias, 0)
+                nn.init.constant_(m.weight, 1.0)
+        if pretrained:
+            self.pretrained = pretrained
+        if isinstance(self.pretrained, str):
+            self.apply(_init_weights)
+            if self.pretrained2d:
+                self.inflate_weights()
+        elif self.pretrained is None:
+            self.apply(_init_weights)
+        else:
+            raise TypeError('pretrained must be a str or None')
+
+    def inflate_weights(self, logger=None):
+        """swin_transformer.py:569-630: inflate a 2-D Swin checkpoint (loaded with
+        weights_only=True) into the 3-D model."""
+        checkpoint = torch.load(self.pretrained, map_location='cpu', weights_only=True)
+        state_dict = checkpoint['model']
+        for k in [k for k in state_dict if "relative_position_index" in k or "attn_mask" in k]:
+            del state_dict[k]
+        state_dict['patch_embed.proj.weight'] = state_dict['patch_embed.proj.weight'].unsqueeze(2).repeat(
+            1, 1, self.patch_size[0], 1, 1) / self.patch_size[0]
+        for k in [k for k in state_dict if "relative_position_bias_table" in k]:
+            pre = state_dict[k]
+            L1, nH1 = pre.size()
+            L2 = (2 * self.window_size[1] - 1) * (2 * self.window_size[2] - 1)
+            wd = self.window_size[0]
+            if nH1 != self.state_dict()[k].size(1):
+                print(f"Error in loading {k}, passing")
+            else:
+                if L1 != L2:
+                    S1 = int(L1 ** 0.5)
+                    pre = torch.nn.functional.interpolate(
+                        pre.permute(1, 0).view(1, nH1, S1, S1),
+                        size=(2 * self.window_size[1] - 1, 2 * self.window_size[2] - 1), mode='bicubic')
+                    pre = pre.view(nH1, L2).permute(1, 0)
+            state_dict[k] = pre.repeat(2 * wd - 1, 1)
+        msg = self.load_state_dict(state_dict, strict=False)
+        print(msg)
+        print(f"=> loaded successfully '{self.pretrained}'")
+
+    def forward(self, x):
+        """swin_transformer.py:668-682 -> pooled features [B, num_features] fp32."""
+        if not x.is_cuda or not self.norm.weight.is_cuda:
+            raise DsvtError("dsvt SwinTransformer3D runs only on the GPU (no CPU fallback)")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("dsvt Swin backward is not implemented: run under torch.no_grad()")
+        if self.training and self._drop[2] > 0:
+            raise NotImplementedError("training-mode DropPath is not implemented for dsvt Swin; call .eval()")
+        if self.patch_embed.norm is not None:
+            raise NotImplementedError("patch_norm=True is not supported by the dsvt Swin forward")
+        mode = self.dsvt_dtype
+        ctx = _SwinCtx(self, mode, x.device)
+        x = x.float().contiguous()
+        B, Cin, D0, H0, W0 = x.shape
+        pd, ph, pw = self.patch_size
+        D, H, W = -(-D0 // pd), -(-H0 // ph), -(-W0 // pw)
+        C = self.embed_dim
+        wpe, ldk = ctx.wp(self.patch_embed.proj.weight, flat=True)
+        ws = torch.empty(B * D * H * W * ldk * (2 if mode == torch.bfloat16 else 4) // 4 + 64, device=x.device,
+                         dtype=torch.float32)
+        X = torch.empty(B * D * H * W, C, device=x.device, dtype=torch.float32)
+        ops.swin_patch_embed(x, wpe, ldk, self.patch_embed.proj.bias, self.patch_size, X, ws)
+        for layer in self.layers:
+            X, H, W = layer.run(X, B, D, H, W, ctx)
+        C = X.shape[1]
+        Y = torch.empty_like(X)
+        ops.layernorm(X, X.shape[0], C, self.norm.weight, self.norm.bias, self.norm.eps, Y)
+        out = torch.empty(B, C, device=x.device, dtype=torch.float32)
+        ops.frame_mean(Y, out, B, D * H * W, C)                 # AdaptiveAvgPool3d((1, 1, 1))
+        return out
+
+    def train(self, mode=True):
+        """swin_transformer.py:684-687 -- kept as in the reference, which returns None (SURVEY §5
+        defect 6: `.eval()` on this model returns None, call it as a statement)."""
+        super(SwinTransformer3D, self).train(mode)
+        self._freeze_stages()

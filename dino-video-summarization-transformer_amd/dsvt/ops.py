@@ -345,3 +345,46 @@ def gemm_kernel_name(tag):
     if variant in persist:
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)
+
+
+# ---------------------------------------------------------------- Video Swin
+def cast_pad(x, out):
+    _check(x, torch.float32, "x")
+    call("dsvt_cast_pad_fwd", _dt(out.dtype), _ptr(x), _ptr(out), x.shape[0], x.shape[1], out.shape[1], _stream())
+    return out
+
+
+def swin_patch_embed(x, w, ldk, bias, patch, X, ws):
+    _check(x, torch.float32, "x")
+    B, Cin, D, H, W = x.shape
+    call("dsvt_swin_patch_embed_fwd", _dt(w.dtype), _ptr(x), B, Cin, D, H, W, patch[0], patch[1], patch[2], _ptr(w),
+         ldk, _ptr(bias), w.shape[0], _ptr(X), _ptr(ws), ws.numel() * ws.element_size(), _stream())
+    return X
+
+
+def swin_ln_rows(x, idx, ln, out, rows):
+    call("dsvt_swin_ln_rows_fwd", _dt(out.dtype), _ptr(x), _ptr(idx), _ptr(ln.weight), _ptr(ln.bias), _ptr(out), rows,
+         x.shape[-1], out.shape[-1], float(ln.eps), _stream())
+    return out
+
+
+def swin_merge_ln(x, ln, out, B, D, H, W):
+    call("dsvt_swin_merge_ln_fwd", _dt(out.dtype), _ptr(x), _ptr(ln.weight), _ptr(ln.bias), _ptr(out), B, D, H, W,
+         x.shape[-1], float(ln.eps), _stream())
+    return out
+
+
+def window_scatter_add(X, y, idx):
+    call("dsvt_window_scatter_add", _ptr(X), _ptr(y), _ptr(idx), y.shape[0], y.shape[1], _stream())
+    return X
+
+
+def relpos_bias(table, index, N, out):
+    call("dsvt_relpos_bias_fwd", _ptr(table), _ptr(index), index.shape[-1], N, table.shape[1], _ptr(out), _stream())
+    return out
+
+
+def attn_window(qkv, out, bias, region, nwin, nwc, N, heads, scale):
+    call("dsvt_attn_window_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.shape[-1], _ptr(bias), _ptr(region), nwin,
+         nwc, N, heads, 32, float(scale), _stream())
+    return out

@@ -66,6 +66,27 @@ class WeightCache:
             return out
         return get
 
+    def padded(self, mode):
+        """W [N, K] as [N, ldk] in the storage dtype with zero columns K..ldk-1 (ldk = K rounded
+        up to the MFMA K tile: 64 bf16 / 32 fp32), cached like the casts.  Returns (w, ldk)."""
+        def get(p, flat=False):
+            t = p.detach()
+            if flat:
+                t = t.reshape(t.shape[0], -1)
+            K = t.shape[1]
+            q = 64 if mode == torch.bfloat16 else 32
+            ldk = (K + q - 1) // q * q
+            key = (id(p), "pad", mode, flat)
+            ent = self._c.get(key)
+            if ent is not None and ent[0] == p._version and ent[1] == p.data_ptr():
+                self._sync(ent)
+                return ent[2], ldk
+            out = torch.empty(t.shape[0], ldk, device=t.device, dtype=mode)
+            ops.cast_pad(t.float().contiguous(), out)
+            self._c[key] = (p._version, p.data_ptr(), out) + self._event()
+            return out, ldk
+        return get
+
     def transposed(self, mode):
         """W^T [in, out] in the storage dtype (dsvt cast-transpose kernel), cached like the
         casts: the B operand of the backward's input-gradient GEMMs dX = dY . W."""

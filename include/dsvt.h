@@ -267,6 +267,41 @@ int dsvt_clip_grads(float *const *grads, const int64_t *sizes, const int32_t *ch
                     int64_t ntensors, float clip, float *norms, void *workspace, int64_t workspace_bytes,
                     void *stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Video Swin Transformer backbone (models/swin_transformer.py, config 5).  Tokens: fp32
+ * X [B, D, H, W, C] channels-last.  Linear layers run on dsvt_gemm_fwd with K zero-padded to
+ * the MFMA tile (ldk: C = 96 -> 128 in bf16); window rows are gathered / scattered through
+ * int32 index maps that encode the cyclic shift and the padding (-1 = zero row).
+ * ------------------------------------------------------------------------------------------ */
+/* PatchEmbed3D (:419-460): Conv3d(k = s = (pd, ph, pw)) with zero padding, as im2col + GEMM;
+ * w [C, ldk] storage dtype (Conv3d weight flattened, zero-padded); X [B*Do*Ho*Wo, C] fp32. */
+int dsvt_swin_patch_embed_fwd(int dtype, const float *x, int64_t B, int64_t Cin, int64_t D, int64_t H,
+                              int64_t W, int64_t pd, int64_t ph, int64_t pw, const void *w, int64_t ldk,
+                              const float *bias, int64_t C, float *X, void *workspace,
+                              int64_t workspace_bytes, void *stream);
+/* out[m] = LayerNorm(x[idx[m]]) (idx NULL = identity; idx[m] < 0 = zero row), columns C..ldo-1
+ * zero: norm1 + pad + roll + window_partition (:221-237) and norm2 (:254). */
+int dsvt_swin_ln_rows_fwd(int dtype, const float *x, const int32_t *idx, const float *gamma,
+                          const float *beta, void *out, int64_t rows, int64_t C, int64_t ldo, float eps,
+                          void *stream);
+/* PatchMerging (:293-315): 2x2 gather (x0, x1, x2, x3 order, zero pad) + LayerNorm(4C). */
+int dsvt_swin_merge_ln_fwd(int dtype, const float *x, const float *gamma, const float *beta, void *out,
+                           int64_t B, int64_t D, int64_t H, int64_t W, int64_t C, float eps, void *stream);
+/* X[idx[m]] += y[m] (idx[m] >= 0): window_reverse + reverse roll + crop + residual (:241-251). */
+int dsvt_window_scatter_add(float *X, const float *y, const int32_t *idx, int64_t rows, int64_t C,
+                            void *stream);
+/* out[h][i][j] = table[index[i*nmax + j]][h], i, j < N (:152-156, the [:N, :N] slice). */
+int dsvt_relpos_bias_fwd(const float *table, const int64_t *index, int64_t nmax, int64_t N,
+                         int64_t heads, float *out, void *stream);
+/* WindowAttention3D (:139-171): qkv [nwin*N, 3C] window-ordered, out [nwin*N, ldo]; scores
+ * q.k*scale + bias[h] + (-100 where region[w % nwc][i] != region[w % nwc][j]); head_dim 32,
+ * N <= 128.  region all-zero = no shift mask. */
+int dsvt_attn_window_fwd(int dtype, const void *qkv, void *out, int64_t ldo, const float *bias,
+                         const int32_t *region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads,
+                         int64_t head_dim, float scale, void *stream);
+/* y [N, ldk] = x [N, K] cast to the storage dtype with zero columns K..ldk-1. */
+int dsvt_cast_pad_fwd(int dtype, const float *x, void *y, int64_t N, int64_t K, int64_t ldk, void *stream);
+
 /* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
  * 1 = 128x128 / 4-wave kernel, 2 = 256x256 / 8-wave, 3 = 256x128 / 8-wave.  Process-global. */
 int dsvt_set_gemm_variant(int variant);

@@ -123,3 +123,23 @@ def clip(seed, shape, std=1.0):
 
 def uniform(seed, shape, lo=-1.0, hi=1.0):
     return rng(seed).uniform(lo, hi, size=shape).astype(np.float32)
+
+
+def swin_state(seed, shapes):
+    """Video Swin (models/swin_transformer.py:463-687) parameters for a given {key: shape} map
+    (the reference's state_dict keys minus the relative_position_index buffers), generated in
+    sorted-key order so any module with the same keys gets the same values.  LayerNorms get a
+    non-trivial affine, relative-position bias tables a wide spread (so the bias matters)."""
+    g = rng(seed)
+    sd = {}
+    for k in sorted(shapes):
+        shape = tuple(shapes[k])
+        if "relative_position_index" in k:
+            continue
+        if "norm" in k and k.endswith(".weight"):
+            sd[k] = (1.0 + _normal(g, shape, 0.1)).astype(np.float32)
+        elif "relative_position_bias_table" in k:
+            sd[k] = _normal(g, shape, 1.0)
+        else:
+            sd[k] = _normal(g, shape, 0.05)
+    return sd

@@ -133,6 +133,37 @@ def train_grads(TL):
     return res
 
 
+SWIN_SMALL = dict(embed_dim=64, depths=[2, 2, 2, 2], num_heads=[2, 4, 8, 16])
+
+
+def swin_outputs():
+    """Reference SwinTransformer3D forwards (eval).  timm is absent: models.swin_transformer
+    imports DropPath / trunc_normal_ from timm.models.layers, stubbed with the reference's own
+    models/vit_utils.py versions (SURVEY §8(c) recipe)."""
+    import models.vit_utils as ref_vu
+    for name in ("timm", "timm.models", "timm.models.layers"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["timm.models.layers"].DropPath = ref_vu.DropPath
+    sys.modules["timm.models.layers"].trunc_normal_ = ref_vu.trunc_normal_
+    import models.swin_transformer as ref_swin
+    res = {}
+    for tag, kw, shape, seed in (("small", SWIN_SMALL, (2, 3, 8, 64, 64), 1301),
+                                 ("small_odd", SWIN_SMALL, (1, 3, 6, 72, 40), 1303),
+                                 ("tiny", {}, (1, 3, 8, 224, 224), 1302)):
+        m = ref_swin.SwinTransformer3D(**kw)
+        sd = P.swin_state(seed, {k: v.shape for k, v in m.state_dict().items()})
+        missing, unexpected = m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+        assert not unexpected and all("relative_position_index" in k for k in missing)
+        m.eval()          # a statement: the reference's train() returns None (SURVEY §5 defect 6)
+        with torch.no_grad():
+            res[tag] = m(torch.from_numpy(P.clip(seed + 10, shape))).numpy()
+        if tag == "tiny":
+            res["keys_tiny"] = np.array(sorted(m.state_dict().keys()))
+            res["shapes_tiny"] = np.array([list(m.state_dict()[k].shape) + [0] * (5 - m.state_dict()[k].dim())
+                                           for k in sorted(m.state_dict().keys())], np.int64)
+    return res
+
+
 def run(m, x, **kw):
     with torch.no_grad():
         return m.forward_features(torch.from_numpy(x), **kw).numpy()
@@ -254,6 +285,9 @@ def main():
     # mask from a seeded CPU generator (recorded, in call order, for the dsvt test to replay).
     out["train_grads"] = train_grads(TL)
     dist.destroy_process_group()
+
+    # ---- 9. Video Swin (config 5): small config with padding / clamped windows, and Swin-T 8x224^2
+    out["swin"] = swin_outputs()
 
     for name, arrays in out.items():
         path = os.path.join(HERE, name + ".npz")
