@@ -209,6 +209,78 @@ def train_bench(args, device, rank, world, steps, warmup):
             "drop_path": 0.1, "teacher_mode": "eval"}
 
 
+# ----------------------------------------------------------------- configs 4 / 5: other backbones
+def joint_flops(T=16, S=224, C=768, depth=12, heads=12, mlp=4, patch=16):
+    """ViT-B/16 joint space-time forward: 899.35 GFLOP at 16x224^2."""
+    N = (S // patch) ** 2
+    L = 1 + N * T
+    per_block = 2 * L * C * 3 * C + 4 * heads * L * L * (C // heads) + 2 * L * C * C + 2 * 2 * L * C * mlp * C
+    return depth * per_block + 2 * N * T * (3 * patch * patch) * C
+
+
+def swin_t_flops(T=8, S=224, C=96, depths=(2, 2, 6, 2), window=(2, 7, 7), patch=(4, 4, 4)):
+    """Video Swin-T forward at 8x224^2: 2*M*N*K of every Linear / Conv3d / window matmul."""
+    D, H, W = T // patch[0], S // patch[1], S // patch[2]
+    fl = 2 * D * H * W * C * 3 * patch[0] * patch[1] * patch[2]
+    for i, depth in enumerate(depths):
+        c = C * 2 ** i
+        rows = D * H * W
+        wd, wh, ww = min(window[0], D), min(window[1], H), min(window[2], W)
+        n = wd * wh * ww
+        rows_w = (-(-D // wd) * wd) * (-(-H // wh) * wh) * (-(-W // ww) * ww)
+        fl += depth * (2 * rows_w * c * 3 * c + 4 * rows_w * n * c + 2 * rows_w * c * c + 2 * 2 * rows * c * 4 * c)
+        if i < len(depths) - 1:
+            H, W = (H + 1) // 2, (W + 1) // 2
+            fl += 2 * D * H * W * 4 * c * 2 * c
+    return fl
+
+
+def other_configs(args, device):
+    """Forward clips/s of BASELINE.json configs 4 (ViT-B/16 joint space-time, 16x224^2) and 5
+    (Video Swin-T, 8x224^2) on one GPU, random init, synthetic normalized frames."""
+    from functools import partial
+
+    import torch.nn as nn
+
+    from dsvt.models import SwinTransformer3D
+    from dsvt.models.timesformer import VisionTransformer
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    res = {}
+
+    def timed(fn, reps=5, warm=2):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    torch.manual_seed(1)
+    jm = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
+                           norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=16,
+                           attention_type="joint_space_time").to(device).eval()
+    jm.dsvt_dtype = dtype
+    xj = torch.randn(2, 3, 16, 224, 224, device=device)
+    with torch.no_grad():
+        t = timed(lambda: jm(xj))
+    res["config4_joint16"] = {"value": round(2 / t, 2), "unit": "clips/s", "clips_per_step": 2,
+                              "gflop_per_clip": round(joint_flops() / 1e9, 1),
+                              "tflops": round(2 * joint_flops() / t / 1e12, 1)}
+    del jm, xj
+    sm = SwinTransformer3D().to(device)
+    sm.eval()
+    sm.dsvt_dtype = dtype
+    xs = torch.randn(8, 3, 8, 224, 224, device=device)
+    with torch.no_grad():
+        t = timed(lambda: sm(xs))
+    res["config5_swin_t"] = {"value": round(8 / t, 2), "unit": "clips/s", "clips_per_step": 8,
+                             "gflop_per_clip": round(swin_t_flops() / 1e9, 2),
+                             "tflops": round(8 * swin_t_flops() / t / 1e12, 1)}
+    return res
+
+
 # ----------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -224,6 +296,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
+    ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
     args = ap.parse_args()
 
@@ -361,6 +434,8 @@ def main():
         graph = None                        # release the captured forward's memory pool
         torch.cuda.empty_cache()
         out["train_step"] = train_bench(args, device, rank, world, args.train_steps, 2)
+    if rank == 0 and world == 1 and not args.no_other:
+        out["other_configs"] = other_configs(args, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
