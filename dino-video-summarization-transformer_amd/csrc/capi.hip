@@ -376,8 +376,8 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 
 int dsvt_set_gemm_variant(int variant) {
   REQUIRE(variant == 0 || variant == 1 || (variant >= 3 && variant <= 6) || (variant >= 9 && variant <= 13) ||
-              variant == 14 || variant == 24 || variant == 34,
-          "gemm variant must be 0, 1, 3-6 or 9-13 (14/24/34: ablation builds)");
+              (variant >= 20 && variant <= 29 && variant != 24) || variant == 14 || variant == 24 || variant == 34,
+          "gemm variant must be 0, 1, 3-6, 9-13 or 20 (14/24/34: ablation builds)");
   set_gemm_variant(variant);
   return 0;
 }

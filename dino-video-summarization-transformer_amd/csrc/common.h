@@ -31,11 +31,18 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 // per lane for ONE 16-byte store: a v_permlane16_swap per packed dword gives lane group g the
 // columns {g0: 0-7, g1: 16-23, g2: 8-15, g3: 24-31} of the 32-column span (offset pair_off(g)).
 // Cross-lane: call with the whole wave active; predicate only the store.
+// two floats -> packed bf16 pair (low = a) in ONE v_cvt_pk_bf16_f32 (RNE)
+__device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  const b2_t h = __builtin_convertvector((f2_t){a, b}, b2_t);
+  return __builtin_bit_cast(unsigned, h);
+}
 __device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
-  const unsigned a0 = (unsigned)f2bf(a[0]) | ((unsigned)f2bf(a[1]) << 16);
-  const unsigned a1 = (unsigned)f2bf(a[2]) | ((unsigned)f2bf(a[3]) << 16);
-  const unsigned b0 = (unsigned)f2bf(b[0]) | ((unsigned)f2bf(b[1]) << 16);
-  const unsigned b1 = (unsigned)f2bf(b[2]) | ((unsigned)f2bf(b[3]) << 16);
+  const unsigned a0 = cvt_pk_bf16(a[0], a[1]);
+  const unsigned a1 = cvt_pk_bf16(a[2], a[3]);
+  const unsigned b0 = cvt_pk_bf16(b[0], b[1]);
+  const unsigned b1 = cvt_pk_bf16(b[2], b[3]);
   const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
   return make_uint4(s0[0], s1[0], s0[1], s1[1]);
@@ -149,6 +156,12 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
 // Output-row map used by every kernel that writes into the [B, L, C] token tensor:
 //   row(m) = (m / rpg) * gstride + goff + (m % rpg)
 // identity: rpg = huge, gstride = 0, goff = 0.
+// (identity: one test; 32-bit operands: a 32-bit division instead of the ~50-op 64-bit one)
 __device__ __forceinline__ long map_row(long m, long rpg, long gstride, long goff) {
+  if (m < rpg) return goff + m;
+  if (((unsigned long)m | (unsigned long)rpg) >> 31 == 0) {
+    const unsigned q = (unsigned)m / (unsigned)rpg;
+    return (long)q * gstride + goff + (long)((unsigned)m - q * (unsigned)rpg);
+  }
   return (m / rpg) * gstride + goff + (m % rpg);
 }

@@ -1,0 +1,193 @@
+// Register epilogue shared by the large-tile GEMM kernels (gemm_big.hip, gemm_8ph.hip).
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+
+namespace dsvt {
+
+// NT: non-temporal (streaming) store -- the output is not re-read by this kernel, keep L2 for
+// the operand panels
+template <bool NT = false, bool NOSTORE = false>
+__device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int g) {
+  const uint4 v = pack_pair_bf16(a, b);
+  if constexpr (NOSTORE) {
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(span));
+  } else if constexpr (NT) {
+    typedef unsigned int uv4 __attribute__((ext_vector_type(4)));
+    const uv4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<uv4*>(span + pair_off(g)));
+  } else {
+    *reinterpret_cast<uint4*>(span + pair_off(g)) = v;
+  }
+}
+
+// Direct (register) epilogue shared by the big and persistent kernels.
+// BIAS_IN_ACC: the accumulators started from the bias (gemm_8ph.hip), none is added here.
+template <int MI, int NJ, int EPI, bool OUT_F32, bool NT = false, bool NOSTORE = false, bool BIAS_IN_ACC = false>
+__device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
+                                                int64_t cbase, int r16, int g) {
+  using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
+  // bias: scalar loads for a full 64-column wave slab (no vmcnt wait behind the in-flight
+  // prefetch of the next tile); per-lane vector loads only at a ragged N edge
+  float4 bias4[NJ];
+  if (BIAS_IN_ACC) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bias4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  } else if (NJ == 4 && cbase + 64 <= p.N) {
+    float4 b4[4];
+    bias_frag4(p.bias, cbase, g, b4);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bias4[j] = b4[j & 3];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t n = cbase + j * 16 + 4 * g;
+      bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // training epilogues (per-element, bf16 aux operand): GELU with the pre-activation saved,
+  // and GELU backward
+  if constexpr (EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = rbase + i * 16 + r16;
+      if (m >= p.M) continue;
+      const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int64_t n = cbase + j * 16 + 4 * g;
+        if (n >= p.N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == EPI_GELU_SAVE) {
+          const float4 bb = bias4[j];
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+          store4((bf16_t*)p.aux + orow * p.ld_aux + n, v[0], v[1], v[2], v[3]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+        } else {
+          float pre[4];
+          load4((const bf16_t*)p.aux + orow * p.ld_aux + n, pre);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= gelu_erf_grad(pre[e]);
+        }
+        store4(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n, v[0], v[1], v[2], v[3]);
+      }
+    }
+    return;
+  }
+  const bool ident = p.rpg >= p.M;   // wave-uniform: no per-lane row-map division
+  // full wave tile (uniform): branch-free bias / GELU / 16-B stores, so the compiler's vmcnt
+  // waits stay exact (a per-lane bounds branch around each store makes it drain every time)
+  if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0) {
+    if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int64_t m = rbase + i * 16 + r16;
+        const int64_t orow = ident ? m : map_row(m, p.rpg, p.gstride, p.goff);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (!BIAS_IN_ACC) {
+            const float4 bb = bias4[j];
+            acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
+          }
+          if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; j += 2)
+          store_pair_bf16<NT, NOSTORE>((bf16_t*)p.out + orow * p.ldo + cbase + j * 16, acc[i][j], acc[i][j + 1], g);
+      }
+      return;
+    }
+  }
+  // full wave tile, fp32 residual add into X: the X fragments of two rows are loaded before
+  // their stores (one HBM round trip per row pair instead of per fragment), branch-free
+  if constexpr (EPI == EPI_RESID && MI % 2 == 0) {
+    if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
+#pragma unroll
+      for (int i = 0; i < MI; i += 2) {
+        float* xr[2];
+        float4 x[2][NJ];
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          xr[ii] = (float*)p.out + map_row(rbase + (i + ii) * 16 + r16, p.rpg, p.gstride, p.goff) * p.ldo + cbase + 4 * g;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) x[ii][j] = *reinterpret_cast<const float4*>(xr[ii] + j * 16);
+        }
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const float4 bb = bias4[j];
+            const fv4 a = acc[i + ii][j];
+            *reinterpret_cast<float4*>(xr[ii] + j * 16) =
+                make_float4(x[ii][j].x + a[0] + bb.x, x[ii][j].y + a[1] + bb.y, x[ii][j].z + a[2] + bb.z,
+                            x[ii][j].w + a[3] + bb.w);
+          }
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int64_t m = rbase + i * 16 + r16;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float4 bb = bias4[j];
+      acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
+      if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+      }
+    }
+    if (m >= p.M) continue;
+    const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
+    if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0) {
+#pragma unroll
+      for (int j = 0; j < NJ; j += 2) {
+        const int64_t span = cbase + j * 16;
+        if (span + 32 <= p.N) {
+          store_pair_bf16<NT, NOSTORE>((bf16_t*)p.out + orow * p.ldo + span, acc[i][j], acc[i][j + 1], g);
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int64_t n = span + jj * 16 + 4 * g;
+            if (n < p.N)
+              store4((bf16_t*)p.out + orow * p.ldo + n, acc[i][j + jj][0], acc[i][j + jj][1], acc[i][j + jj][2],
+                     acc[i][j + jj][3]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int64_t n = cbase + j * 16 + 4 * g;
+        if (n >= p.N) continue;
+        const float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
+          store4(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n, v0, v1, v2, v3);
+        } else if constexpr (EPI == EPI_RESID) {
+          float4* xo = reinterpret_cast<float4*>((float*)p.out + orow * p.ldo + n);
+          float4 x = *xo;
+          x.x += v0; x.y += v1; x.z += v2; x.w += v3;
+          *xo = x;
+        } else {  // EPI_PATCH
+          const int64_t rrw = m % p.rpg;
+          const int64_t np = rrw / p.T, tt = rrw % p.T;
+          const float4 pe = *reinterpret_cast<const float4*>(p.pos + (1 + (int64_t)p.pidx[np]) * p.N + n);
+          float4 o = make_float4(v0 + pe.x, v1 + pe.y, v2 + pe.z, v3 + pe.w);
+          if (p.temb) {
+            const float4 te = *reinterpret_cast<const float4*>(p.temb + (int64_t)p.tidx[tt] * p.N + n);
+            o.x += te.x; o.y += te.y; o.z += te.z; o.w += te.w;
+          }
+          *reinterpret_cast<float4*>((float*)p.out + orow * p.ldo + n) = o;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace dsvt

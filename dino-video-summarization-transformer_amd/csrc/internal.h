@@ -17,6 +17,8 @@ struct GemmParams {
   int64_t T;  // frames per patch group (1 for the frame-major order)
   // backward / training epilogues: second operand in the storage dtype, row-major, ld_aux
   void* aux; int64_t ld_aux;
+  // persistent 256x256 kernel: tile order, GM m-tile rows per group walked n-column-major (0 = row-major)
+  int tile_group;
 };
 
 // EPI_GELU_SAVE: out = GELU(acc + bias), aux = acc + bias (the pre-activation, for the backward)
@@ -26,6 +28,8 @@ enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_PATCH = 3, EPI_GELU_SAVE =
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s);
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // the kernel launch_gemm dispatches
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
+hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
+bool gemm_8ph_ok(const GemmParams& p, int epi);
 void set_gemm_variant(int v);
 
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,

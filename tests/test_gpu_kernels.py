@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 3, 4, 5, 6, 9, 10, 11, 12, 13])
+@pytest.fixture(params=[0, 1, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -67,6 +67,38 @@ def test_gemm_bias_gelu(dtype, M, N, K, gemm_variant):
             ops.gemm(A, W, Bt, out, epilogue=epi, out_f32=out_f32)
             torch.cuda.synchronize()
             check(back(out), f(ref), dtype, "gemm epi=%d f32out=%d" % (epi, out_f32))
+
+
+@pytest.mark.parametrize("variant", [10, 20])
+@pytest.mark.parametrize("M,N,K", [(8200, 2304, 768), (8200, 2304, 64), (6000, 3072, 128), (25104, 768, 3072)])
+def test_gemm_persistent_stream(M, N, K, variant):
+    """Persistent kernels with several output tiles per workgroup (the K-tile stream crosses
+    tile boundaries; ragged last M tile), every epilogue, against torch fp32 of the bf16 operands."""
+    from dsvt import _lib, ops
+    g = torch.Generator(device=dev()).manual_seed(M + N + K)
+    A = (torch.randn(M, K, device=dev(), generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev(), generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=dev(), generator=g)
+    ref = torch.addmm(b, A.float(), W.float().t())
+    _lib.call("dsvt_set_gemm_variant", variant)
+    try:
+        for epi in (_lib.EPI_BIAS, _lib.EPI_BIAS_GELU, _lib.EPI_BIAS_RESID):
+            want = torch.nn.functional.gelu(ref) if epi == _lib.EPI_BIAS_GELU else ref
+            for out_f32 in ((True,) if epi == _lib.EPI_BIAS_RESID else (False, True)):
+                if epi == _lib.EPI_BIAS_RESID:
+                    x0 = torch.randn(M, N, device=dev(), generator=g)
+                    out = x0.clone()
+                    want_e = want + x0
+                else:
+                    out = torch.full((M, N), float("nan"), device=dev(),
+                                     dtype=torch.float32 if out_f32 else torch.bfloat16)
+                    want_e = want
+                ops.gemm(A, W, b, out, epilogue=epi, out_f32=out_f32)
+                torch.cuda.synchronize()
+                err = ((out.float() - want_e).abs().max() / want_e.abs().max()).item()
+                assert err < (2e-2 if out.dtype == torch.bfloat16 else 2e-3), (epi, out_f32, err)
+    finally:
+        _lib.call("dsvt_set_gemm_variant", 0)
 
 
 def test_gelu_epilogue_accuracy():

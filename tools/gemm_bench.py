@@ -72,22 +72,31 @@ def main():
     variants = [int(v) for v in sys.argv[1:]] or [0]
     print("hipBLASLt (torch F.linear bf16):")
     for name, M, N, K, epi in SHAPES:
+        if os.environ.get("DSVT_SHAPES"):
+            break
         tf, ms = torch_ref(M, N, K)
         print("  %-7s %6d %6d %5d  %7.1f TF/s (%7.1f us)" % (name, M, N, K, tf, ms * 1e3), flush=True)
     print("%-7s %6s %6s %5s | " % ("shape", "M", "N", "K") + " | ".join("v%d TF/s (us)" % v for v in variants))
+    only = os.environ.get("DSVT_SHAPES")
     for name, M, N, K, epi in SHAPES:
-        if any(v >= 10 for v in variants):
+        if only and name not in only.split(","):
+            continue
+        if any(v in (14, 24, 34) for v in variants):
             epi = _lib.EPI_BIAS          # ablation builds exist for EPI_BIAS only
-        cells, ref = [], None
-        for v in variants:
-            set_variant(v)
-            tf, ms, out = run(M, N, K, epi)
-            if ref is None:
-                ref = out.float()
-                d = 0.0
-            else:
-                d = (out.float() - ref).abs().max().item()
-            cells.append("%7.1f (%7.1f) d=%.1e" % (tf, ms * 1e3, d))
+        best, ref, diffs = {}, None, {}
+        for _round in range(3):          # interleaved rounds in one process; best of 3
+            for v in variants:
+                set_variant(v)
+                try:
+                    tf, ms, out = run(M, N, K, epi)
+                except _lib.DsvtError:           # variant does not take this epilogue
+                    tf, ms, out = 0.0, float("inf"), ref if ref is not None else torch.zeros(1)
+                if ref is None:
+                    ref = out.float()
+                diffs[v] = (out.float() - ref).abs().max().item()
+                if v not in best or ms < best[v][1]:
+                    best[v] = (tf, ms)
+        cells = ["%7.1f (%7.1f) d=%.1e" % (best[v][0], best[v][1] * 1e3, diffs[v]) for v in variants]
         print("%-7s %6d %6d %5d | " % (name, M, N, K) + " | ".join(cells), flush=True)
     set_variant(0)
 
