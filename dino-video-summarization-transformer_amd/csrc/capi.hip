@@ -120,6 +120,8 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_COLSUM: return up(colsum_parts(M) * N * 4);                        // M = rows, N = C
     case DSVT_WS_ATTN_BWD: return up(M * 3 * N * 4 + M * (N / 64) * K * 2 * 4);     // M = nb*tin, N = C, K = seqlen
     case DSVT_WS_EMBED_BWD: return up((M + N + 2 + M * N) * K * 4);                 // M = Np, N = T, K = C
+    case DSVT_WS_SELECT: return up(select_frames_ws_bytes(M, N));                    // M = scores, N = unsampled
+    case DSVT_WS_AUGMENT: return up(augment_ws_bytes(M, N));                          // M = frames, N = size
     default: return -1;
   }
 }
@@ -703,6 +705,51 @@ int dsvt_attn_window_fwd(int dtype, const void* qkv, void* out, int64_t ldo, con
     return launch_attn_window(dtype, qkv, out, ldo, bias, region, nwin, nwc, N, heads, heads * 32, scale,
                               (hipStream_t)stream);
   });
+}
+
+int dsvt_select_frames(const double* loss, int64_t n_loss, int64_t n_frames, int64_t n_unsampled, int64_t rate,
+                       int64_t N, int64_t* indices, int32_t* frame_pos, double* cdf_out, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  REQUIRE(loss && indices && frame_pos, "select_frames: null pointer");
+  REQUIRE(n_loss >= 1 && n_frames >= 1 && n_unsampled >= 1 && rate >= 1, "select_frames: bad sizes");
+  REQUIRE(N >= 1 && N <= 65535, "select_frames: need 1 <= N <= 65535");
+  const int64_t n = n_loss < n_frames ? n_loss : n_frames;
+  REQUIRE((n - 1) * rate < n_unsampled, "select_frames: (scores - 1) * rate must index the unsampled video");
+  REQUIRE(workspace && workspace_bytes >= (size_t)dsvt_workspace_bytes(DSVT_WS_SELECT, 1, n, n_unsampled, 0),
+          "select_frames: workspace too small");
+  hipError_t e = launch_select_frames(loss, n, n_frames, n_unsampled, rate, N, indices, frame_pos, cdf_out, workspace,
+                                      (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "select_frames");
+}
+
+int dsvt_video_augment(const void* frames, int frames_u8, int64_t T_in, int64_t T, const int32_t* frame_index,
+                       int64_t H, int64_t W, int64_t sT, int64_t sC, int64_t sH, int64_t sW,
+                       const dsvt_aug_params* params, float* out, int out_layout, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  REQUIRE(frames && params && out, "video_augment: null pointer");
+  REQUIRE(T_in >= 1 && T >= 1 && T <= 65535 && H >= 1 && W >= 1, "video_augment: bad sizes");
+  REQUIRE(frame_index || T <= T_in, "video_augment: T > T_in needs a frame_index");
+  REQUIRE(out_layout == 0 || out_layout == 1, "video_augment: out_layout must be 0 or 1");
+  const dsvt_aug_params& p = *params;
+  REQUIRE(p.h >= 1 && p.w >= 1 && p.y0 >= 0 && p.x0 >= 0 && p.y0 + p.h <= H && p.x0 + p.w <= W,
+          "video_augment: crop window outside the frame");
+  REQUIRE(p.size >= 1 && p.size <= 4096, "video_augment: bad output size");
+  REQUIRE(p.n_ops >= 0 && p.n_ops <= 3, "video_augment: n_ops must be 0..3");
+  for (int k = 0; k < p.n_ops; ++k)
+    REQUIRE(p.op[k] >= DSVT_AUG_BRIGHTNESS && p.op[k] <= DSVT_AUG_SATURATION, "video_augment: bad op code");
+  for (int c = 0; c < 3; ++c) REQUIRE(p.std[c] != 0.f, "video_augment: zero std");
+  REQUIRE(sT >= 0 && sC >= 0 && sH >= 0 && sW >= 0, "video_augment: negative stride");
+  REQUIRE(workspace && workspace_bytes >= (size_t)dsvt_workspace_bytes(DSVT_WS_AUGMENT, 1, T, p.size, 0),
+          "video_augment: workspace too small");
+  hipError_t e = launch_video_augment(frames, frames_u8, T_in, T, frame_index, H, W, sT, sC, sH, sW, p, out,
+                                      out_layout, workspace, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "video_augment");
+}
+
+int dsvt_gather_rows(const void* src, int64_t row_bytes, const int32_t* idx, int64_t rows, void* dst, void* stream) {
+  REQUIRE(src && idx && dst && row_bytes > 0 && rows >= 1 && rows <= 65535, "gather_rows: bad args");
+  hipError_t e = launch_gather_rows(src, row_bytes, idx, rows, dst, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gather_rows");
 }
 
 int dsvt_cast_pad_fwd(int dtype, const float* x, void* y, int64_t N, int64_t K, int64_t ldk, void* stream) {

@@ -9,6 +9,8 @@
 // linear per 1 KB LDS-DMA piece (16 rows x 64 B); the swizzle chunk' = chunk ^ H[(row>>2)&3],
 // H = {0,2,3,1}, is applied to the SOURCE address and to the ds_read_b128 address, which makes
 // all four 16-lane groups of a fragment read bank-conflict free.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "gemm_epi.h"
@@ -313,9 +315,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
   }
 
   int64_t a_off[A_PIECES], b_off[B_PIECES];
+  const int tilesM = (int)((p.M + BM - 1) / BM), GM = p.tile_group;
   auto set_tile = [&](int t, int64_t& m0, int64_t& n0) {
-    m0 = (int64_t)(t / tilesN) * BM;
-    n0 = (int64_t)(t % tilesN) * BN;
+    if (GM <= 0) {
+      m0 = (int64_t)(t / tilesN) * BM;
+      n0 = (int64_t)(t % tilesN) * BN;
+    } else {                            // groups of GM m-tile rows, n-column-major inside
+      const int grp = t / (GM * tilesN), w = t - grp * GM * tilesN;
+      const int fm = grp * GM, gm = min(GM, tilesM - fm);
+      m0 = (int64_t)(fm + w % gm) * BM;
+      n0 = (int64_t)(w / gm) * BN;
+    }
 #pragma unroll
     for (int i = 0; i < A_PIECES; ++i) {
       const int r = (wave * A_PIECES + i) * 16 + prow;
@@ -407,7 +417,9 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
   const int64_t per_x = (tiles + 7) / 8;
   if (per_x * 8 < G) G = per_x * 8;
   dim3 grid((unsigned)G), block(64 * WM * WN);
-#define DSVT_K(E, F) gemm_persist_kernel<BM, BN, WM, WN, NST, E, F, STAGGER><<<grid, block, 0, s>>>(p)
+  GemmParams q = p;
+  if (const char* e = getenv("DSVT_TILE_GROUP")) q.tile_group = atoi(e);
+#define DSVT_K(E, F) gemm_persist_kernel<BM, BN, WM, WN, NST, E, F, STAGGER><<<grid, block, 0, s>>>(q)
   switch (epi) {
     case EPI_BIAS: if (out_f32) DSVT_K(EPI_BIAS, true); else DSVT_K(EPI_BIAS, false); break;
     case EPI_GELU: if (out_f32) DSVT_K(EPI_GELU, true); else DSVT_K(EPI_GELU, false); break;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/dsvt.h"
+
 namespace dsvt {
 
 struct GemmParams {
@@ -135,6 +137,20 @@ hipError_t launch_attn_window(int dtype, const void* qkv, void* out, int64_t ldo
                               const int32_t* region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C,
                               float scale, hipStream_t s);
 hipError_t launch_cast_pad(int dtype, const float* x, void* y, int64_t N, int64_t K, int64_t ldk, hipStream_t s);
+
+// frame selection (select.hip)
+int64_t select_frames_ws_bytes(int64_t n, int64_t n_unsampled);
+hipError_t launch_select_frames(const double* loss, int64_t n, int64_t n_frames, int64_t n_unsampled, int64_t rate,
+                                int64_t N, int64_t* indices, int32_t* frame_pos, double* cdf_out, void* ws,
+                                hipStream_t s);
+hipError_t launch_gather_rows(const void* src, int64_t row_bytes, const int32_t* idx, int64_t rows, void* dst,
+                              hipStream_t s);
+
+// video augmentation (augment.hip)
+int64_t augment_ws_bytes(int64_t T, int64_t size);
+hipError_t launch_video_augment(const void* frames, int u8, int64_t T_in, int64_t T, const int32_t* fidx, int64_t H,
+                                int64_t W, int64_t sT, int64_t sC, int64_t sH, int64_t sW, const ::dsvt_aug_params& p,
+                                float* out, int layout, void* ws, hipStream_t s);
 
 hipError_t launch_softmax_stats(const float* x, const float* center, float inv_temp, int64_t rows,
                                 int64_t D, float* m_out, float* z_out, hipStream_t s);

@@ -15,6 +15,7 @@ TOKENS_NT, TOKENS_FRAME = 0, 1
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
 WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
 WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
+WS_SELECT, WS_AUGMENT = 10, 11
 
 _i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -71,6 +72,11 @@ SIGNATURES = {
     "dsvt_relpos_bias_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p]),
     "dsvt_attn_window_fwd": (_i32, [_i32, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_cast_pad_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _p]),
+    "dsvt_select_frames": (_i32, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
+    "dsvt_gather_rows": (_i32, [_p, _i64, _p, _i64, _p, _p]),
+    # the params struct pointer is bound with its ctypes.Structure type in dsvt/augment.py
+    "dsvt_video_augment": (_i32, [_p, _i32, _i64, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _i32, _p,
+                                  ctypes.c_size_t, _p]),
     "dsvt_set_gemm_variant": (_i32, [_i32]),
     "dsvt_set_attn_variant": (_i32, [_i32]),
     "dsvt_set_attn_bwd_variant": (_i32, [_i32]),

@@ -344,6 +344,8 @@ def gemm_kernel_name(tag):
     persist = {9: "256, 128, 2, 2, 3, %d, %s, false", 10: "256, 128, 2, 2, 3, %d, %s, true"}
     if variant in persist:
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
+    if variant == 20:
+        return "void dsvt::gemm_8ph_kernel<%d, %s, 0>" % (epi, f32)
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)
 
 

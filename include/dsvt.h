@@ -61,6 +61,8 @@ extern "C" {
 #define DSVT_WS_COLSUM 7
 #define DSVT_WS_ATTN_BWD 8
 #define DSVT_WS_EMBED_BWD 9
+#define DSVT_WS_SELECT 10      /* M = number of scores, N = frames of the unsampled video */
+#define DSVT_WS_AUGMENT 11     /* M = output frames T, N = output size S */
 
 int dsvt_version(void);
 const char *dsvt_last_error(void);
@@ -302,8 +304,63 @@ int dsvt_attn_window_fwd(int dtype, const void *qkv, void *out, int64_t ldo, con
 /* y [N, ldk] = x [N, K] cast to the storage dtype with zero columns K..ldk-1. */
 int dsvt_cast_pad_fwd(int dtype, const float *x, void *y, int64_t N, int64_t K, int64_t ldk, void *stream);
 
+/* Score -> frame-index selection, the "adaptive" method of
+ * datasets_custom/frame_selection_loader.py:115-166 (replaces that inline numpy loop), bit-exact
+ * in float64: pdf = loss / np.sum(loss) (numpy pairwise summation), cdf = np.cumsum(pdf),
+ * idx_i = argmin |cdf - i/N| (first minimum), then the reference's collision walk over multiples
+ * of `rate` (pre_sampling_rate) below n_unsampled (frames_unsampled.size(0)).
+ * loss [n_loss] float64 device; only the first min(n_loss, n_frames) values are used (the
+ * reference truncates to frames.size(0) = n_frames).  Outputs (device): indices [N] int64 (the
+ * reference's `indices` list, in unsampled-video frame numbers) and frame_pos [N] int32 (which
+ * pre-sampled frame the reference stacks for slot i: idx_i, or n_frames - 1 for frames[-1]);
+ * cdf_out [n] float64 optional (NULL: kept in the workspace).
+ * workspace >= dsvt_workspace_bytes(DSVT_WS_SELECT, ., n, n_unsampled, 0), n = min(n_loss,
+ * n_frames).  Errors: a size < 1, N > 65535, or (n - 1) * rate >= n_unsampled (the pre-sampled
+ * frames are frames_unsampled[::rate], so every score indexes the unsampled video). */
+int dsvt_select_frames(const double *loss, int64_t n_loss, int64_t n_frames, int64_t n_unsampled, int64_t rate,
+                       int64_t N, int64_t *indices, int32_t *frame_pos, double *cdf_out, void *workspace,
+                       size_t workspace_bytes, void *stream);
+/* Video DINO augmentation of one crop, VideoDataAugmentationDINO (datasets_custom/transform.py:
+ * 661-749): replaces random_resized_crop (:134-173, bicubic F.interpolate), horizontal_flip
+ * (:176-203), color_jitter (:371-461: brightness / contrast / saturation in the drawn order),
+ * grayscale (:349-368) and color_normalization (:494-516) applied to one clip.  The random draws
+ * stay on the host (dsvt/augment.py makes the reference's own RNG calls); the parameters below
+ * are their results. */
+#define DSVT_AUG_BRIGHTNESS 1
+#define DSVT_AUG_CONTRAST 2
+#define DSVT_AUG_SATURATION 3
+typedef struct dsvt_aug_params {
+  int32_t y0, x0, h, w; /* crop window of the input frame, already clipped to it (the reference slices) */
+  int32_t size;         /* output S x S (bicubic, align_corners=False) */
+  int32_t flip;         /* horizontal flip of the resized crop */
+  int32_t n_ops;        /* colour-jitter ops applied, in order (0 = jitter not drawn) */
+  int32_t op[3];        /* DSVT_AUG_* */
+  float alpha[3];       /* blend weight as the float tensor op sees it: (float)alpha */
+  float beta[3];        /* (float)(1 - alpha) */
+  int32_t gray;         /* grayscale after the jitter */
+  float mean[3], std[3];
+} dsvt_aug_params;
+/* frames: T_in frames, 3 channels, H x W, uint8 (frames_u8 = 1, scaled by 1/255 as
+ * `x.float() / 255.0`) or fp32, addressed by element strides (sT, sC, sH, sW) -- the decoder's
+ * [T, H, W, C] and the reference's [T, C, H, W] both work.  frame_index [T] int32 device
+ * (nullable = identity; values clamped to [0, T_in)) picks the input frame of each output frame
+ * (the loader's temporal index_select, which commutes with the per-frame augmentation).
+ * out fp32: out_layout 0 = [T, 3, S, S] (the reference crop), 1 = [3, T, S, S] (the model input
+ * after the loader's `t c h w -> c t h w`).  workspace >= dsvt_workspace_bytes(DSVT_WS_AUGMENT,
+ * ., T, S, 0) (the per-frame contrast-mean partial sums). */
+int dsvt_video_augment(const void *frames, int frames_u8, int64_t T_in, int64_t T, const int32_t *frame_index,
+                       int64_t H, int64_t W, int64_t sT, int64_t sC, int64_t sH, int64_t sW,
+                       const dsvt_aug_params *params, float *out, int out_layout, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
+/* dst[r] = src[idx[r]], rows of row_bytes bytes (the `torch.stack(selected_frames)` of
+ * frame_selection_loader.py:166 / any frame gather); rows <= 65535. */
+int dsvt_gather_rows(const void *src, int64_t row_bytes, const int32_t *idx, int64_t rows, void *dst, void *stream);
+
 /* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
- * 1 = 128x128 / 4-wave kernel, 2 = 256x256 / 8-wave, 3 = 256x128 / 8-wave.  Process-global. */
+ * 1 = 128x128 / 4-wave kernel, 3-6 / 9-13 = 256x128 and 256x256 staged / persistent kernels,
+ * 20 = 256x256 phase-interleaved persistent kernel (21-29: its diagnostic builds).
+ * Process-global. */
 int dsvt_set_gemm_variant(int variant);
 /* Tuning knob (benchmarking / tests only): bf16 short-sequence attention kernel. 0 = automatic,
  * 1 = 16-key-tile x 4 waves, 2 = 13 x 8 waves, 3 = 13 x 4 waves, 4 = streaming flash kernel

@@ -324,3 +324,101 @@ def view_index_map(F, local_size, global_size):
         out[2 * i, :k - j] = np.arange(j, k) + 1
         out[2 * i + 1, :m - l] = np.arange(l, m) + 1
     return out
+
+
+# --------------------------------------------------------------------------- frame selection
+def adaptive_frame_selection(loss_list, n_frames, n_unsampled, rate, N):
+    """The "adaptive" branch of FrameSelectionLoader.__getitem__,
+    datasets_custom/frame_selection_loader.py:115-166, with the frames replaced by their
+    positions: returns (indices int64 [N] -- the reference's `indices` list, frame_pos int32
+    [N] -- which pre-sampled frame it stacks per slot, cdf float64).  The min-max line 129 is
+    dead (overwritten at 132) and omitted; float64 numpy throughout, as the reference."""
+    loss = np.asarray(loss_list, dtype=np.float64)
+    if len(loss) > n_frames:                         # :123-124
+        loss = loss[:n_frames]
+    pdf = loss / np.sum(loss)                        # :132
+    cdf = np.cumsum(pdf)                             # :135
+    indices, pos = [], []
+    for i in range(N):                               # :141-166
+        j = i / N
+        idx = int(np.abs(cdf - j).argmin())
+        s = idx * rate
+        if s not in indices:
+            indices.append(s)
+            pos.append(idx)
+        else:
+            t = s + rate
+            while True:
+                if t not in indices and t < n_unsampled:
+                    indices.append(t)
+                    pos.append(idx)                  # frames[idx], as the reference stacks
+                    break
+                elif t >= n_unsampled:
+                    indices.append(t - rate)
+                    pos.append(n_frames - 1)         # frames[-1]
+                    break
+                else:
+                    t = t + rate
+    return np.array(indices, np.int64), np.array(pos, np.int32), cdf
+
+
+# --------------------------------------------------------------------------- video augmentation
+def _torch_cubic_weights(t, A=-0.75):
+    """upsample_bicubic2d's cubic convolution coefficients for fractional offsets t."""
+    x1, x2, x3, x4 = t + 1.0, t, 1.0 - t, 2.0 - t
+    return np.stack([((A * x1 - 5 * A) * x1 + 8 * A) * x1 - 4 * A,
+                     ((A + 2) * x2 - (A + 3)) * x2 * x2 + 1,
+                     ((A + 2) * x3 - (A + 3)) * x3 * x3 + 1,
+                     ((A * x4 - 5 * A) * x4 + 8 * A) * x4 - 4 * A], -1)
+
+
+def resize_bicubic(x, size):
+    """F.interpolate(x, (size, size), mode="bicubic", align_corners=False) as resize() at
+    datasets_custom/transform.py:66-76 calls it: source = in/out * (o + 0.5) - 0.5, A = -0.75,
+    border taps clamped; float64 weights and sums, float32 out."""
+    def axis(n_in):
+        o = np.arange(size, dtype=np.float64)
+        src = (np.float32(n_in) / np.float32(size)) * (o + 0.5) - 0.5
+        f = np.floor(src)
+        idx = np.clip(f[:, None].astype(np.int64) + np.arange(-1, 3)[None, :], 0, n_in - 1)
+        return idx, _torch_cubic_weights(src - f)
+    iy, wy = axis(x.shape[-2])
+    ix, wx = axis(x.shape[-1])
+    xd = x.astype(np.float64)
+    rows = np.einsum("...ok,ok->...o", xd[..., ix], wx)                 # along W: [..., H, S]
+    out = np.einsum("...oks,ok->...os", rows[..., iy, :], wy)          # along H: [..., S, S]
+    return out.astype(np.float32)
+
+
+def _gray(x):
+    """grayscale() transform.py:349-368 (the reference's BGR weights), fp32 ops."""
+    return (np.float32(0.299) * x[:, 2] + np.float32(0.587) * x[:, 1]) + np.float32(0.114) * x[:, 0]
+
+
+def video_augment(frames, window, size, flip=False, ops=(), gray=False,
+                  mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)):
+    """One crop of VideoDataAugmentationDINO (datasets_custom/transform.py:661-749) with its
+    random draws given: frames [T, C, H, W] uint8 (-> /255) or float32; window (y0, x0, h, w)
+    already clipped (random_resized_crop :134-173); flip (:176-203); ops [(code, alpha)] in
+    order, 1 brightness / 2 contrast / 3 saturation (color_jitter :371-461 via blend :333-346);
+    gray (:349-368); color_normalization (:494-516).  Returns float32 [T, C, size, size]."""
+    x = frames.astype(np.float32) / np.float32(255.0) if frames.dtype == np.uint8 else frames.astype(np.float32)
+    y0, x0, h, w = window
+    r = resize_bicubic(x[:, :, y0:y0 + h, x0:x0 + w], size)
+    if flip:
+        r = r[..., ::-1]
+    for code, alpha in ops:
+        a, b = np.float32(alpha), np.float32(1.0 - alpha)
+        if code == 1:
+            r = r * a + np.zeros_like(r) * b
+        elif code == 2:
+            m = np.float32(_gray(r).astype(np.float64).mean(axis=(1, 2)))
+            r = r * a + (m * b)[:, None, None, None].astype(np.float32)
+        else:
+            r = r * a + (_gray(r) * b)[:, None]
+    if gray:
+        g = _gray(r)
+        r = np.stack([g, g, g], 1)
+    m = np.asarray(mean, np.float32)[None, :, None, None]
+    s = np.asarray(std, np.float32)[None, :, None, None]
+    return ((r - m) / s).astype(np.float32)

@@ -288,6 +288,8 @@ def main():
 
     # ---- 9. Video Swin (config 5): small config with padding / clamped windows, and Swin-T 8x224^2
     out["swin"] = swin_outputs()
+    for name, fn in GROUPS.items():
+        out[name] = fn()
 
     for name, arrays in out.items():
         path = os.path.join(HERE, name + ".npz")
@@ -295,5 +297,109 @@ def main():
         print("wrote", path, os.path.getsize(path))
 
 
+def _method_branch(path, cls, method, test_src, args, returns):
+    """The body of the `if <test_src>:` statement inside cls.method of a reference source file,
+    as a standalone function f(*args) -> returns (the branch reads only these names)."""
+    tree = ast.parse(open(path).read())
+    c = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls)
+    m = next(n for n in c.body if isinstance(n, ast.FunctionDef) and n.name == method)
+    br = next(n for n in ast.walk(m) if isinstance(n, ast.If) and ast.unparse(n.test) == test_src)
+    fn = ast.FunctionDef(name="_branch", args=ast.arguments(posonlyargs=[], args=[ast.arg(a) for a in args],
+                                                              kwonlyargs=[], kw_defaults=[], defaults=[]),
+                         body=br.body + [ast.Return(ast.Tuple([ast.Name(r, ast.Load()) for r in returns],
+                                                              ast.Load()))],
+                         decorator_list=[], returns=None, type_params=[])
+    mod = ast.fix_missing_locations(ast.Module(body=[fn], type_ignores=[]))
+    ns = {"np": np, "torch": torch, "os": os}
+    exec(compile(mod, path, "exec"), ns)
+    return ns["_branch"]
+
+
+def selection_cases():
+    """Score -> frame-index selection: the "adaptive" branch of FrameSelectionLoader.__getitem__
+    (datasets_custom/frame_selection_loader.py:115-166) run as written, frames replaced by
+    their positions (frames[p] = p) so the stacked output names the frames it picked."""
+    br = _method_branch(os.path.join(REF, "datasets_custom", "frame_selection_loader.py"), "FrameSelectionLoader",
+                        "__getitem__", "self.selection_method == 'adaptive'",
+                        ["self", "file_name", "frames", "frames_unsampled", "N"], ["frames", "indices", "cdf"])
+    rng = np.random.default_rng(1234)
+
+    def f32(x):
+        return np.asarray(x, np.float32).astype(np.float64)    # JSON scores are fp32 .item() values
+
+    cases = {
+        "random": (f32(rng.random(50) * 3 + 0.1), 50, 100, 2, 8),
+        "spike_collisions": (f32(np.r_[np.full(20, 0.01), [50.0], np.full(19, 0.01)]), 40, 120, 3, 16),
+        "spike_at_end": (f32(np.r_[np.full(30, 0.02), [40.0]]), 31, 61, 2, 12),
+        "longer_than_frames": (f32(rng.random(70) + 0.5), 60, 120, 2, 10),
+        "ragged_unsampled": (f32(rng.random(51) + 0.2), 51, 101, 2, 9),
+        "uniform_ties": (np.ones(32), 32, 64, 2, 16),
+        "rate1": (f32(rng.gamma(2.0, 1.0, 25)), 25, 25, 1, 20),
+        "many_scores": (f32(rng.random(9000) ** 3 + 1e-3), 9000, 27000, 3, 64),
+        "one_score": (np.array([0.7]), 1, 4, 4, 3),
+    }
+    out = {}
+    for name, (loss, F_, U, rate, N) in cases.items():
+        self = types.SimpleNamespace(loss_dict={"vid": loss.tolist()}, pre_sampling_rate=rate)
+        frames = torch.arange(F_, dtype=torch.int64).view(F_, 1)
+        picked, indices, cdf = br(self, "vid.mp4", frames, torch.zeros(U, 1), N)
+        out[name + "_loss"] = loss
+        out[name + "_shape"] = np.array([F_, U, rate, N], np.int64)
+        out[name + "_indices"] = np.array(indices, np.int64)
+        out[name + "_frame_pos"] = picked.view(-1).numpy().astype(np.int32)
+        out[name + "_cdf"] = np.asarray(cdf, np.float64)
+    return out
+
+
+def augment_cases():
+    """VideoDataAugmentationDINO (datasets_custom/transform.py:661-749), loaded on its own (it
+    imports only math / numpy / torch), run with seeded RNGs on seeded uint8 frames.
+      comp_<k>: random_resized_crop(size 20) -> flip_and_color_jitter -> normalize, full output;
+      cls_<k>:  the class on a from_list clip list (2 global 224^2 + 2 local 96^2 crops) and the
+                no_aug path: every 7th row / column of each crop plus each crop's full mean."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_transform", os.path.join(REF, "datasets_custom", "transform.py"))
+    T = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(T)
+    aug_cls = T.VideoDataAugmentationDINO
+    out = {}
+    g = np.random.default_rng(77)
+    frames = g.integers(0, 256, (3, 3, 60, 76), dtype=np.uint8)
+    out["frames"] = frames
+    img = torch.from_numpy(frames).float() / 255.0
+    for k, (seed, scale) in enumerate([(s, (0.4, 1.0) if s % 2 else (0.05, 0.4)) for s in range(10)]):
+        torch.manual_seed(1000 + seed)
+        np.random.seed(2000 + seed)
+        x = T.random_resized_crop(img, size=20, scale=scale, interpolation="bicubic")
+        x = aug_cls.flip_and_color_jitter(x)
+        x = aug_cls.normalize(x)
+        out["comp_%d" % k] = x.numpy()
+        out["comp_%d_seed" % k] = np.array([1000 + seed, 2000 + seed], np.int64)
+        out["comp_%d_scale" % k] = np.array(scale, np.float64)
+    clips = [g.integers(0, 256, (2, 3, 64, 80), dtype=np.uint8) for _ in range(4)]
+    for k in range(2):
+        torch.manual_seed(3000 + k)
+        np.random.seed(4000 + k)
+        crops = aug_cls()([torch.from_numpy(c) for c in clips], from_list=True)
+        for c, crop in enumerate(crops):
+            out["cls_%d_%d_sub" % (k, c)] = crop.numpy()[..., ::7, ::7]
+            out["cls_%d_%d_mean" % (k, c)] = np.array(crop.double().mean().item())
+    for c, crop in enumerate(aug_cls()([torch.from_numpy(c) for c in clips[:1]], no_aug=True)):
+        out["noaug_%d_sub" % c] = crop.numpy()[..., ::7, ::7]
+        out["noaug_%d_mean" % c] = np.array(crop.double().mean().item())
+    for c, arr in enumerate(clips):
+        out["clip_%d" % c] = arr
+    return out
+
+
+GROUPS = {"selection": selection_cases, "augment": augment_cases}
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:             # regenerate only the named fixture groups
+        for name in sys.argv[1:]:
+            arrays = GROUPS[name]()
+            path = os.path.join(HERE, name + ".npz")
+            np.savez_compressed(path, torch_version=np.array(torch.__version__), **arrays)
+            print("wrote", path, os.path.getsize(path))
+    else:
+        main()

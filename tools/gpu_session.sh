@@ -24,10 +24,10 @@ for stage in "$@"; do
     gputests) run gputests 1500 python -m pytest tests -m gpu -q -rf ;;
     smoke)   run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 900 python bench.py ;;
-    prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --serial --no-graph &&
+    prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --serial --no-graph --no-train --no-other &&
              python tools/prof_summary.py "$OUT/prof" 7 > "$OUT/prof_summary.txt" ;;
-    pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph &&
-             run pmc2 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph &&
+    pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
+             run pmc2 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
              python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" > "$OUT/pmc_summary.txt" ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
