@@ -279,7 +279,12 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (g_gemm_variant) return g_gemm_variant;
   // wide bias-only projections with a bf16 output (qkv, N = 2304): the 256x256 phase-interleaved
   // kernel (v20) -- measured 895 vs 828 TF/s (global crops) and 933 vs 786 (local crops)
-  if (epi == EPI_BIAS && !out_f32 && p.M >= 4096 && p.N >= 1024 && gemm_8ph_ok(p, epi)) return 20;
+  // fc1 + GELU likewise (728 vs 709 TF/s global crops; its epilogue uses the general store path)
+  if ((epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.M >= 4096 && p.N >= 1024 && gemm_8ph_ok(p, epi))
+    return 20;
+  // fp32 residual GEMMs (N = 768: proj / temporal fc / fc2): the 128x128 kernel, whose epilogue
+  // issues every X load before its first store (527 vs 505 TF/s proj, 871 vs 752 fc2)
+  if (epi == EPI_RESID) return 1;
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }
 

@@ -64,7 +64,7 @@ __device__ __forceinline__ void p8_barrier() {
 template <int EPI, bool OUT_F32, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores
-  constexpr int S_EPI = ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
+  constexpr int S_EPI = (EPI == EPI_BIAS && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
   __shared__ __attribute__((aligned(16))) char smem[2 * P8_BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(acc[i][jj]));
       } else {
-        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC>(p, acc, rbase, cbase,
+        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC, EPI == EPI_GELU>(p, acc, rbase, cbase,
                                                                                           r16, g);
       }
       post = S_EPI > 0 && rbase + 128 <= p.M && cbase + 64 <= p.N;
@@ -298,11 +298,11 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #undef P8_COMPUTE
 }
 
-// K a multiple of 64, 32-bit LDS-DMA source offsets, no patch-embed epilogue, no inference GELU
-// epilogue (its 128 erf-GELUs per lane do not fit beside the loop state without spilling; fc1
-// stays on the 2-workgroups-per-CU kernel, which hides that VALU behind the other workgroup)
+// K a multiple of 64, 32-bit LDS-DMA source offsets, no patch-embed epilogue.  (The GELU
+// epilogue takes the general per-fragment store path: with the 16-byte pair packing its 128
+// erf-GELUs per lane do not fit beside the loop state without spilling.)
 bool gemm_8ph_ok(const GemmParams& p, int epi) {
-  return p.K >= 64 && p.K % 64 == 0 && p.M >= 1 && p.N >= 1 && epi != EPI_PATCH && epi != EPI_GELU &&
+  return p.K >= 64 && p.K % 64 == 0 && p.M >= 1 && p.N >= 1 && epi != EPI_PATCH &&
          (p.M - 1) * p.lda * 2 + p.K * 2 <= (int64_t)UINT32_MAX && (p.N - 1) * p.ldw * 2 + p.K * 2 <= (int64_t)UINT32_MAX;
 }
 
@@ -334,6 +334,7 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
   switch (epi) {
     case EPI_BIAS: if (out_f32) DSVT_K(EPI_BIAS, true); else DSVT_K(EPI_BIAS, false); break;
     case EPI_RESID: DSVT_K(EPI_RESID, true); break;
+    case EPI_GELU: if (out_f32) DSVT_K(EPI_GELU, true); else DSVT_K(EPI_GELU, false); break;
     case EPI_GELU_SAVE: DSVT_K(EPI_GELU_SAVE, false); break;
     case EPI_DGELU: if (out_f32) DSVT_K(EPI_DGELU, true); else DSVT_K(EPI_DGELU, false); break;
     default: return hipErrorInvalidValue;

@@ -24,7 +24,10 @@ __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int 
 
 // Direct (register) epilogue shared by the big and persistent kernels.
 // BIAS_IN_ACC: the accumulators started from the bias (gemm_8ph.hip), none is added here.
-template <int MI, int NJ, int EPI, bool OUT_F32, bool NT = false, bool NOSTORE = false, bool BIAS_IN_ACC = false>
+// NOFAST: skip the full-tile 16-byte pair-store path (its cross-lane packing keeps more values
+// live; gemm_8ph.hip's GELU instantiation spills with it)
+template <int MI, int NJ, int EPI, bool OUT_F32, bool NT = false, bool NOSTORE = false, bool BIAS_IN_ACC = false,
+          bool NOFAST = false>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
@@ -79,7 +82,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
   const bool ident = p.rpg >= p.M;   // wave-uniform: no per-lane row-map division
   // full wave tile (uniform): branch-free bias / GELU / 16-B stores, so the compiler's vmcnt
   // waits stay exact (a per-lane bounds branch around each store makes it drain every time)
-  if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0) {
+  if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0 && !NOFAST) {
     if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
