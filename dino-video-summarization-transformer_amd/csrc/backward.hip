@@ -34,14 +34,14 @@ namespace dsvt {
 // One wave per row (grid-stride).  VEC (C % 256 == 0): lane owns columns i*256 + 4*lane + e
 // (16-B x / dx accesses); else columns i*64 + lane.  dgamma / dbeta are accumulated in
 // registers, reduced over the 4 waves in LDS and written per block.
-template <typename DyT, bool VEC>
+template <typename DyT, bool VEC, int NI = 4>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
                                                      const float* __restrict__ gamma, float* __restrict__ dx,
                                                      int64_t rows, int C, int64_t rpg, int64_t gstride, int64_t goff,
                                                      float eps, float* __restrict__ partial) {
   __shared__ float red[4][2][1024];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n = VEC ? 4 * (C >> 8) : (C >> 6);                 // slots in use (<= 16)
+  const int n = VEC ? 4 * NI : (C >> 6);                        // slots in use (<= 16; VEC: C = 256 NI)
   auto col = [&](int k) { return VEC ? (k >> 2) * 256 + lane * 4 + (k & 3) : k * 64 + lane; };
   float dg[16], db[16], g[16];
 #pragma unroll
@@ -49,62 +49,120 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
     dg[k] = 0.f; db[k] = 0.f;
     g[k] = k < n ? gamma[col(k)] : 0.f;
   }
-  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
-    const int64_t xr = map_row(r, rpg, gstride, goff) * C;
-    float v[16], d[16];
-    float s = 0.f;
-    if constexpr (VEC) {
+  if constexpr (VEC) {
+    // one row per wave per iteration, software-pipelined: the next row's x, dy AND the dx it
+    // read-modify-writes are loaded before this row's reductions (one HBM round trip per row
+    // in flight behind the compute instead of two in series)
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    constexpr int NK = 4 * NI;
+    float cx[NK], cd[NK], co[NK], nx[NK], nd[NK], no[NK];
+    auto load_row = [&](int64_t r, float (&vx)[NK], float (&vd)[NK], float (&vo)[NK]) {
+      const int64_t xr = map_row(r, rpg, gstride, goff) * C;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (4 * i < n) {
-          load4(x + xr + i * 256 + lane * 4, v + 4 * i);
-          load4(dy + r * C + i * 256 + lane * 4, d + 4 * i);
-          s += (v[4 * i] + v[4 * i + 1]) + (v[4 * i + 2] + v[4 * i + 3]);
+      for (int i = 0; i < NI; ++i) {
+          load4(x + xr + i * 256 + lane * 4, vx + 4 * i);
+          load4(dy + r * C + i * 256 + lane * 4, vd + 4 * i);
+          load4(dx + xr + i * 256 + lane * 4, vo + 4 * i);
         }
-    } else {
+    };
+    int64_t r = (int64_t)blockIdx.x * 4 + wave;
+    if (r < rows) load_row(r, cx, cd, co);
+    for (; r < rows; r += stride) {
+      if (r + stride < rows) load_row(r + stride, nx, nd, no);
+      const int64_t xr = map_row(r, rpg, gstride, goff) * C;
+      float s = 0.f;
 #pragma unroll
+      for (int k = 0; k < NK; ++k)
+        s += cx[k];
+      const float mean = wave_sum(s) / C;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        { cx[k] -= mean; q += cx[k] * cx[k]; }
+      const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        {
+          const float xh = cx[k] * rstd, gd = g[k] * cd[k];
+          cx[k] = xh;
+          s1 += gd;
+          s2 += gd * xh;
+          dg[k] += cd[k] * xh;
+          db[k] += cd[k];
+        }
+      s1 = wave_sum(s1) / C;
+      s2 = wave_sum(s2) / C;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+          float4 o;
+          o.x = co[4 * i] + rstd * (g[4 * i] * cd[4 * i] - s1 - cx[4 * i] * s2);
+          o.y = co[4 * i + 1] + rstd * (g[4 * i + 1] * cd[4 * i + 1] - s1 - cx[4 * i + 1] * s2);
+          o.z = co[4 * i + 2] + rstd * (g[4 * i + 2] * cd[4 * i + 2] - s1 - cx[4 * i + 2] * s2);
+          o.w = co[4 * i + 3] + rstd * (g[4 * i + 3] * cd[4 * i + 3] - s1 - cx[4 * i + 3] * s2);
+          *reinterpret_cast<float4*>(dx + xr + i * 256 + lane * 4) = o;
+        }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) { cx[k] = nx[k]; cd[k] = nd[k]; co[k] = no[k]; }
+    }
+  } else {
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
+      const int64_t xr = map_row(r, rpg, gstride, goff) * C;
+      float v[16], d[16];
+      float s = 0.f;
+      if constexpr (VEC) {
+  #pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * i < n) {
+            load4(x + xr + i * 256 + lane * 4, v + 4 * i);
+            load4(dy + r * C + i * 256 + lane * 4, d + 4 * i);
+            s += (v[4 * i] + v[4 * i + 1]) + (v[4 * i + 2] + v[4 * i + 3]);
+          }
+      } else {
+  #pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k < n) {
+            v[k] = x[xr + col(k)];
+            d[k] = Elem<DyT>::to_f(dy[r * C + col(k)]);
+            s += v[k];
+          }
+      }
+      const float mean = wave_sum(s) / C;
+      float q = 0.f;
+  #pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < n) { v[k] -= mean; q += v[k] * v[k]; }
+      const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+      float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
       for (int k = 0; k < 16; ++k)
         if (k < n) {
-          v[k] = x[xr + col(k)];
-          d[k] = Elem<DyT>::to_f(dy[r * C + col(k)]);
-          s += v[k];
+          const float xh = v[k] * rstd, gd = g[k] * d[k];
+          v[k] = xh;
+          s1 += gd;
+          s2 += gd * xh;
+          dg[k] += d[k] * xh;
+          db[k] += d[k];
         }
-    }
-    const float mean = wave_sum(s) / C;
-    float q = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k < n) { v[k] -= mean; q += v[k] * v[k]; }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k < n) {
-        const float xh = v[k] * rstd, gd = g[k] * d[k];
-        v[k] = xh;
-        s1 += gd;
-        s2 += gd * xh;
-        dg[k] += d[k] * xh;
-        db[k] += d[k];
+      s1 = wave_sum(s1) / C;
+      s2 = wave_sum(s2) / C;
+      if constexpr (VEC) {
+  #pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * i < n) {
+            float4* p = reinterpret_cast<float4*>(dx + xr + i * 256 + lane * 4);
+            float4 o = *p;
+            o.x += rstd * (g[4 * i] * d[4 * i] - s1 - v[4 * i] * s2);
+            o.y += rstd * (g[4 * i + 1] * d[4 * i + 1] - s1 - v[4 * i + 1] * s2);
+            o.z += rstd * (g[4 * i + 2] * d[4 * i + 2] - s1 - v[4 * i + 2] * s2);
+            o.w += rstd * (g[4 * i + 3] * d[4 * i + 3] - s1 - v[4 * i + 3] * s2);
+            *p = o;
+          }
+      } else {
+  #pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k < n) dx[xr + col(k)] += rstd * (g[k] * d[k] - s1 - v[k] * s2);
       }
-    s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
-    if constexpr (VEC) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (4 * i < n) {
-          float4* p = reinterpret_cast<float4*>(dx + xr + i * 256 + lane * 4);
-          float4 o = *p;
-          o.x += rstd * (g[4 * i] * d[4 * i] - s1 - v[4 * i] * s2);
-          o.y += rstd * (g[4 * i + 1] * d[4 * i + 1] - s1 - v[4 * i + 1] * s2);
-          o.z += rstd * (g[4 * i + 2] * d[4 * i + 2] - s1 - v[4 * i + 2] * s2);
-          o.w += rstd * (g[4 * i + 3] * d[4 * i + 3] - s1 - v[4 * i + 3] * s2);
-          *p = o;
-        }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < n) dx[xr + col(k)] += rstd * (g[k] * d[k] - s1 - v[k] * s2);
     }
   }
 #pragma unroll
@@ -117,9 +175,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
+// >= 4 rows per wave; at most 768 blocks = 3 per CU, what the C = 768 kernel's 163 VGPRs keep
+// resident (a 1024-block grid left a second, partial round on a third of the CUs)
 int ln_bwd_blocks(int64_t rows) {
-  int64_t b = (rows + 15) / 16;   // >= 4 rows per wave
-  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+  int64_t b = (rows + 15) / 16;
+  return (int)(b < 1 ? 1 : (b > 768 ? 768 : b));
 }
 
 hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
@@ -128,12 +188,17 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
   const int nb = ln_bwd_blocks(rows);
 #define DSVT_LNB(T, V) ln_bwd_kernel<T, V><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, gstride, \
                                                              goff, eps, partial)
-  if (C % 256 == 0) {
+#define DSVT_LNB3(T) ln_bwd_kernel<T, true, 3><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, \
+                                                                  gstride, goff, eps, partial)
+  if (C == 768) {                      // ViT-B: 3 float4 chunks per lane, a tighter register file
+    if (dy_dtype == 0) DSVT_LNB3(bf16_t); else DSVT_LNB3(float);
+  } else if (C % 256 == 0 && C <= 1024) {
     if (dy_dtype == 0) DSVT_LNB(bf16_t, true); else DSVT_LNB(float, true);
   } else {
     if (dy_dtype == 0) DSVT_LNB(bf16_t, false); else DSVT_LNB(float, false);
   }
 #undef DSVT_LNB
+#undef DSVT_LNB3
   return hipGetLastError();
 }
 
