@@ -339,14 +339,24 @@ __global__ __launch_bounds__(256) void attn_temporal_bwd_kernel(const T* __restr
   const int h0 = blockIdx.y * G;
   const int gh = (heads - h0) < G ? (heads - h0) : G;
   const int per_head = 4 * Tf * 64 + 2 * Tf * Tf;
-  // stage q, k, v, dO of the group's heads as fp32
-  for (int e = tid; e < gh * Tf * 64 * 4; e += 256) {
-    const int d = e & 63, rest = e >> 6;
+  // stage q, k, v, dO of the group's heads as fp32, one 16-byte piece (8 bf16 / 4 fp32) per load
+  constexpr int PE = 16 / (int)sizeof(T);                   // elements per piece
+  for (int e = tid; e < gh * Tf * 4 * (64 / PE); e += 256) {
+    const int d = (e % (64 / PE)) * PE, rest = e / (64 / PE);
     const int which = rest % 4, tt = (rest / 4) % Tf, hh = rest / (4 * Tf);
     const int64_t row = sq * Tf + tt;
     const int64_t col = (int64_t)(h0 + hh) * 64 + d;
-    const float v = which < 3 ? Elem<T>::to_f(qkv[row * 3 * C + which * C + col]) : Elem<T>::to_f(dout[row * C + col]);
-    sm[hh * per_head + (which * Tf + tt) * 64 + d] = v;
+    const T* src = which < 3 ? qkv + row * 3 * C + which * C + col : dout + row * C + col;
+    const uint4 u = *reinterpret_cast<const uint4*>(src);
+    float* dst = sm + hh * per_head + (which * Tf + tt) * 64 + d;
+    if constexpr (sizeof(T) == 2) {
+      const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { dst[2 * k] = bf16_lo(w[k]); dst[2 * k + 1] = bf16_hi(w[k]); }
+    } else {
+      dst[0] = __uint_as_float(u.x); dst[1] = __uint_as_float(u.y);
+      dst[2] = __uint_as_float(u.z); dst[3] = __uint_as_float(u.w);
+    }
   }
   __syncthreads();
   const int sub = tid & 15, d0 = sub * 4;
@@ -365,33 +375,32 @@ __global__ __launch_bounds__(256) void attn_temporal_bwd_kernel(const T* __restr
       m = fmaxf(m, s);
     }
     __builtin_amdgcn_wave_barrier();
+    // probabilities once per (i, j): exp2 of the log2e-scaled logits, written back over them
     float l = 0.f;
-    for (int j = 0; j < Tf; ++j) l += expf(P[i * Tf + j] - m);
+    for (int j = 0; j < Tf; ++j) l += exp2f((P[i * Tf + j] - m) * 1.4426950408889634f);
     const float inv = 1.0f / l;
+    __builtin_amdgcn_wave_barrier();
+    if (sub == 0)
+      for (int j = 0; j < Tf; ++j) P[i * Tf + j] = exp2f((P[i * Tf + j] - m) * 1.4426950408889634f) * inv;
+    __builtin_amdgcn_wave_barrier();
     float D = 0.f;
     for (int j = 0; j < Tf; ++j) {
       const float* v = H + (2 * Tf + j) * 64 + d0;
       const float dp = sum16(dO[0] * v[0] + dO[1] * v[1] + dO[2] * v[2] + dO[3] * v[3]);
-      const float p = expf(P[i * Tf + j] - m) * inv;
-      D += p * dp;
+      D += P[i * Tf + j] * dp;
       if (sub == 0) dS[i * Tf + j] = dp;
     }
     __builtin_amdgcn_wave_barrier();
     float dq[4] = {0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < Tf; ++j) {
-      const float p = expf(P[i * Tf + j] - m) * inv;
-      const float ds = p * (dS[i * Tf + j] - D);
+      const float ds = P[i * Tf + j] * (dS[i * Tf + j] - D);
       const float* k = H + (Tf + j) * 64 + d0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) dq[e] = fmaf(ds, k[e], dq[e]);
     }
     __builtin_amdgcn_wave_barrier();
     if (sub == 0)
-      for (int j = 0; j < Tf; ++j) {
-        const float p = expf(P[i * Tf + j] - m) * inv;
-        dS[i * Tf + j] = p * (dS[i * Tf + j] - D);
-        P[i * Tf + j] = p;
-      }
+      for (int j = 0; j < Tf; ++j) dS[i * Tf + j] = P[i * Tf + j] * (dS[i * Tf + j] - D);
     store4(dqkv + (sq * Tf + i) * 3 * C + (int64_t)(h0 + hh) * 64 + d0, dq[0] * scale, dq[1] * scale, dq[2] * scale,
            dq[3] * scale);
   }
