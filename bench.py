@@ -236,8 +236,9 @@ def swin_t_flops(T=8, S=224, C=96, depths=(2, 2, 6, 2), window=(2, 7, 7), patch=
 
 
 def other_configs(args, device):
-    """Forward clips/s of BASELINE.json configs 4 (ViT-B/16 joint space-time, 16x224^2) and 5
-    (Video Swin-T, 8x224^2) on one GPU, random init, synthetic normalized frames."""
+    """Forward clips/s of the config-2 backbone alone (16 divided-attention 8x224^2 clips) and of
+    BASELINE.json configs 4 (ViT-B/16 joint space-time, 16x224^2) and 5 (Video Swin-T, 8x224^2)
+    on one GPU, random init, synthetic normalized frames."""
     from functools import partial
 
     import torch.nn as nn
@@ -257,7 +258,24 @@ def other_configs(args, device):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps
 
+    # the north-star's own unit: the ViT-B/16 8x224^2 divided-attention backbone forward alone
+    # (16 clips = the global crops of one 8-sample step), against the bf16 MFMA roofline
     torch.manual_seed(1)
+    dm = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
+                           norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=8,
+                           attention_type="divided_space_time").to(device).eval()
+    dm.dsvt_dtype = dtype
+    xd = torch.randn(16, 3, 8, 224, 224, device=device)
+    with torch.no_grad():
+        t = timed(lambda: dm(xd))
+    ref_gf, exe_gf = vit_fwd_flops(8, 224), vit_fwd_flops(8, 224, folded=True)
+    peak = PEAK_TFLOPS[args.dtype]
+    res["config2_backbone_fwd"] = {"value": round(16 / t, 2), "unit": "clips/s", "clips_per_step": 16,
+                                   "gflop_per_clip": round(ref_gf / 1e9, 2),
+                                   "tflops_executed": round(16 * exe_gf / t / 1e12, 1),
+                                   "frac_executed": round(16 * exe_gf / t / 1e12 / peak, 4),
+                                   "frac_reference_flops": round(16 * ref_gf / t / 1e12 / peak, 4)}
+    del dm, xd
     jm = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
                            norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=16,
                            attention_type="joint_space_time").to(device).eval()

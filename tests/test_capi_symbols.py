@@ -72,6 +72,22 @@ def test_validation_rejects_before_launch(L):
     # LayerNorm width limits
     rc = L.dsvt_layernorm_fwd(_lib.BF16, 0, fake, fake, fake, fake, 4, 100, 0, 0, 0, ctypes.c_float(1e-6), None)
     assert rc == 1
+    # frame selection: N out of range; a score that indexes past the unsampled video
+    rc = L.dsvt_select_frames(fake, 10, 10, 20, 2, 0, fake, fake, None, fake, 1 << 20, None)
+    assert rc == 1 and b"N" in L.dsvt_last_error()
+    rc = L.dsvt_select_frames(fake, 10, 10, 15, 2, 4, fake, fake, None, fake, 1 << 20, None)
+    assert rc == 1 and b"unsampled" in L.dsvt_last_error()
+    # augmentation: crop window outside the frame, bad op code
+    from dsvt.augment import _bind, make_params
+    _bind()
+    p = make_params((10, 10, 60, 20), 16)
+    rc = L.dsvt_video_augment(fake, 1, 2, 2, None, 64, 64, 3 * 64 * 64, 64 * 64, 64, 1, ctypes.byref(p), fake, 0,
+                              fake, 1 << 20, None)
+    assert rc == 1 and b"crop window" in L.dsvt_last_error()
+    p = make_params((0, 0, 8, 8), 16, ops=[(7, 1.1)])
+    rc = L.dsvt_video_augment(fake, 1, 2, 2, None, 64, 64, 3 * 64 * 64, 64 * 64, 64, 1, ctypes.byref(p), fake, 0,
+                              fake, 1 << 20, None)
+    assert rc == 1 and b"op code" in L.dsvt_last_error()
 
 
 def test_ops_raise_with_dsvt_error(L):
