@@ -271,6 +271,8 @@ def other_configs(args, device):
     ref_gf, exe_gf = vit_fwd_flops(8, 224), vit_fwd_flops(8, 224, folded=True)
     peak = PEAK_TFLOPS[args.dtype]
     res["config2_backbone_fwd"] = {"value": round(16 / t, 2), "unit": "clips/s", "clips_per_step": 16,
+                                   "streams": "batch split over concurrent HIP streams (dsvt_streams=%s)"
+                                              % dm.dsvt_streams,
                                    "gflop_per_clip": round(ref_gf / 1e9, 2),
                                    "tflops_executed": round(16 * exe_gf / t / 1e12, 1),
                                    "frac_executed": round(16 * exe_gf / t / 1e12 / peak, 4),
@@ -338,6 +340,8 @@ def main():
 
     def forward_loss(concurrent=not args.serial):
         student.concurrent_groups = teacher.concurrent_groups = concurrent
+        # the serial probe pass keeps every kernel alone on the chip: no split batches either
+        student.backbone.dsvt_streams = teacher.backbone.dsvt_streams = "auto" if concurrent else 1
         with torch.no_grad():
             # student: 2 backbone calls (224 / 96 groups) + head on (2+6)*clips rows; teacher:
             # 1 backbone call + head on 2*clips rows -- three independent calls, overlapped

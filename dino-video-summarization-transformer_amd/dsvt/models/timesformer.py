@@ -11,6 +11,7 @@ Storage precision: `model.dsvt_dtype` (torch.bfloat16 = bf16 MFMA perf mode, def
 torch.float32 = fp32 parity mode).  The residual token stream is always fp32.
 """
 import math
+import os
 from functools import partial
 
 import numpy as np
@@ -24,6 +25,7 @@ from ..weights import WeightCache
 from .vit_utils import DropPath, to_2tuple, trunc_normal_
 
 _DEFAULT_DTYPE = [torch.bfloat16]
+SPLIT_ROWS = 8192           # token rows per concurrent chunk of an auto-split inference batch
 
 
 def set_default_dtype(dtype):
@@ -210,6 +212,11 @@ class VisionTransformer(nn.Module):
         # fold temporal_attn.proj and temporal_fc into one Linear (exact algebra, one GEMM less
         # per block); False runs the two GEMMs of the reference literally
         self.fold_temporal_fc = True
+        # inference: split a batch into this many clip chunks on concurrent HIP streams (each
+        # kernel's last partly-filled wave of tiles then runs beside the other chunk's kernels);
+        # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
+        # bit-identical to the unsplit batch at 16 clips (tools/split_bench.py)
+        self.dsvt_streams = os.environ.get("DSVT_STREAMS", "auto")
         self._wcache = WeightCache()
         self._index_cache = {}
 
@@ -302,8 +309,46 @@ class VisionTransformer(nn.Module):
         shape = tuple(clips[0].shape[1:])
         if any(tuple(c.shape[1:]) != shape for c in clips):
             raise ValueError("all clips of one forward must share (C, T, H, W)")
+        k = self.dsvt_streams
+        if k == "auto":
+            rows = B * (1 + (shape[2] // 16) * (shape[3] // 16) * shape[1])
+            k = max(1, min(3, rows // SPLIT_ROWS))
+        k = min(int(k), B)
+        if k > 1 and not get_attn and clips[0].is_cuda and not self._grad_path() \
+                and not torch.cuda.is_current_stream_capturing():     # (nested forks crash HIP capture)
+            return self._forward_split(clips, B, k, shape, get_all, out)
         srcs = [(c, None, c.shape[0]) for c in clips]
         return self._forward_sources(srcs, B, shape[1], shape[2], shape[3], shape[0], get_all, get_attn, out)
+
+    def _forward_split(self, clips, B, k, shape, get_all, out):
+        """forward_features on k clip chunks, one HIP stream each, writing into one output."""
+        from ..utils import run_concurrent, stream_slot
+        C, T, H, W = shape
+        L = 1 + (H // 16) * (W // 16) * (1 if self.attention_type == 'space_only' else T)
+        dev = clips[0].device
+        if out is None:
+            out = torch.empty((B, L, self.embed_dim) if get_all else (B, self.embed_dim), device=dev,
+                              dtype=torch.float32)
+        bounds = [B * i // k for i in range(k + 1)]
+        offs = [0]
+        for c in clips:
+            offs.append(offs[-1] + c.shape[0])
+
+        def chunk(b0, b1):      # the clips of rows [b0, b1) as (views of) the input tensors
+            srcs = []
+            for c, o0, o1 in zip(clips, offs[:-1], offs[1:]):
+                lo, hi = max(b0, o0), min(b1, o1)
+                if lo < hi:
+                    srcs.append((c[lo - o0:hi - o0], None, hi - lo))
+            return srcs
+
+        def job(b0, b1):
+            return lambda: self._forward_sources(chunk(b0, b1), b1 - b0, T, H, W, C, get_all, False, out[b0:b1])
+        self.prepare_weights()              # weight copies and index maps made before the fork
+        self._indices(H // 16, W // 16, T, dev)
+        run_concurrent([job(b0, b1) for b0, b1 in zip(bounds[:-1], bounds[1:])], dev,
+                       slot0=("split", stream_slot(dev)))
+        return out
 
     def forward_frame_bank(self, frames, frame_index, B, T, get_all=False, out=None):
         """Clips gathered from a frame bank [F, Cin, H, W] by frame_index [B*T] int32 (-1 =

@@ -4,6 +4,7 @@ import torch
 import torch.nn as nn
 
 _SIDE_STREAMS = {}
+_SLOT_OF = {}          # cuda_stream handle of a side stream -> its slot
 
 
 def side_stream(device, slot):
@@ -12,7 +13,15 @@ def side_stream(device, slot):
     st = _SIDE_STREAMS.get(key)
     if st is None:
         st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=key[0])
+        _SLOT_OF[st.cuda_stream] = slot
     return st
+
+
+def stream_slot(device):
+    """The slot of the current stream if it is one of ours, else "main" (the default stream or
+    a graph-capture stream): nested forks key their side streams on it, so the same streams
+    serve eager warm-up and HIP-graph capture."""
+    return _SLOT_OF.get(torch.cuda.current_stream(device).cuda_stream, "main")
 
 
 def run_concurrent(thunks, device, slot0=0):
@@ -26,7 +35,7 @@ def run_concurrent(thunks, device, slot0=0):
     for i, fn in enumerate(thunks):
         if i == 0:
             continue
-        st = side_stream(device, slot0 + i - 1)
+        st = side_stream(device, slot0 + i - 1 if isinstance(slot0, int) else (slot0, i))
         st.wait_stream(cur)
         with torch.cuda.stream(st):
             results[i] = fn()

@@ -269,3 +269,23 @@ def test_bench_shape_repeatable_and_finite(base_sd):
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
     assert rel(one.cpu(), outs[0][5:6].cpu()) < BF16_TOL
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_split_streams_bitwise_equal(base_sd, dtype):
+    """Inference batches split over concurrent HIP streams (VisionTransformer.dsvt_streams):
+    features, all-token outputs and list inputs (MultiCropWrapper groups, ragged 3 + 4 clips)
+    are bit-identical to the unsplit batch."""
+    m = tsf(base_sd, dtype)
+    xs = [cu(P.clip(51, (3, 3, 4, 64, 64))), cu(P.clip(52, (4, 3, 4, 64, 64)))]
+    outs = {}
+    with torch.no_grad():
+        for k in (1, 2, 3, 7):
+            m.dsvt_streams = k
+            outs[k] = (m.forward_features(xs), m.forward_features(xs[1], get_all=True))
+        torch.cuda.synchronize()
+        m.dsvt_streams = 1
+        cat = m(torch.cat(xs))
+    for k in (2, 3, 7):
+        assert torch.equal(outs[k][0], outs[1][0]) and torch.equal(outs[k][1], outs[1][1]), k
+    assert torch.equal(cat, outs[1][0])
