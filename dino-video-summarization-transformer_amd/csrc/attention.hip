@@ -11,7 +11,7 @@
 //   Used for sequences longer than 256 keys (joint space-time attention).
 // attn_short_bf16 (L <= 256: spatial 1+N per frame, 2-D ViT): one workgroup per (sequence,
 //   head) with the whole K/V sequence staged in LDS once, 16-query tiles per wave, 16-key
-//   tiles, exact two-pass softmax in registers.
+//   tiles, exact two-pass softmax in registers (1 + 196 keys: XOR-swizzled 52 KB, 3 WGs / CU).
 // attn_seq_f32 (parity mode): same decomposition on the fp32 VALU, one query per lane.
 // attn_temporal_reg (K5, bf16, T <= 8): register-only, 16 lanes per (patch, head), butterfly
 //   reduce-scatter of Q.K^T; HBM-bound.  attn_temporal_kernel: LDS-staged general-T fallback.
@@ -246,12 +246,20 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
 // O^T = V^T.P^T with the k-slot permutation and ds_read_b64_tr_b16 V^T fragments.
 // DBG (diagnostic builds only): 1 = drain lgkmcnt before every P.V MFMA, 2 = V^T fragments by
 // scalar LDS reads instead of ds_read_b64_tr_b16.
-template <int NKT, int NW, int DBG = 0>
-__global__ __launch_bounds__(64 * NW, 2) void attn_short_bf16(AttnParams p) {
-  constexpr int NKP = (NKT + 1) / 2;         // 32-key PV steps
-  constexpr int SN = 2 * NKP;                // score tiles held (the last one of an odd NKT is 0)
-  constexpr int LP = NKP * 32;               // LDS rows: whole PV steps
-  __shared__ __attribute__((aligned(16))) bf16_t kv[2][LP * KV_ROW];
+// SWZ: LDS rows of exactly 64 bf16 with the 16-B chunks XOR-swizzled by (row & 7) instead of the
+// 72-element padded rows, and only the NKT staged key tiles (an odd last tile takes one
+// 16x16x16 P.V MFMA instead of a zero-padded 32-key step): 2 x 208 x 128 B = 52 KB per
+// workgroup at 1 + 196 keys, so 3 workgroups (12 waves) share a CU instead of 2.
+template <int NKT, int NW, int DBG = 0, bool SWZ = false>
+__global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnParams p) {
+  constexpr int NKP = SWZ ? NKT / 2 : (NKT + 1) / 2;   // full 32-key PV steps
+  constexpr bool HALF = SWZ && (NKT & 1);              // + one 16-key step
+  constexpr int SN = SWZ ? NKT : 2 * NKP;    // score tiles held (padded: the last of an odd NKT is 0)
+  constexpr int LP = SWZ ? NKT * 16 : NKP * 32;        // LDS rows
+  constexpr int ROW = SWZ ? 64 : KV_ROW;
+  // element offset of (row r, 16-B chunk c) inside a K or V buffer
+  auto lds = [](int r, int c) { return SWZ ? r * 64 + ((c ^ (r & 7)) << 3) : r * KV_ROW + c * 8; };
+  __shared__ __attribute__((aligned(16))) bf16_t kv[2][LP * ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int h = blockIdx.x;
@@ -293,8 +301,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_short_bf16(AttnParams p) {
   for (int i = 0; i < PCS; ++i) {
     const int pc = tid + NT * i, r = pc >> 3, ch = pc & 7;
     if (r < LP) {
-      *reinterpret_cast<uint4*>(&kv[0][r * KV_ROW + ch * 8]) = kq[i];
-      *reinterpret_cast<uint4*>(&kv[1][r * KV_ROW + ch * 8]) = vq[i];
+      *reinterpret_cast<uint4*>(&kv[0][lds(r, ch)]) = kq[i];
+      *reinterpret_cast<uint4*>(&kv[1][lds(r, ch)]) = vq[i];
     }
   }
   __syncthreads();
@@ -317,9 +325,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_short_bf16(AttnParams p) {
     fv4 s[SN];
 #pragma unroll
     for (int kt = 0; kt < SN; ++kt) {
-      const bf16_t* kr = Ks + (kt * 16 + r16) * KV_ROW + g * 8;
-      const sv8 k0 = *reinterpret_cast<const sv8*>(kr);
-      const sv8 k1 = *reinterpret_cast<const sv8*>(kr + 32);
+      const int kr = kt * 16 + r16;
+      const sv8 k0 = *reinterpret_cast<const sv8*>(Ks + lds(kr, g));
+      const sv8 k1 = *reinterpret_cast<const sv8*>(Ks + lds(kr, g + 4));
       fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
       z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
       s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
@@ -372,12 +380,30 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_short_bf16(AttnParams p) {
           }
         } else {
           const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) sv4*)(Vs + vr0 * KV_ROW + col));
+              (__attribute__((address_space(3))) sv4*)(Vs + lds(vr0, col >> 3) + (col & 7)));
           const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) sv4*)(Vs + vr1 * KV_ROW + col));
+              (__attribute__((address_space(3))) sv4*)(Vs + lds(vr1, col >> 3) + (col & 7)));
           vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
         if constexpr (DBG == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+      }
+    }
+    if constexpr (HALF) {   // odd last key tile: the same 16x16x32 step with the second key tile's
+      constexpr int kt = 2 * NKP;   // k-slots zero in both operands (one MFMA shape in the chain:
+      sv8 pb;                       // mixing in 16x16x16 left a srcC hazard under 3-WG occupancy)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[kt][j]);
+        pb[4 + j] = 0;
+      }
+      const int vr0 = kt * 16 + 4 * g + (r16 >> 2);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + lds(vr0, col >> 3) + (col & 7)));
+        const sv8 vf = __builtin_shufflevector(lo, sv4{0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
       }
     }
@@ -428,8 +454,12 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
     else if (v == 2 && p.seqlen <= 208) attn_short_bf16<13, 8><<<grid, 512, 0, s>>>(p);
     else if (v == 5 && p.seqlen <= 208) attn_short_bf16<13, 4, 1><<<grid, 256, 0, s>>>(p);
     else if (v == 6 && p.seqlen <= 208) attn_short_bf16<13, 4, 2><<<grid, 256, 0, s>>>(p);
+    else if (v == 7 && p.seqlen <= 48) attn_short_bf16<3, 4, 0, true><<<grid, 256, 0, s>>>(p);
     else if (p.seqlen <= 64 && v == 0) attn_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
-    else if (p.seqlen <= 208) attn_short_bf16<13, 4><<<grid, 256, 0, s>>>(p);   // 1 + 196 patches
+    else if (v == 3 && p.seqlen <= 208) attn_short_bf16<13, 4><<<grid, 256, 0, s>>>(p);   // padded rows
+    // 1 + 196 patches: swizzled exact-tile LDS, 3 workgroups per CU -- 53.4 vs 62.2 us at the
+    // bench's global call (16 clips x 8 frames x 12 heads); 25.3 vs 24.5 us at 1 + 36 (kept <4, 4>)
+    else if (p.seqlen <= 208) attn_short_bf16<13, 4, 0, true><<<grid, 256, 0, s>>>(p);
     else attn_short_bf16<16, 4><<<grid, 256, 0, s>>>(p);
     return hipGetLastError();
   }

@@ -385,7 +385,7 @@ int dsvt_set_gemm_variant(int variant) {
 }
 
 int dsvt_set_attn_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 6, "attention variant must be 0-6");
+  REQUIRE(variant >= 0 && variant <= 7, "attention variant must be 0-7");
   set_attn_variant(variant);
   return 0;
 }

@@ -220,7 +220,7 @@ def test_attn_spatial_cls_mean(dtype, B, T, N, heads):
     check(back(out), spatial_ref(back(Q), B, T, L, heads, 0.125), dtype, "spatial")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 7])
 def test_attn_spatial_variants_repeatable(variant):
     """Every bf16 short-sequence kernel at a multi-clip global shape (B=4, 8x196 patches, 12 heads,
     N(0,1) q/k/v): finite, within tolerance of the float64 reference, and bitwise identical over

@@ -22,6 +22,8 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("qkv_l", M_L, 2304, 768, _lib.EPI_BIAS),
     ("fc1_l", M_L, 3072, 768, _lib.EPI_BIAS_GELU),
     ("head", 64, 65536, 256, _lib.EPI_BIAS),
+    ("fc1b_g", M_G, 3072, 768, _lib.EPI_BIAS),     # fc1 without the GELU: the epilogue's price
+    ("fc1b_l", M_L, 3072, 768, _lib.EPI_BIAS),
 ]
 
 
