@@ -302,6 +302,25 @@ def other_configs(args, device):
 
 
 # ----------------------------------------------------------------- main
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) outside torch.distributed.run: start N ranks of this script
+    through torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as CHILD
+    processes -- this process never initialises the GPU -- and return their exit status.
+    Fails loudly when fewer than N GPUs are visible (unless --shared-gpu rehearses it)."""
+    import socket
+    import subprocess
+    ndev = torch.cuda.device_count()                    # does not initialise HIP
+    if ndev < args.gpus and not args.shared_gpu:
+        print("bench: --gpus %d requested but only %d GPU(s) are visible" % (args.gpus, ndev), file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -318,15 +337,32 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
     ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' only to rehearse "
+                         "several ranks on one GPU with --shared-gpu)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal: allow N ranks on fewer GPUs (rank r uses GPU r %% count; needs --backend gloo)")
     args = ap.parse_args()
 
     from dsvt import dist as ddist
-    from dsvt import ops
 
     rank, world, local_rank = ddist.env_ranks()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start the N ranks before this process touches the GPU
+        raise SystemExit(launch_ranks(args))
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but the torch.distributed.run environment has WORLD_SIZE=%d"
+                         % (args.gpus, world))
+    ndev = torch.cuda.device_count()                    # does not initialise HIP
+    if world > ndev and not args.shared_gpu:
+        raise SystemExit("bench: %d ranks but only %d GPU(s) visible" % (world, ndev))
+    if args.shared_gpu and world > 1 and args.backend != "gloo":
+        raise SystemExit("bench: --shared-gpu needs --backend gloo (RCCL refuses two ranks on one GPU)")
+    local_rank = local_rank % max(ndev, 1)
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    rank, world = ddist.init_from_env(device)          # 'nccl' = RCCL over xGMI when world > 1
+    rank, world = ddist.init_from_env(device, backend=args.backend)   # 'nccl' = RCCL over xGMI when world > 1
+    from dsvt import ops
     from dsvt._lib import PROBE_GEMM
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -451,7 +487,9 @@ def main():
                              "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4),
                              "frac_reference_flops": round(value * clip_flops() / 1e12 / world
                                                            / PEAK_TFLOPS[args.dtype], 4)},
-           "roofline": roofline, "loss": round(loss_val, 5)}
+           "roofline": roofline, "loss": round(loss_val, 5),
+           "world_size": world, "backend": ddist.backend() or "none",
+           "rccl_ranks": world if ddist.backend() == "nccl" else 0}
     if not args.no_train:
         graph = None                        # release the captured forward's memory pool
         torch.cuda.empty_cache()

@@ -247,9 +247,10 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
 // DBG (diagnostic builds only): 1 = drain lgkmcnt before every P.V MFMA, 2 = V^T fragments by
 // scalar LDS reads instead of ds_read_b64_tr_b16.
 // SWZ: LDS rows of exactly 64 bf16 with the 16-B chunks XOR-swizzled by (row & 7) instead of the
-// 72-element padded rows, and only the NKT staged key tiles (an odd last tile takes one
-// 16x16x16 P.V MFMA instead of a zero-padded 32-key step): 2 x 208 x 128 B = 52 KB per
-// workgroup at 1 + 196 keys, so 3 workgroups (12 waves) share a CU instead of 2.
+// 72-element padded rows, and only the NKT staged key tiles (an odd last tile finishes with a
+// 16x16x32 P.V step whose second 16-key half is zero in both operands -- one MFMA shape per
+// accumulator chain): 2 x 208 x 128 B = 52 KB per workgroup at 1 + 196 keys, so
+// 3 workgroups (12 waves) share a CU instead of 2.
 template <int NKT, int NW, int DBG = 0, bool SWZ = false>
 __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnParams p) {
   constexpr int NKP = SWZ ? NKT / 2 : (NKT + 1) / 2;   // full 32-key PV steps
@@ -441,7 +442,9 @@ __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnPara
   }
 }
 
-static int g_attn_variant = 0;  // 0 = auto; otherwise forced (tools/attn_check.py, tests)
+// 0 = auto; otherwise forced (tools/attn_check.py, tests).  Per calling thread: a diagnostic
+// override on one thread never changes the kernels another thread's launches pick.
+static thread_local int g_attn_variant = 0;
 void set_attn_variant(int v) { g_attn_variant = v; }
 
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {

@@ -815,7 +815,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_short_bf16(AttnBwdParams 
   }
 }
 
-static int g_attn_bwd_variant = 0;   // 0 = auto, 1 = force the generic VALU kernels (tests / tools)
+static thread_local int g_attn_bwd_variant = 0;  // 0 = auto, 1 = force the generic VALU kernels (tests / tools)
 void set_attn_bwd_variant(int v) { g_attn_bwd_variant = v; }
 
 hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s) {
@@ -1158,6 +1158,42 @@ __global__ __launch_bounds__(256) void clip_scale_kernel(float* const* __restric
   const int64_t s0 = cstart[blockIdx.x], n = sizes[ti];
   float* p = x[ti];
   for (int64_t i = s0 + threadIdx.x; i < s0 + 4096 && i < n; i += 256) p[i] *= coef;
+}
+
+// AdamW (decoupled weight decay), the update torch.optim.AdamW applies for the reference's
+// `torch.optim.AdamW(params_groups)` (train_ssl.py:384, step at :551), per element:
+//   p *= 1 - lr*wd;  m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2;
+//   p += step_size * m / (sqrt(v) / sqrt(1 - b2^t) + eps),  step_size = -lr / (1 - b1^t)
+// One launch per (param group, step count) tensor list; one workgroup per 4096-element chunk.
+__global__ __launch_bounds__(256) void adamw_kernel(float* const* __restrict__ param, const float* const* __restrict__ grad,
+                                                    float* const* __restrict__ exp_avg,
+                                                    float* const* __restrict__ exp_avg_sq,
+                                                    const int64_t* __restrict__ sizes, const int32_t* __restrict__ ctensor,
+                                                    const int64_t* __restrict__ cstart, AdamWArgs a) {
+  const int ti = ctensor[blockIdx.x];
+  const int64_t s0 = cstart[blockIdx.x], n = sizes[ti];
+  float* p = param[ti];
+  const float* g = grad[ti];
+  float* m = exp_avg[ti];
+  float* v = exp_avg_sq[ti];
+  const float decay = 1.0f - a.lr * a.wd, w1 = 1.0f - a.beta1, w2 = 1.0f - a.beta2;
+  const int64_t end = s0 + 4096 < n ? s0 + 4096 : n;
+  for (int64_t i = s0 + threadIdx.x; i < end; i += 256) {
+    const float gi = g[i];
+    const float mi = m[i] + w1 * (gi - m[i]);
+    const float vi = v[i] * a.beta2 + w2 * gi * gi;
+    const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = p[i] * decay + a.step_size * (mi / denom);
+  }
+}
+
+hipError_t launch_adamw(float* const* param, const float* const* grad, float* const* exp_avg, float* const* exp_avg_sq,
+                        const int64_t* sizes, const int32_t* ctensor, const int64_t* cstart, int64_t nchunks,
+                        const AdamWArgs& a, hipStream_t s) {
+  adamw_kernel<<<(unsigned)nchunks, 256, 0, s>>>(param, grad, exp_avg, exp_avg_sq, sizes, ctensor, cstart, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_ema(float* const* teacher, const float* const* student, const int64_t* sizes, const int32_t* ctensor,

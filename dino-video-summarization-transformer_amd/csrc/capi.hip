@@ -2,6 +2,7 @@
 // Every entry point checks the shapes/alignments its kernels assume BEFORE launching (a
 // mis-shaped launch would fault the GPU), returns non-zero on error and never aborts.
 #include <stdarg.h>
+#include <cmath>
 #include <stdio.h>
 
 #include <string>
@@ -51,7 +52,7 @@ struct Probe {
     ev0.clear(); ev1.clear(); work.clear(); fam.clear(); tag.clear();
     mask = cap = count = 0;
   }
-} g_probe;
+} thread_local g_probe;   // per calling thread, like the variant knobs
 
 template <typename F>
 int probed(int family, double work, hipStream_t s, const char* where, F&& launch, int tag = 0) {
@@ -641,6 +642,27 @@ int dsvt_clip_grads(float* const* grads, const int64_t* sizes, const int32_t* ch
   hipError_t e = launch_clip_grads(grads, sizes, chunk_tensor, chunk_start, first_chunk, nchunks, ntensors, clip,
                                    (float*)workspace, norms, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "clip_grads");
+}
+
+int dsvt_adamw(float* const* params, const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+               const int64_t* sizes, const int32_t* chunk_tensor, const int64_t* chunk_start, int64_t nchunks, float lr,
+               float weight_decay, float beta1, float beta2, float eps, int64_t step, void* stream) {
+  REQUIRE(params && grads && exp_avg && exp_avg_sq && sizes && chunk_tensor && chunk_start && nchunks > 0,
+          "adamw: bad args");
+  REQUIRE(step >= 1 && beta1 >= 0.f && beta1 < 1.f && beta2 >= 0.f && beta2 < 1.f && eps > 0.f,
+          "adamw: bad hyper-parameters");
+  AdamWArgs a;
+  a.lr = lr;
+  a.wd = weight_decay;
+  a.beta1 = beta1;
+  a.beta2 = beta2;
+  a.eps = eps;
+  // bias corrections in double, as the reference's Python floats
+  a.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)beta2, (double)step));
+  a.step_size = (float)(-(double)lr / (1.0 - std::pow((double)beta1, (double)step)));
+  hipError_t e = launch_adamw(params, grads, exp_avg, exp_avg_sq, sizes, chunk_tensor, chunk_start, nchunks, a,
+                              (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "adamw");
 }
 
 // ================================================================ Video Swin (swin.hip)

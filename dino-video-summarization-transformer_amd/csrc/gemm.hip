@@ -258,7 +258,7 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
   return hipGetLastError();
 }
 
-static int g_gemm_variant = 0;  // 0 = auto; otherwise forced (tools/gemm_bench.py, tests)
+static thread_local int g_gemm_variant = 0; // 0 = auto; otherwise forced (tools/gemm_bench.py, tests)
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 

@@ -121,6 +121,12 @@ hipError_t launch_ema(float* const* teacher, const float* const* student, const 
 hipError_t launch_clip_grads(float* const* grads, const int64_t* sizes, const int32_t* ctensor, const int64_t* cstart,
                              const int32_t* first_chunk, int64_t nchunks, int64_t ntensors, float clip, float* partial,
                              float* norms, hipStream_t s);
+struct AdamWArgs {
+  float lr, wd, beta1, beta2, eps, bc2_sqrt, step_size;
+};
+hipError_t launch_adamw(float* const* param, const float* const* grad, float* const* exp_avg, float* const* exp_avg_sq,
+                        const int64_t* sizes, const int32_t* ctensor, const int64_t* cstart, int64_t nchunks,
+                        const AdamWArgs& a, hipStream_t s);
 
 // Video Swin (swin.hip)
 hipError_t launch_im2col3d(int dtype, const float* x, void* a, int64_t B, int64_t Cin, int64_t D, int64_t H,

@@ -17,16 +17,23 @@ def env_ranks():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init_from_env(device=None, backend=None):
+def init_from_env(device=None, backend=None, timeout_s=None):
     """Initialise the default process group when WORLD_SIZE > 1 (env:// rendezvous; use
-    MASTER_ADDR=127.0.0.1).  backend defaults to 'nccl' (RCCL) for a GPU device, else gloo."""
+    MASTER_ADDR=127.0.0.1) -- utils/utils.py:437-469 of the reference.  backend defaults to
+    'nccl' (RCCL over xGMI) for a GPU device, else gloo.  gloo on GPU tensors is the
+    rehearsal mode for several ranks sharing one GPU (RCCL refuses duplicate devices)."""
     rank, world, _ = env_ranks()
     if world <= 1 or dist.is_initialized():
         return rank, world
     if backend is None:
         backend = "nccl" if device is not None and torch.device(device).type == "cuda" else "gloo"
     kw = {"device_id": torch.device(device)} if backend == "nccl" and device is not None else {}
+    if timeout_s is not None:
+        import datetime
+        kw["timeout"] = datetime.timedelta(seconds=timeout_s)
     dist.init_process_group(backend, init_method="env://", **kw)
+    if dist.get_world_size() != world:
+        raise RuntimeError("process group has %d ranks, WORLD_SIZE says %d" % (dist.get_world_size(), world))
     return dist.get_rank(), dist.get_world_size()
 
 
@@ -44,10 +51,17 @@ def center_batch_sum(colsum, rows):
     return 1.0 / (rows * world)
 
 
+def backend():
+    """The default process group's backend ('nccl' = RCCL, 'gloo'), or None at world size 1."""
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
+
+
 def max_over_ranks(value, device=None):
     """MAX of a host float over all ranks (bench timing: the slowest rank defines the step)."""
     if world_size() == 1:
         return float(value)
+    if backend() == "gloo":
+        device = None          # a host tensor: gloo reduces on the CPU anyway
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

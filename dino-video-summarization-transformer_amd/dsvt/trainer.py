@@ -5,6 +5,12 @@
   -> per-parameter gradient clipping -> cancel last-layer grads in the first epoch(s)
   -> AdamW with the lr / wd schedules -> teacher EMA (one multi-tensor launch)
 
+The order of the two forwards is the reference's (student first, train_ssl.py:523-527), so a
+seeded run draws the DropPath masks in the same order.  The lr schedule applies the
+reference's linear scaling rule lr * batch_size_per_gpu * world_size / 256
+(train_ssl.py:395-400) when `batch_size_per_gpu` is given; without it `lr` is taken as the
+already-scaled peak value.
+
 Differences from the reference loop, all deliberate and documented:
   * no fp16 GradScaler: dsvt computes in bf16 storage / fp32 accumulate with fp32 master
     weights and fp32 gradients (no loss scaling needed);
@@ -22,7 +28,8 @@ from .utils import cancel_gradients_last_layer, clip_gradients, ema_update_, get
 class DINOTrainer:
     def __init__(self, student, teacher, dino_loss, lr=5e-4, min_lr=1e-6, weight_decay=0.04, weight_decay_end=0.4,
                  momentum_teacher=0.996, clip_grad=3.0, freeze_last_layer=1, epochs=100, niter_per_ep=1000,
-                 warmup_epochs=10, n_global=2, ddp=None):
+                 warmup_epochs=10, n_global=2, ddp=None, batch_size_per_gpu=None, world_size=None,
+                 optimizer="dsvt"):
         self.student = student                      # MultiCropWrapper (possibly DDP-wrapped: ddp)
         self.model = ddp if ddp is not None else student
         self.teacher = teacher
@@ -31,15 +38,24 @@ class DINOTrainer:
         self.freeze_last_layer = freeze_last_layer
         self.n_global = n_global
         self.niter_per_ep = niter_per_ep
-        # train_ssl.py:367-407: schedules
+        if batch_size_per_gpu is not None:          # linear scaling rule (train_ssl.py:395-400)
+            if world_size is None:
+                from .dist import world_size as _ws
+                world_size = _ws()
+            lr = lr * (batch_size_per_gpu * world_size) / 256.
+        self.peak_lr = lr
+        # train_ssl.py:394-407: schedules
         self.lr_schedule = np_cosine_scheduler(lr, min_lr, epochs, niter_per_ep, warmup_epochs=warmup_epochs)
         self.wd_schedule = np_cosine_scheduler(weight_decay, weight_decay_end, epochs, niter_per_ep)
         self.momentum_schedule = np_cosine_scheduler(momentum_teacher, 1, epochs, niter_per_ep)
         groups = get_params_groups(student)
-        try:
-            self.optimizer = torch.optim.AdamW(groups, fused=True)
-        except (RuntimeError, TypeError):  # pragma: no cover
-            self.optimizer = torch.optim.AdamW(groups, foreach=True)
+        if optimizer == "dsvt":                     # multi-tensor HIP AdamW (csrc/backward.hip)
+            from .optim import AdamW
+            self.optimizer = AdamW(groups)
+        elif optimizer == "torch":
+            self.optimizer = torch.optim.AdamW(groups)      # train_ssl.py:384
+        else:
+            raise ValueError("optimizer must be 'dsvt' or 'torch'")
         for p in teacher.parameters():
             p.requires_grad_(False)
         self._s_params = [p for p in student.parameters()]
@@ -51,9 +67,9 @@ class DINOTrainer:
             pg["lr"] = float(self.lr_schedule[it])
             if i == 0:
                 pg["weight_decay"] = float(self.wd_schedule[it])
+        s_out = self.model(images)                                 # :523
         with torch.no_grad():
             t_out = self.teacher(images[:self.n_global])           # :527 (teacher on global views)
-        s_out = self.model(images)                                 # :528
         loss = self.dino_loss(s_out, t_out, epoch)
         if check_finite and not math.isfinite(loss.item()):        # :530-532
             raise FloatingPointError("Loss is %s, stopping training" % loss.item())

@@ -268,6 +268,14 @@ int dsvt_clip_grads(float *const *grads, const int64_t *sizes, const int32_t *ch
                     const int64_t *chunk_start, const int32_t *first_chunk, int64_t nchunks,
                     int64_t ntensors, float clip, float *norms, void *workspace, int64_t workspace_bytes,
                     void *stream);
+/* AdamW step over one tensor list that shares lr / weight decay / step count (replaces
+ * torch.optim.AdamW(params_groups).step(), train_ssl.py:384 / :551): per element
+ * p *= 1 - lr*wd; m += (1-beta1)(g-m); v = beta2 v + (1-beta2) g^2;
+ * p += -lr/(1-beta1^step) * m / (sqrt(v)/sqrt(1-beta2^step) + eps).  step >= 1. */
+int dsvt_adamw(float *const *params, const float *const *grads, float *const *exp_avg,
+               float *const *exp_avg_sq, const int64_t *sizes, const int32_t *chunk_tensor,
+               const int64_t *chunk_start, int64_t nchunks, float lr, float weight_decay, float beta1,
+               float beta2, float eps, int64_t step, void *stream);
 
 /* ------------------------------------------------------------------------------------------
  * Video Swin Transformer backbone (models/swin_transformer.py, config 5).  Tokens: fp32

@@ -1,0 +1,194 @@
+"""One rank of the data-parallel DINO step test (tests/test_gpu_dist.py starts two of these).
+
+The reference's config-3 data path (train_ssl.py:329 DDP wrap, :523-545 forward / loss /
+backward, :686-688 center all-reduce, utils/utils.py:437-469 process-group init) on dsvt:
+DDP(MultiCropWrapper(dsvt TimeSformer, DINOHead)) -> dsvt.loss.DINOLoss -> backward, each rank
+on its half of the clips.  RCCL refuses two ranks on one GPU, so the two ranks share the box's
+GPU over gloo (same DDP reducer, same bucketed all-reduce code path; only the transport
+differs).  Rank 0 then re-runs the same step in one process on the WHOLE batch and checks the
+all-reduced gradients, the loss and the center against it (fp32 parity mode, 1e-3 relative
+to max |ref| per tensor), and both ranks check they hold bitwise-identical gradients.  A second
+phase runs dsvt.trainer.DINOTrainer.step (clip + AdamW + EMA) under DDP and checks the student
+and teacher parameters stay identical across the ranks.
+
+Writes {"ok": bool, "msg": str, ...} to $DSVT_TEST_OUT.  Run by the test only.
+"""
+import json
+import os
+import sys
+import traceback
+from functools import partial
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "dino-video-summarization-transformer_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+from oracle import params as P  # noqa: E402
+
+CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
+OUT_DIM, B_ALL, NCROPS = 512, 4, 4
+TOL = 1e-3
+
+
+def build(seed_bb, seed_hd):
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+    bb = VisionTransformer(img_size=64, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
+                           qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_path_rate=0.0,
+                           num_frames=4, attention_type="divided_space_time")
+    bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(seed_bb, **CFG).items()})
+    hd = DINOHead(64, OUT_DIM, hidden_dim=128, bottleneck_dim=64)
+    hd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                        P.dino_head_state(seed_hd, 64, OUT_DIM, hidden_dim=128, bottleneck_dim=64).items()})
+    bb.dsvt_dtype = hd.dsvt_dtype = torch.float32
+    return MultiCropWrapper(bb, hd).cuda()
+
+
+def crops_all():
+    """The whole batch: 2 global 4x64^2 and 2 local 4x32^2 crops of B_ALL clips."""
+    return [P.clip(3100 + i, (B_ALL, 3, 4, 64, 64)) for i in range(2)] + \
+           [P.clip(3110 + i, (B_ALL, 3, 4, 32, 32)) for i in range(2)]
+
+
+def make_loss(center0):
+    from dsvt.loss import DINOLoss
+    lf = DINOLoss(OUT_DIM, NCROPS, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    lf.center.copy_(torch.from_numpy(center0))
+    return lf
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-12))
+
+
+_LOG = [None]
+
+
+def log(msg):
+    if _LOG[0] is not None:
+        _LOG[0].write(msg + "\n")
+        _LOG[0].flush()
+
+
+def main():
+    from dsvt import dist as ddist
+    rank, world, _ = ddist.env_ranks()
+    if os.environ.get("DSVT_TEST_LOGDIR"):
+        _LOG[0] = open(os.path.join(os.environ["DSVT_TEST_LOGDIR"], "ddp_rank%d.log" % rank), "w")
+    log("start")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    r, w = ddist.init_from_env(dev, backend="gloo", timeout_s=60)
+    log("process group up")
+    assert (r, w) == (rank, world) and world == 2, (r, w)
+    info = {"rank": rank, "world": world, "backend": dist.get_backend()}
+
+    center0 = (0.1 * P.clip(3120, (1, OUT_DIM))).astype(np.float32)
+    full = crops_all()
+    lo, hi = ddist.shard_range(B_ALL, rank, world)
+    mine = [torch.from_numpy(c[lo:hi].copy()).to(dev) for c in full]
+
+    # ---- phase 1: DDP gradients + center vs the single-process whole batch
+    student = build(4101, 4102).train()
+    teacher = build(4201, 4202).eval()
+    for p in teacher.parameters():
+        p.requires_grad_(False)
+    log("models built")
+    ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[0], broadcast_buffers=False)
+    log("ddp wrapped")
+    loss_fn = make_loss(center0)
+    s_out = ddp(mine)                                   # train_ssl.py:523
+    with torch.no_grad():
+        t_out = teacher(mine[:2])                       # :527
+    loss = loss_fn(s_out, t_out, 0)                     # center all-reduce inside (update_center)
+    log("forward + loss done")
+    loss.backward()                                     # DDP bucketed gradient all-reduce
+    log("backward done")
+    torch.cuda.synchronize()
+    names = [n for n, p in student.named_parameters() if p.requires_grad]
+    grads = {n: p.grad.detach().float().cpu().numpy() for n, p in student.named_parameters() if p.requires_grad}
+    missing = [n for n in names if student.get_parameter(n).grad is None]
+    assert not missing, "no gradient for %s" % missing
+    flat = torch.cat([torch.from_numpy(grads[n]).reshape(-1) for n in names])
+    peers = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(peers, flat)
+    assert all(torch.equal(peers[0], x) for x in peers[1:]), "ranks hold different averaged gradients"
+    loss_sum = torch.tensor([float(loss.item())], dtype=torch.float64)
+    dist.all_reduce(loss_sum)
+    center_dp = loss_fn.center.detach().cpu().numpy()
+    info["n_params"] = len(names)
+
+    log("phase 1 collectives done")
+    if rank == 0:
+        from dsvt import ops
+        ref = build(4101, 4102).train()
+        lf = make_loss(center0)
+        lf.defer_center_update = True      # a single process: its center update has no all-reduce
+        allc = [torch.from_numpy(c).to(dev) for c in full]
+        so = ref(allc)
+        with torch.no_grad():
+            to = teacher(allc[:2])
+        l_ref = lf(so, to, 0)
+        colsum, rows = lf.last_colsum
+        ops.center_ema(lf.center, colsum, lf.center_momentum, 1.0 / rows)
+        l_ref.backward()
+        torch.cuda.synchronize()
+        errs = {}
+        for n, p in ref.named_parameters():
+            if p.requires_grad:
+                errs[n] = rel(grads[n], p.grad.cpu().numpy())
+        worst = max(errs, key=errs.get)
+        info["worst_grad"] = [worst, errs[worst]]
+        assert errs[worst] < TOL, "DDP grad %s rel err %.3g vs single-process full batch" % (worst, errs[worst])
+        l_mean = float(loss_sum.item()) / world
+        info["loss"] = [l_mean, float(l_ref.item())]
+        assert abs(l_mean - float(l_ref.item())) < TOL * abs(float(l_ref.item())), info["loss"]
+        ec = rel(center_dp, lf.center.cpu().numpy())
+        info["center_err"] = ec
+        assert ec < 1e-5, "center after the all-reduced update differs: %.3g" % ec
+        del ref, lf
+    dist.barrier()
+    del ddp, student
+
+    # ---- phase 2: whole training steps under DDP stay in sync across ranks
+    from dsvt.trainer import DINOTrainer
+    student = build(4101, 4102).train()
+    teacher = build(4101, 4102).eval()
+    ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[0], broadcast_buffers=False)
+    tr = DINOTrainer(student, teacher, make_loss(center0), ddp=ddp, epochs=2, niter_per_ep=4, warmup_epochs=1,
+                     batch_size_per_gpu=hi - lo, world_size=world)
+    for it in (3, 4):                                  # it 3: last layer frozen (epoch 0); it 4: epoch 1
+        tr.step(mine, it)
+        log("trainer step %d done" % it)
+    torch.cuda.synchronize()
+    for tag, net in (("student", student), ("teacher", teacher)):
+        flat = torch.cat([p.detach().float().reshape(-1).cpu() for p in net.parameters()])
+        assert torch.isfinite(flat).all(), tag
+        peers = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(peers, flat)
+        assert all(torch.equal(peers[0], x) for x in peers[1:]), "%s parameters diverged across ranks" % tag
+    dist.barrier()
+    dist.destroy_process_group()
+    return info
+
+
+if __name__ == "__main__":
+    out = os.environ["DSVT_TEST_OUT"]
+    try:
+        res = main()
+        res["ok"] = True
+        res["msg"] = "ok"
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent test
+        res = {"ok": False, "msg": "%r\n%s" % (e, traceback.format_exc())}
+    log("result: %s" % res["msg"][:2000])
+    with open(out, "w") as f:
+        json.dump(res, f)
+    sys.exit(0 if res["ok"] else 1)

@@ -1,7 +1,8 @@
 """N > 1 data-parallel path on the CPU: gloo, world_size 2, one process per rank (the GPU runs
-the same code over RCCL).  Covers dsvt.dist: the center column-sum all-reduce of
-DINOLoss.update_center (train_ssl.py:673-691), the bench's max-over-ranks timing, and the
-video sharding of frame scoring."""
+the same code over RCCL).  Covers dsvt.dist and the product's dsvt.loss.DINOLoss.update_center
+(the center column-sum all-reduce of train_ssl.py:673-691), the trainer's world-size lr
+scaling, the bench's max-over-ranks timing, and the video sharding of frame scoring.
+The GPU leg (DDP gradients through the HIP backward) is tests/test_gpu_dist.py."""
 import os
 import socket
 import sys
@@ -46,14 +47,32 @@ def _worker(rank, world, port, errq):
         t_loc = np.concatenate([teacher[c * B_all + lo:c * B_all + hi] for c in range(2)])
         s_loc = np.concatenate([student[c * B_all + lo:c * B_all + hi] for c in range(ncrops)])
 
-        # the rank's local column sum, all-reduced exactly like DINOLoss.update_center
-        colsum = torch.from_numpy(t_loc.astype(np.float64).sum(0, keepdims=True))
-        scale = ddist.center_batch_sum(colsum, t_loc.shape[0])
-        assert scale == pytest.approx(1.0 / (t_loc.shape[0] * world))
-        _, c_dp = O.dino_loss(s_loc, t_loc, center, ncrops, temp, world_size=world,
-                              teacher_sum_all=colsum.numpy())
+        # the product's DINOLoss.update_center on the rank's local column sum: the all-reduce and
+        # the 1/(rows*world) scale run as shipped; only the center-EMA kernel launch (a GPU op,
+        # csrc/dino_loss.hip) is replaced by its host arithmetic for this CPU test
+        from dsvt import loss as dloss
+        from dsvt import ops
+
+        def center_ema_host(c, colsum, momentum, inv_count):
+            c.mul_(momentum).add_(colsum.reshape(c.shape) * (inv_count * (1.0 - momentum)))
+        ops.center_ema = center_ema_host
+        lf = dloss.DINOLoss(D, ncrops, temp, temp, 0, 10)
+        lf.center.copy_(torch.from_numpy(center))
+        colsum = torch.from_numpy(t_loc.sum(0, keepdims=True))
+        lf.update_center(colsum, t_loc.shape[0])
+        c_dp = lf.center.numpy()
         _, c_full = O.dino_loss(student, teacher, center, ncrops, temp)   # single process, whole batch
-        np.testing.assert_allclose(c_dp, c_full, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(c_dp, c_full, rtol=1e-5, atol=1e-7)
+        assert ddist.center_batch_sum(torch.zeros(1, D), t_loc.shape[0]) == pytest.approx(1.0 / (t_loc.shape[0] * world))
+        # the oracle's own DP restatement agrees as well
+        _, c_or = O.dino_loss(s_loc, t_loc, center, ncrops, temp, world_size=world, teacher_sum_all=colsum.numpy())
+        np.testing.assert_allclose(c_or, c_full, rtol=1e-5, atol=1e-7)
+        # DINOTrainer's linear lr scaling uses the world size (train_ssl.py:395-400)
+        from dsvt.trainer import DINOTrainer
+        net = torch.nn.Linear(4, 4)
+        tr = DINOTrainer(net, torch.nn.Linear(4, 4), lf, lr=5e-4, epochs=2, niter_per_ep=3, warmup_epochs=1,
+                         batch_size_per_gpu=8)
+        assert tr.peak_lr == pytest.approx(5e-4 * 8 * world / 256.0)
         # every rank ends with the identical center (train_ssl.py: teacher stays in sync)
         got = [torch.zeros(1, D) for _ in range(world)]
         dist.all_gather(got, torch.from_numpy(c_dp))

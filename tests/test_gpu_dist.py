@@ -1,0 +1,64 @@
+"""Config 3's data-parallel leg on the GPU (train_ssl.py:329 DDP, :538-545 backward with the
+bucketed gradient all-reduce, :686-688 center all-reduce): two ranks of tests/ddp_worker.py
+share the box's one GPU over gloo (RCCL refuses two ranks per device) and check the averaged
+gradients / loss / center against a single-process whole-batch step, plus DINOTrainer steps
+staying in sync.  Also: `bench.py --gpus 2` must refuse to run on fewer GPUs than ranks."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+LOGDIR = os.path.join(ROOT, "gpurun_out")      # per-rank progress logs (copied back from the GPU box)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_ddp_two_ranks_match_single_process(tmp_path):
+    world, port = 2, _free_port()
+    procs, outs = [], []
+    for r in range(world):
+        out = tmp_path / ("rank%d.json" % r)
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(world), DSVT_TEST_OUT=str(out),
+                   DSVT_TEST_LOGDIR=str(LOGDIR if os.path.isdir(LOGDIR) else tmp_path))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ddp_worker.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        outs.append(out)
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=150)[0].decode(errors="replace"))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("a DDP rank hung")
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert out.exists(), "rank %d wrote no result (exit %s):\n%s" % (r, p.returncode, logs[r][-3000:])
+        res = json.loads(out.read_text())
+        assert res["ok"], "rank %d: %s" % (r, res["msg"])
+        assert res["world"] == world and res["backend"] == "gloo"
+        if r == 0:
+            print("ddp rank0:", res)
+            assert res["worst_grad"][1] < 1e-3 and res["center_err"] < 1e-5
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """On the 1-GPU box `bench.py --gpus 2` must fail loudly, never time one GPU as two."""
+    import torch
+    n = torch.cuda.device_count()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n + 1), "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "GPU" in (r.stderr + r.stdout)
+    assert '"metric"' not in r.stdout

@@ -368,3 +368,85 @@ def test_pair_loss_golden():
     pl = PairwiseDINOLoss(768, 0.02, 0.3).to(dev())
     got = back(pl.per_row(to(P.clip(901, (10, 768)), torch.float32), to(P.clip(902, (10, 768)), torch.float32)))
     np.testing.assert_allclose(got, np.load("tests/golden/pair_loss.npz")["loss"], rtol=2e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_attn_joint_config4_size(dtype):
+    """Config 4 at its own size (ViT-B joint space-time 16x224^2: L = 1 + 196*16 = 3137, 12 heads,
+    2 clips) vs torch fp32 scaled_dot_product_attention on the same storage-rounded q/k/v;
+    repeated launches are bitwise identical (the flash kernel's MFMA chains are the same
+    hazard class as the spatial kernel's)."""
+    import torch.nn.functional as F
+    from dsvt import ops
+    nb, L, heads = 2, 3137, 12
+    C = heads * 64
+    gen = torch.Generator(device="cuda").manual_seed(17)
+    Q = torch.randn(nb * L, 3 * C, device="cuda", generator=gen).to(dtype)
+    outs = []
+    for _ in range(3):
+        out = torch.full((nb * L, C), 7.0, device="cuda", dtype=dtype)
+        ops.attn_joint(Q, out, nb, L, heads, 0.125)
+        outs.append(out)
+    x = Q.float().view(nb, L, 3, heads, 64)
+    ref = F.scaled_dot_product_attention(x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2),
+                                         x[:, :, 2].transpose(1, 2), scale=0.125)
+    ref = ref.transpose(1, 2).reshape(nb * L, C)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "repeat launches differ"
+    check(back(outs[0]), ref.double().cpu().numpy(), dtype, "joint L=3137")
+
+
+@pytest.mark.parametrize("rows", [25104, 4623, 7])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mapped", [False, True])
+def test_layernorm_c768_multirow(rows, out_dtype, mapped):
+    """The C = 768 LayerNorm kernel's grid-stride path (rows > 4096: one wave handles several
+    rows, prefetching the next row, clamped last row) at the bench's 25104 rows and at ragged
+    counts, with and without a row map, fp32 and bf16 output, vs the oracle; and bitwise equal
+    to a launch over the first <= 4096 rows only (one row per wave there)."""
+    from dsvt import ops
+    C, L = 768, 1569
+    nclip = -(-rows // (L - 1))
+    src_rows = nclip * L if mapped else rows
+    x = rnd((src_rows, C), 18, 2.0) + 0.3
+    g, bb = 1 + rnd((C,), 19, 0.1), rnd((C,), 20, 0.1)
+    X = to(x, torch.float32)
+    gg, bt = to(g, torch.float32), to(bb, torch.float32)
+    rowmap = (L - 1, L, 1) if mapped else None
+    idx = (np.arange(rows) // (L - 1)) * L + 1 + np.arange(rows) % (L - 1) if mapped else np.arange(rows)
+    out = torch.empty(rows, C, device=dev(), dtype=out_dtype)
+    ops.layernorm(X, rows, C, gg, bt, 1e-6, out, rowmap=rowmap, out_f32=out_dtype == torch.float32)
+    sub = min(rows, 2 * (L - 1))                  # whole clips when mapped; <= 4096 rows
+    part = torch.empty(sub, C, device=dev(), dtype=out_dtype)
+    ops.layernorm(X, sub, C, gg, bt, 1e-6, part, rowmap=rowmap, out_f32=out_dtype == torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:sub], part)
+    check(back(out), O.layer_norm(x[idx], g, bb), out_dtype, "ln768")
+
+
+@pytest.mark.parametrize("variant", [0, 7])
+def test_attn_spatial_short_local_shape(variant):
+    """The 96^2 local-crop spatial shape (1 + 36 keys, B=6 clips x 8 frames, 12 heads): the
+    default <4,4> kernel and variant 7 = the swizzled exact-tile kernel attn_short_bf16<3,4,0,SWZ>
+    (3 key tiles: its odd-last-tile zero-padded 16x16x32 step), bitwise repeatable and within
+    bf16 tolerance of float64."""
+    from dsvt import _lib, ops
+    from dsvt._lib import WS_ATTN_SPATIAL
+    B, T, N, heads = 6, 8, 36, 12
+    C, L = heads * 64, 1 + N * T
+    Q = to(rnd((B * L, 3 * C), 22, 1.0), torch.bfloat16)
+    ws = torch.empty(ops.workspace_bytes(WS_ATTN_SPATIAL, torch.bfloat16, B * T, C, 0) // 4, device=dev())
+    _lib.call("dsvt_set_attn_variant", variant)
+    try:
+        outs = []
+        for _ in range(3):
+            out = torch.full((B * L, C), 7.0, device=dev(), dtype=torch.bfloat16)
+            ops.attn_spatial(Q, out, B, T, L, heads, 0.125, ws)
+            outs.append(out)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("dsvt_set_attn_variant", 0)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "repeat launches differ"
+    check(back(outs[0]), spatial_ref(back(Q), B, T, L, heads, 0.125), torch.bfloat16, "spatial v%d" % variant)

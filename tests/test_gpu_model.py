@@ -2,7 +2,7 @@
 (tests/golden/*.npz, produced by running the reference itself) and the oracle.
 
 fp32 parity mode: CLS embeddings / head outputs / DINO loss within 1e-3 of the reference
-(the north-star bar; observed errors are ~1e-5).  bf16 perf mode: within BF16_TOL (relative
+(the north-star bar; observed errors are ~1e-5).  bf16 perf mode: within BF16_TOL = 2e-2 (relative
 to max|ref|) -- the survey measured 2.6e-2 CLS drift for bf16 vs fp32 INSIDE the reference
 itself (SURVEY §7 'Hard parts')."""
 from functools import partial
@@ -17,7 +17,7 @@ from oracle import params as P
 
 pytestmark = pytest.mark.gpu
 FP32_TOL = 1e-3
-BF16_TOL = 6e-2
+BF16_TOL = 2e-2          # observed bf16 drift <= 8.5e-3 (r02 GPU run); the north-star loss bar is separate
 
 
 def g(name):
@@ -289,3 +289,26 @@ def test_split_streams_bitwise_equal(base_sd, dtype):
     for k in (2, 3, 7):
         assert torch.equal(outs[k][0], outs[1][0]) and torch.equal(outs[k][1], outs[1][1]), k
     assert torch.equal(cat, outs[1][0])
+
+
+def test_joint16_config4_full_size():
+    """Config 4 at its own size: ViT-B/16 joint space-time on 16x224^2 (L = 3137 tokens).
+    fp32 parity mode vs the oracle (one clip, 1e-3), the bf16 perf mode vs fp32 on two clips
+    (BF16_TOL), and three bf16 forwards bitwise identical (the flash kernel at the bench shape)."""
+    sd = P.timesformer_state(8, attention_type="joint_space_time", num_frames=16)
+    x = P.clip(801, (2, 3, 16, 224, 224))
+    with torch.no_grad():
+        m32 = tsf(sd, torch.float32, attention_type="joint_space_time", num_frames=16)
+        a = m32(cu(x)).cpu()
+        del m32
+        mb = tsf(sd, torch.bfloat16, attention_type="joint_space_time", num_frames=16)
+        outs = [mb(cu(x)) for _ in range(3)]
+    torch.cuda.synchronize()
+    ref = O.forward_features(sd, x[:1], 12, attention_type="joint_space_time")
+    e32 = rel(a[:1], ref)
+    eb = rel(outs[0].cpu(), a)
+    print("joint16 fp32 vs oracle %.3g, bf16 vs fp32 %.3g" % (e32, eb))
+    assert e32 < FP32_TOL
+    assert eb < BF16_TOL
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
