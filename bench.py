@@ -177,7 +177,9 @@ def train_bench(args, device, rank, world, steps, warmup):
     if world > 1:
         ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[device.index],
                                                         gradient_as_bucket_view=True, broadcast_buffers=False)
-    trainer = DINOTrainer(student, teacher, dino_loss, ddp=ddp, niter_per_ep=1000, epochs=100)
+    # the reference's defaults (train_ssl.py:50-151): lr 5e-4 scaled by clips * world / 256
+    trainer = DINOTrainer(student, teacher, dino_loss, ddp=ddp, niter_per_ep=1000, epochs=100,
+                          batch_size_per_gpu=args.clips, world_size=world)
     crops = synthetic_crops(args.clips, device, seed=4321 + rank)
     for i in range(warmup):
         trainer.step(crops, 2000 + i)       # past warm-up / first epoch: the last layer trains too
@@ -205,7 +207,9 @@ def train_bench(args, device, rank, world, steps, warmup):
             "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3), "gflop_per_clip": round(clip_gf, 1),
             "tflops_per_gpu": round(value * clip_gf / 1e3 / world, 1), "loss": round(loss_val, 5),
-            "parallelism": "dp%d (DDP, RCCL bucketed all-reduce)" % world if world > 1 else "dp1",
+            "parallelism": ("dp%d (DDP, %s bucketed all-reduce)" % (world, "RCCL" if ddist.backend() == "nccl"
+                                                                      else ddist.backend())) if world > 1 else "dp1",
+            "optimizer": "dsvt AdamW (multi-tensor HIP kernel)",
             "drop_path": 0.1, "teacher_mode": "eval"}
 
 

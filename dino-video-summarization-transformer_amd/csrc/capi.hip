@@ -73,6 +73,8 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
 // GEMM instantiation id: gemm_kernel<T = dtype ? float : bf16, EPI = epi, OUT_F32 = f32>
 // probe tag of a GEMM launch: variant * 32 + dtype * 16 + epilogue * 2 + fp32-output, so the
 // host can name the exact kernel instantiation rocprofv3 reports (dsvt/ops.py gemm_kernel_name)
+constexpr int ROWLN_PROBE_TAG = 30 * 32 + 2 * 2 + 1;   // "variant 30": gemm_rowln_kernel (dsvt/ops.py)
+
 int gemm_tag(const GemmParams& p, int dtype, int epi, int out_f32) {
   const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
   return gemm_variant_for(p, dtype, epi, out_f32) * 32 + dtype * 16 + epi * 2 + f32;
@@ -146,11 +148,38 @@ int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const fl
   REQUIRE(x && y && gamma && beta, "layernorm: null pointer");
   REQUIRE(rows > 0 && C > 0 && C % 64 == 0 && C <= 1024, "layernorm: need 0 < C <= 1024, C %% 64 == 0 (C=%lld)", (long long)C);
   REQUIRE(aligned16(x) && aligned16(y) && aligned16(gamma) && aligned16(beta), "layernorm: pointers must be 16-byte aligned");
+  REQUIRE(out_f32 >= 0 && out_f32 <= 3, "layernorm: out_f32 flags must be in [0, 3]");
   norm_map(rpg, gstride, goff);
-  const double bytes = (double)rows * C * (4 + (out_f32 || dtype == DSVT_F32 ? 4 : 2));
+  const double bytes = (double)rows * C * (4 + ((out_f32 & 1) || dtype == DSVT_F32 ? 4 : 2));
   return probed(DSVT_PROBE_NORM, bytes, (hipStream_t)stream, "dsvt_layernorm_fwd", [&] {
     return launch_layernorm(dtype, out_f32, x, y, gamma, beta, rows, C, rpg, gstride, goff, eps, (hipStream_t)stream);
   });
+}
+
+int dsvt_gemm_resid_ln_fwd(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, float* X,
+                           int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
+                           const float* gamma, const float* beta, float eps, void* Y, int ymode, int64_t L,
+                           void* stream) {
+  REQUIRE(A && W && X, "gemm_resid_ln: null pointer");
+  REQUIRE(N == 768, "gemm_resid_ln: N must be 768 (got %lld)", (long long)N);
+  REQUIRE(M > 0 && K > 0 && K % 128 == 0, "gemm_resid_ln: need M > 0, K > 0, K %% 128 == 0 (M=%lld K=%lld)",
+          (long long)M, (long long)K);
+  REQUIRE(lda >= K && ldw >= K && lda % 8 == 0 && ldw % 8 == 0, "gemm_resid_ln: lda/ldw must be >= K, multiples of 8");
+  REQUIRE(M * lda * 2 <= (int64_t)UINT32_MAX && N * ldw * 2 <= (int64_t)UINT32_MAX,
+          "gemm_resid_ln: A and W must span < 4 GiB (32-bit DMA offsets)");
+  REQUIRE(aligned16(A) && aligned16(W) && aligned16(X) && (!bias || aligned16(bias)),
+          "gemm_resid_ln: pointers must be 16-byte aligned");
+  REQUIRE(ymode == DSVT_ROWLN_NONE || ymode == DSVT_ROWLN_X || ymode == DSVT_ROWLN_COMPACT, "gemm_resid_ln: bad ymode");
+  REQUIRE(ymode == DSVT_ROWLN_NONE || (gamma && beta && Y && aligned16(gamma) && aligned16(beta) && aligned16(Y)),
+          "gemm_resid_ln: LayerNorm output needs gamma, beta, Y (16-byte aligned)");
+  REQUIRE(ymode != DSVT_ROWLN_COMPACT || L > 1, "gemm_resid_ln: compact output needs L > 1");
+  norm_map(rpg, gstride, goff);
+  RowLnParams p{};
+  p.A = A; p.lda = lda; p.W = W; p.ldw = ldw; p.bias = bias; p.X = X; p.M = M; p.K = K;
+  p.rpg = rpg; p.gstride = gstride; p.goff = goff;
+  p.gamma = gamma; p.beta = beta; p.eps = eps; p.Y = (unsigned short*)Y; p.ymode = ymode; p.L = L;
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_resid_ln_fwd",
+                [&] { return launch_gemm_rowln(p, (hipStream_t)stream); }, ROWLN_PROBE_TAG);
 }
 
 int dsvt_ln_gemm_fwd(int dtype, int epilogue, int out_f32, const float* x, int64_t in_rpg, int64_t in_gstride,

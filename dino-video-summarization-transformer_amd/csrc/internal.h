@@ -34,6 +34,23 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
 bool gemm_8ph_ok(const GemmParams& p, int epi);
 void set_gemm_variant(int v);
 
+// Full-row residual GEMM + fused LayerNorm (gemm_rowln.hip), bf16, N = 768:
+//   X[map(m)] += A[m] . W^T + bias;  Y[yrow] = LN(X[map(m)]) (ymode: see ROWLN_Y_*)
+enum { ROWLN_Y_NONE = 0, ROWLN_Y_X = 1, ROWLN_Y_COMPACT = 2 };
+struct RowLnParams {
+  const void* A; int64_t lda;
+  const void* W; int64_t ldw;
+  const float* bias;
+  float* X;                         // fp32 token rows, ld 768
+  int64_t M, K;
+  int64_t rpg, gstride, goff;       // X row of GEMM row m (map_row)
+  const float* gamma; const float* beta; float eps;
+  unsigned short* Y;                // LayerNorm output rows, ld 768
+  int ymode;
+  int64_t L;                        // tokens per clip (ROWLN_Y_COMPACT: row t == 0 of a clip is CLS)
+};
+hipError_t launch_gemm_rowln(const RowLnParams& p, hipStream_t s);
+
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
                             int64_t goff, float eps, hipStream_t s);

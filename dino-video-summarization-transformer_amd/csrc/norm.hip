@@ -10,7 +10,7 @@ namespace dsvt {
 
 // ---------------------------------------------------------------- LayerNorm
 // One wave per row; VEC: C % 256 == 0 (float4 per lane per 256 cols), else C % 64 == 0.
-template <typename OutT, bool VEC>
+template <typename OutT, bool VEC, bool MAPOUT = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, OutT* __restrict__ y,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int64_t rows,
@@ -19,8 +19,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   if (r >= rows) return;
-  const float* xr = x + map_row(r, rpg, gstride, goff) * C;
-  OutT* yr = y + r * C;
+  const int64_t xrow = map_row(r, rpg, gstride, goff);
+  const float* xr = x + xrow * C;
+  OutT* yr = y + (MAPOUT ? xrow : r) * C;
   float v[16];
   float s = 0.f;
   if constexpr (VEC) {
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // per row).  gamma / beta stay in registers.  Same formula and summation order as
 // layernorm_kernel<., true>; a row's result does not depend on the grid size.
 // Measured (tools/ln_bench.py, fp32 -> bf16): 25104 rows 21.0 -> 18.9 us, 13872 rows 13.6 -> 10.7 us.
-template <typename OutT>
+template <typename OutT, bool MAPOUT = false>
 __global__ __launch_bounds__(256) void layernorm768_kernel(const float* __restrict__ x, OutT* __restrict__ y,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, int64_t rows,
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void layernorm768_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < 12; ++i) { v[i] -= mean; q += v[i] * v[i]; }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
-    OutT* yr = y + r * C;
+    OutT* yr = y + (MAPOUT ? map_row(r, rpg, gstride, goff) : r) * C;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const float4 g4 = gg[i], b4 = bb[i];
@@ -133,26 +134,30 @@ static int ln_grid_cap() {   // workgroups of the C = 768 kernel (0: the one-row
   return cap;
 }
 
-template <typename OutT>
+template <typename OutT, bool MAPOUT>
 static hipError_t ln_t(const float* x, OutT* y, const float* g, const float* b, int64_t rows, int64_t C,
                        int64_t rpg, int64_t gstride, int64_t goff, float eps, hipStream_t s) {
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   const int cap = ln_grid_cap();
   if (C == 768 && cap > 0) {
     if (grid.x > (unsigned)cap) grid.x = (unsigned)cap;
-    layernorm768_kernel<OutT><<<grid, block, 0, s>>>(x, y, g, b, rows, rpg, gstride, goff, eps);
+    layernorm768_kernel<OutT, MAPOUT><<<grid, block, 0, s>>>(x, y, g, b, rows, rpg, gstride, goff, eps);
   } else if (C % 256 == 0)
-    layernorm_kernel<OutT, true><<<grid, block, 0, s>>>(x, y, g, b, rows, (int)C, rpg, gstride, goff, eps);
+    layernorm_kernel<OutT, true, MAPOUT><<<grid, block, 0, s>>>(x, y, g, b, rows, (int)C, rpg, gstride, goff, eps);
   else
-    layernorm_kernel<OutT, false><<<grid, block, 0, s>>>(x, y, g, b, rows, (int)C, rpg, gstride, goff, eps);
+    layernorm_kernel<OutT, false, MAPOUT><<<grid, block, 0, s>>>(x, y, g, b, rows, (int)C, rpg, gstride, goff, eps);
   return hipGetLastError();
 }
 
+// out_f32 bit 0: fp32 output; bit 1: output row = input row (the row map applies to both)
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
                             int64_t goff, float eps, hipStream_t s) {
-  if (dtype == 1 || out_f32) return ln_t<float>(x, (float*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
-  return ln_t<bf16_t>(x, (bf16_t*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
+  const bool f32 = dtype == 1 || (out_f32 & 1), mapout = (out_f32 & 2) != 0;
+  if (f32 && mapout) return ln_t<float, true>(x, (float*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
+  if (f32) return ln_t<float, false>(x, (float*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
+  if (mapout) return ln_t<bf16_t, true>(x, (bf16_t*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
+  return ln_t<bf16_t, false>(x, (bf16_t*)y, g, b, rows, C, rpg, gstride, goff, eps, s);
 }
 
 // ---------------------------------------------------------------- L2 row norms

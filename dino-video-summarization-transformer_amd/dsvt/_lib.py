@@ -12,6 +12,7 @@ BF16, F32 = 0, 1
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID = 0, 1, 2
 EPI_GELU_SAVE, EPI_DGELU = 4, 5
 TOKENS_NT, TOKENS_FRAME = 0, 1
+ROWLN_NONE, ROWLN_X, ROWLN_COMPACT = 0, 1, 2
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
 WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
 WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
@@ -26,6 +27,8 @@ SIGNATURES = {
     "dsvt_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
     "dsvt_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
                              _i64, _i64, _i64, _p]),
+    "dsvt_gemm_resid_ln_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _f32,
+                                      _p, _i32, _i64, _p]),
     "dsvt_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_ln_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _i64, _i64, _p, _p, _f32, _p, _p, _p, _i64,
                                 _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),

@@ -19,8 +19,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .._lib import EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, TOKENS_FRAME, TOKENS_NT, WS_ATTN_SPATIAL, \
-    WS_LN_GEMM, WS_PATCH_EMBED, DsvtError
+from .._lib import EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, ROWLN_COMPACT, ROWLN_NONE, ROWLN_X, TOKENS_FRAME, \
+    TOKENS_NT, WS_ATTN_SPATIAL, WS_LN_GEMM, WS_PATCH_EMBED, DsvtError
 from ..weights import WeightCache
 from .vit_utils import DropPath, to_2tuple, trunc_normal_
 
@@ -107,6 +107,8 @@ class Block(nn.Module):
         w = ctx.w
         C, heads = ctx.C, self.attn.num_heads
         eps1, eps2 = self.norm1.eps, self.norm2.eps
+        if getattr(ctx, "fuse_ln", False) and self.attention_type == "divided_space_time":
+            return self._run_fused(X, ctx, probs)
         if self.attention_type == 'divided_space_time':
             B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
             R = B * Np * T
@@ -141,6 +143,44 @@ class Block(nn.Module):
         ops.ln_gemm(X, None, rows, self.norm2.weight, self.norm2.bias, eps2, w(self.mlp.fc1.weight),
                     self.mlp.fc1.bias, ctx.hid, ctx.ws, epilogue=EPI_BIAS_GELU)
         ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
+
+
+    def _run_fused(self, X, ctx, probs):
+        """Divided block with every residual projection fused with the LayerNorm that follows
+        it (csrc/gemm_rowln.hip): ctx.a enters holding temporal_norm1 of the patch rows
+        (compact) and leaves holding the NEXT block's (ctx.next_ln; none after the last)."""
+        w = ctx.w
+        B, T, Np, L, C = ctx.B, ctx.T, ctx.Np, ctx.L, ctx.C
+        heads = self.attn.num_heads
+        R, rows = B * Np * T, ctx.rows
+        patch_map = (Np * T, L, 1)
+        ta = self.temporal_attn
+        a = ctx.a
+        # temporal: qkv (LN already applied) -> attention -> proj . temporal_fc + residual, norm1
+        ops.gemm(a[:R], w(ta.qkv.weight), ta.qkv.bias, ctx.qkv[:R])
+        ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
+        if ctx.fold_temporal:
+            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
+            src, wt, bt = ctx.o[:R], wf, bf
+        else:
+            ops.gemm(ctx.o[:R], w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
+            src, wt, bt = ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias
+        ops.gemm_resid_ln(src, wt, bt, X, M=R, rowmap=patch_map, ln=self.norm1, Y=a, ymode=ROWLN_X)
+        # norm1 of the CLS rows (untouched by the temporal branch), written to their own rows of a
+        ops.layernorm(X, B, C, self.norm1.weight, self.norm1.bias, self.norm1.eps, a, rowmap=(1, L, 0), out_f32=2)
+        # spatial with CLS replicate / mean, proj + residual, norm2
+        ops.gemm(a, w(self.attn.qkv.weight), self.attn.qkv.bias, ctx.qkv)
+        if probs is not None:
+            ops.attn_spatial_probs(ctx.qkv, ctx.o, probs, B, T, L, heads, self.attn.scale, ctx.cls_ws)
+            return
+        ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
+        ops.gemm_resid_ln(ctx.o, w(self.attn.proj.weight), self.attn.proj.bias, X, M=rows, ln=self.norm2, Y=a,
+                          ymode=ROWLN_X)
+        # MLP: fc1 + GELU, fc2 + residual, the next block's temporal_norm1 (patch rows, compact)
+        ops.gemm(a, w(self.mlp.fc1.weight), self.mlp.fc1.bias, ctx.hid, epilogue=EPI_BIAS_GELU)
+        nxt = ctx.next_ln
+        ops.gemm_resid_ln(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, M=rows, ln=nxt, Y=a,
+                          ymode=ROWLN_COMPACT if nxt is not None else ROWLN_NONE, L=L)
 
 
 class PatchEmbed(nn.Module):
@@ -212,6 +252,12 @@ class VisionTransformer(nn.Module):
         # fold temporal_attn.proj and temporal_fc into one Linear (exact algebra, one GEMM less
         # per block); False runs the two GEMMs of the reference literally
         self.fold_temporal_fc = True
+        # opt-in (bf16, divided, C = 768): every residual projection (temporal_fc, attn.proj,
+        # mlp.fc2) as one full-row kernel that also writes the LayerNorm the next GEMM reads
+        # (csrc/gemm_rowln.hip).  Off by default: measured slower than GEMM + LayerNorm (95 vs 87 us
+        # at K = 768, 210 vs 185 us at K = 3072, 25k rows) -- a full-row workgroup must pull all of
+        # W through LDS-DMA for only ~100 rows, which caps it at ~20-25 GB/s per CU
+        self.fuse_ln = os.environ.get("DSVT_FUSE_LN", "0") == "1"
         # inference: split a batch into this many clip chunks on concurrent HIP streams (each
         # kernel's last partly-filled wave of tiles then runs beside the other chunk's kernels);
         # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
@@ -402,13 +448,22 @@ class VisionTransformer(nn.Module):
         ctx.hid = torch.empty(ctx.rows, self.blocks[0].mlp.fc1.out_features, device=dev, dtype=mode)
         ctx.fold_temporal = self.fold_temporal_fc
         ctx.fold = lambda outer, inner: self._wcache.folded(mode, outer, inner)
+        ctx.fuse_ln = (self.fuse_ln and mode == torch.bfloat16 and C == 768
+                       and self.attention_type == 'divided_space_time')
         if self.attention_type == 'divided_space_time':
             if not ctx.fold_temporal:
                 ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
             nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
             ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+        if ctx.fuse_ln:      # block 0's temporal_norm1 on the patch rows (compact) into ctx.a
+            ctx.a = torch.empty(ctx.rows, C, device=dev, dtype=mode)
+            tn = self.blocks[0].temporal_norm1
+            ops.layernorm(X, B * Np * T, C, tn.weight, tn.bias, tn.eps, ctx.a, rowmap=(Np * T, ctx.L, 1),
+                          out_f32=False)
+        nblk = len(self.blocks)
         if get_attn:            # timesformer.py:325-331: the last block's attention instead of features
-            for blk in self.blocks[:-1]:
+            for i, blk in enumerate(self.blocks[:-1]):
+                ctx.next_ln = self.blocks[i + 1].temporal_norm1 if ctx.fuse_ln else None
                 blk.run(X, ctx)
             if self.attention_type == 'divided_space_time':
                 heads = self.blocks[-1].attn.num_heads
@@ -419,7 +474,8 @@ class VisionTransformer(nn.Module):
             # output tokens (un-normed)
             self.blocks[-1].run(X, ctx)
             return X.view(ctx.nb, ctx.L, C)
-        for blk in self.blocks:
+        for i, blk in enumerate(self.blocks):
+            ctx.next_ln = self.blocks[i + 1].temporal_norm1 if (ctx.fuse_ln and i + 1 < nblk) else None
             blk.run(X, ctx)
         L = ctx.L
         if self.attention_type == 'space_only':      # mean over frames (:338-340)

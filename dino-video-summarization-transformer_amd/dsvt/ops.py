@@ -55,6 +55,25 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     return out
 
 
+def gemm_resid_ln(a, w, bias, X, M=None, rowmap=None, ln=None, Y=None, ymode=_lib.ROWLN_NONE, L=0):
+    """X[row(m)] += a[m] . w^T + bias (fp32 X, N = 768), then (ymode != NONE) Y[yrow] =
+    LayerNorm(X[row(m)]) in bf16 -- one full-row kernel (csrc/gemm_rowln.hip).  ln = the
+    nn.LayerNorm whose weight / bias / eps apply."""
+    _check(a, torch.bfloat16, "A")
+    _check(w, torch.bfloat16, "W")
+    _check(X, torch.float32, "X")
+    M = a.shape[0] if M is None else M
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    if ymode != _lib.ROWLN_NONE:
+        _check(Y, torch.bfloat16, "Y")
+    g = ln.weight if ln is not None else None
+    b = ln.bias if ln is not None else None
+    eps = ln.eps if ln is not None else 0.0
+    call("dsvt_gemm_resid_ln_fwd", _ptr(a), a.shape[-1], _ptr(w), w.shape[1], _ptr(bias), _ptr(X), M, w.shape[0],
+         a.shape[-1], rpg, gs, go, _ptr(g), _ptr(b), float(eps), _ptr(Y), int(ymode), int(L), _stream())
+    return X
+
+
 def ln_gemm(x, in_rowmap, M, ln_w, ln_b, eps, w, bias, out, ws, epilogue=_lib.EPI_BIAS, out_f32=False,
             rowmap=None):
     """LayerNorm(rows of fp32 x through in_rowmap) -> GEMM with epilogue."""
@@ -346,6 +365,8 @@ def gemm_kernel_name(tag):
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
     if variant == 20:
         return "void dsvt::gemm_8ph_kernel<%d, %s, 0>" % (epi, f32)
+    if variant == 30:
+        return "void dsvt::gemm_rowln_kernel<"
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)
 
 

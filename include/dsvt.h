@@ -83,8 +83,26 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t l
                   int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N,
                   int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void *stream);
 
+/* K7 + K3 fused, bf16 only, N = 768 (ViT-B): the residual projections attn.proj / temporal_fc /
+ * mlp.fc2 with their residual add (models/timesformer.py:133-135, 181, 184) and the LayerNorm
+ * that reads the updated rows next (norm1 :105, norm2 :112/184, the next block's
+ * temporal_norm1 :99), in one full-row kernel:
+ *   X[row(m)] += A[m] . W^T + bias        m < M; row(m) = map (rpg, gstride, goff); X fp32, ld 768
+ *   Y[yrow] = LayerNorm(X[row(m)])*gamma + beta   (bf16, ld 768)
+ * ymode DSVT_ROWLN_NONE: no Y;  DSVT_ROWLN_X: yrow = row(m);  DSVT_ROWLN_COMPACT: yrow = the
+ * patch-row index of X row r in clips of L tokens ((r/L)*(L-1) + r%L - 1; CLS rows, r%L == 0,
+ * get none).  A [M, K] bf16 (lda), W [768, K] bf16 (ldw), K % 128 == 0, A and W < 4 GiB. */
+#define DSVT_ROWLN_NONE 0
+#define DSVT_ROWLN_X 1
+#define DSVT_ROWLN_COMPACT 2
+int dsvt_gemm_resid_ln_fwd(const void *A, int64_t lda, const void *W, int64_t ldw, const float *bias,
+                           float *X, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride,
+                           int64_t goff, const float *gamma, const float *beta, float eps, void *Y,
+                           int ymode, int64_t L, void *stream);
+
 /* K3: LayerNorm(eps) over rows of fp32 X read through a row map, written compact
- * (rows x C) in dtype (or fp32 when out_f32).  nn.LayerNorm(eps=1e-6) at
+ * (rows x C) in dtype (or fp32 when out_f32 bit 0); with out_f32 bit 1 the output rows follow
+ * the same row map as the input.  nn.LayerNorm(eps=1e-6) at
  * models/timesformer.py:99,105,112,131,159,184,245,342. */
 int dsvt_layernorm_fwd(int dtype, int out_f32, const float *x, void *y, const float *gamma,
                        const float *beta, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,

@@ -392,7 +392,111 @@ def augment_cases():
     return out
 
 
-GROUPS = {"selection": selection_cases, "augment": augment_cases}
+STEP_CFG = dict(embed_dim=64, num_heads=1, depth=1, img_size=48, num_frames=2)
+STEP_HEAD = dict(hidden_dim=64, bottleneck_dim=32)
+STEP_ARGS = dict(lr=0.0256, min_lr=1e-6, weight_decay=0.04, weight_decay_end=0.4, momentum_teacher=0.996,
+                 clip_grad=3.0, freeze_last_layer=1, epochs=2, warmup_epochs=1, batch_size_per_gpu=2,
+                 out_dim=128, local_crops_number=2, warmup_teacher_temp=0.04, teacher_temp=0.04,
+                 warmup_teacher_temp_epochs=0, use_fp16=False)
+STEP_ITERS = 2                      # iterations per epoch: 2 epochs x 2 = 4 steps
+
+
+def step_crops(it):
+    """the multi-crop batch of iteration `it`: 2 global 2x48^2 + 2 local 2x32^2 crops, B = 2 clips"""
+    return [P.clip(1500 + 10 * it + i, (2, 3, 2, 48, 48)) for i in range(2)] + \
+           [P.clip(1505 + 10 * it + i, (2, 3, 2, 32, 32)) for i in range(2)]
+
+
+def train_step_cases():
+    """Whole SSL training steps (train_ssl.py:466-573): the reference's own `train_one_epoch`,
+    extracted with `ast` and run as written for 2 epochs x 2 iterations on a tiny divided
+    TimeSformer student / teacher (drop_path 0: both nets deterministic) with DINOHead and
+    DINOLoss -- lr / wd / momentum schedules (train_ssl.py:394-407, linear lr scaling),
+    autocast off (fp32), per-parameter clip 3.0, last-layer cancel in epoch 0, AdamW,
+    teacher EMA, center update.  Records the loss, lr, wd, momentum and center of every step
+    and the student / teacher parameters after the last step."""
+    import argparse
+    import math
+
+    import torch.distributed as dist
+    from utils import utils as ref_utils
+    A = argparse.Namespace(**STEP_ARGS)
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    TL = _extract(os.path.join(REF, "train_ssl.py"), ["DINOLoss"])["DINOLoss"]
+    ns = {"torch": torch, "np": np, "math": math, "sys": sys, "utils": ref_utils, "nn": nn}
+    tree = ast.parse(open(os.path.join(REF, "train_ssl.py")).read())
+    fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "train_one_epoch")
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), "train_ssl.py", "exec"), ns)
+    train_one_epoch = ns["train_one_epoch"]
+
+    def net():
+        bb = ref_tsf.VisionTransformer(img_size=48, patch_size=16, num_classes=0, embed_dim=64, depth=1, num_heads=1,
+                                       mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                                       drop_rate=0., attn_drop_rate=0., drop_path_rate=0.0, num_frames=2,
+                                       attention_type="divided_space_time")
+        _load(bb, P.timesformer_state(1401, **STEP_CFG))
+        hd = ref_vit.DINOHead(64, A.out_dim, norm_last_layer=True, **STEP_HEAD)
+        _load(hd, P.dino_head_state(1402, 64, A.out_dim, **STEP_HEAD))
+        return ref_utils.MultiCropWrapper(bb, hd)
+
+    class _DDP(nn.Module):                      # the `.module` the step's EMA loop reads
+        def __init__(self, m):
+            super().__init__()
+            self.module = m
+
+        def forward(self, *a, **k):
+            return self.module(*a, **k)
+
+    student = _DDP(net())
+    teacher = net()
+    teacher.load_state_dict(student.module.state_dict())         # train_ssl.py:330-333
+    for p in teacher.parameters():
+        p.requires_grad = False
+    loss_fn = TL(A.out_dim, A.local_crops_number + 2, A.warmup_teacher_temp, A.teacher_temp,
+                 A.warmup_teacher_temp_epochs, A.epochs, global_crops=2)
+    optimizer = torch.optim.AdamW(ref_utils.get_params_groups(student))          # :377-384
+    world = dist.get_world_size()
+    lr_s = ref_utils.cosine_scheduler(A.lr * (A.batch_size_per_gpu * world) / 256., A.min_lr, A.epochs, STEP_ITERS,
+                                      warmup_epochs=A.warmup_epochs)
+    wd_s = ref_utils.cosine_scheduler(A.weight_decay, A.weight_decay_end, A.epochs, STEP_ITERS)
+    mom_s = ref_utils.cosine_scheduler(A.momentum_teacher, 1, A.epochs, STEP_ITERS)
+    cfg = types.SimpleNamespace(MODEL=types.SimpleNamespace(TWO_STREAM=False, TWO_TOKEN=False))
+    rec = {"loss": [], "center": []}
+    orig_dl = TL.forward
+
+    def fwd(self, s, t, epoch):                 # record every step's loss and updated center
+        out = orig_dl(self, s, t, epoch)
+        rec["loss"].append(float(out.item()))
+        rec["center"].append(self.center.detach().numpy().copy())
+        return out
+    patches = [(torch.Tensor, "cuda", lambda self, *a, **k: self), (torch.cuda, "synchronize", lambda *a: None),
+               (ref_utils, "is_dist_avail_and_initialized", lambda: False), (TL, "forward", fwd)]
+    saved = [(o, n, getattr(o, n)) for o, n, _ in patches]
+    try:
+        for o, n, v in patches:
+            setattr(o, n, v)
+        for epoch in range(A.epochs):
+            loader = [([torch.from_numpy(c) for c in step_crops(epoch * STEP_ITERS + i)], None, None, {})
+                      for i in range(STEP_ITERS)]
+            train_one_epoch(student, teacher, teacher, loss_fn, loader, optimizer, lr_s, wd_s, mom_s, epoch, None,
+                            A, cfg=cfg)
+    finally:
+        for o, n, v in saved:
+            setattr(o, n, v)
+    out = {"loss": np.array(rec["loss"], np.float64), "center": np.stack(rec["center"]).astype(np.float32),
+           "lr": np.asarray(lr_s, np.float64), "wd": np.asarray(wd_s, np.float64),
+           "momentum": np.asarray(mom_s, np.float64)}
+    for k, p in student.module.named_parameters():
+        out["student." + k] = p.detach().numpy().copy()
+    for k, p in teacher.named_parameters():
+        out["teacher." + k] = p.detach().numpy().copy()
+    return out
+
+
+GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases}
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:             # regenerate only the named fixture groups

@@ -342,3 +342,70 @@ def test_adamw_matches_torch():
     torch.cuda.synchronize()
     for a, b in zip(*runs):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-7), (a - b).abs().max().item()
+
+
+def _step_nets():
+    """tests/golden/make_golden.py STEP_CFG / STEP_HEAD: tiny divided TimeSformer (C=64, depth 1,
+    48^2 crops, T=2, drop_path 0) + DINOHead(64 -> 64 -> 64 -> 32 -> 128), fp32 parity mode."""
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+    cfg = dict(embed_dim=64, num_heads=1, depth=1, img_size=48, num_frames=2)
+    nets = []
+    for _ in range(2):
+        bb = VisionTransformer(img_size=48, patch_size=16, num_classes=0, embed_dim=64, depth=1, num_heads=1,
+                               mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                               drop_path_rate=0.0, num_frames=2, attention_type="divided_space_time")
+        bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(1401, **cfg).items()})
+        hd = DINOHead(64, 128, norm_last_layer=True, hidden_dim=64, bottleneck_dim=32)
+        hd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                            P.dino_head_state(1402, 64, 128, hidden_dim=64, bottleneck_dim=32).items()})
+        bb.dsvt_dtype = hd.dsvt_dtype = torch.float32
+        nets.append(MultiCropWrapper(bb, hd).cuda().train())
+    return nets
+
+
+def test_train_steps_match_reference():
+    """a17: four whole SSL steps (train_ssl.py:466-573, 2 epochs x 2 iterations) of
+    dsvt.trainer.DINOTrainer against the reference's own train_one_epoch run on the same
+    weights and crops (tests/golden/train_step.npz): per-step loss and center within 1e-3, and
+    the student / teacher parameters after the last step (per-parameter clip 3.0, last-layer
+    cancel in epoch 0, AdamW with the lr / wd schedules, teacher EMA).
+
+    Parameter bar: AdamW's first steps move each element by about lr * sign(grad), so an
+    element whose gradient lies within fp32 noise of zero may legitimately step the other way.
+    Every tensor must have >= 99.9 % of its elements within 1e-3 of max|ref| and all of them
+    within 2 lr-steps; the parameter-wise relative L2 error must stay below 1e-3."""
+    from dsvt.loss import DINOLoss
+    from dsvt.trainer import DINOTrainer
+    gold = dict(np.load("tests/golden/train_step.npz"))
+    student, teacher = _step_nets()
+    teacher.load_state_dict(student.state_dict())
+    loss_fn = DINOLoss(128, 4, 0.04, 0.04, 0, 2).cuda()
+    tr = DINOTrainer(student, teacher, loss_fn, lr=0.0256, min_lr=1e-6, weight_decay=0.04, weight_decay_end=0.4,
+                     momentum_teacher=0.996, clip_grad=3.0, freeze_last_layer=1, epochs=2, niter_per_ep=2,
+                     warmup_epochs=1, batch_size_per_gpu=2, world_size=1)
+    np.testing.assert_allclose(tr.lr_schedule, gold["lr"], rtol=1e-12)
+    for it in range(4):
+        crops = [torch.from_numpy(P.clip(1500 + 10 * it + i, (2, 3, 2, 48, 48))).cuda() for i in range(2)] + \
+                [torch.from_numpy(P.clip(1505 + 10 * it + i, (2, 3, 2, 32, 32))).cuda() for i in range(2)]
+        loss = tr.step(crops, it)
+        torch.cuda.synchronize()
+        assert abs(loss.item() - gold["loss"][it]) < 1e-3 * abs(gold["loss"][it]), (it, loss.item(), gold["loss"][it])
+        assert rel(loss_fn.center.cpu().numpy(), gold["center"][it]) < 1e-3, it
+    lr_step = float(max(gold["lr"]))
+    report = []
+    for tag, net in (("student", student), ("teacher", teacher)):
+        for k, p in net.named_parameters():
+            ref = gold["%s.%s" % (tag, k)]
+            got = p.detach().cpu().numpy()
+            scale = max(np.max(np.abs(ref)), 1e-12)
+            err = np.abs(got.astype(np.float64) - ref)
+            frac_ok = float(np.mean(err <= 1e-3 * scale))
+            l2 = float(np.linalg.norm(err) / max(np.linalg.norm(ref), 1e-12))
+            report.append((tag + "." + k, frac_ok, float(err.max() / scale), l2))
+            assert frac_ok >= 0.999, report[-1]
+            assert err.max() <= 2 * lr_step + 1e-3 * scale, report[-1]
+            assert l2 < 1e-3, report[-1]
+    worst = max(report, key=lambda r: r[2])
+    print("train steps: worst param %s frac_ok %.5f max rel %.3g l2 %.3g" % worst)

@@ -11,6 +11,9 @@ import torch.nn as nn
 from oracle import dsvt_oracle as O
 from oracle import params as P
 
+from conftest import GOLDEN
+import os
+
 
 def cfg(crop=224, frames=8, attn="divided_space_time", classes=400, pretrained=""):
     return SimpleNamespace(DATA=SimpleNamespace(TRAIN_CROP_SIZE=crop, NUM_FRAMES=frames),
@@ -135,3 +138,19 @@ def test_dino_loss_api_and_schedule():
     assert tuple(l.center.shape) == (1, 65536)
     with pytest.raises(NotImplementedError):
         DINOLoss(10, 4, .04, .04, 0, 1, two_token=True)
+
+
+def test_trainer_schedules_match_reference_run():
+    """DINOTrainer's lr / wd / momentum schedules (train_ssl.py:394-407, linear lr scaling rule)
+    equal the ones the reference's own train_one_epoch run used (tests/golden/train_step.npz)."""
+    import numpy as np
+    import torch
+    from dsvt.trainer import DINOTrainer
+    gold = np.load(os.path.join(GOLDEN, "train_step.npz"))
+    net = torch.nn.Linear(4, 4)
+    tr = DINOTrainer(net, torch.nn.Linear(4, 4), None, lr=0.0256, min_lr=1e-6, weight_decay=0.04,
+                     weight_decay_end=0.4, momentum_teacher=0.996, epochs=2, niter_per_ep=2, warmup_epochs=1,
+                     batch_size_per_gpu=2, world_size=1)
+    np.testing.assert_allclose(tr.lr_schedule, gold["lr"], rtol=1e-12)
+    np.testing.assert_allclose(tr.wd_schedule, gold["wd"], rtol=1e-12)
+    np.testing.assert_allclose(tr.momentum_schedule, gold["momentum"], rtol=1e-12)
