@@ -424,8 +424,195 @@ __global__ __launch_bounds__(256) void attn_temporal_bwd_kernel(const T* __restr
   }
 }
 
+static thread_local int g_attn_bwd_variant = 0;  // 0 = auto, 1 = force the generic VALU kernels (tests / tools)
+
+// 16-lane butterflies of the register temporal kernels: reduce-scatter (after the stage with
+// mask m the lane keeps the half selected by sub & m) and the reverse all-gather of the lane's
+// VPL entries (natural index order)
+template <int NV, int S>
+__device__ __forceinline__ void tb_rs_stage(float (&vals)[NV], int sub) {
+  constexpr int mask = 8 >> S, half = NV >> (S + 1);   // compile-time trip counts: fully unrolled
+  const bool hi = (sub & mask) != 0;
+#pragma unroll
+  for (int k = 0; k < half; ++k) {
+    const float mine = hi ? vals[half + k] : vals[k];
+    const float oth = hi ? vals[k] : vals[half + k];
+    vals[k] = mine + __shfl_xor(oth, mask, 64);
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void tb_reduce_scatter(float (&vals)[NV], int sub) {
+  tb_rs_stage<NV, 0>(vals, sub);
+  tb_rs_stage<NV, 1>(vals, sub);
+  tb_rs_stage<NV, 2>(vals, sub);
+  tb_rs_stage<NV, 3>(vals, sub);
+}
+
+template <int NV, int VPL, int S>
+__device__ __forceinline__ void tb_ag_stage(float (&vals)[NV], int sub) {
+  constexpr int mask = 1 << S, n = VPL << S;
+  const bool hi = (sub & mask) != 0;
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    const float recv = __shfl_xor(vals[k], mask, 64);
+    const float mine = vals[k];
+    vals[k] = hi ? recv : mine;
+    vals[n + k] = hi ? mine : recv;
+  }
+}
+
+template <int NV, int VPL>
+__device__ __forceinline__ void tb_all_gather(float (&vals)[NV], int sub) {
+  tb_ag_stage<NV, VPL, 0>(vals, sub);
+  tb_ag_stage<NV, VPL, 1>(vals, sub);
+  tb_ag_stage<NV, VPL, 2>(vals, sub);
+  tb_ag_stage<NV, VPL, 3>(vals, sub);
+}
+
+// bf16, T <= TP (4 or 8): the register-resident form of the kernel above, laid out like the
+// forward attn_temporal_reg (attention.hip): 16 lanes per (sequence, head), 4 of the 64 dims
+// per lane, q / k / v / dO of the T rows held as packed bf16.  S = Q.K^T and dP = dO.V^T are
+// lane-partial dots reduce-scattered over the 16 lanes (butterfly 8,4,2,1), so lane `sub` owns
+// the VPL = TP*TP/16 entries idx = sub*VPL + k (row i = sub / LPR) of both: softmax, the row
+// sums D_i = sum_j P dP (LPR lanes) and dS = P (dP - D) stay in-lane; the reverse butterfly
+// all-gathers dS (for dq = scale dS.K and dk = scale dS^T.Q) and then P (for dv = P^T.dO).  Rows
+// and keys past T are masked by P = 0.  Reads qkv + dO and writes dqkv once: HBM-bound.
+template <int TP>
+__global__ __launch_bounds__(256) void attn_temporal_bwd_reg(const bf16_t* __restrict__ qkv,
+                                                             const bf16_t* __restrict__ dout,
+                                                             bf16_t* __restrict__ dqkv, int64_t groups, int Tf,
+                                                             int heads, int64_t C, float scale) {
+  constexpr int NV = TP * TP, VPL = NV / 16, LPR = TP / VPL;
+  static_assert(NV >= 16 && NV % 16 == 0, "TP must be 4 or 8");
+  const int64_t grp = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15;
+  if (grp >= groups) return;  // the whole 16-lane group leaves together
+  const int64_t sq = grp / heads;
+  const int h = (int)(grp % heads);
+  const bf16_t* base = qkv + sq * Tf * 3 * C + (int64_t)h * 64 + sub * 4;
+  const bf16_t* dbase = dout + sq * Tf * C + (int64_t)h * 64 + sub * 4;
+  uint2 rq[TP], rk[TP], rv[TP], rd[TP];
+#pragma unroll
+  for (int t = 0; t < TP; ++t) {
+    const int tt = t < Tf ? t : Tf - 1;
+    const bf16_t* r = base + (int64_t)tt * 3 * C;
+    rq[t] = *reinterpret_cast<const uint2*>(r);
+    rk[t] = *reinterpret_cast<const uint2*>(r + C);
+    rv[t] = *reinterpret_cast<const uint2*>(r + 2 * C);
+    rd[t] = *reinterpret_cast<const uint2*>(dbase + (int64_t)tt * C);
+  }
+  // 4-dim partial dot straight from the packed operands (v_dot2c_f32_bf16: no unpacking, so
+  // the 64 partials of S or dP fit beside the four packed row sets)
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  auto dot4 = [](uint2 a, uint2 b) {
+    const float lo = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, a.x), __builtin_bit_cast(bf2_t, b.x),
+                                                     0.f, false);
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, a.y), __builtin_bit_cast(bf2_t, b.y), lo, false);
+  };
+  const int i0 = sub / LPR, j0 = (sub % LPR) * VPL;   // the lane's row and first key
+  // ---- P (recomputed exactly as the forward), lane entries only
+  float vals[NV];
+#pragma unroll
+  for (int i = 0; i < TP; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) vals[i * TP + j] = dot4(rq[i], rk[j]);
+  tb_reduce_scatter<NV>(vals, sub);
+  const float sl2 = scale * 1.4426950408889634f;
+  float p[VPL];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    p[k] = (j0 + k < Tf) ? vals[k] * sl2 : -INFINITY;
+    mx = fmaxf(mx, p[k]);
+  }
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    p[k] = exp2f(p[k] - mx);
+    sum += p[k];
+  }
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) sum += __shfl_xor(sum, m, 64);
+  const float inv = i0 < Tf ? 1.0f / sum : 0.f;      // padded query rows: P = 0 (no dk / dv share)
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) p[k] *= inv;
+  // ---- dP = dO.V^T on the same entries; D_i; dS = P (dP - D)
+#pragma unroll
+  for (int i = 0; i < TP; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) vals[i * TP + j] = dot4(rd[i], rv[j]);
+  tb_reduce_scatter<NV>(vals, sub);
+  float D = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) D += p[k] * vals[k];
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) D += __shfl_xor(D, m, 64);
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) vals[k] = p[k] * (vals[k] - D);
+  tb_all_gather<NV, VPL>(vals, sub);                 // vals = dS (full, row-major)
+  bf16_t* obase = dqkv + sq * Tf * 3 * C + (int64_t)h * 64 + sub * 4;
+  auto store_bf16x4 = [](bf16_t* dst, float a, float b, float c, float d) {
+    uint2 w;
+    w.x = pack_bf16x2(a, b);
+    w.y = pack_bf16x2(c, d);
+    *reinterpret_cast<uint2*>(dst) = w;
+  };
+  // dq_i = scale sum_j dS_ij k_j ; dk_j = scale sum_i dS_ij q_i
+#pragma unroll
+  for (int i = 0; i < TP; ++i) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const float ds = vals[i * TP + j];
+      a0 = fmaf(ds, bf16_lo(rk[j].x), a0); a1 = fmaf(ds, bf16_hi(rk[j].x), a1);
+      a2 = fmaf(ds, bf16_lo(rk[j].y), a2); a3 = fmaf(ds, bf16_hi(rk[j].y), a3);
+    }
+    if (i < Tf) store_bf16x4(obase + (int64_t)i * 3 * C, a0 * scale, a1 * scale, a2 * scale, a3 * scale);
+  }
+#pragma unroll
+  for (int j = 0; j < TP; ++j) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int i = 0; i < TP; ++i) {
+      const float ds = vals[i * TP + j];
+      a0 = fmaf(ds, bf16_lo(rq[i].x), a0); a1 = fmaf(ds, bf16_hi(rq[i].x), a1);
+      a2 = fmaf(ds, bf16_lo(rq[i].y), a2); a3 = fmaf(ds, bf16_hi(rq[i].y), a3);
+    }
+    if (j < Tf) store_bf16x4(obase + (int64_t)j * 3 * C + C, a0 * scale, a1 * scale, a2 * scale, a3 * scale);
+  }
+  // dv_j = sum_i P_ij dO_i
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) vals[k] = p[k];
+  tb_all_gather<NV, VPL>(vals, sub);                 // vals = P (full)
+#pragma unroll
+  for (int j = 0; j < TP; ++j) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int i = 0; i < TP; ++i) {
+      const float pp = vals[i * TP + j];
+      a0 = fmaf(pp, bf16_lo(rd[i].x), a0); a1 = fmaf(pp, bf16_hi(rd[i].x), a1);
+      a2 = fmaf(pp, bf16_lo(rd[i].y), a2); a3 = fmaf(pp, bf16_hi(rd[i].y), a3);
+    }
+    if (j < Tf) store_bf16x4(obase + (int64_t)j * 3 * C + 2 * C, a0, a1, a2, a3);
+  }
+}
+
 hipError_t launch_attn_temporal_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nseq, int64_t T,
                                     int64_t heads, int64_t C, float scale, hipStream_t s) {
+  if (dtype == 0 && T <= 8 && g_attn_bwd_variant == 0) {
+    const int64_t groups = nseq * heads;
+    const unsigned blocks = (unsigned)((groups * 16 + 255) / 256);
+    if (T <= 4)
+      attn_temporal_bwd_reg<4><<<blocks, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, (bf16_t*)dqkv, groups,
+                                                      (int)T, (int)heads, C, scale);
+    else
+      attn_temporal_bwd_reg<8><<<blocks, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, (bf16_t*)dqkv, groups,
+                                                      (int)T, (int)heads, C, scale);
+    return hipGetLastError();
+  }
   const int64_t per_head = (4 * T * 64 + 2 * T * T) * 4;
   int64_t G = (48 * 1024) / per_head;
   if (G < 1) G = 1;
@@ -815,7 +1002,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_short_bf16(AttnBwdParams 
   }
 }
 
-static thread_local int g_attn_bwd_variant = 0;  // 0 = auto, 1 = force the generic VALU kernels (tests / tools)
 void set_attn_bwd_variant(int v) { g_attn_bwd_variant = v; }
 
 hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s) {

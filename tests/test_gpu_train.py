@@ -4,7 +4,8 @@ the DINO loss through libdsvt.so against the reference's own loss.backward()
 plus kernel-level backward checks against torch fp32 autograd of the same op.
 
 Tolerances: fp32 parity mode 1e-3 relative to max|ref| per tensor (the north-star bar);
-bf16 perf mode 6e-2 (bf16 storage of activations and of dY in the weight-gradient GEMMs)."""
+bf16 perf mode 4e-2 (bf16 storage of activations and of dY in the weight-gradient GEMMs;
+observed <= 2.1e-2)."""
 from functools import partial
 
 import numpy as np
@@ -16,7 +17,7 @@ import torch.nn.functional as F
 from oracle import params as P
 
 pytestmark = pytest.mark.gpu
-TOL = {torch.float32: 1e-3, torch.bfloat16: 6e-2}
+TOL = {torch.float32: 1e-3, torch.bfloat16: 4e-2}   # bf16: observed <= 2.1e-2 (r02)
 CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
 
 
