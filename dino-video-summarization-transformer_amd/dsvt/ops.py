@@ -314,6 +314,23 @@ def rowscale_bias_add(X, row_scale_, bias):
     return X
 
 
+def wgrad(dy, x, out, accumulate=False):
+    """out[n, k] (+)= sum_m dy[m, n] x[m, k]: the weight gradient dY^T . X of an nn.Linear
+    (bf16 operands, fp32 out; csrc/wgrad.hip, deterministic M-slice reduction)."""
+    _check(dy, torch.bfloat16, "dY")
+    _check(x, torch.bfloat16, "X")
+    _check(out, torch.float32, "G")
+    M, N, K = dy.shape[0], dy.shape[1], x.shape[1]
+    if x.shape[0] != M or tuple(out.shape) != (N, K):
+        raise _lib.DsvtError("wgrad: dY %s, X %s, G %s do not match" % (tuple(dy.shape), tuple(x.shape),
+                                                                       tuple(out.shape)))
+    nbytes = workspace_bytes(_lib.WS_WGRAD, torch.bfloat16, M, N, K)
+    ws = torch.empty(max(nbytes, 4) // 4, device=dy.device, dtype=torch.float32)
+    call("dsvt_wgrad_bwd", _lib.BF16, _ptr(dy), N, _ptr(x), K, _ptr(out), M, N, K, int(accumulate), _ptr(ws),
+         ws.numel() * 4, _stream())
+    return out
+
+
 def cast_transpose(x, out):
     _check(x, torch.float32, "x")
     call("dsvt_cast_transpose", _dt(out.dtype), _ptr(x), _ptr(out), x.shape[0], x.shape[1], _stream())
@@ -367,6 +384,8 @@ def gemm_kernel_name(tag):
         return "void dsvt::gemm_8ph_kernel<%d, %s, 0>" % (epi, f32)
     if variant == 30:
         return "void dsvt::gemm_rowln_kernel<"
+    if variant == 31:
+        return "dsvt::wgrad_kernel("
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)
 
 

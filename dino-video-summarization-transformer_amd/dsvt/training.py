@@ -7,8 +7,8 @@ kernels:
                training forward that keeps the activations each backward GEMM needs, and the
                block-by-block backward -- LayerNorm / attention / GELU / embedding gradients
                in HIP (backward.hip), input-gradient GEMMs on the dsvt MFMA GEMM (cached W^T,
-               fused GELU' epilogue), weight-gradient GEMMs dW = dY^T.X on hipBLASLt (plain
-               library GEMMs via torch.mm), fp32 gradient accumulation.
+               fused GELU' epilogue), weight-gradient GEMMs dW = dY^T.X on the dsvt wgrad
+               kernel (wgrad.hip; the fp32 parity mode uses a library GEMM), fp32 gradients.
   HeadFn       DINOHead (vision_transformer.py:278-282): GELU MLP, F.normalize, weight-norm.
   LossFn       DINOLoss.forward (train_ssl.py:633-671); the teacher branch is detached.
 
@@ -30,11 +30,15 @@ from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SP
 
 
 def wgrad(dy, x, G, p, view=None):
-    """grad(p) (+)= dy^T [N, M] . x [M, K]: a plain library GEMM (hipBLASLt); the first write
-    of a gradient buffer is a copy (no zero fill)."""
+    """grad(p) (+)= dy^T [N, M] . x [M, K]: the dsvt weight-gradient kernel in bf16 (fp32
+    result written / accumulated in place); the fp32 parity mode takes a plain library GEMM.
+    The first write of a gradient buffer is a copy (no zero fill)."""
     buf, acc = G.acc(p)
     if view is not None:
         buf = buf.view(view)
+    if dy.dtype == torch.bfloat16:
+        ops.wgrad(dy, x, buf, accumulate=acc)
+        return
     r = torch.mm(dy.t(), x)
     if acc:
         buf.add_(r)
@@ -365,10 +369,25 @@ def _head_backward(head, st, dlogits):
     ll = head.last_layer
     dl = torch.empty(R, dlogits.shape[1], device=dev, dtype=mode)
     ops.cast(dlogits, dl)
-    dW = torch.mm(dl.t(), st.z).float()                       # d(effective weight) [out, bottleneck]
+    if mode == torch.bfloat16:
+        dW = torch.empty(ll.out_features, ll.in_features, device=dev, dtype=torch.float32)
+        ops.wgrad(dl, st.z, dW)                               # d(effective weight) [out, bottleneck]
+    else:
+        dW = torch.mm(dl.t(), st.z)
     ops.weight_norm_bwd(ll.weight_v.detach(), ll.weight_g.detach(), dW, G.acc(ll.weight_v)[0],
                         G.acc(ll.weight_g)[0].view(-1) if ll.weight_g.requires_grad else None, accumulate=False)
-    dz = torch.mm(dl, st.wn).float()                          # [R, bottleneck]
+    if mode == torch.bfloat16:
+        # dz [R, bottleneck] = dl . wn, a sum over the out_dim outputs o: the weight-gradient
+        # kernel with m = o, G[r, b] = sum_o dl^T[o, r] wn[o, b] (rows padded to a multiple of 8)
+        R8 = (R + 7) // 8 * 8
+        src = dlogits if R8 == R else torch.cat([dlogits, dlogits.new_zeros(R8 - R, dlogits.shape[1])])
+        dlT = torch.empty(dlogits.shape[1], R8, device=dev, dtype=mode)
+        ops.cast_transpose(src, dlT)
+        dz = torch.empty(R8, ll.in_features, device=dev, dtype=torch.float32)
+        ops.wgrad(dlT, st.wn, dz)
+        dz = dz[:R]
+    else:
+        dz = torch.mm(dl, st.wn)                              # [R, bottleneck]
     dy = ops.head_norm_bwd(st.y, dz.contiguous())
     lins = _head_linears(head)
     g = dy                                                    # gradient w.r.t. the current linear's output

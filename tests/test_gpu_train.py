@@ -410,3 +410,27 @@ def test_train_steps_match_reference():
             assert l2 < 1e-3, report[-1]
     worst = max(report, key=lambda r: r[2])
     print("train steps: worst param %s frac_ok %.5f max rel %.3g l2 %.3g" % worst)
+
+
+@pytest.mark.parametrize("M,N,K", [(25104, 2304, 768), (13872, 768, 3072), (300, 192, 64), (8, 512, 64),
+                                   (77, 136, 40), (4096, 65536, 256)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_vs_fp64(M, N, K, accumulate):
+    """csrc/wgrad.hip: G (+)= dY^T . X (bf16 operands, fp32 out) against float64 from the same
+    bf16 values -- the bench's qkv / fc2 shapes, ragged small shapes (tile edges, rows past M)
+    and the head's 65536-row product; two launches are bitwise identical (fixed-order slices)."""
+    from dsvt import ops
+    gen = torch.Generator(device="cuda").manual_seed(31)
+    dy = torch.randn(M, N, device="cuda", generator=gen).to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", generator=gen).to(torch.bfloat16)
+    g0 = torch.randn(N, K, device="cuda", generator=gen)
+    outs = []
+    for _ in range(2):
+        g = g0.clone()
+        ops.wgrad(dy, x, g, accumulate=accumulate)
+        outs.append(g)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = dy.double().t() @ x.double() + (g0.double() if accumulate else 0)
+    err = ((outs[0].double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-5, err
