@@ -64,34 +64,73 @@ def clip_flops(n_global=2, n_local=6, folded=False):
 
 
 # ----------------------------------------------------------------- CPU baseline (oracle)
-def cpu_baseline(budget_s=10.0, max_clips=4):
-    """The oracle's numpy fp32 restatement (the checker, never the product) timed on the
-    host cores on a bounded sample: whole multi-crop clips, fwd + heads + loss."""
-    from oracle import dsvt_oracle as O
-    from oracle import params as P
+def host_cpu():
+    """(model name, usable cores): the CPU model from /proc/cpuinfo (lscpu's "Model name"), and
+    the cores this process may use -- its affinity mask, capped by the cgroup CPU quota."""
+    model = "unknown"
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    sd_s, sd_t = P.timesformer_state(11), P.timesformer_state(12)
-    hsd = P.dino_head_state(13, 768, 65536)
-    center = np.zeros((1, 65536), np.float32)
-    done, t_all = 0, 0.0
-    while done < max_clips and (t_all < budget_s or done == 0):
-        gl = [P.clip(100 + 8 * done + i, (1, 3, 8, 224, 224)) for i in range(2)]
-        lo = [P.clip(102 + 8 * done + i, (1, 3, 8, 96, 96)) for i in range(6)]
-        t0 = time.perf_counter()
-        fs = np.concatenate([O.forward_features(sd_s, np.concatenate(gl), 12),
-                             O.forward_features(sd_s, np.concatenate(lo), 12)])
-        s_out = O.dino_head(hsd, fs)
-        t_out = O.dino_head(hsd, O.forward_features(sd_t, np.concatenate(gl), 12))
-        _, center = O.dino_loss(s_out, t_out, center, 8, 0.04)
-        t_all += time.perf_counter() - t0
-        done += 1
-    return {"value": round(done / t_all, 4), "unit": "clips/s", "cores": int(cores), "kind": "port",
-            "sample": "%d clip(s) x (teacher 2x8x224^2 + student 2x8x224^2 + 6x8x96^2 + DINOHead(65536) + "
-                      "DINOLoss), numpy fp32 oracle, %.1f s" % (done, t_all)}
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:  # pragma: no cover
+        pass
+    cores = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            cores = max(1, min(cores, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return model, cores
+
+
+def cpu_baseline(batches=(1, 4), reps=5):
+    """The reference's own execution model on the host: eager torch fp32 on CPU, restated op
+    for op in oracle/torch_cpu.py (the checker, pinned to the reference's golden vectors; never
+    the product).  One DINO fwd+loss step of `b` multi-crop clips as the reference runs it
+    (train_ssl.py:523-530: student on the 2b global + 6b local crops, one call per resolution
+    group; teacher on the 2b global crops; DINOHead(65536) on every row; DINOLoss ncrops 8),
+    1 warm-up + median of `reps`, torch.set_num_threads(usable cores)."""
+    from oracle import params as P
+    from oracle import torch_cpu as TC
+    model, cores = host_cpu()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        student, teacher = TC.TimeSformerCPU(P.timesformer_state(11), 12), TC.TimeSformerCPU(P.timesformer_state(12), 12)
+        head_s = TC.DINOHeadCPU(P.dino_head_state(13, 768, 65536))
+        head_t = TC.DINOHeadCPU(P.dino_head_state(14, 768, 65536))
+        per_batch = {}
+        for b in batches:
+            gl = torch.from_numpy(P.clip(100 + b, (2 * b, 3, 8, 224, 224)))
+            lo = torch.from_numpy(P.clip(200 + b, (6 * b, 3, 8, 96, 96)))
+            center = torch.zeros(1, 65536)
+
+            def step():
+                s_out = head_s(torch.cat([student.forward_features(gl), student.forward_features(lo)]))
+                t_out = head_t(teacher.forward_features(gl))
+                return TC.dino_loss(s_out, t_out, center, 8, 0.04)
+            step()
+            times = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                step()
+                times.append(time.perf_counter() - t0)
+            per_batch[b] = (float(np.median(times)), times)
+    finally:
+        torch.set_num_threads(prev)
+    best = max(per_batch, key=lambda b: b / per_batch[b][0])
+    return {"value": round(best / per_batch[best][0], 4), "unit": "clips/s", "cores": int(cores), "kind": "port",
+            "cpu_model": model,
+            "per_batch": {str(b): {"clips_per_s": round(b / t, 4), "median_s": round(t, 3),
+                                   "runs_s": [round(x, 3) for x in ts]} for b, (t, ts) in per_batch.items()},
+            "sample": "DINO fwd+loss steps of %s multi-crop clip(s) (teacher 2x8x224^2 + student 2x8x224^2 + "
+                      "6x8x96^2, DINOHead(65536), DINOLoss ncrops 8), torch %s CPU fp32 eager (oracle/torch_cpu.py), "
+                      "%d threads, 1 warm-up + median of %d; value = the faster batch"
+                      % ("/".join(map(str, batches)), torch.__version__, cores, reps)}
 
 
 def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "pmc_traffic.json")):

@@ -43,18 +43,33 @@ def view_windows(F, local_size, global_size):
 
 
 def view_index(F, local_size, global_size):
-    """(local_idx [F, local_size], global_idx [F, G]) int32 frame indices of the views the
-    model consumes (dino_similarity.py:78-79: local = padded view[:, :, :local_size])."""
-    if local_size % 2 == 0 or global_size % 2 == 1:
-        # the reference's views only stack for odd local / even global sizes
-        raise ValueError("local_clip_size must be odd and global_clip_size even (reference window rule)")
-    if F < local_size:
-        raise ValueError("video has %d frames < local_clip_size %d" % (F, local_size))
+    """(local_idx [F, Ts], global_idx [F, G]) int32 frame indices of the views the model
+    consumes (dino_similarity.py:78-79: local = padded view[:, :, :local_size]).
+
+    Same window arithmetic as dino_loss_loader.py:126-171, including its clamped edge cases:
+    windows are Python slices (a negative start counts from the end), the local frames fill
+    the first Ts = min(local_size, G) slots of the G-slot padded view with torch broadcasting
+    (equal length, or one frame repeated -- e.g. F = 2, local 3: both local views are frame 1
+    twice), G = min(global_size, F).  Raises ValueError exactly where the reference's view
+    construction raises (assignment or stack shape mismatch: even local / odd global sizes in
+    the middle of a video, some F < local_size)."""
+    if F < 1:
+        raise ValueError("empty video")
     w = view_windows(F, local_size, global_size)
     G = w[0][4]
-    li = np.stack([np.arange(j, k) for (j, k, _, _, _) in w]).astype(np.int32)
-    gi = np.stack([np.arange(l, m) for (_, _, l, m, _) in w]).astype(np.int32)
-    assert li.shape == (F, local_size) and gi.shape == (F, G)
+    ts = min(local_size, G)
+    ids = list(range(F))
+    li = np.empty((F, ts), np.int32)
+    gi = np.empty((F, G), np.int32)
+    for i, (j, k, l, m, _) in enumerate(w):
+        loc, glo = ids[j:k], ids[l:m]
+        if len(loc) == 1:
+            loc = loc * ts
+        if len(loc) != ts or len(glo) != G:
+            raise ValueError("the reference cannot build the views of a %d-frame video with local_clip_size %d "
+                             "and global_clip_size %d (window %d has %d local / %d global frames)"
+                             % (F, local_size, global_size, i, len(loc), len(glo)))
+        li[i], gi[i] = loc, glo
     return li, gi
 
 
@@ -73,21 +88,47 @@ def get_views_of_video_same_size(frames, local_size, global_size):
     return torch.stack(views)
 
 
+DUMMY_FRAMES = 60   # dino_loss_loader.py:37-38: zeros(3, 60, crop, crop), 2 * global_clip_size of them
+
+
 class FrameScorer:
-    """Per-frame DINO-loss scores of a video with a (pretrained) dsvt TimeSformer."""
+    """Per-frame DINO-loss scores of a video with a (pretrained) dsvt TimeSformer.
+
+    crop_size: the loader's center-crop size (dino_loss_loader.py:33, 92; 224 for the ViT-B
+    checkpoints, default = the model's img_size).  A video whose frames are not crop_size^2
+    takes the reference's dummy path (size_match, :103-107 and :115-123): its views are
+    2 * global_clip_size all-zero clips of 60 frames, so the scoring loop yields
+    global_clip_size identical scores -- DINO loss(model(zeros, local_clip_size frames),
+    model(zeros, 60 frames)) -- whatever the video's length."""
 
     def __init__(self, model, local_clip_size=3, global_clip_size=30, teacher_temp=0.02, student_temp=0.3,
-                 frames_per_call=16):
+                 frames_per_call=16, crop_size=None):
         self.model = model
         self.local_clip_size = local_clip_size
         self.global_clip_size = global_clip_size
         self.loss = PairwiseDINOLoss(model.embed_dim, teacher_temp, student_temp).to(model.pos_embed.device)
         self.frames_per_call = frames_per_call
+        self.crop_size = crop_size if crop_size is not None else model.patch_embed.img_size[0]
+
+    @torch.no_grad()
+    def dummy_scores(self, device):
+        """The constant scores of a size-mismatched video (dino_similarity.py:73-90 over the
+        dummy views): one score of the zero local / zero 60-frame global pair, repeated."""
+        c = self.crop_size
+        bank = torch.zeros(1, 3, c, c, device=device)
+        ts = min(self.local_clip_size, DUMMY_FRAMES)
+        st = self.model.forward_frame_bank(bank, torch.zeros(ts, dtype=torch.int32, device=device), 1, ts)
+        te = self.model.forward_frame_bank(bank, torch.zeros(DUMMY_FRAMES, dtype=torch.int32, device=device), 1,
+                                           DUMMY_FRAMES)
+        return self.loss.per_row(st, te).expand(self.global_clip_size).contiguous()
 
     @torch.no_grad()
     def score(self, frames):
-        """frames [F, 3, H, W] fp32 on the GPU -> scores [F] fp32 (device)."""
+        """frames [F, 3, H, W] fp32 on the GPU -> scores fp32 (device): [F], or
+        [global_clip_size] constant scores when H, W != crop_size (the dummy path)."""
         F = frames.shape[0]
+        if tuple(frames.shape[-2:]) != (self.crop_size, self.crop_size):
+            return self.dummy_scores(frames.device)
         li, gi = view_index(F, self.local_clip_size, self.global_clip_size)
         dev = frames.device
         li_t = torch.from_numpy(li).to(dev)

@@ -316,13 +316,26 @@ def view_windows(F, local_size, global_size):
 
 def view_index_map(F, local_size, global_size):
     """1-based frame index per (view, slot), 0 = zero padding; views interleaved
-    (local_0, global_0, local_1, ...) exactly like dino_loss_loader.py:164-171."""
+    (local_0, global_0, local_1, ...) exactly like dino_loss_loader.py:164-171.
+    The windows are Python slices (a negative start counts from the end, :159-160), the
+    local slice is assigned into the first min(local_size, G) slots of a G-slot zero tensor
+    with torch broadcasting (:163-164: equal length, or a single frame repeated), and the
+    views must stack (:171).  Returns None where the reference raises."""
     w = view_windows(F, local_size, global_size)
+    if F < 1:
+        return None
     G = w[0][4]
+    ids = list(range(1, F + 1))
+    nslot = min(local_size, G)
     out = np.zeros((2 * F, G), np.int32)
     for i, (j, k, l, m, _) in enumerate(w):
-        out[2 * i, :k - j] = np.arange(j, k) + 1
-        out[2 * i + 1, :m - l] = np.arange(l, m) + 1
+        loc, glo = ids[j:k], ids[l:m]
+        if len(loc) == 1:
+            loc = loc * nslot
+        if len(loc) != nslot or len(glo) != G:
+            return None
+        out[2 * i, :nslot] = loc
+        out[2 * i + 1] = glo
     return out
 
 

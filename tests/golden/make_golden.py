@@ -496,7 +496,51 @@ def train_step_cases():
     return out
 
 
-GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases}
+def views_edge_cases():
+    """get_views_of_video_same_size (dino_loss_loader.py:126-171) where the windows clamp past
+    the video: F < local_clip_size (negative slice starts, broadcast assignment), F < global,
+    and the shapes the reference cannot stack (recorded as err = 1); size_match (:115-123) on
+    224^2 and non-224 views; the dummy views a mismatched video yields (:36-38, :103-107)."""
+    import tempfile
+    from types import SimpleNamespace
+    path = os.path.join(REF, "datasets_custom", "dino_loss_loader.py")
+    ns = _extract(path, ["get_views_of_video_same_size", "size_match"])
+    gv, sm = ns["get_views_of_video_same_size"], ns["size_match"]
+    out = {}
+    for F_, loc, glob in [(1, 3, 30), (2, 3, 30), (1, 5, 10), (2, 5, 10), (3, 5, 10), (4, 5, 10), (5, 5, 10),
+                          (3, 7, 10), (4, 7, 10), (6, 7, 10), (7, 3, 4), (9, 3, 4), (12, 4, 10), (12, 3, 9)]:
+        frames = torch.arange(1, F_ + 1, dtype=torch.float32).view(F_, 1, 1, 1).expand(F_, 3, 2, 2).contiguous()
+        key = "F%d_%d_%d" % (F_, loc, glob)
+        try:
+            views = gv(frames, loc, glob)
+            out[key] = views[:, 0, :, 0, 0].numpy().astype(np.int32)
+        except RuntimeError:
+            out[key] = np.zeros((0, 0), np.int32)            # the reference raises for this shape
+    fr = torch.zeros(5, 3, 224, 224)
+    out["size_match"] = np.array([sm(gv(fr, 3, 4)), sm(gv(torch.zeros(5, 3, 200, 224), 3, 4)),
+                                  sm(gv(torch.zeros(5, 3, 224, 160), 3, 4))], np.int32)
+    # DinoLossLoader.__init__ (:16-77) with a one-line csv, for its dummy return tensor
+    src = ast.parse(open(path).read())
+    cls = next(n for n in src.body if isinstance(n, ast.ClassDef) and n.name == "DinoLossLoader")
+    cns = {"torch": torch, "os": os}
+    exec(compile(ast.Module(body=[cls], type_ignores=[]), path, "exec"), cns)
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "test.csv"), "w") as f:
+            f.write("v.mp4 0\n")
+        cfg = SimpleNamespace(TEST=SimpleNamespace(NUM_ENSEMBLE_VIEWS=1),
+                              DATA=SimpleNamespace(PATH_TO_DATA_DIR=d, PATH_LABEL_SEPARATOR=" ", PATH_PREFIX=""))
+        ds = cns["DinoLossLoader"](cfg, "test", 3, 30, 4)
+        dummy = torch.stack(ds.dummy_list)
+    out["dummy_shape"] = np.array(dummy.shape, np.int64)
+    out["dummy_absmax"] = np.float32(dummy.abs().max())
+    # what the scoring loop (dino_similarity.py:73-90) feeds the model from those views
+    out["dummy_local_shape"] = np.array(dummy[::2][:, :, :3].shape, np.int64)
+    out["dummy_global_shape"] = np.array(dummy[1::2].shape, np.int64)
+    return out
+
+
+GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases,
+          "views_edge": views_edge_cases}
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:             # regenerate only the named fixture groups

@@ -193,6 +193,49 @@ def test_e2e_cfg1_multicrop_head_loss(tiny_sd, dtype, tol):
     assert rel(loss_fn.center.cpu(), f["center"]) < tol
 
 
+def test_config2_chain_loss_bf16_vs_fp32(base_sd):
+    """Config-2-shaped chain (the bench's workload, 2 clips): ViT-B/16 student on 2 global
+    8x224^2 + 6 local 8x96^2 crops and teacher on the globals -> DINOHead(768 -> 65536) ->
+    DINOLoss(ncrops 8).  The fp32 parity path's loss is within 1e-3 of the torch-CPU oracle,
+    and the bf16 perf path's loss within 1e-3 (relative) of the fp32 one -- the north-star's
+    loss bar, asserted on the benchmarked mode."""
+    from oracle import torch_cpu as TC
+    from dsvt.loss import DINOLoss
+    from dsvt.utils import MultiCropWrapper, dino_forward
+    from dsvt.vision_transformer import DINOHead
+    t_sd = P.timesformer_state(12)
+    hs, ht = P.dino_head_state(7, 768, 65536), P.dino_head_state(8, 768, 65536)
+    glob = [P.clip(1201 + i, (2, 3, 8, 224, 224)) for i in range(2)]
+    loc = [P.clip(1203 + i, (2, 3, 8, 96, 96)) for i in range(6)]
+
+    def net(sd, hsd, dtype):
+        hd = DINOHead(768, 65536)
+        hd.load_state_dict({k: torch.from_numpy(v) for k, v in hsd.items()})
+        hd = hd.cuda()
+        hd.dsvt_dtype = dtype
+        return MultiCropWrapper(tsf(sd, dtype), hd)
+    losses = {}
+    for dtype in (torch.float32, torch.bfloat16):
+        student, teacher = net(base_sd, hs, dtype), net(t_sd, ht, dtype)
+        lf = DINOLoss(65536, 8, 0.04, 0.04, 0, 100).cuda()
+        with torch.no_grad():
+            s_out, t_out = dino_forward(student, teacher, [cu(x) for x in glob + loc])
+            losses[dtype] = lf(s_out, t_out, 0).item()
+        del student, teacher
+    # torch-CPU oracle: reference module order, one backbone call per resolution group
+    cs, ct = TC.TimeSformerCPU(base_sd, 12), TC.TimeSformerCPU(t_sd, 12)
+    g_in = torch.from_numpy(np.concatenate(glob))
+    l_in = torch.from_numpy(np.concatenate(loc))
+    s_ref = TC.DINOHeadCPU(hs)(torch.cat([cs.forward_features(g_in), cs.forward_features(l_in)]))
+    t_ref = TC.DINOHeadCPU(ht)(ct.forward_features(g_in))
+    ref, _ = TC.dino_loss(s_ref, t_ref, torch.zeros(1, 65536), 8, 0.04)
+    ref = float(ref)
+    print("config-2 chain loss: oracle %.6f fp32 %.6f bf16 %.6f" % (ref, losses[torch.float32],
+                                                                    losses[torch.bfloat16]))
+    assert abs(losses[torch.float32] - ref) / abs(ref) < 1e-3
+    assert abs(losses[torch.bfloat16] - losses[torch.float32]) / abs(losses[torch.float32]) < 1e-3
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_concurrent_streams_bitwise_equal_serial(tiny_sd, dtype):
     """MultiCropWrapper's concurrent resolution groups and dino_forward's concurrent teacher /
@@ -240,6 +283,72 @@ def test_frame_scores_vs_oracle(dtype, tol):
         ref.append(O.pair_loss(s, t, np.zeros((1, 192)))[0])
     ref = np.array(ref)
     assert np.max(np.abs(scores - ref)) / np.max(np.abs(ref)) < tol, (scores, ref)
+
+
+def _ref_scores(fwd, frames, F_, local, glob):
+    """Scores the reference's loop (dino_similarity.py:73-90) computes on the views its loader
+    builds (oracle view_index_map), with `fwd` the oracle forward; windows deduplicated."""
+    idx = O.view_index_map(F_, local, glob)
+    cache = {}
+
+    def feat(ids):
+        key = tuple(ids)
+        if key not in cache:
+            cache[key] = np.asarray(fwd(frames[np.asarray(ids) - 1].transpose(1, 0, 2, 3)[None]))
+        return cache[key]
+    out = []
+    for i in range(F_):
+        s = feat(idx[2 * i, :local])
+        t = feat(idx[2 * i + 1])
+        out.append(O.pair_loss(s, t, np.zeros((1, s.shape[-1])))[0])
+    return np.array(out)
+
+
+@pytest.mark.parametrize("F_", [1, 2, 4])
+def test_frame_scores_short_video(F_):
+    """Videos shorter than the local clip (F < 3) or the global clip: the reference's clamped
+    windows (negative slice start, one frame broadcast over the local slots, T = F)."""
+    from dsvt.scoring import FrameScorer
+    sd = P.timesformer_state(31, embed_dim=192, depth=2, num_heads=3, img_size=32, num_frames=4)
+    m = tsf(sd, torch.float32, embed_dim=192, depth=2, num_heads=3, img_size=32, num_frames=4)
+    frames = P.clip(33 + F_, (F_, 3, 32, 32))
+    scores = FrameScorer(m, 3, 10, frames_per_call=4).score(cu(frames)).cpu().numpy()
+    ref = _ref_scores(lambda x: O.forward_features(sd, x, 3), frames, F_, 3, 10)
+    assert scores.shape == (F_,)
+    assert rel(scores, ref) < FP32_TOL, (scores, ref)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
+def test_frame_scores_dummy_video(dtype, tol):
+    """A video whose crop is not crop_size^2 takes the dummy path (dino_loss_loader.py:103-107):
+    global_clip_size constant scores of the zero 3-frame / zero 60-frame pair."""
+    from dsvt.scoring import FrameScorer
+    sd = P.timesformer_state(31, embed_dim=192, depth=2, num_heads=3, img_size=32, num_frames=4)
+    m = tsf(sd, dtype, embed_dim=192, depth=2, num_heads=3, img_size=32, num_frames=4)
+    frames = P.clip(40, (14, 3, 48, 32))           # 48 x 32: size_match fails
+    scores = FrameScorer(m, 3, 10, frames_per_call=4).score(cu(frames)).cpu().numpy()
+    s = O.forward_features(sd, np.zeros((1, 3, 3, 32, 32), np.float32), 3)
+    t = O.forward_features(sd, np.zeros((1, 3, 60, 32, 32), np.float32), 3)
+    ref = O.pair_loss(s, t, np.zeros((1, 192)))[0]
+    assert scores.shape == (10,) and np.all(scores == scores[0])
+    assert abs(scores[0] - ref) / abs(ref) < tol, (scores[0], ref)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
+def test_frame_scores_vitb_local3_global30(base_sd, dtype, tol):
+    """The reference's scoring configuration (dino_similarity.py:186-188: ViT-B/16 224^2, local
+    3 / global 30) on a 31-frame video: every local window and both distinct 30-frame global
+    windows, against the torch-CPU oracle (pinned to the reference's goldens)."""
+    from oracle import torch_cpu as TC
+    from dsvt.scoring import FrameScorer
+    m = tsf(base_sd, dtype)
+    F_ = 31
+    frames = P.clip(44, (F_, 3, 224, 224))
+    scores = FrameScorer(m, 3, 30, frames_per_call=8).score(cu(frames)).cpu().numpy()
+    ref_model = TC.TimeSformerCPU(base_sd, 12)
+    ref = _ref_scores(lambda x: ref_model.forward_features(x).numpy(), frames, F_, 3, 30)
+    assert scores.shape == (F_,)
+    assert rel(scores, ref) < tol, (np.max(np.abs(scores - ref)), scores, ref)
 
 
 def test_bf16_vs_fp32_full_size(base_sd):

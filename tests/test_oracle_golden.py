@@ -102,6 +102,21 @@ def test_views():
         np.testing.assert_array_equal(O.view_index_map(F_, loc, glob), f[key])
 
 
+def test_views_edge():
+    """Clamped windows past the video (F < local size, F < global size) and the shapes the
+    reference cannot build (stored empty)."""
+    f = g("views_edge")
+    for key in f.files:
+        if not key.startswith("F"):
+            continue
+        F_, loc, glob = map(int, key[1:].split("_"))
+        got = O.view_index_map(F_, loc, glob)
+        if f[key].size == 0:
+            assert got is None, key
+        else:
+            np.testing.assert_array_equal(got, f[key], err_msg=key)
+
+
 def test_e2e_cfg1(tiny_sd):
     f = g("e2e_cfg1")
     hsd = P.dino_head_state(6, 192, 4096)

@@ -1,10 +1,15 @@
 """Summarize a rocprofv3 kernel trace (SQLite results.db or kernel_stats/kernel_trace CSV)
-into a per-kernel table: calls, total ms, avg us, share."""
+into a per-kernel table: calls, total ms, avg us, share.
+
+The per-step figure is DERIVED, never hand-entered: `--step-kernel NAME` names a kernel
+launched a known number of times per step (`--per-step`, default 1), and steps = its calls /
+per-step count.  E.g. the train step launches `ema_kernel` once (teacher EMA) and the
+forward+loss step `loss_reduce_kernel` once per DINO loss."""
+import argparse
 import csv
 import glob
 import os
 import sqlite3
-import sys
 
 
 def rows_from(path):
@@ -18,7 +23,7 @@ def rows_from(path):
     return out
 
 
-def main(path, steps=None):
+def main(path, step_kernel=None, per_step=1):
     if os.path.isdir(path):
         cands = glob.glob(os.path.join(path, "**", "*.db"), recursive=True) + \
             glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
@@ -33,9 +38,22 @@ def main(path, steps=None):
     print("%-100s %7s %11s %10s %6s" % ("kernel", "calls", "total_ms", "avg_us", "share"))
     for n, (c, d) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         print("%-100s %7d %11.3f %10.2f %5.1f%%" % (n[:100], c, d / 1e6, d / c / 1e3, 100.0 * d / tot))
-    print("total kernel time: %.3f ms%s" % (tot / 1e6, "" if not steps else "  (%.3f ms per step over %d steps)"
-                                             % (tot / 1e6 / steps, steps)))
+    line = "total kernel time: %.3f ms" % (tot / 1e6)
+    if step_kernel:
+        calls = sum(c for n, (c, _) in agg.items() if step_kernel in n)
+        if calls and calls % per_step == 0:
+            steps = calls // per_step
+            line += "  (%.3f ms per step over %d steps: %d launches of '%s' / %d per step)" % (
+                tot / 1e6 / steps, steps, calls, step_kernel, per_step)
+        else:
+            line += "  (steps not derivable: %d launches of '%s', %d per step)" % (calls, step_kernel, per_step)
+    print(line)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--step-kernel", default=None, help="kernel-name substring launched a known number of times per step")
+    ap.add_argument("--per-step", type=int, default=1)
+    a = ap.parse_args()
+    main(a.path, a.step_kernel, a.per_step)

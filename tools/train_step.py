@@ -1,0 +1,23 @@
+"""Config-3 training step alone (bench.train_bench): for rocprofv3 kernel traces of the train
+step without the forward bench around it.  python tools/train_step.py [--steps K --warmup W]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--clips", type=int, default=8)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    print(json.dumps(bench.train_bench(a, torch.device("cuda", 0), 0, 1, a.steps, a.warmup)), flush=True)
