@@ -126,10 +126,7 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_EMBED_BWD: return up((M + N + 2 + M * N) * K * 4);                 // M = Np, N = T, K = C
     case DSVT_WS_SELECT: return up(select_frames_ws_bytes(M, N));                    // M = scores, N = unsampled
     case DSVT_WS_AUGMENT: return up(augment_ws_bytes(M, N));                          // M = frames, N = size
-    case DSVT_WS_WGRAD: {                                                              // M = rows, N, K: G [N, K]
-      const int64_t S = wgrad_slices(M, N, K);
-      return S > 1 ? up(S * N * K * 4) : 0;
-    }
+    case DSVT_WS_WGRAD: return up(wgrad_workspace_floats(M, N, K) * 4);              // M = rows, N, K: G [N, K]
     default: return -1;
   }
 }
@@ -660,19 +657,20 @@ int dsvt_embed_bwd(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C,
   return 0;
 }
 
-int dsvt_wgrad_bwd(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* G, int64_t M, int64_t N,
-                   int64_t K, int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
+int dsvt_wgrad_bwd(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* G, float* db, int64_t M,
+                   int64_t N, int64_t K, int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
   REQUIRE(dtype == DSVT_BF16, "wgrad: bf16 operands only");
   REQUIRE(dy && x && G, "wgrad: null pointer");
   REQUIRE(M > 0 && N >= 8 && K >= 8 && N % 8 == 0 && K % 8 == 0, "wgrad: need M > 0, N, K multiples of 8 (N=%lld K=%lld)",
           (long long)N, (long long)K);
   REQUIRE(ldy >= N && ldx >= K && ldy % 8 == 0 && ldx % 8 == 0, "wgrad: ldy / ldx must be >= N / K, multiples of 8");
-  REQUIRE(aligned16(dy) && aligned16(x) && aligned16(G) && (K % 4 == 0), "wgrad: pointers must be 16-byte aligned");
+  REQUIRE(aligned16(dy) && aligned16(x) && aligned16(G) && (db == nullptr || aligned16(db)),
+          "wgrad: pointers must be 16-byte aligned");
   const int64_t need = dsvt_workspace_bytes(DSVT_WS_WGRAD, dtype, M, N, K);
   REQUIRE(workspace_bytes >= need && (need == 0 || (workspace && aligned16(workspace))),
           "wgrad: workspace too small (%lld < %lld)", (long long)workspace_bytes, (long long)need);
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_wgrad_bwd", [&] {
-    return launch_wgrad((const unsigned short*)dy, ldy, (const unsigned short*)x, ldx, G, M, N, K, accumulate,
+    return launch_wgrad((const unsigned short*)dy, ldy, (const unsigned short*)x, ldx, G, db, M, N, K, accumulate,
                         (float*)workspace, (hipStream_t)stream);
   }, WGRAD_PROBE_TAG);
 }

@@ -51,10 +51,12 @@ struct RowLnParams {
 };
 hipError_t launch_gemm_rowln(const RowLnParams& p, hipStream_t s);
 
-// Weight gradients (wgrad.hip): G[n, k] (+)= sum_m dY[m, n] X[m, k], bf16 in, fp32 out
+// Weight gradients (wgrad.hip): G[n, k] (+)= sum_m dY[m, n] X[m, k] and optionally
+// db[n] (+)= sum_m dY[m, n], bf16 in, fp32 out
 int64_t wgrad_slices(int64_t M, int64_t N, int64_t K);
+int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
 hipError_t launch_wgrad(const unsigned short* dy, int64_t ldy, const unsigned short* x, int64_t ldx, float* G,
-                        int64_t M, int64_t N, int64_t K, int accumulate, float* partial, hipStream_t s);
+                        float* db, int64_t M, int64_t N, int64_t K, int accumulate, float* partial, hipStream_t s);
 
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,

@@ -1,113 +1,156 @@
 // Weight gradients of every nn.Linear on the student's backward path (loss.backward(),
-// train_ssl.py:538): G[n, k] (+)= sum_m dY[m, n] * X[m, k], bf16 operands, fp32 result.
+// train_ssl.py:538): G[n, k] (+)= sum_m dY[m, n] * X[m, k], bf16 operands, fp32 result, and
+// optionally the bias gradient db[n] (+)= sum_m dY[m, n] of the same Linear, fused.
 //
-// Both operands are read along their ROWS (m), the reduction dimension: a tile of dY rows
-// [64 m][128 n] and of X rows [64 m][128 k] is staged by LDS-DMA exactly as it lies in HBM
-// (256-byte rows, 16-byte chunks XOR-swizzled by ((row & 3) << 2) | ((row >> 2) & 3) on the
-// source address), and both MFMA operands come out of LDS by ds_read_b64_tr_b16 transposed
-// reads: lane (r16, g) of a 16-lane group gets one column of 4 consecutive m-rows, twice (rows
-// 4g.. and 16 + 4g.. of a 32-row block), i.e. the same permuted 8 m-values for the X fragment
-// (A operand: rows = k) and the dY fragment (B operand: columns = n), so the products pair up.
-// The output lane then holds G[n = col][k = 4g .. 4g + 3]: one 16-byte store.
+// Both operands are read along their ROWS (m), the reduction dimension: a stage of dY rows
+// [32 m][256 n] and of X rows [32 m][256 k] is staged by LDS-DMA exactly as it lies in HBM
+// (512-byte rows; 16-byte chunk' = chunk ^ ((row & 7) << 1) on the source address, so the 8
+// rows one ds_read_b64_tr_b16 lane group touches land on 8 distinct 32-byte bank pairs), and
+// both MFMA operands come out of LDS by transposed reads: lane (r16, g) of a 16-lane group gets
+// one column of m-rows 4g..4g+3 and 16+4g..16+4g+3 of the 32-row stage -- the same permuted 8
+// m-values for the X fragment (A operand: rows = k) and the dY fragment (B operand: columns =
+// n), so the products pair up.  The output lane holds G[n = col][k = 4g .. 4g + 3]: one 16-byte
+// store.
 //
-// 128 x 128 output tile per 256-thread workgroup (2 x 2 waves of 64 x 64), 2-stage LDS ring
-// (64 KiB: 2 workgroups per CU).  M is split over gridDim.y slices (a few hundred workgroups
-// for the 768..3072-wide weights); each slice writes an fp32 partial tile and a second kernel
-// sums the slices in a fixed order into G (deterministic; `accumulate` adds to G's old value).
-// Rows past M are zeroed in the X tile of the last step (the product then contributes 0).
+// 256 x 256 output tile per 512-thread workgroup (8 waves, 2 (k) x 4 (n) of 128 x 64), one
+// workgroup per CU, a 4-stage LDS ring (128 KiB) with loads three stages ahead and counted
+// vmcnt waits; the two wave rows run one barrier apart so that every SIMD overlaps one wave's
+// transposed fragment reads with the other's MFMAs.  M is split over S slices so that tiles x S fills
+// the 256 CUs once; each slice writes an fp32 partial tile and wgrad_reduce_kernel sums the
+// slices in a fixed order into G (deterministic; `accumulate` adds to G's old value).  Work is
+// laid out slice-major over XCD-contiguous ranges (block b runs on XCD b % 8), so the tiles that
+// share a slice's dY / X rows share one L2.  Rows past M are clamped on load and their dY values
+// zeroed in registers in the last stage (the product and the column sum then get 0).
+// The bias column sum rides on the dY fragments the k-tile-0 workgroups already hold: 4
+// v_dot2_f32_bf16 against ones per fragment, reduced over the 4 lane groups at the end.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace dsvt {
 
 namespace {
 
-constexpr int WG_BM = 64;                  // m rows per step
-constexpr int WG_TN = 128, WG_TK = 128;    // output tile: n x k
-constexpr int WG_ROWB = 256;               // bytes per staged row (128 bf16)
-constexpr int WG_TILE = WG_BM * WG_ROWB;   // 16 KiB per operand per stage
+constexpr int WG_BM = 32;                  // m rows per stage
+constexpr int WG_T = 256;                  // output tile: 256 n x 256 k
+constexpr int WG_ROWB = 512;               // bytes per staged row (256 bf16)
+constexpr int WG_OP = WG_BM * WG_ROWB;     // 16 KiB per operand per stage
+constexpr int WG_STAGE = 2 * WG_OP;        // [dY | X]
+constexpr int WG_NST = 4;                  // ring depth (128 KiB)
 
-__device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// byte offset of (row, column c) in a staged [32][256] operand (c % 4 == 0 for the 8-byte reads)
+__device__ __forceinline__ int wg_off(int row, int c) {
+  return row * WG_ROWB + ((((c >> 3) ^ ((row & 7) << 1))) << 4) + ((c & 7) << 1);
+}
 
-// byte offset of (row, column c) in a staged [64][128] tile (c % 4 == 0 for the 8-byte reads)
-__device__ __forceinline__ int wg_off(int row, int c) { return row * WG_ROWB + (((c >> 3) ^ wg_swz(row)) << 4) + ((c & 7) << 1); }
+template <int N>
+__device__ __forceinline__ void wg_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
+__device__ __forceinline__ void wg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 typedef __attribute__((address_space(3))) sv4* LDS4;
+typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
 
 }  // namespace
 
 struct WgradParams {
   const bf16_t* dy; int64_t ldy;           // [M, N]
   const bf16_t* x; int64_t ldx;            // [M, K]
-  float* out; int64_t ldo;                 // slices > 1: partials [S][N][K] (ldo = K); else G
+  float* out;                              // S > 1: partials [S][N][K]; else G (row stride K)
+  float* db;                               // optional; S > 1: partials [S][N]; else db
   int64_t M, N, K;
-  int accumulate;                          // single slice: G += (else G =)
+  int S, tilesN, tilesK;
+  int accumulate;                          // S == 1: G += / db += (else =)
 };
 
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2 * WG_TILE];   // [stage][dY | X]
+// ABL (diagnostic builds, tools/wgrad_bench.py only; 0 = normal): bit 0 no loads after the
+// prologue (stale stages), bit 1 no MFMA (fragments kept live), bit 2 no fragment reads
+template <int ABL = 0>
+__global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[WG_NST * WG_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
-  const int wk = wave >> 1, wn = wave & 1;      // wave's 64 x 64 block: k rows wk*64.., n cols wn*64..
-  const int tilesK = (int)((p.K + WG_TK - 1) / WG_TK);
-  const int64_t n0 = (int64_t)(blockIdx.x / tilesK) * WG_TN, k0 = (int64_t)(blockIdx.x % tilesK) * WG_TK;
-  const int64_t steps = (p.M + WG_BM - 1) / WG_BM, S = gridDim.y, sl = blockIdx.y;
-  const int64_t s_begin = sl * steps / S, s_end = (sl + 1) * steps / S;
+  const int wk = wave >> 2, wn = wave & 3;      // wave's block: k rows wk*128.., n cols wn*64..
+  const int tiles = p.tilesN * p.tilesK;
+  const int per_x = (int)(gridDim.x >> 3);
+  const int t = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+  if (t >= tiles * p.S) return;
+  const int sl = t / tiles, tile = t - sl * tiles;
+  const int64_t n0 = (int64_t)(tile / p.tilesK) * WG_T, k0 = (int64_t)(tile % p.tilesK) * WG_T;
+  const int64_t steps = (p.M + WG_BM - 1) / WG_BM;
+  const int64_t s_begin = sl * steps / p.S, s_end = (sl + 1) * steps / p.S;
+  const int nst = (int)(s_end - s_begin);
 
-  // DMA roles: a wave-instruction moves 4 rows x 256 B; lane -> (row in 4, physical chunk)
-  const int prow = lane >> 4, pch = lane & 15;
-  auto stage = [&](int st, int64_t step) {
-    const int64_t m0 = step * WG_BM;
+  // DMA roles: a wave-instruction moves 2 rows x 512 B; lane -> (row in 2, physical chunk)
+  int prow[2];
+  int64_t cy[2], cx[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {                  // 16 pieces per operand, 4 per wave
-      const int row = (wave * 4 + i) * 4 + prow;
-      int64_t m = m0 + row;
-      m = m < p.M ? m : p.M - 1;                   // clamped; the X rows are zeroed below
-      const int lc = pch ^ wg_swz(row);            // logical chunk landing in physical chunk pch
-      int64_t cn = n0 + lc * 8, ck = k0 + lc * 8;  // column chunks past N / K re-read the last one
-      cn = cn < p.N ? cn : p.N - 8;
-      ck = ck < p.K ? ck : p.K - 8;
-      __builtin_amdgcn_global_load_lds((const void*)(p.dy + m * p.ldy + cn),
-                                       LDS_PTR(smem[st] + (wave * 4 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + ck),
-                                       LDS_PTR(smem[st] + WG_TILE + (wave * 4 + i) * 1024), 16, 0, 0);
+  for (int q = 0; q < 2; ++q) {
+    prow[q] = (wave * 2 + q) * 2 + (lane >> 5);
+    const int lc = (lane & 31) ^ ((prow[q] & 7) << 1);    // logical chunk landing in physical chunk lane & 31
+    const int64_t cn = n0 + lc * 8, ck = k0 + lc * 8;      // chunks past N / K re-read the last one
+    cy[q] = cn < p.N ? cn : p.N - 8;
+    cx[q] = ck < p.K ? ck : p.K - 8;
+  }
+  auto stage = [&](int buf, int64_t step) {
+    const int64_t m0 = step * WG_BM;
+    char* base = smem + buf * WG_STAGE;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      int64_t m = m0 + prow[q];
+      m = m < p.M ? m : p.M - 1;                             // clamped; zeroed in registers
+      __builtin_amdgcn_global_load_lds((const void*)(p.dy + m * p.ldy + cy[q]),
+                                       LDS_PTR(base + (wave * 2 + q) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + cx[q]),
+                                       LDS_PTR(base + WG_OP + (wave * 2 + q) * 1024), 16, 0, 0);
     }
   };
 
-  fv4 acc[4][4];   // [k fragment][n fragment]
+  fv4 acc[8][4];   // [k fragment][n fragment]
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+  const bool do_cs = p.db != nullptr && k0 == 0 && wk == 0;   // wave-uniform
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf2_t ones = {(__bf16)1.0f, (__bf16)1.0f};
 
-  if (s_begin < s_end) stage(0, s_begin);
-  for (int64_t step = s_begin; step < s_end; ++step) {
-    const int st = (int)((step - s_begin) & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (step + 1 < s_end) stage(st ^ 1, step + 1);
-    if ((step + 1) * WG_BM > p.M) {                 // tail step: zero the X rows past M
-      const int r0 = (int)(p.M - step * WG_BM);
-      for (int e = tid; e < (WG_BM - r0) * 16; e += 256) {
-        const int row = r0 + e / 16;
-        *reinterpret_cast<uint4*>(smem[st] + WG_TILE + row * WG_ROWB + (e % 16) * 16) = make_uint4(0, 0, 0, 0);
-      }
-      __syncthreads();
-    }
-    const char* ty = smem[st];
-    const char* tx = smem[st] + WG_TILE;
+  for (int i = 0; i < WG_NST - 1 && i < nst; ++i) stage(i, s_begin + i);
+  // own pieces of stage `u` landed: the stages issued after it (at most 2) may stay in flight
+  auto wait_stage = [&](int u) {
+    const int later = min(nst - 1, u + WG_NST - 2) - u;
+    if (later >= 2) wg_vm_wait<8>();
+    else if (later == 1) wg_vm_wait<4>();
+    else wg_vm_wait<0>();
+  };
+  wait_stage(0);
+  wg_barrier();
+  // the k-row-1 waves run one barrier behind: each SIMD holds one wave of each row, so the
+  // fragment reads of one overlap the MFMAs of the other (two barriers per stage: A after the
+  // reads, B after the MFMAs; a stage's loads are issued after B, into the buffer every wave
+  // finished reading before its A)
+  const bool lag = wk == 1;
+  if (lag) wg_barrier();
+  // lane (r16, g) supplies row 4g + (r16 >> 2) (+16) and columns 4 (r16 & 3) of each 16-column block
+  const int ra = 4 * g + (r16 >> 2), rb = ra + 16, cq = 4 * (r16 & 3);
+  for (int it = 0; it < nst; ++it) {
+    if (!(ABL & 1) && it + WG_NST - 1 < nst) stage((it + WG_NST - 1) & (WG_NST - 1), s_begin + it + WG_NST - 1);
+    const char* ty = smem + (it & (WG_NST - 1)) * WG_STAGE;
+    const char* tx = ty + WG_OP;
+    sv8 fb[4], fa[8];
+    if constexpr ((ABL & 4) != 0) {
 #pragma unroll
-    for (int kb = 0; kb < WG_BM / 32; ++kb) {
-      // lane (r16, g) supplies row 4g + (r16 >> 2) (+16) and columns 4 (r16 & 3) of each 16-column block
-      const int ra = kb * 32 + 4 * g + (r16 >> 2), rb = ra + 16;
-      const int cq = 4 * (r16 & 3);
-      sv8 fa[4], fb[4];
+      for (int j = 0; j < 4; ++j) fb[j] = sv8{(short)it, 1, 2, 3, 4, 5, 6, 7};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = wk * 64 + i * 16 + cq;
-        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(tx + wg_off(ra, c)));
-        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(tx + wg_off(rb, c)));
-        fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
+      for (int i = 0; i < 8; ++i) fa[i] = sv8{(short)i, 1, 2, 3, 4, 5, 6, (short)it};
+    } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = wn * 64 + j * 16 + cq;
@@ -116,26 +159,70 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
         fb[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 8; ++i) {
+        const int c = wk * 128 + i * 16 + cq;
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(tx + wg_off(ra, c)));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(tx + wg_off(rb, c)));
+        fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+    const int64_t m0 = (s_begin + it) * WG_BM;
+    if (m0 + WG_BM > p.M) {                                   // last stage: dY rows past M -> 0
+      const int valid = (int)(p.M - m0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int row = (e < 4 ? 4 * g + e : 16 + 4 * g + e - 4);
+          if (row >= valid) fb[j][e] = 0;
+        }
+    }
+    if (do_cs) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 u = __builtin_bit_cast(uint4, fb[j]);
+        float s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.x), ones, cs[j], false);
+        s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.y), ones, s, false);
+        s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.z), ones, s, false);
+        cs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.w), ones, s, false);
+      }
+    }
+    if (lag) wait_stage(it + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // this stage's reads are done (ring reuse)
+    wg_barrier();                                             // A
+    if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(fb[j]));
+    } else {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
+    if (!lag) wait_stage(it + 1);
+    wg_barrier();                                             // B
   }
+  if (!lag) wg_barrier();                                     // balance the stagger barrier
 
-  // lane holds G[n = n0 + wn*64 + 16 j + r16][k = k0 + wk*64 + 16 i + 4 g .. + 3]
+  // lane holds G[n = n0 + wn*64 + 16 j + r16][k = k0 + wk*128 + 16 i + 4 g .. + 3]
   mfma_result_fence();
-  float* out = p.out + (S > 1 ? sl * p.N * p.ldo : 0);
+  const bool direct = p.S == 1;
+  float* out = p.out + (direct ? 0 : (int64_t)sl * p.N * p.K);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t n = n0 + wn * 64 + j * 16 + r16;
     if (n >= p.N) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t k = k0 + wk * 64 + i * 16 + 4 * g;
+    for (int i = 0; i < 8; ++i) {
+      const int64_t k = k0 + wk * 128 + i * 16 + 4 * g;
       if (k >= p.K) continue;
-      float4* o = reinterpret_cast<float4*>(out + n * p.ldo + k);
+      float4* o = reinterpret_cast<float4*>(out + n * p.K + k);
       const fv4 a = acc[i][j];
-      if (S == 1 && p.accumulate) {
+      if (direct && p.accumulate) {
         const float4 old = *o;
         *o = make_float4(old.x + a[0], old.y + a[1], old.z + a[2], old.w + a[3]);
       } else {
@@ -143,41 +230,71 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradParams p) {
       }
     }
   }
+  if (do_cs) {
+    float* dbo = p.db + (direct ? 0 : (int64_t)sl * p.N);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = cs[j];
+      v += __shfl_xor(v, 16, 64);                          // the 4 lane groups hold disjoint rows
+      v += __shfl_xor(v, 32, 64);
+      const int64_t n = n0 + wn * 64 + j * 16 + r16;
+      if (g == 0 && n < p.N) dbo[n] = (direct && p.accumulate) ? dbo[n] + v : v;
+    }
+  }
 }
 
-// G (+)= sum over the S slices of the partials, in slice order (float4 per thread)
+// dst (+)= sum over the S slices of the partials, in slice order (float4 per thread)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int64_t S, int64_t n4,
-                                                           float* __restrict__ G, int accumulate) {
+                                                           float* __restrict__ dst, int accumulate) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 a = accumulate ? reinterpret_cast<const float4*>(G)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t s = 0; s < S; ++s) {
       const float4 v = reinterpret_cast<const float4*>(part)[s * n4 + i];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
-    reinterpret_cast<float4*>(G)[i] = a;
+    reinterpret_cast<float4*>(dst)[i] = a;
   }
 }
 
-// M-slices: enough workgroups for 2 per CU over the output tiles, each slice >= 8 steps
+// M-slices: tiles x S <= 256 workgroups (one per CU, one round), each slice >= 8 stages
 int64_t wgrad_slices(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ((N + WG_TN - 1) / WG_TN) * ((K + WG_TK - 1) / WG_TK);
+  const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
   const int64_t steps = (M + WG_BM - 1) / WG_BM;
-  int64_t S = (512 + tiles - 1) / tiles;
+  int64_t S = 256 / tiles;
   if (S > steps / 8) S = steps / 8;
   return S < 1 ? 1 : S;
 }
 
-hipError_t launch_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* G, int64_t M, int64_t N,
-                        int64_t K, int accumulate, float* partial, hipStream_t s) {
+// workspace floats: the G partial slabs, then (with a bias) the db partial rows
+int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K) {
   const int64_t S = wgrad_slices(M, N, K);
-  WgradParams p{dy, ldy, x, ldx, S > 1 ? partial : G, K, M, N, K, accumulate};
-  const int64_t tiles = ((N + WG_TN - 1) / WG_TN) * ((K + WG_TK - 1) / WG_TK);
-  wgrad_kernel<<<dim3((unsigned)tiles, (unsigned)S), 256, 0, s>>>(p);
+  return S > 1 ? S * N * K + S * N : 0;
+}
+
+hipError_t launch_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* G, float* db, int64_t M,
+                        int64_t N, int64_t K, int accumulate, float* partial, hipStream_t s) {
+  const int64_t S = wgrad_slices(M, N, K);
+  const int tilesN = (int)((N + WG_T - 1) / WG_T), tilesK = (int)((K + WG_T - 1) / WG_T);
+  float* dbp = db == nullptr ? nullptr : (S > 1 ? partial + S * N * K : db);
+  WgradParams p{dy, ldy, x, ldx, S > 1 ? partial : G, dbp, M, N, K, (int)S, tilesN, tilesK, accumulate};
+  const int64_t total = (int64_t)tilesN * tilesK * S;
+  const dim3 grid((unsigned)((total + 7) / 8 * 8));
+  static const int abl = getenv("DSVT_WGRAD_ABL") ? atoi(getenv("DSVT_WGRAD_ABL")) : 0;   // diagnostics only
+  switch (abl) {
+    case 1: wgrad_kernel<1><<<grid, 512, 0, s>>>(p); break;
+    case 2: wgrad_kernel<2><<<grid, 512, 0, s>>>(p); break;
+    case 3: wgrad_kernel<3><<<grid, 512, 0, s>>>(p); break;
+    case 4: wgrad_kernel<4><<<grid, 512, 0, s>>>(p); break;
+    case 6: wgrad_kernel<6><<<grid, 512, 0, s>>>(p); break;
+    default: wgrad_kernel<0><<<grid, 512, 0, s>>>(p); break;
+  }
   if (S > 1) {
     const int64_t n4 = N * K / 4;
     unsigned blocks = (unsigned)((n4 + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     wgrad_reduce_kernel<<<blocks, 256, 0, s>>>(partial, S, n4, G, accumulate);
+    if (db) wgrad_reduce_kernel<<<(unsigned)((N / 4 + 255) / 256), 256, 0, s>>>(partial + S * N * K, S, N / 4, db,
+                                                                                accumulate);
   }
   return hipGetLastError();
 }

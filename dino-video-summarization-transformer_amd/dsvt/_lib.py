@@ -66,7 +66,7 @@ SIGNATURES = {
     "dsvt_embed_bwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "dsvt_ema": (_i32, [_p, _p, _p, _p, _p, _i64, _f32, _p]),
     "dsvt_clip_grads": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _f32, _p, _p, _i64, _p]),
-    "dsvt_wgrad_bwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i32, _p, _i64, _p]),
+    "dsvt_wgrad_bwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i32, _p, _i64, _p]),
     "dsvt_adamw": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i64, _p]),
     # Video Swin
     "dsvt_swin_patch_embed_fwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p,

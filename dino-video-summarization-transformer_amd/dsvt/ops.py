@@ -314,19 +314,24 @@ def rowscale_bias_add(X, row_scale_, bias):
     return X
 
 
-def wgrad(dy, x, out, accumulate=False):
+def wgrad(dy, x, out, accumulate=False, db=None):
     """out[n, k] (+)= sum_m dy[m, n] x[m, k]: the weight gradient dY^T . X of an nn.Linear
-    (bf16 operands, fp32 out; csrc/wgrad.hip, deterministic M-slice reduction)."""
+    (bf16 operands, fp32 out; csrc/wgrad.hip, deterministic M-slice reduction); with `db`
+    (fp32 [N]) also the bias gradient db[n] (+)= sum_m dy[m, n], fused."""
     _check(dy, torch.bfloat16, "dY")
     _check(x, torch.bfloat16, "X")
     _check(out, torch.float32, "G")
+    if db is not None:
+        _check(db, torch.float32, "db")
+        if db.numel() != dy.shape[1]:
+            raise _lib.DsvtError("wgrad: db has %d elements, dY %d columns" % (db.numel(), dy.shape[1]))
     M, N, K = dy.shape[0], dy.shape[1], x.shape[1]
     if x.shape[0] != M or tuple(out.shape) != (N, K):
         raise _lib.DsvtError("wgrad: dY %s, X %s, G %s do not match" % (tuple(dy.shape), tuple(x.shape),
                                                                        tuple(out.shape)))
     nbytes = workspace_bytes(_lib.WS_WGRAD, torch.bfloat16, M, N, K)
     ws = torch.empty(max(nbytes, 4) // 4, device=dy.device, dtype=torch.float32)
-    call("dsvt_wgrad_bwd", _lib.BF16, _ptr(dy), N, _ptr(x), K, _ptr(out), M, N, K, int(accumulate), _ptr(ws),
+    call("dsvt_wgrad_bwd", _lib.BF16, _ptr(dy), N, _ptr(x), K, _ptr(out), _ptr(db), M, N, K, int(accumulate), _ptr(ws),
          ws.numel() * 4, _stream())
     return out
 
@@ -385,7 +390,7 @@ def gemm_kernel_name(tag):
     if variant == 30:
         return "void dsvt::gemm_rowln_kernel<"
     if variant == 31:
-        return "dsvt::wgrad_kernel("
+        return "void dsvt::wgrad_kernel<0>"
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)
 
 

@@ -58,6 +58,12 @@ class DINOTrainer:
             raise ValueError("optimizer must be 'dsvt' or 'torch'")
         for p in teacher.parameters():
             p.requires_grad_(False)
+        # the EMA changes the teacher's weights every step, so folding temporal_attn.proj into
+        # temporal_fc (an fp32 768^3 product per block, redone each step) costs more than the
+        # extra bf16 GEMM of the unfolded pair it saves
+        bb = getattr(teacher, "backbone", teacher)
+        if hasattr(bb, "fold_temporal_fc"):
+            bb.fold_temporal_fc = False
         self._s_params = [p for p in student.parameters()]
         self._t_params = [p for p in teacher.parameters()]
 

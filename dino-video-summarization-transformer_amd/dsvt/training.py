@@ -29,21 +29,31 @@ from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SP
     DsvtError
 
 
-def wgrad(dy, x, G, p, view=None):
-    """grad(p) (+)= dy^T [N, M] . x [M, K]: the dsvt weight-gradient kernel in bf16 (fp32
-    result written / accumulated in place); the fp32 parity mode takes a plain library GEMM.
-    The first write of a gradient buffer is a copy (no zero fill)."""
+def wgrad(dy, x, G, p, view=None, bias=None):
+    """grad(p) (+)= dy^T [N, M] . x [M, K] and, with `bias`, grad(bias) (+)= colsum(dy): the
+    dsvt weight-gradient kernel in bf16 (fp32 results written / accumulated in place, the
+    column sum fused into it); the fp32 parity mode takes a plain library GEMM and the dsvt
+    column-sum kernel.  The first write of a gradient buffer is a copy (no zero fill)."""
     buf, acc = G.acc(p)
     if view is not None:
         buf = buf.view(view)
-    if dy.dtype == torch.bfloat16:
-        ops.wgrad(dy, x, buf, accumulate=acc)
-        return
-    r = torch.mm(dy.t(), x)
-    if acc:
-        buf.add_(r)
-    else:
-        buf.copy_(r)
+    dbuf = None
+    if bias is not None:
+        dbuf, acc_b = G.acc(bias)
+        assert acc_b == acc, "weight and bias gradients are written together"
+
+    def run():
+        if dy.dtype == torch.bfloat16:
+            ops.wgrad(dy, x, buf, accumulate=acc, db=dbuf)
+            return
+        r = torch.mm(dy.t(), x)
+        if acc:
+            buf.add_(r)
+        else:
+            buf.copy_(r)
+        if dbuf is not None:
+            ops.colsum(dy, dbuf, accumulate=acc)
+    G.run_side(run, (dy, x))
 
 
 class _Grads:
@@ -51,8 +61,30 @@ class _Grads:
     buffer and whether it already holds a partial sum (False on the first write: the kernels
     then overwrite instead of accumulating, so no zero fill is needed)."""
 
-    def __init__(self):
+    def __init__(self, side=None):
         self.g = {}
+        self.side = side               # weight gradients on this stream (None: the current one)
+        self._main = None
+
+    def run_side(self, fn, inputs):
+        """Run fn (a weight-gradient product) on the side stream after the current stream's
+        prior work.  Its inputs are marked used there, so the caching allocator does not hand
+        their memory to the current stream before the side stream is done with them."""
+        if self.side is None:
+            fn()
+            return
+        if self._main is None:
+            self._main = torch.cuda.current_stream(self.side.device)
+        self.side.wait_stream(self._main)
+        with torch.cuda.stream(self.side):
+            fn()
+        for t in inputs:
+            t.record_stream(self.side)
+
+    def join(self):
+        """The current stream waits for every side-stream product (before the grads are used)."""
+        if self.side is not None and self._main is not None:
+            self._main.wait_stream(self.side)
 
     def acc(self, p):
         buf = self.g.get(id(p))
@@ -226,7 +258,10 @@ def _backbone_backward(model, st, dfeat):
     rows, R = B * L, B * Np * T
     dev = dfeat.device
     wt = model._wcache.transposed(mode)
-    G = _Grads()
+    # the weight gradients depend only on (dY, X) and nothing reads them before the optimizer
+    # step: they run on a second stream, overlapping the dX chain (GEMM tails, LayerNorm and
+    # attention backward, casts, the split-K reductions)
+    G = _Grads(side=_wgrad_stream(dev) if getattr(model, "dsvt_wgrad_stream", True) else None)
     patch_map = (Np * T, L, 1)
     # final norm on the CLS rows (timesformer.py:342-345)
     dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
@@ -248,8 +283,7 @@ def _backbone_backward(model, st, dfeat):
         wgrad(dXb, S.h, G, fc2.weight)
         dpre = torch.empty(rows, fc1.out_features, device=dev, dtype=mode)
         ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
-        wgrad(dpre, S.a_m, G, fc1.weight)
-        _colsum(dpre, G, fc1.bias)
+        wgrad(dpre, S.a_m, G, fc1.weight, bias=fc1.bias)
         da = torch.empty(rows, C, device=dev, dtype=mode)       # LN input gradient (storage dtype)
         ops.gemm(dpre, wt(fc1.weight), None, da)
         del dpre
@@ -263,28 +297,24 @@ def _backbone_backward(model, st, dfeat):
         dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
         ops.attn_spatial_bwd(S.qkv_s, do, dqkv, B, T, L, heads, blk.attn.scale,
                              seq_scale=None if mk is None else mk.s)
-        wgrad(dqkv, S.a_s, G, blk.attn.qkv.weight)
-        _colsum(dqkv, G, blk.attn.qkv.bias)
+        wgrad(dqkv, S.a_s, G, blk.attn.qkv.weight, bias=blk.attn.qkv.bias)
         ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da)
         del dqkv, do
         _ln_bwd(S.X1, da, blk.norm1, dX, rows, G)
         # ---- temporal (patch rows of X only)
         dY = torch.empty(R, C, device=dev, dtype=mode)
         ops.cast_rows(dX, dY, R, rowmap=patch_map)
-        wgrad(dY, S.u, G, blk.temporal_fc.weight)
-        _colsum(dY, G, blk.temporal_fc.bias)
+        wgrad(dY, S.u, G, blk.temporal_fc.weight, bias=blk.temporal_fc.bias)
         du = torch.empty(R, C, device=dev, dtype=mode)
         ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
         if mk is not None:
             ops.row_scale(du, mk.t, T)
-        wgrad(du, S.o_t, G, ta.proj.weight)
-        _colsum(du, G, ta.proj.bias)
+        wgrad(du, S.o_t, G, ta.proj.weight, bias=ta.proj.bias)
         do_t = torch.empty(R, C, device=dev, dtype=mode)
         ops.gemm(du, wt(ta.proj.weight), None, do_t)
         dqkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
         ops.attn_temporal_bwd(S.qkv_t, do_t, dqkv_t, B * Np, T, heads, ta.scale)
-        wgrad(dqkv_t, S.a_t, G, ta.qkv.weight)
-        _colsum(dqkv_t, G, ta.qkv.bias)
+        wgrad(dqkv_t, S.a_t, G, ta.qkv.weight, bias=ta.qkv.bias)
         da_t = torch.empty(R, C, device=dev, dtype=mode)
         ops.gemm(dqkv_t, wt(ta.qkv.weight), None, da_t)
         _ln_bwd(S.X0, da_t, blk.temporal_norm1, dX, R, G, rowmap=patch_map)
@@ -296,11 +326,16 @@ def _backbone_backward(model, st, dfeat):
     conv = model.patch_embed.proj
     for row0, nb, a in st.im2col:
         r0 = row0 * Np * T
-        wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1))
-    _colsum(dP, G, conv.bias)
+        wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
     ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
                   G.zeros(model.cls_token))
+    G.join()
     return G
+
+
+def _wgrad_stream(device):
+    from .utils import side_stream
+    return side_stream(device, "wgrad")
 
 
 # ================================================================================ DINO head
@@ -397,8 +432,11 @@ def _head_backward(head, st, dlogits):
         gb = g if g.dtype == mode else torch.empty(R, g.shape[1], device=dev, dtype=mode)
         if gb is not g:
             ops.cast(g.contiguous(), gb)
-        wgrad(gb, st.a[i], G, lin.weight)
-        _colsum(g, G, lin.bias)
+        if gb is g:                                           # bf16 gradient: bias sum fused
+            wgrad(gb, st.a[i], G, lin.weight, bias=lin.bias)
+        else:                                                 # fp32 gradient: exact column sum
+            wgrad(gb, st.a[i], G, lin.weight)
+            _colsum(g, G, lin.bias)
         if i > 0:
             nxt = torch.empty(R, lin.in_features, device=dev, dtype=mode)
             ops.gemm_aux(gb, wt(lin.weight), None, nxt, st.pre[i - 1], EPI_DGELU)

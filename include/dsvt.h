@@ -287,13 +287,14 @@ int dsvt_clip_grads(float *const *grads, const int64_t *sizes, const int32_t *ch
                     const int64_t *chunk_start, const int32_t *first_chunk, int64_t nchunks,
                     int64_t ntensors, float clip, float *norms, void *workspace, int64_t workspace_bytes,
                     void *stream);
-/* Weight gradient of an nn.Linear in the backward of loss.backward() (train_ssl.py:538):
- * G[n, k] (+)= sum_m dY[m, n] * X[m, k] over m < M, i.e. dW = dY^T . X with dY [M, N] (ldy)
- * and X [M, K] (ldx) in bf16 and G [N, K] fp32 (row stride K); accumulate != 0 adds to G.
- * Deterministic (M slices reduced in a fixed order through the workspace,
+/* Weight (and bias) gradient of an nn.Linear in the backward of loss.backward()
+ * (train_ssl.py:538): G[n, k] (+)= sum_m dY[m, n] * X[m, k] over m < M, i.e. dW = dY^T . X
+ * with dY [M, N] (ldy) and X [M, K] (ldx) in bf16 and G [N, K] fp32 (row stride K); db
+ * (optional, fp32 [N]) (+)= sum_m dY[m, n], the bias gradient, fused; accumulate != 0 adds
+ * to G and db.  Deterministic (M slices reduced in a fixed order through the workspace,
  * DSVT_WS_WGRAD).  N, K multiples of 8. */
 int dsvt_wgrad_bwd(int dtype, const void *dy, int64_t ldy, const void *x, int64_t ldx, float *G,
-                   int64_t M, int64_t N, int64_t K, int accumulate, void *workspace,
+                   float *db, int64_t M, int64_t N, int64_t K, int accumulate, void *workspace,
                    int64_t workspace_bytes, void *stream);
 /* AdamW step over one tensor list that shares lr / weight decay / step count (replaces
  * torch.optim.AdamW(params_groups).step(), train_ssl.py:384 / :551): per element

@@ -413,24 +413,33 @@ def test_train_steps_match_reference():
 
 
 @pytest.mark.parametrize("M,N,K", [(25104, 2304, 768), (13872, 768, 3072), (300, 192, 64), (8, 512, 64),
-                                   (77, 136, 40), (4096, 65536, 256)])
+                                   (77, 136, 40), (4096, 65536, 256), (25104, 768, 768), (1000, 3072, 768),
+                                   (33, 264, 520)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_vs_fp64(M, N, K, accumulate):
-    """csrc/wgrad.hip: G (+)= dY^T . X (bf16 operands, fp32 out) against float64 from the same
-    bf16 values -- the bench's qkv / fc2 shapes, ragged small shapes (tile edges, rows past M)
-    and the head's 65536-row product; two launches are bitwise identical (fixed-order slices)."""
+    """csrc/wgrad.hip: G (+)= dY^T . X (bf16 operands, fp32 out) and the fused bias gradient
+    db (+)= colsum(dY) against float64 from the same bf16 values -- the bench's qkv / proj /
+    fc2 shapes, ragged small shapes (tile edges, rows past M, partial 256-column tiles) and the
+    head's 65536-row product; two launches are bitwise identical (fixed-order slices)."""
     from dsvt import ops
     gen = torch.Generator(device="cuda").manual_seed(31)
     dy = torch.randn(M, N, device="cuda", generator=gen).to(torch.bfloat16)
     x = torch.randn(M, K, device="cuda", generator=gen).to(torch.bfloat16)
     g0 = torch.randn(N, K, device="cuda", generator=gen)
+    b0 = torch.randn(N, device="cuda", generator=gen)
     outs = []
     for _ in range(2):
-        g = g0.clone()
-        ops.wgrad(dy, x, g, accumulate=accumulate)
-        outs.append(g)
+        g, b = g0.clone(), b0.clone()
+        ops.wgrad(dy, x, g, accumulate=accumulate, db=b)
+        outs.append((g, b))
+    g_plain = g0.clone()
+    ops.wgrad(dy, x, g_plain, accumulate=accumulate)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], g_plain)             # the fused column sum leaves G untouched
     ref = dy.double().t() @ x.double() + (g0.double() if accumulate else 0)
-    err = ((outs[0].double() - ref).abs().max() / ref.abs().max()).item()
+    err = ((outs[0][0].double() - ref).abs().max() / ref.abs().max()).item()
     assert err < 1e-5, err
+    ref_b = dy.double().sum(0) + (b0.double() if accumulate else 0)
+    err_b = ((outs[0][1].double() - ref_b).abs().max() / ref_b.abs().max()).item()
+    assert err_b < 1e-5, err_b

@@ -1,6 +1,6 @@
 """Weight-gradient GEMM dW = dY^T . X at the training step's shapes (16 global clips: 25 104
 rows; 48 local clips: 13 872 rows): dsvt wgrad kernel vs hipBLASLt (torch.mm, bf16 out).
-usage: python tools/wgrad_bench.py"""
+usage: python tools/wgrad_bench.py [shape names]   (DSVT_WGRAD_ABL=n: csrc/wgrad.hip diagnostic builds)"""
 import os
 import sys
 
@@ -28,12 +28,17 @@ def timeit(fn, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+only = sys.argv[1:]          # optional shape names
 for name, M, N, K in SHAPES:
+    if only and name not in only:
+        continue
     dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     g = torch.zeros(N, K, device="cuda")
+    b = torch.zeros(N, device="cuda")
     t_d = timeit(lambda: ops.wgrad(dy, x, g, accumulate=True))
+    t_b = timeit(lambda: ops.wgrad(dy, x, g, accumulate=True, db=b))
     t_t = timeit(lambda: g.add_(torch.mm(dy.t(), x)))
     fl = 2.0 * M * N * K
-    print("%-10s M=%6d N=%6d K=%5d  dsvt %7.1f us %6.0f TF/s   hipBLASLt+add %7.1f us %6.0f TF/s" %
-          (name, M, N, K, t_d * 1e3, fl / t_d / 1e9, t_t * 1e3, fl / t_t / 1e9), flush=True)
+    print("%-10s M=%6d N=%6d K=%5d  dsvt %7.1f us %6.0f TF/s  (+bias %7.1f us)  hipBLASLt+add %7.1f us %6.0f TF/s" %
+          (name, M, N, K, t_d * 1e3, fl / t_d / 1e9, t_b * 1e3, t_t * 1e3, fl / t_t / 1e9), flush=True)
