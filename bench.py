@@ -29,6 +29,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "clips/sec (8-frame 224², ViT-B/16 DINO fwd+loss) at 1/2/4/8 MI355X; % MFMA roofline"
 PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3}   # dense, MI355X_MICROARCH.md chip table (2.4 GHz)
+HBM_PEAK_GBS = 8000.0                          # HBM3E, MI355X_MICROARCH.md
 IMAGENET_MEAN = (0.45, 0.45, 0.45)             # DATA.MEAN / STD defaults of the reference loader
 IMAGENET_STD = (0.225, 0.225, 0.225)
 
@@ -449,7 +450,7 @@ def main():
         for _ in range(min(args.steps, 5)):
             step(concurrent=False)
         torch.cuda.synchronize()
-        probe = ops.probe_read(1 << 16)
+        probe = ops.probe_read(1 << 16, with_bytes=True)
         ops.probe_disable()
 
     # ---- the timed run: the whole forward + loss of a step as ONE captured HIP graph (every
@@ -485,7 +486,7 @@ def main():
 
     roofline = None
     if probe is not None:
-        ms, work, fam, tag = probe
+        ms, work, fam, tag, nbytes = probe
         if len(ms):
             by_tag = {}
             for t, m_, w_ in zip(tag, ms, work):
@@ -495,17 +496,46 @@ def main():
                 a[2] += float(w_)
             dom = max(by_tag, key=lambda t: by_tag[t][1])
             n, tms, tfl = by_tag[dom]
-            achieved = tfl / (tms * 1e-3) / 1e12          # = (flops per launch) / (avg launch time)
             peak = PEAK_TFLOPS[args.dtype]
+            # per-launch roofline of the dominant kernel: each launch class (shape) is bound by
+            # max(FLOP / MFMA peak, algorithmic bytes / HBM peak)
+            classes = {}
+            for t, m_, w_, b_ in zip(tag, ms, work, nbytes):
+                if int(t) != dom:
+                    continue
+                c = classes.setdefault((float(w_), float(b_)), [0, 0.0])
+                c[0] += 1
+                c[1] += float(m_)
+            cls_out, t_att, share = [], 0.0, {"mfma": 0.0, "hbm": 0.0}
+            for (w_, b_), (cn, cms) in sorted(classes.items(), key=lambda kv: -kv[1][1]):
+                avg_s = cms / cn * 1e-3
+                t_f, t_b = w_ / (peak * 1e12), b_ / (HBM_PEAK_GBS * 1e9)
+                bound = "hbm" if t_b > t_f else "mfma"
+                share[bound] += cms
+                t_att += cn * max(t_f, t_b)
+                cls_out.append({"launches": cn, "gflop": round(w_ / 1e9, 2), "mbytes": round(b_ / 1e6, 1),
+                                "bound": bound, "avg_us": round(avg_s * 1e6, 2),
+                                "tflops": round(w_ / avg_s / 1e12, 1), "gbs": round(b_ / avg_s / 1e9, 1),
+                                "frac_of_bound": round(max(t_f, t_b) / avg_s, 4)})
+            bound = "hbm" if share["hbm"] > share["mfma"] else "mfma"
+            if bound == "mfma":
+                achieved, unit, pk = tfl / (tms * 1e-3) / 1e12, "TFLOP/s", peak
+            else:
+                tb = sum(c["mbytes"] * 1e6 * c["launches"] for c in cls_out)
+                achieved, unit, pk = tb / (tms * 1e-3) / 1e9, "GB/s", HBM_PEAK_GBS
             all_ms = float(np.sum(ms))
             kname = ops.gemm_kernel_name(dom)
-            roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                        "frac": round(achieved / peak, 4), "traffic": pmc_traffic(kname),
+            roofline = {"bound": bound, "achieved": round(achieved, 1), "peak": pk, "unit": unit,
+                        "frac": round(achieved / pk, 4), "traffic": pmc_traffic(kname),
+                        "frac_attainable": round(t_att / (tms * 1e-3), 4),
                         "kernel": kname, "launches": n,
                         "avg_launch_us": round(tms / n * 1e3, 2),
                         "flops_per_launch": tfl / n,
+                        "launch_classes": cls_out,
                         "gemm_kernel_ms_per_step": round(all_ms / min(args.steps, 5), 3),
-                        "measured": "HIP events around each launch, serial eager pass of the same step",
+                        "measured": "HIP events around each launch, serial eager pass of the same step; "
+                                    "frac_attainable = sum over launches of max(FLOP/MFMA peak, bytes/HBM peak) "
+                                    "/ measured time",
                         "all_gemm_tflops": round(float(np.sum(work)) / (all_ms * 1e-3) / 1e12, 1)}
 
     value = world * args.clips * args.steps / elapsed

@@ -44,18 +44,18 @@ int64_t esize(int dtype) { return dtype == DSVT_BF16 ? 2 : 4; }
 struct Probe {
   int mask = 0, cap = 0, count = 0;
   std::vector<hipEvent_t> ev0, ev1;
-  std::vector<double> work;
+  std::vector<double> work, bytes;
   std::vector<int32_t> fam, tag;
   void clear() {
     for (auto e : ev0) (void)hipEventDestroy(e);
     for (auto e : ev1) (void)hipEventDestroy(e);
-    ev0.clear(); ev1.clear(); work.clear(); fam.clear(); tag.clear();
+    ev0.clear(); ev1.clear(); work.clear(); bytes.clear(); fam.clear(); tag.clear();
     mask = cap = count = 0;
   }
 } thread_local g_probe;   // per calling thread, like the variant knobs
 
 template <typename F>
-int probed(int family, double work, hipStream_t s, const char* where, F&& launch, int tag = 0) {
+int probed(int family, double work, hipStream_t s, const char* where, F&& launch, int tag = 0, double bytes = 0) {
   const bool on = (g_probe.mask & family) && g_probe.count < g_probe.cap;
   if (on) (void)hipEventRecord(g_probe.ev0[g_probe.count], s);
   hipError_t e = launch();
@@ -63,6 +63,7 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
   if (on) {
     (void)hipEventRecord(g_probe.ev1[g_probe.count], s);
     g_probe.work[g_probe.count] = work;
+    g_probe.bytes[g_probe.count] = bytes;
     g_probe.fam[g_probe.count] = family;
     g_probe.tag[g_probe.count] = tag;
     g_probe.count++;
@@ -75,6 +76,17 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
 // host can name the exact kernel instantiation rocprofv3 reports (dsvt/ops.py gemm_kernel_name)
 constexpr int ROWLN_PROBE_TAG = 30 * 32 + 2 * 2 + 1;   // "variant 30": gemm_rowln_kernel (dsvt/ops.py)
 constexpr int WGRAD_PROBE_TAG = 31 * 32 + 1;            // "variant 31": wgrad_kernel
+
+// algorithmic HBM bytes of one GEMM launch: A and W once, the output once (+ the fp32 residual
+// X read for EPI_RESID, + the aux tensor for the training epilogues), the bias
+double gemm_bytes(int dtype, int epi, int out_f32, int64_t M, int64_t N, int64_t K) {
+  const double es = (double)esize(dtype);
+  const double out_es = (epi == EPI_RESID || epi == EPI_PATCH || out_f32) ? 4.0 : es;
+  double b = es * ((double)M * K + (double)N * K) + out_es * (double)M * N + 4.0 * N;
+  if (epi == EPI_RESID) b += 4.0 * (double)M * N;
+  if (epi == EPI_GELU_SAVE || epi == EPI_DGELU) b += es * (double)M * N;
+  return b;
+}
 
 int gemm_tag(const GemmParams& p, int dtype, int epi, int out_f32) {
   const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
@@ -141,7 +153,7 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t l
   GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
                 [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
-                gemm_tag(p, dtype, epilogue, out_f32));
+                gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
 }
 
 int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const float* gamma, const float* beta,
@@ -441,6 +453,7 @@ int dsvt_probe_enable(int mask, int capacity) {
     }
   }
   g_probe.work.assign(capacity, 0.0);
+  g_probe.bytes.assign(capacity, 0.0);
   g_probe.fam.assign(capacity, 0);
   g_probe.tag.assign(capacity, 0);
   g_probe.cap = capacity;
@@ -453,7 +466,7 @@ int dsvt_probe_disable(void) {
   return 0;
 }
 
-int dsvt_probe_read(float* ms, double* work, int32_t* family, int32_t* tag, int capacity) {
+int dsvt_probe_read(float* ms, double* work, double* bytes, int32_t* family, int32_t* tag, int capacity) {
   const int n = g_probe.count < capacity ? g_probe.count : capacity;
   for (int i = 0; i < n; ++i) {
     if (hipEventSynchronize(g_probe.ev1[i]) != hipSuccess) return -fail("probe: event sync failed");
@@ -461,6 +474,7 @@ int dsvt_probe_read(float* ms, double* work, int32_t* family, int32_t* tag, int 
     (void)hipEventElapsedTime(&t, g_probe.ev0[i], g_probe.ev1[i]);
     if (ms) ms[i] = t;
     if (work) work[i] = g_probe.work[i];
+    if (bytes) bytes[i] = g_probe.bytes[i];
     if (family) family[i] = g_probe.fam[i];
     if (tag) tag[i] = g_probe.tag[i];
   }
@@ -481,7 +495,7 @@ int dsvt_gemm_aux_fwd(int dtype, int epilogue, int out_f32, const void* A, int64
                aux, ld_aux};
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_aux_fwd",
                 [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
-                gemm_tag(p, dtype, epilogue, out_f32));
+                gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
 }
 
 int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
@@ -672,7 +686,7 @@ int dsvt_wgrad_bwd(int dtype, const void* dy, int64_t ldy, const void* x, int64_
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_wgrad_bwd", [&] {
     return launch_wgrad((const unsigned short*)dy, ldy, (const unsigned short*)x, ldx, G, db, M, N, K, accumulate,
                         (float*)workspace, (hipStream_t)stream);
-  }, WGRAD_PROBE_TAG);
+  }, WGRAD_PROBE_TAG, 2.0 * M * (N + K) + 4.0 * N * K * (accumulate ? 2 : 1));
 }
 
 int dsvt_ema(float* const* teacher, const float* const* student, const int64_t* sizes, const int32_t* chunk_tensor,

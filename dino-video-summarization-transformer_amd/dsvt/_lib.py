@@ -87,7 +87,7 @@ SIGNATURES = {
     "dsvt_set_attn_bwd_variant": (_i32, [_i32]),
     "dsvt_probe_enable": (_i32, [_i32, _i32]),
     "dsvt_probe_disable": (_i32, []),
-    "dsvt_probe_read": (_i32, [_p, _p, _p, _p, _i32]),
+    "dsvt_probe_read": (_i32, [_p, _p, _p, _p, _p, _i32]),
 }
 
 

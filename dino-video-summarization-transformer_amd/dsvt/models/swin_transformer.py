@@ -28,18 +28,13 @@ from .vit_utils import DropPath, trunc_normal_
 
 
 def get_window_size(x_size, window_size, shift_size=None):
-    """swin_transformer.py:71-84."""
-    use_window_size = list(window_size)
-    if shift_size is not None:
-        use_shift_size = list(shift_size)
-    for i in range(len(x_size)):
-        if x_size[i] <= window_size[i]:
-            use_window_size[i] = x_size[i]
-            if shift_size is not None:
-                use_shift_size[i] = 0
+    """swin_transformer.py:71-84: a window dimension that covers the whole input dimension
+    shrinks to it, and its shift drops to 0."""
+    fits = [x <= w for x, w in zip(x_size, window_size)]
+    ws = tuple(x if f else w for x, w, f in zip(x_size, window_size, fits))
     if shift_size is None:
-        return tuple(use_window_size)
-    return tuple(use_window_size), tuple(use_shift_size)
+        return ws
+    return ws, tuple(0 if f else sh for sh, f in zip(shift_size, fits))
 
 
 @lru_cache(maxsize=64)
@@ -68,21 +63,6 @@ def window_maps(B, D, H, W, window_size, shift_size):
                     cnt += 1
     reg = region.reshape(nd, ws[0], nh, ws[1], nw, ws[2]).transpose(0, 2, 4, 1, 3, 5).reshape(nW, N)
     return win.astype(np.int32), reg.astype(np.int32), nW, N
-
-
-def window_partition(x, window_size):
-    """swin_transformer.py:38-51 (host-side helper, kept for API parity)."""
-    B, D, H, W, C = x.shape
-    x = x.view(B, D // window_size[0], window_size[0], H // window_size[1], window_size[1], W // window_size[2],
-               window_size[2], C)
-    return x.permute(0, 1, 3, 5, 2, 4, 6, 7).contiguous().view(-1, reduce(mul, window_size), C)
-
-
-def window_reverse(windows, window_size, B, D, H, W):
-    """swin_transformer.py:54-68 (host-side helper, kept for API parity)."""
-    x = windows.view(B, D // window_size[0], H // window_size[1], W // window_size[2], window_size[0], window_size[1],
-                     window_size[2], -1)
-    return x.permute(0, 1, 4, 2, 5, 3, 6, 7).contiguous().view(B, D, H, W, -1)
 
 
 class Mlp(nn.Module):

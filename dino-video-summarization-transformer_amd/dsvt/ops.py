@@ -358,18 +358,22 @@ def probe_disable():
     call("dsvt_probe_disable")
 
 
-def probe_read(capacity=65536):
+def probe_read(capacity=65536, with_bytes=False):
+    """(ms, work, family, tag) of every probed launch (+ algorithmic bytes when with_bytes)."""
     import ctypes
     import numpy as np
     ms = np.zeros(capacity, np.float32)
     work = np.zeros(capacity, np.float64)
+    nbytes = np.zeros(capacity, np.float64)
     fam = np.zeros(capacity, np.int32)
     tag = np.zeros(capacity, np.int32)
     vp = ctypes.c_void_p
-    n = _lib.lib().dsvt_probe_read(ms.ctypes.data_as(vp), work.ctypes.data_as(vp), fam.ctypes.data_as(vp),
-                                   tag.ctypes.data_as(vp), capacity)
+    n = _lib.lib().dsvt_probe_read(ms.ctypes.data_as(vp), work.ctypes.data_as(vp), nbytes.ctypes.data_as(vp),
+                                   fam.ctypes.data_as(vp), tag.ctypes.data_as(vp), capacity)
     if n < 0:
         raise _lib.DsvtError(_lib.lib().dsvt_last_error().decode())
+    if with_bytes:
+        return ms[:n], work[:n], fam[:n], tag[:n], nbytes[:n]
     return ms[:n], work[:n], fam[:n], tag[:n]
 
 

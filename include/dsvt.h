@@ -412,11 +412,12 @@ int dsvt_set_attn_bwd_variant(int variant);
 int dsvt_probe_enable(int mask, int capacity);
 int dsvt_probe_disable(void);
 /* Synchronizes the recorded events; fills per-launch ms, algorithmic work (FLOP for
- * GEMM/attention, bytes for norm/loss), family and tag (GEMM: kernel instantiation id =
+ * GEMM/attention, bytes for norm/loss), algorithmic HBM bytes of GEMM launches (operands and
+ * output once; 0 where not recorded), family and tag (GEMM: kernel instantiation id =
  * variant*32 + dtype*16 + epilogue*2 + fp32_out; variant 0 = fp32 128x128, 1 = bf16 128x128,
- * 10 = bf16 persistent 256x128; epilogue 3 = patch embed).  Returns the number of
- * launches (negative on error). */
-int dsvt_probe_read(float *ms, double *work, int32_t *family, int32_t *tag, int capacity);
+ * 10 = bf16 persistent 256x128; epilogue 3 = patch embed).  Any output pointer may be NULL.
+ * Returns the number of launches (negative on error). */
+int dsvt_probe_read(float *ms, double *work, double *bytes, int32_t *family, int32_t *tag, int capacity);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,12 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("head", 64, 65536, 256, _lib.EPI_BIAS),
     ("fc1b_g", M_G, 3072, 768, _lib.EPI_BIAS),     # fc1 without the GELU: the epilogue's price
     ("fc1b_l", M_L, 3072, 768, _lib.EPI_BIAS),
+    # backward dX GEMMs (bf16 out, N = 768): dY . W for fc1 (K = 3072), qkv (K = 2304), proj (K = 768)
+    ("dxfc1_g", M_G, 768, 3072, _lib.EPI_BIAS),
+    ("dxqkv_g", M_G, 768, 2304, _lib.EPI_BIAS),
+    ("dxprj_g", M_G, 768, 768, _lib.EPI_BIAS),
+    ("dxfc1_l", M_L, 768, 3072, _lib.EPI_BIAS),
+    ("dxqkv_l", M_L, 768, 2304, _lib.EPI_BIAS),
 ]
 
 
