@@ -219,7 +219,9 @@ def train_bench(args, device, rank, world, steps, warmup):
                                                         gradient_as_bucket_view=True, broadcast_buffers=False)
     # the reference's defaults (train_ssl.py:50-151): lr 5e-4 scaled by clips * world / 256
     trainer = DINOTrainer(student, teacher, dino_loss, ddp=ddp, niter_per_ep=1000, epochs=100,
-                          batch_size_per_gpu=args.clips, world_size=world)
+                          batch_size_per_gpu=args.clips, world_size=world,
+                          concurrent_teacher=getattr(args, "concurrent_teacher", True))
+    student.concurrent_grad_groups = getattr(args, "concurrent_groups", False)
     crops = synthetic_crops(args.clips, device, seed=4321 + rank)
     for i in range(warmup):
         trainer.step(crops, 2000 + i)       # past warm-up / first epoch: the last layer trains too

@@ -71,7 +71,8 @@ struct WgradParams {
 };
 
 // ABL (diagnostic builds, tools/wgrad_bench.py only; 0 = normal): bit 0 no loads after the
-// prologue (stale stages), bit 1 no MFMA (fragments kept live), bit 2 no fragment reads
+// prologue (stale stages), bit 1 no MFMA (fragments kept live), bit 2 no fragment reads, bit 3
+// no X loads (vmcnt counts then off: timing only)
 template <int ABL = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[WG_NST * WG_STAGE];
@@ -108,8 +109,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
       m = m < p.M ? m : p.M - 1;                             // clamped; zeroed in registers
       __builtin_amdgcn_global_load_lds((const void*)(p.dy + m * p.ldy + cy[q]),
                                        LDS_PTR(base + (wave * 2 + q) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + cx[q]),
-                                       LDS_PTR(base + WG_OP + (wave * 2 + q) * 1024), 16, 0, 0);
+      if (!(ABL & 8))
+        __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + cx[q]),
+                                         LDS_PTR(base + WG_OP + (wave * 2 + q) * 1024), 16, 0, 0);
     }
   };
 
@@ -286,6 +288,7 @@ hipError_t launch_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t 
     case 3: wgrad_kernel<3><<<grid, 512, 0, s>>>(p); break;
     case 4: wgrad_kernel<4><<<grid, 512, 0, s>>>(p); break;
     case 6: wgrad_kernel<6><<<grid, 512, 0, s>>>(p); break;
+    case 14: wgrad_kernel<14><<<grid, 512, 0, s>>>(p); break;
     default: wgrad_kernel<0><<<grid, 512, 0, s>>>(p); break;
   }
   if (S > 1) {

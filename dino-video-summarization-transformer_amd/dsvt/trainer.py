@@ -29,12 +29,13 @@ class DINOTrainer:
     def __init__(self, student, teacher, dino_loss, lr=5e-4, min_lr=1e-6, weight_decay=0.04, weight_decay_end=0.4,
                  momentum_teacher=0.996, clip_grad=3.0, freeze_last_layer=1, epochs=100, niter_per_ep=1000,
                  warmup_epochs=10, n_global=2, ddp=None, batch_size_per_gpu=None, world_size=None,
-                 optimizer="dsvt"):
+                 optimizer="dsvt", concurrent_teacher=True):
         self.student = student                      # MultiCropWrapper (possibly DDP-wrapped: ddp)
         self.model = ddp if ddp is not None else student
         self.teacher = teacher
         self.dino_loss = dino_loss
         self.clip_grad = clip_grad
+        self.concurrent_teacher = concurrent_teacher
         self.freeze_last_layer = freeze_last_layer
         self.n_global = n_global
         self.niter_per_ep = niter_per_ep
@@ -73,9 +74,22 @@ class DINOTrainer:
             pg["lr"] = float(self.lr_schedule[it])
             if i == 0:
                 pg["weight_decay"] = float(self.wd_schedule[it])
-        s_out = self.model(images)                                 # :523
-        with torch.no_grad():
-            t_out = self.teacher(images[:self.n_global])           # :527 (teacher on global views)
+        if self.concurrent_teacher and images[0].is_cuda:
+            # the teacher forward (no grad, no RNG draws) is independent of the student's: it runs
+            # on its own stream, overlapping the student forward's GEMM tails and short kernels
+            from .utils import side_stream
+            main = torch.cuda.current_stream(images[0].device)
+            side = side_stream(images[0].device, "teacher")
+            side.wait_stream(main)
+            with torch.cuda.stream(side), torch.no_grad():
+                t_out = self.teacher(images[:self.n_global])       # :527 (teacher on global views)
+            s_out = self.model(images)                             # :523
+            main.wait_stream(side)
+            t_out.record_stream(main)
+        else:
+            s_out = self.model(images)                             # :523
+            with torch.no_grad():
+                t_out = self.teacher(images[:self.n_global])       # :527 (teacher on global views)
         loss = self.dino_loss(s_out, t_out, epoch)
         if check_finite and not math.isfinite(loss.item()):        # :530-532
             raise FloatingPointError("Loss is %s, stopping training" % loss.item())

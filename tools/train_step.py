@@ -18,6 +18,8 @@ if __name__ == "__main__":
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--clips", type=int, default=8)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--serial-teacher", dest="concurrent_teacher", action="store_false")
+    ap.add_argument("--concurrent-groups", dest="concurrent_groups", action="store_true")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     print(json.dumps(bench.train_bench(a, torch.device("cuda", 0), 0, 1, a.steps, a.warmup)), flush=True)
