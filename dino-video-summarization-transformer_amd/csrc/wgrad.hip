@@ -13,9 +13,8 @@
 // store.
 //
 // 256 x 256 output tile per 512-thread workgroup (8 waves, 2 (k) x 4 (n) of 128 x 64), one
-// workgroup per CU, a 4-stage LDS ring (128 KiB) with loads three stages ahead and counted
-// vmcnt waits; the two wave rows run one barrier apart so that every SIMD overlaps one wave's
-// transposed fragment reads with the other's MFMAs.  M is split over S slices so that tiles x S fills
+// workgroup per CU, a 4-stage LDS ring (128 KiB) with loads three stages ahead and a counted
+// vmcnt wait: one barrier per 32-row stage.  M is split over S slices so that tiles x S fills
 // the 256 CUs once; each slice writes an fp32 partial tile and wgrad_reduce_kernel sums the
 // slices in a fixed order into G (deterministic; `accumulate` adds to G's old value).  Work is
 // laid out slice-major over XCD-contiguous ranges (block b runs on XCD b % 8), so the tiles that
@@ -71,8 +70,9 @@ struct WgradParams {
 };
 
 // ABL (diagnostic builds, tools/wgrad_bench.py only; 0 = normal): bit 0 no loads after the
-// prologue (stale stages), bit 1 no MFMA (fragments kept live), bit 2 no fragment reads, bit 3
-// no X loads (vmcnt counts then off: timing only)
+// prologue (stale stages), bit 1 no MFMA (fragments kept live), bit 2 no fragment reads.
+// (Measured and dropped: staggering the two wave rows a barrier apart, 2 barriers per stage,
+// -4 %; staging X through registers beside the LDS-DMA of dY, -6 %.)
 template <int ABL = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[WG_NST * WG_STAGE];
@@ -109,9 +109,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
       m = m < p.M ? m : p.M - 1;                             // clamped; zeroed in registers
       __builtin_amdgcn_global_load_lds((const void*)(p.dy + m * p.ldy + cy[q]),
                                        LDS_PTR(base + (wave * 2 + q) * 1024), 16, 0, 0);
-      if (!(ABL & 8))
-        __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + cx[q]),
-                                         LDS_PTR(base + WG_OP + (wave * 2 + q) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + cx[q]),
+                                       LDS_PTR(base + WG_OP + (wave * 2 + q) * 1024), 16, 0, 0);
     }
   };
 
@@ -125,24 +124,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
   const bf2_t ones = {(__bf16)1.0f, (__bf16)1.0f};
 
   for (int i = 0; i < WG_NST - 1 && i < nst; ++i) stage(i, s_begin + i);
-  // own pieces of stage `u` landed: the stages issued after it (at most 2) may stay in flight
-  auto wait_stage = [&](int u) {
-    const int later = min(nst - 1, u + WG_NST - 2) - u;
-    if (later >= 2) wg_vm_wait<8>();
-    else if (later == 1) wg_vm_wait<4>();
-    else wg_vm_wait<0>();
-  };
-  wait_stage(0);
-  wg_barrier();
-  // the k-row-1 waves run one barrier behind: each SIMD holds one wave of each row, so the
-  // fragment reads of one overlap the MFMAs of the other (two barriers per stage: A after the
-  // reads, B after the MFMAs; a stage's loads are issued after B, into the buffer every wave
-  // finished reading before its A)
-  const bool lag = wk == 1;
-  if (lag) wg_barrier();
   // lane (r16, g) supplies row 4g + (r16 >> 2) (+16) and columns 4 (r16 & 3) of each 16-column block
   const int ra = 4 * g + (r16 >> 2), rb = ra + 16, cq = 4 * (r16 & 3);
   for (int it = 0; it < nst; ++it) {
+    const int later = min(nst - 1, it + WG_NST - 2) - it;   // stages issued beyond this one (<= 2)
+    if (later >= 2) wg_vm_wait<8>();
+    else if (later == 1) wg_vm_wait<4>();
+    else wg_vm_wait<0>();
+    wg_barrier();                 // stage `it` landed for every wave; stage it-1 read by every wave
     if (!(ABL & 1) && it + WG_NST - 1 < nst) stage((it + WG_NST - 1) & (WG_NST - 1), s_begin + it + WG_NST - 1);
     const char* ty = smem + (it & (WG_NST - 1)) * WG_STAGE;
     const char* tx = ty + WG_OP;
@@ -189,9 +178,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
         cs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.w), ones, s, false);
       }
     }
-    if (lag) wait_stage(it + 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // this stage's reads are done (ring reuse)
-    wg_barrier();                                             // A
     if constexpr ((ABL & 2) != 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(fa[i]));
@@ -205,10 +191,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    if (!lag) wait_stage(it + 1);
-    wg_barrier();                                             // B
   }
-  if (!lag) wg_barrier();                                     // balance the stagger barrier
 
   // lane holds G[n = n0 + wn*64 + 16 j + r16][k = k0 + wk*128 + 16 i + 4 g .. + 3]
   mfma_result_fence();
@@ -245,13 +228,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
   }
 }
 
-// dst (+)= sum over the S slices of the partials, in slice order (float4 per thread)
+// dst (+)= sum over the S slices of the partials, in slice order (float4 per thread); the
+// workgroups past `gblocks` do the same for the bias partials (one launch for both)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int64_t S, int64_t n4,
-                                                           float* __restrict__ dst, int accumulate) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+                                                           float* __restrict__ G, const float* __restrict__ dpart,
+                                                           int64_t d4, float* __restrict__ db, int gblocks,
+                                                           int accumulate) {
+  const bool bias = (int)blockIdx.x >= gblocks;
+  const float* src = bias ? dpart : part;
+  float* dst = bias ? db : G;
+  const int64_t n = bias ? d4 : n4;
+  const int64_t b0 = bias ? blockIdx.x - gblocks : blockIdx.x, nb = bias ? gridDim.x - gblocks : gblocks;
+  for (int64_t i = b0 * 256 + threadIdx.x; i < n; i += nb * 256) {
     float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t s = 0; s < S; ++s) {
-      const float4 v = reinterpret_cast<const float4*>(part)[s * n4 + i];
+      const float4 v = reinterpret_cast<const float4*>(src)[s * n + i];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
     reinterpret_cast<float4*>(dst)[i] = a;
@@ -288,16 +279,15 @@ hipError_t launch_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t 
     case 3: wgrad_kernel<3><<<grid, 512, 0, s>>>(p); break;
     case 4: wgrad_kernel<4><<<grid, 512, 0, s>>>(p); break;
     case 6: wgrad_kernel<6><<<grid, 512, 0, s>>>(p); break;
-    case 14: wgrad_kernel<14><<<grid, 512, 0, s>>>(p); break;
     default: wgrad_kernel<0><<<grid, 512, 0, s>>>(p); break;
   }
   if (S > 1) {
-    const int64_t n4 = N * K / 4;
-    unsigned blocks = (unsigned)((n4 + 255) / 256);
-    if (blocks > 2048) blocks = 2048;
-    wgrad_reduce_kernel<<<blocks, 256, 0, s>>>(partial, S, n4, G, accumulate);
-    if (db) wgrad_reduce_kernel<<<(unsigned)((N / 4 + 255) / 256), 256, 0, s>>>(partial + S * N * K, S, N / 4, db,
-                                                                                accumulate);
+    const int64_t n4 = N * K / 4, d4 = db ? N / 4 : 0;
+    int gblocks = (int)((n4 + 255) / 256);
+    if (gblocks > 2048) gblocks = 2048;
+    const int dblocks = (int)((d4 + 255) / 256);
+    wgrad_reduce_kernel<<<gblocks + dblocks, 256, 0, s>>>(partial, S, n4, G, partial + S * N * K, d4, db, gblocks,
+                                                          accumulate);
   }
   return hipGetLastError();
 }
