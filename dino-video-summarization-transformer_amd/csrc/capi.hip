@@ -156,6 +156,19 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t l
                 gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
 }
 
+int dsvt_gemm_resid_fwd(int dtype, const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                        const float* x_in, float* x_out, int64_t ldx, int64_t M, int64_t N, int64_t K, int64_t rpg,
+                        int64_t gstride, int64_t goff, void* stream) {
+  if (int e = check_gemm(dtype, EPI_RESID, A, lda, W, ldw, bias, x_out, ldx, M, N, K)) return e;
+  REQUIRE(x_in && aligned16(x_in), "gemm_resid: x_in must be a 16-byte aligned fp32 tensor");
+  norm_map(rpg, gstride, goff);
+  GemmParams p{A, lda, W, ldw, bias, x_out, ldx, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.resid = x_in;
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_resid_fwd",
+                [&] { return launch_gemm(p, dtype, EPI_RESID, 1, (hipStream_t)stream); },
+                gemm_tag(p, dtype, EPI_RESID, 1), gemm_bytes(dtype, EPI_RESID, 1, M, N, K));
+}
+
 int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const float* gamma, const float* beta,
                        int64_t rows, int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "layernorm: bad dtype");

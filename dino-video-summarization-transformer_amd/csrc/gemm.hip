@@ -132,7 +132,7 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
         add[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (CHECK && (!vrow[i] || n >= p.N)) continue;
         if constexpr (EPI == EPI_RESID) {
-          add[i][j] = *reinterpret_cast<const float4*>((const float*)p.out + orow[i] * p.ldo + n);
+          add[i][j] = *reinterpret_cast<const float4*>(resid_src(p) + orow[i] * p.ldo + n);
         } else {
           const int64_t rr = m % p.rpg;
           const int64_t np = rr / p.T, t = rr % p.T;

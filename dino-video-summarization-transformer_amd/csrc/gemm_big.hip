@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_big_kernel(GemmParams p)
         *reinterpret_cast<uint4*>(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n) = v;
       } else if constexpr (EPI == EPI_RESID) {
         float4* xo = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + orow * p.ldo + n);
-        float4 x = *xo;
+        float4 x = *reinterpret_cast<const float4*>(resid_src(p) + orow * p.ldo + n);
         x.x += __uint_as_float(v.x); x.y += __uint_as_float(v.y);
         x.z += __uint_as_float(v.z); x.w += __uint_as_float(v.w);
         *xo = x;

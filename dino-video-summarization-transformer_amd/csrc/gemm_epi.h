@@ -116,9 +116,10 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
         float4 x[2][NJ];
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii) {
-          xr[ii] = (float*)p.out + map_row(rbase + (i + ii) * 16 + r16, p.rpg, p.gstride, p.goff) * p.ldo + cbase + 4 * g;
+          const int64_t off = map_row(rbase + (i + ii) * 16 + r16, p.rpg, p.gstride, p.goff) * p.ldo + cbase + 4 * g;
+          xr[ii] = (float*)p.out + off;
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) x[ii][j] = *reinterpret_cast<const float4*>(xr[ii] + j * 16);
+          for (int j = 0; j < NJ; ++j) x[ii][j] = *reinterpret_cast<const float4*>(resid_src(p) + off + j * 16);
         }
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
@@ -174,7 +175,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           store4(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n, v0, v1, v2, v3);
         } else if constexpr (EPI == EPI_RESID) {
           float4* xo = reinterpret_cast<float4*>((float*)p.out + orow * p.ldo + n);
-          float4 x = *xo;
+          float4 x = *reinterpret_cast<const float4*>(resid_src(p) + orow * p.ldo + n);
           x.x += v0; x.y += v1; x.z += v2; x.w += v3;
           *xo = x;
         } else {  // EPI_PATCH

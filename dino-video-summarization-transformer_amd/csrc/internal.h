@@ -21,7 +21,15 @@ struct GemmParams {
   void* aux; int64_t ld_aux;
   // persistent 256x256 kernel: tile order, GM m-tile rows per group walked n-column-major (0 = row-major)
   int tile_group;
+  // EPI_RESID: the residual read (same row map and ldo as out); nullptr = out itself (in place)
+  const float* resid = nullptr;
 };
+
+// EPI_RESID residual source: out-of-place (training keeps the pre-sublayer X as its saved
+// activation) or the output rows themselves
+__host__ __device__ inline const float* resid_src(const GemmParams& p) {
+  return p.resid ? p.resid : (const float*)p.out;
+}
 
 // EPI_GELU_SAVE: out = GELU(acc + bias), aux = acc + bias (the pre-activation, for the backward)
 // EPI_DGELU:     out = acc * GELU'(aux)   (Mlp.fc1 backward through nn.GELU, bias ignored)

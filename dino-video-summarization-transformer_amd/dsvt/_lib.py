@@ -27,6 +27,7 @@ SIGNATURES = {
     "dsvt_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
     "dsvt_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
                              _i64, _i64, _i64, _p]),
+    "dsvt_gemm_resid_fwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "dsvt_gemm_resid_ln_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _f32,
                                       _p, _i32, _i64, _p]),
     "dsvt_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),

@@ -55,6 +55,23 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     return out
 
 
+def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None):
+    """x_out[row(m)] = x_in[row(m)] + a[m] . w^T + bias (fp32 token rows; out of place)."""
+    mode = w.dtype
+    _check(a, mode, "A")
+    _check(w, mode, "W")
+    _check(x_in, torch.float32, "x_in")
+    _check(x_out, torch.float32, "x_out")
+    if x_in.shape != x_out.shape:
+        raise _lib.DsvtError("gemm_resid: x_in %s and x_out %s differ" % (tuple(x_in.shape), tuple(x_out.shape)))
+    M = a.shape[0] if M is None else M
+    K = a.shape[-1]
+    rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+    call("dsvt_gemm_resid_fwd", _dt(mode), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias), _ptr(x_in), _ptr(x_out),
+         x_out.shape[-1], M, w.shape[0], K, rpg, gs, go, _stream())
+    return x_out
+
+
 def gemm_resid_ln(a, w, bias, X, M=None, rowmap=None, ln=None, Y=None, ymode=_lib.ROWLN_NONE, L=0):
     """X[row(m)] += a[m] . w^T + bias (fp32 X, N = 768), then (ymode != NONE) Y[yrow] =
     LayerNorm(X[row(m)]) in bf16 -- one full-row kernel (csrc/gemm_rowln.hip).  ln = the

@@ -203,8 +203,9 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
         S = _S()
         heads = blk.attn.num_heads
         ta = blk.temporal_attn
-        # ---- temporal (timesformer.py:127-137)
-        S.X0 = X.clone()
+        # ---- temporal (timesformer.py:127-137).  Each residual GEMM writes a NEW token tensor
+        # (out of place), so the pre-sublayer X the LayerNorm backward needs is kept, not copied
+        S.X0 = X
         S.a_t = torch.empty(R, C, device=dev, dtype=mode)
         ops.layernorm(X, R, C, blk.temporal_norm1.weight, blk.temporal_norm1.bias, blk.temporal_norm1.eps, S.a_t,
                       rowmap=patch_map, out_f32=False)
@@ -216,35 +217,38 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
         ops.gemm(S.o_t, w(ta.proj.weight), ta.proj.bias, S.u)
         if mk is not None:
             ops.row_scale(S.u, mk.t, T)                           # drop_path before temporal_fc
-        ops.gemm(S.u, w(blk.temporal_fc.weight), blk.temporal_fc.bias, X, epilogue=EPI_BIAS_RESID,
-                 rowmap=patch_map, M=R)
+        X = torch.empty_like(X)
+        X.view(B, L, C)[:, 0].copy_(S.X0.view(B, L, C)[:, 0])    # CLS rows: untouched by the temporal branch
+        ops.gemm_resid(S.u, w(blk.temporal_fc.weight), blk.temporal_fc.bias, S.X0, X, rowmap=patch_map, M=R)
         # ---- spatial with CLS replicate / mean (:139-181)
-        S.X1 = X.clone()
+        S.X1 = X
         S.a_s = torch.empty(rows, C, device=dev, dtype=mode)
         ops.layernorm(X, rows, C, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, S.a_s, out_f32=False)
         S.qkv_s = torch.empty(rows, 3 * C, device=dev, dtype=mode)
         ops.gemm(S.a_s, w(blk.attn.qkv.weight), blk.attn.qkv.bias, S.qkv_s)
         S.o_s = torch.empty(rows, C, device=dev, dtype=mode)
+        X = torch.empty_like(X)
         if mk is None:
             ops.attn_spatial(S.qkv_s, S.o_s, B, T, L, heads, blk.attn.scale, cls_ws)
-            ops.gemm(S.o_s, w(blk.attn.proj.weight), blk.attn.proj.bias, X, epilogue=EPI_BIAS_RESID)
+            ops.gemm_resid(S.o_s, w(blk.attn.proj.weight), blk.attn.proj.bias, S.X1, X)
         else:
             ops.attn_spatial_scaled(S.qkv_s, S.o_s, mk.s, B, T, L, heads, blk.attn.scale, cls_ws)
-            ops.gemm(S.o_s, w(blk.attn.proj.weight), None, X, epilogue=EPI_BIAS_RESID)
+            ops.gemm_resid(S.o_s, w(blk.attn.proj.weight), None, S.X1, X)
             ops.rowscale_bias_add(X, mk.s_rows, blk.attn.proj.bias)
         # ---- MLP (:184)
-        S.X2 = X.clone()
+        S.X2 = X
         S.a_m = torch.empty(rows, C, device=dev, dtype=mode)
         ops.layernorm(X, rows, C, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, S.a_m, out_f32=False)
         hid = blk.mlp.fc1.out_features
         S.pre = torch.empty(rows, hid, device=dev, dtype=mode)
         S.h = torch.empty(rows, hid, device=dev, dtype=mode)
         ops.gemm_aux(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, S.pre, EPI_GELU_SAVE)
+        X = torch.empty_like(X)
         if mk is None:
-            ops.gemm(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID)
+            ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, S.X2, X)
         else:
             ops.row_scale(S.h, mk.m, L)
-            ops.gemm(S.h, w(blk.mlp.fc2.weight), None, X, epilogue=EPI_BIAS_RESID)
+            ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), None, S.X2, X)
             ops.rowscale_bias_add(X, mk.m_rows, blk.mlp.fc2.bias)
         st.blocks.append(S)
     st.X = X

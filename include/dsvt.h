@@ -83,6 +83,14 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
 int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
                   int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N,
                   int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void *stream);
+/* Out-of-place residual GEMM (training forward): x_out[row(m)] = x_in[row(m)] + A[m] . W^T +
+ * bias, fp32 x_in / x_out with the same row map and row stride ldx, rows of x_out outside the
+ * map untouched.  The reference's `x = x + drop_path(sublayer(norm(x)))`
+ * (models/timesformer.py:133-135, 181, 184) with the pre-sublayer x kept intact for the
+ * LayerNorm backward instead of copied. */
+int dsvt_gemm_resid_fwd(int dtype, const void *A, int64_t lda, const void *W, int64_t ldw, const float *bias,
+                        const float *x_in, float *x_out, int64_t ldx, int64_t M, int64_t N, int64_t K,
+                        int64_t rpg, int64_t gstride, int64_t goff, void *stream);
 
 /* K7 + K3 fused, bf16 only, N = 768 (ViT-B): the residual projections attn.proj / temporal_fc /
  * mlp.fc2 with their residual add (models/timesformer.py:133-135, 181, 184) and the LayerNorm

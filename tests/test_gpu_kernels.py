@@ -141,6 +141,38 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8)])
+def test_gemm_resid_out_of_place(dtype, B, Np, T, gemm_variant):
+    """dsvt_gemm_resid_fwd: X_out[map] = X_in[map] + A.W^T + bias, bit-identical to the in-place
+    residual GEMM; X_in unchanged; X_out rows outside the map untouched (training forward)."""
+    from dsvt import ops
+    from dsvt._lib import EPI_BIAS_RESID
+    if dtype == torch.float32 and gemm_variant:
+        pytest.skip("variants are bf16-only")
+    C = 192
+    L, R = 1 + Np * T, B * Np * T
+    a, w, b = rnd((R, C), 14), rnd((C, C), 15, 0.05), rnd((C,), 16)
+    x0 = rnd((B * L, C), 17)
+    A, W, bias = to(a, dtype), to(w, dtype), to(b, torch.float32)
+    for rowmap, M in (((Np * T, L, 1), R), (None, None)):
+        if rowmap is None:
+            A = to(rnd((B * L, C), 18), dtype)
+        X_in = to(x0, torch.float32)
+        X_out = torch.full_like(X_in, 7.0)
+        ops.gemm_resid(A, W, bias, X_in, X_out, rowmap=rowmap, M=M)
+        X_ip = to(x0, torch.float32)
+        ops.gemm(A, W, bias, X_ip, epilogue=EPI_BIAS_RESID, rowmap=rowmap, M=M)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(back(X_in), x0)
+        if rowmap is None:
+            assert torch.equal(X_out, X_ip)
+        else:
+            rows = (np.arange(R) // (Np * T)) * L + 1 + np.arange(R) % (Np * T)
+            np.testing.assert_array_equal(back(X_out)[rows], back(X_ip)[rows])
+            assert np.all(back(X_out)[np.arange(B) * L] == 7.0)
+
+
 # ------------------------------------------------------------------ LayerNorm
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("C", [192, 384, 768])
