@@ -396,6 +396,22 @@ class VisionTransformer(nn.Module):
                        slot0=("split", stream_slot(dev)))
         return out
 
+    def forward_features_groups(self, groups):
+        """Training: the CLS features [sum B, C] of several resolution groups (each a list of clip
+        tensors of one shape, MultiCropWrapper order) through ONE autograd node, so the groups'
+        backward share one set of gradient buffers."""
+        from ..training import BackboneFn
+        args = []
+        for clips in groups:
+            shape = tuple(clips[0].shape[1:])
+            if any(tuple(c.shape[1:]) != shape for c in clips):
+                raise ValueError("all clips of one group must share (C, T, H, W)")
+            for c in clips:
+                self._check_supported(c)
+            Cin, T, H, W = shape
+            args.append(([(c, None, c.shape[0]) for c in clips], sum(c.shape[0] for c in clips), T, H, W, Cin))
+        return BackboneFn.apply(self, args, *self.parameters())
+
     def forward_frame_bank(self, frames, frame_index, B, T, get_all=False, out=None):
         """Clips gathered from a frame bank [F, Cin, H, W] by frame_index [B*T] int32 (-1 =
         zero frame) inside the patch-embed kernel (frame scoring: the per-frame local/global
@@ -410,7 +426,7 @@ class VisionTransformer(nn.Module):
             if get_all or get_attn:
                 raise NotImplementedError("get_all / get_attn are inference exports (no backward)")
             from ..training import BackboneFn
-            feats = BackboneFn.apply(self, srcs, B, T, H, W, Cin, *self.parameters())
+            feats = BackboneFn.apply(self, [(srcs, B, T, H, W, Cin)], *self.parameters())
             if out is not None:
                 with torch.no_grad():
                     out.copy_(feats)

@@ -127,19 +127,35 @@ class _S:
 
 # ================================================================================ backbone
 class BackboneFn(torch.autograd.Function):
+    """ONE autograd node for all resolution groups of a MultiCropWrapper call (`groups`: a list of
+    (srcs, B, T, H, W, Cin)): each group's forward saves its own activations; the backward runs
+    the groups into one set of gradient buffers (the second group accumulates inside the
+    weight-gradient / reduction kernels), so autograd has no per-parameter adds and the groups'
+    weight-gradient products share one side stream."""
+
     @staticmethod
-    def forward(ctx, model, srcs, B, T, H, W, Cin, *params):
-        feats, state = _backbone_forward(model, srcs, B, T, H, W, Cin)
-        ctx.model, ctx.state, ctx.params = model, state, params
-        return feats
+    def forward(ctx, model, groups, *params):
+        feats, states = [], []
+        for srcs, B, T, H, W, Cin in groups:      # in order: the DropPath masks are drawn per group
+            f, st = _backbone_forward(model, srcs, B, T, H, W, Cin)
+            feats.append(f)
+            states.append(st)
+        ctx.model, ctx.states, ctx.params = model, states, params
+        ctx.rows = [f.shape[0] for f in feats]
+        return feats[0] if len(feats) == 1 else torch.cat(feats)
 
     @staticmethod
     def backward(ctx, dfeat):
-        grads = _backbone_backward(ctx.model, ctx.state, dfeat.float().contiguous())
-        ctx.state = None
-        out = [None] * 7
+        model, dfeat = ctx.model, dfeat.float().contiguous()
+        G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None)
+        offs = np.cumsum([0] + ctx.rows)
+        for i in reversed(range(len(ctx.states))):
+            _backbone_backward(model, ctx.states[i], dfeat[offs[i]:offs[i + 1]], G)
+            ctx.states[i] = None
+        G.join()
+        out = [None, None]
         for p in ctx.params:
-            g = grads.get(p)
+            g = G.get(p)
             out.append(g if (g is not None and p.requires_grad) else None)
         return tuple(out)
 
@@ -257,15 +273,15 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
     return feats, st
 
 
-def _backbone_backward(model, st, dfeat):
+def _backbone_backward(model, st, dfeat, G):
+    """One group's backward into the gradient buffers G (written on first use, accumulated
+    after).  The weight gradients depend only on (dY, X) and nothing reads them before the
+    optimizer step: G runs them on a second stream, overlapping the dX chain (GEMM tails,
+    LayerNorm and attention backward, casts, the split-K reductions)."""
     mode, B, T, Np, L, C = st.mode, st.B, st.T, st.Np, st.L, st.C
     rows, R = B * L, B * Np * T
     dev = dfeat.device
     wt = model._wcache.transposed(mode)
-    # the weight gradients depend only on (dY, X) and nothing reads them before the optimizer
-    # step: they run on a second stream, overlapping the dX chain (GEMM tails, LayerNorm and
-    # attention backward, casts, the split-K reductions)
-    G = _Grads(side=_wgrad_stream(dev) if getattr(model, "dsvt_wgrad_stream", True) else None)
     patch_map = (Np * T, L, 1)
     # final norm on the CLS rows (timesformer.py:342-345)
     dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
@@ -333,7 +349,6 @@ def _backbone_backward(model, st, dfeat):
         wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
     ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
                   G.zeros(model.cls_token))
-    G.join()
     return G
 
 

@@ -119,6 +119,12 @@ class MultiCropWrapper(nn.Module):
             # DropPath masks are drawn in that order).  Group i > 0 is launched on its own stream
             # when concurrent_grad_groups: autograd runs each group's backward on its forward's stream,
             # so the groups overlap in the backward as well
+            if (len(idx_crops) > 1 and not kwargs and not self.concurrent_grad_groups
+                    and hasattr(self.backbone, "forward_features_groups") and self.backbone._grad_path()):
+                # dsvt: all groups through one autograd node (one set of gradient buffers)
+                bounds = [0] + idx_crops
+                feats = self.backbone.forward_features_groups([x[a:b] for a, b in zip(bounds[:-1], bounds[1:])])
+                return self.head(feats)
             outs, start = [], 0
             cur = torch.cuda.current_stream(x[0].device) if x[0].is_cuda else None
             # DDP's reducer hooks stay bound to the stream its AccumulateGrad nodes were made on:
