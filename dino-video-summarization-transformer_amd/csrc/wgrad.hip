@@ -249,11 +249,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
-// M-slices: tiles x S <= 256 workgroups (one per CU, one round), each slice >= 8 stages
+// M-slices: tiles x S <= 256 workgroups (one per CU, one round), each slice >= 8 stages, and
+// at most 8 slices: every slice adds an N x K fp32 partial written and re-read, and in the
+// training step these products run on a side stream beside the dX chain, so total traffic
+// counts more than filling the chip (train step: cap 8 > 6, 10, 12, 16 > uncapped (28 for the
+// 768 x 768 weights) > 4 > 2; tools/train_step.py, DSVT_WGRAD_MAXS)
 int64_t wgrad_slices(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
   const int64_t steps = (M + WG_BM - 1) / WG_BM;
+  static const int64_t max_s = getenv("DSVT_WGRAD_MAXS") ? atoll(getenv("DSVT_WGRAD_MAXS")) : 8;
   int64_t S = 256 / tiles;
+  if (S > max_s) S = max_s;
   if (S > steps / 8) S = steps / 8;
   return S < 1 ? 1 : S;
 }
