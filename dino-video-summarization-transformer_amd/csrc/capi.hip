@@ -511,6 +511,23 @@ int dsvt_gemm_aux_fwd(int dtype, int epilogue, int out_f32, const void* A, int64
                 gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
 }
 
+int dsvt_gemm_rowscale_fwd(int dtype, int epilogue, const void* A, int64_t lda, const void* W, int64_t ldw,
+                           const float* bias, void* out, int64_t ldo, void* aux, int64_t ld_aux, int64_t M, int64_t N,
+                           int64_t K, const float* row_scale, int64_t rs_group, void* stream) {
+  if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
+  REQUIRE(epilogue == DSVT_EPI_BIAS || epilogue == DSVT_EPI_GELU_SAVE, "gemm_rowscale: epilogue must be BIAS/GELU_SAVE");
+  REQUIRE(row_scale && rs_group > 0 && M < INT32_MAX, "gemm_rowscale: need row_scale and rs_group > 0");
+  REQUIRE(epilogue != DSVT_EPI_GELU_SAVE || (aux && ld_aux >= N && ld_aux % 4 == 0 && ((uintptr_t)aux & 7) == 0),
+          "gemm_rowscale: bad aux operand");
+  GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, INT64_MAX, 0, 0, nullptr, nullptr, nullptr, nullptr, 1,
+               aux, ld_aux};
+  p.row_scale = row_scale;
+  p.rs_group = rs_group;
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_rowscale_fwd",
+                [&] { return launch_gemm(p, dtype, epilogue, 0, (hipStream_t)stream); },
+                gemm_tag(p, dtype, epilogue, 0), gemm_bytes(dtype, epilogue, 0, M, N, K));
+}
+
 int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
                        int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* dgamma, float* dbeta,
                        int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {

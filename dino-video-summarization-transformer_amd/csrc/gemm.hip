@@ -146,6 +146,13 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
       }
     }
   }
+  float rsc[4];                        // DropPath row scales (EPI_BIAS / EPI_GELU_SAVE)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rsc[i] = 1.0f;
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE)
+      if (p.row_scale) rsc[i] = row_scale_of(p, m0 + wm * 64 + i * 16 + r16);
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (CHECK && !vrow[i]) continue;
@@ -160,6 +167,9 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
       }
       if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_SAVE) {
         v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+      }
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE) {
+        v0 *= rsc[i]; v1 *= rsc[i]; v2 *= rsc[i]; v3 *= rsc[i];
       }
       if constexpr (EPI == EPI_DGELU) {
         float pre[4];
@@ -271,6 +281,8 @@ void set_gemm_variant(int v) { g_gemm_variant = v; }
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
+  if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
+    return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (g_gemm_variant >= 20 && g_gemm_variant <= 29) return gemm_8ph_ok(p, epi) ? g_gemm_variant : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
     if (g_gemm_variant == 1 || g_gemm_variant == 9 || g_gemm_variant == 10) return g_gemm_variant;

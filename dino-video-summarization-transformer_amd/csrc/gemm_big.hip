@@ -401,7 +401,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
     }
     // ---- direct epilogue of tile (cm0, cn0)
     mfma_result_fence();
-    epilogue_direct<MI, NJ, EPI, OUT_F32>(p, acc, cm0 + wm * WTM, cn0 + wn * WTN, r16, g);
+    epilogue_direct<MI, NJ, EPI, OUT_F32, false, false, false, false, true>(p, acc, cm0 + wm * WTM, cn0 + wn * WTN,
+                                                                          r16, g);
     if (tn >= t_end) break;
     t = tn;
   }

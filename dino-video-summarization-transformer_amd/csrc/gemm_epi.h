@@ -26,11 +26,19 @@ __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int 
 // BIAS_IN_ACC: the accumulators started from the bias (gemm_8ph.hip), none is added here.
 // NOFAST: skip the full-tile 16-byte pair-store path (its cross-lane packing keeps more values
 // live; gemm_8ph.hip's GELU instantiation spills with it)
+// ROWSCALE: honour p.row_scale (EPI_BIAS / EPI_GELU_SAVE; the persistent kernel's instantiation)
 template <int MI, int NJ, int EPI, bool OUT_F32, bool NT = false, bool NOSTORE = false, bool BIAS_IN_ACC = false,
-          bool NOFAST = false>
+          bool NOFAST = false, bool ROWSCALE = false>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
+  constexpr bool RS = ROWSCALE && (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE);
+  float rsc[RS ? MI : 1];
+  const bool scaled = RS && p.row_scale != nullptr;          // workgroup-uniform
+  if constexpr (RS) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) rsc[i] = scaled ? row_scale_of(p, rbase + i * 16 + r16) : 1.0f;
+  }
   // bias: scalar loads for a full 64-column wave slab (no vmcnt wait behind the in-flight
   // prefetch of the next tile); per-lane vector loads only at a ragged N edge
   float4 bias4[NJ];
@@ -68,6 +76,10 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           store4((bf16_t*)p.aux + orow * p.ld_aux + n, v[0], v[1], v[2], v[3]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+          if constexpr (RS) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= rsc[i];
+          }
         } else {
           float pre[4];
           load4((const bf16_t*)p.aux + orow * p.ld_aux + n, pre);
@@ -97,6 +109,12 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           if constexpr (EPI == EPI_GELU) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+          }
+          if constexpr (RS) {
+            if (scaled) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[i][j][e] *= rsc[i];
+            }
           }
         }
 #pragma unroll
@@ -145,6 +163,10 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
       if constexpr (EPI == EPI_GELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+      }
+      if constexpr (RS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] *= rsc[i];
       }
     }
     if (m >= p.M) continue;

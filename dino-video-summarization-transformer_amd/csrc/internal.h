@@ -23,7 +23,18 @@ struct GemmParams {
   int tile_group;
   // EPI_RESID: the residual read (same row map and ldo as out); nullptr = out itself (in place)
   const float* resid = nullptr;
+  // EPI_BIAS / EPI_GELU_SAVE: output row m scaled by row_scale[m / rs_group] after the bias /
+  // GELU (DropPath's per-sample scale, models/vit_utils.py:152-167); the saved pre-activation
+  // is not scaled.  Only the 128x128 and persistent kernels take it (gemm_variant_for).
+  const float* row_scale = nullptr;
+  int64_t rs_group = 1;
 };
+
+// the DropPath scale of GEMM row m (1 when none)
+__device__ __forceinline__ float row_scale_of(const GemmParams& p, int64_t m) {
+  if (!p.row_scale || m >= p.M) return 1.0f;
+  return p.row_scale[(uint32_t)m / (uint32_t)p.rs_group];
+}
 
 // EPI_RESID residual source: out-of-place (training keeps the pre-sublayer X as its saved
 // activation) or the output rows themselves

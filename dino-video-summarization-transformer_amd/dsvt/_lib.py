@@ -51,6 +51,8 @@ SIGNATURES = {
     # backward / training
     "dsvt_gemm_aux_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64,
                                  _i64, _i64, _i64, _p]),
+    "dsvt_gemm_rowscale_fwd": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _p,
+                                      _i64, _p]),
     "dsvt_layernorm_bwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _p, _i32, _p, _i64,
                                   _p]),
     "dsvt_colsum_bwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _i32, _p, _i64, _p]),

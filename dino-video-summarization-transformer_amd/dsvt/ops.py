@@ -246,6 +246,22 @@ def gemm_aux(a, w, bias, out, aux, epilogue, out_f32=False, rowmap=None, M=None)
     return out
 
 
+def gemm_rowscale(a, w, bias, out, row_scale, group, aux=None, epilogue=_lib.EPI_BIAS):
+    """out[m] = (a[m] . w^T + bias) * row_scale[m // group] (EPI_BIAS), or with aux:
+    aux = a.w^T + b, out = GELU(aux) * row_scale[m // group] (EPI_GELU_SAVE)."""
+    mode = w.dtype
+    _check(a, mode, "A")
+    _check(w, mode, "W")
+    _check(row_scale, torch.float32, "row_scale")
+    M, K, N = a.shape[0], a.shape[-1], w.shape[0]
+    if row_scale.numel() * group < M:
+        raise _lib.DsvtError("gemm_rowscale: %d scales x group %d < %d rows" % (row_scale.numel(), group, M))
+    call("dsvt_gemm_rowscale_fwd", _dt(mode), epilogue, _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias), _ptr(out),
+         out.shape[-1], _ptr(aux), 0 if aux is None else aux.shape[-1], M, N, K, _ptr(row_scale), int(group),
+         _stream())
+    return out
+
+
 def layernorm_bwd(x, dy, gamma, eps, dx, rows, dgamma, dbeta, rowmap=None, accumulate=True):
     """dx[row(m)] += dLN(x[row(m)], dy[m]); dgamma / dbeta (+)= the affine-parameter grads."""
     C = x.shape[-1]

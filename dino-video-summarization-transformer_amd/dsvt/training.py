@@ -230,9 +230,10 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
         S.o_t = torch.empty(R, C, device=dev, dtype=mode)
         ops.attn_temporal(S.qkv_t, S.o_t, B * Np, T, heads, ta.scale)
         S.u = torch.empty(R, C, device=dev, dtype=mode)          # temporal_attn.proj output
-        ops.gemm(S.o_t, w(ta.proj.weight), ta.proj.bias, S.u)
-        if mk is not None:
-            ops.row_scale(S.u, mk.t, T)                           # drop_path before temporal_fc
+        if mk is None:
+            ops.gemm(S.o_t, w(ta.proj.weight), ta.proj.bias, S.u)
+        else:                                                    # drop_path before temporal_fc
+            ops.gemm_rowscale(S.o_t, w(ta.proj.weight), ta.proj.bias, S.u, mk.t, T)
         X = torch.empty_like(X)
         X.view(B, L, C)[:, 0].copy_(S.X0.view(B, L, C)[:, 0])    # CLS rows: untouched by the temporal branch
         ops.gemm_resid(S.u, w(blk.temporal_fc.weight), blk.temporal_fc.bias, S.X0, X, rowmap=patch_map, M=R)
@@ -258,12 +259,13 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
         hid = blk.mlp.fc1.out_features
         S.pre = torch.empty(rows, hid, device=dev, dtype=mode)
         S.h = torch.empty(rows, hid, device=dev, dtype=mode)
-        ops.gemm_aux(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, S.pre, EPI_GELU_SAVE)
         X = torch.empty_like(X)
         if mk is None:
+            ops.gemm_aux(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, S.pre, EPI_GELU_SAVE)
             ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, S.X2, X)
-        else:
-            ops.row_scale(S.h, mk.m, L)
+        else:                       # drop_path of the MLP branch: h scaled per sample (fc2 is linear)
+            ops.gemm_rowscale(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, mk.m, L, aux=S.pre,
+                              epilogue=EPI_GELU_SAVE)
             ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), None, S.X2, X)
             ops.rowscale_bias_add(X, mk.m_rows, blk.mlp.fc2.bias)
         st.blocks.append(S)
@@ -326,9 +328,10 @@ def _backbone_backward(model, st, dfeat, G):
         ops.cast_rows(dX, dY, R, rowmap=patch_map)
         wgrad(dY, S.u, G, blk.temporal_fc.weight, bias=blk.temporal_fc.bias)
         du = torch.empty(R, C, device=dev, dtype=mode)
-        ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
-        if mk is not None:
-            ops.row_scale(du, mk.t, T)
+        if mk is None:
+            ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
+        else:
+            ops.gemm_rowscale(dY, wt(blk.temporal_fc.weight), None, du, mk.t, T)
         wgrad(du, S.o_t, G, ta.proj.weight, bias=ta.proj.bias)
         do_t = torch.empty(R, C, device=dev, dtype=mode)
         ops.gemm(du, wt(ta.proj.weight), None, do_t)

@@ -230,6 +230,14 @@ int dsvt_gemm_aux_fwd(int dtype, int epilogue, int out_f32, const void *A, int64
                       int64_t ldw, const float *bias, void *out, int64_t ldo, void *aux, int64_t ld_aux,
                       int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
                       void *stream);
+/* dsvt_gemm_fwd (DSVT_EPI_BIAS, storage-dtype out) / dsvt_gemm_aux_fwd (DSVT_EPI_GELU_SAVE) with
+ * output row m scaled by row_scale[m / rs_group] after the bias / GELU -- the training
+ * DropPath of the sample that row belongs to (models/vit_utils.py:152-167; timesformer.py:
+ * 133 temporal branch before temporal_fc, :184 MLP branch); the saved pre-activation aux is
+ * not scaled.  No row map (rows are the GEMM's own). */
+int dsvt_gemm_rowscale_fwd(int dtype, int epilogue, const void *A, int64_t lda, const void *W, int64_t ldw,
+                           const float *bias, void *out, int64_t ldo, void *aux, int64_t ld_aux, int64_t M,
+                           int64_t N, int64_t K, const float *row_scale, int64_t rs_group, void *stream);
 /* nn.LayerNorm backward: dx[row(m)] += dLN(x[row(m)], dy[m]) (dx has x's layout: the residual
  * gradient of the pre-LN sub-layer), dgamma/dbeta (+)= column sums.  dy_dtype: storage dtype of
  * dy (DSVT_BF16 or DSVT_F32).  workspace >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, ., rows, 0, C). */

@@ -173,6 +173,36 @@ def test_gemm_resid_out_of_place(dtype, B, Np, T, gemm_variant):
             assert np.all(back(X_out)[np.arange(B) * L] == 7.0)
 
 
+@pytest.mark.parametrize("M,group", [(300, 7), (4000, 8), (4624, 289)])
+@pytest.mark.parametrize("epi", ["bias", "gelu_save"])
+def test_gemm_rowscale(M, group, epi):
+    """dsvt_gemm_rowscale_fwd (training DropPath fused into the GEMM epilogue) is bit-identical
+    to the unscaled GEMM followed by the row-scale kernel; the saved pre-activation is unscaled.
+    M = 300 runs the 128x128 kernel, the others the persistent one."""
+    from dsvt import ops
+    from dsvt._lib import EPI_BIAS, EPI_GELU_SAVE
+    C, N = 192, 256
+    A = to(rnd((M, C), 21), torch.bfloat16)
+    W = to(rnd((N, C), 22, 0.05), torch.bfloat16)
+    b = to(rnd((N,), 23), torch.float32)
+    ngroups = (M + group - 1) // group
+    sc = torch.from_numpy(np.floor(0.5 + np.random.default_rng(24).random(ngroups)).astype(np.float32) / 0.5).cuda()
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ref = torch.empty_like(out)
+    if epi == "bias":
+        ops.gemm_rowscale(A, W, b, out, sc, group)
+        ops.gemm(A, W, b, ref, epilogue=EPI_BIAS)
+    else:
+        aux, aux_ref = torch.empty_like(out), torch.empty_like(out)
+        ops.gemm_rowscale(A, W, b, out, sc, group, aux=aux, epilogue=EPI_GELU_SAVE)
+        ops.gemm_aux(A, W, b, ref, aux_ref, EPI_GELU_SAVE)
+    ops.row_scale(ref, sc, group)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    if epi != "bias":
+        assert torch.equal(aux, aux_ref)
+
+
 # ------------------------------------------------------------------ LayerNorm
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("C", [192, 384, 768])
