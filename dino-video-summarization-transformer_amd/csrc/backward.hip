@@ -1235,6 +1235,62 @@ hipError_t launch_cast_transpose(int dtype, const float* x, void* y, int64_t R, 
   return hipGetLastError();
 }
 
+// ================================================================ multi-tensor weight casts
+// The bf16 copies of a whole model's weights in ONE launch each (after every optimizer / EMA
+// step the weight cache refreshes them all): tensor i = src[i] (fp32, sizes[i] elements) ->
+// dst[i]; work items are (tensor, 4096-element chunk) pairs like the EMA's.
+__global__ __launch_bounds__(256) void cast_multi_kernel(const float* const* __restrict__ src,
+                                                         bf16_t* const* __restrict__ dst,
+                                                         const int64_t* __restrict__ sizes,
+                                                         const int32_t* __restrict__ ctensor,
+                                                         const int64_t* __restrict__ cstart) {
+  const int ti = ctensor[blockIdx.x];
+  const int64_t s0 = cstart[blockIdx.x], n = sizes[ti];
+  const float* x = src[ti];
+  bf16_t* y = dst[ti];
+  const int64_t end = s0 + 4096 < n ? s0 + 4096 : n;
+  for (int64_t i = s0 + threadIdx.x; i < end; i += 256) y[i] = f2bf(x[i]);
+}
+
+// W^T copies ([R, C] fp32 -> [C, R] bf16) of a tensor list: one 64 x 64 tile per workgroup,
+// tile table entries (tensor, row tile << 16 | column tile)
+__global__ __launch_bounds__(256) void cast_transpose_multi_kernel(const float* const* __restrict__ src,
+                                                                   bf16_t* const* __restrict__ dst,
+                                                                   const int64_t* __restrict__ rows,
+                                                                   const int64_t* __restrict__ cols,
+                                                                   const int32_t* __restrict__ tile_tensor,
+                                                                   const int32_t* __restrict__ tile_rc) {
+  __shared__ float tile[64][65];
+  const int ti = tile_tensor[blockIdx.x], rc = tile_rc[blockIdx.x];
+  const int64_t R = rows[ti], C = cols[ti], r0 = (int64_t)(rc >> 16) * 64, c0 = (int64_t)(rc & 0xffff) * 64;
+  const float* x = src[ti];
+  bf16_t* y = dst[ti];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? x[r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) y[c * R + r] = f2bf(tile[tx][i]);
+  }
+}
+
+hipError_t launch_cast_multi(const float* const* src, void* const* dst, const int64_t* sizes, const int32_t* ctensor,
+                             const int64_t* cstart, int64_t nchunks, hipStream_t s) {
+  cast_multi_kernel<<<(unsigned)nchunks, 256, 0, s>>>(src, (bf16_t* const*)dst, sizes, ctensor, cstart);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_transpose_multi(const float* const* src, void* const* dst, const int64_t* rows,
+                                       const int64_t* cols, const int32_t* tile_tensor, const int32_t* tile_rc,
+                                       int64_t ntiles, hipStream_t s) {
+  cast_transpose_multi_kernel<<<(unsigned)ntiles, 256, 0, s>>>(src, (bf16_t* const*)dst, rows, cols, tile_tensor,
+                                                               tile_rc);
+  return hipGetLastError();
+}
+
 // ================================================================ token-embedding gradients
 // Token gradient dX [B, L = 1 + Np*T, C] (NT order).  gn[n][c] = sum_{b,t} dX[b][1 + n*T + t][c],
 // gt[t][c] = sum_{b,n} dX[b][1 + n*T + t][c], gc[c] = sum_b dX[b][0][c].
@@ -1323,14 +1379,20 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* const* __restri
   if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// norms[i] = sqrt(sum of the tensor's chunk partials) (chunks of one tensor are contiguous)
-__global__ void chunk_norms_kernel(const float* __restrict__ partial, const int32_t* __restrict__ first_chunk,
-                                   int ntensors, float* __restrict__ norms) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= ntensors) return;
+// norms[i] = sqrt(sum of the tensor's chunk partials) (chunks of one tensor are contiguous):
+// one workgroup per tensor, lane-strided partial sums then a fixed-order tree (deterministic;
+// the head's 65536 x 256 last layer alone has 4096 chunks, a serial loop took 0.36 ms)
+__global__ __launch_bounds__(256) void chunk_norms_kernel(const float* __restrict__ partial,
+                                                          const int32_t* __restrict__ first_chunk, int ntensors,
+                                                          float* __restrict__ norms) {
+  __shared__ float red[4];
+  const int i = blockIdx.x;
   float a = 0.f;
-  for (int c = first_chunk[i]; c < first_chunk[i + 1]; ++c) a += partial[c];
-  norms[i] = sqrtf(a);
+  for (int c = first_chunk[i] + (int)threadIdx.x; c < first_chunk[i + 1]; c += 256) a += partial[c];
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) norms[i] = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
 }
 
 // utils/utils.py:102-111: clip_coef = clip / (norm + 1e-6); grad *= clip_coef if < 1
@@ -1392,7 +1454,7 @@ hipError_t launch_clip_grads(float* const* grads, const int64_t* sizes, const in
                              const int32_t* first_chunk, int64_t nchunks, int64_t ntensors, float clip, float* partial,
                              float* norms, hipStream_t s) {
   sumsq_kernel<<<(unsigned)nchunks, 256, 0, s>>>(grads, sizes, ctensor, cstart, partial);
-  chunk_norms_kernel<<<(unsigned)((ntensors + 255) / 256), 256, 0, s>>>(partial, first_chunk, (int)ntensors, norms);
+  chunk_norms_kernel<<<(unsigned)ntensors, 256, 0, s>>>(partial, first_chunk, (int)ntensors, norms);
   if (clip > 0.f) clip_scale_kernel<<<(unsigned)nchunks, 256, 0, s>>>(grads, sizes, ctensor, cstart, norms, clip);
   return hipGetLastError();
 }

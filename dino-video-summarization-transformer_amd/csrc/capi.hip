@@ -680,6 +680,20 @@ int dsvt_cast_transpose(int dtype, const float* x, void* y, int64_t R, int64_t C
   return e == hipSuccess ? 0 : hip_fail(e, "cast_transpose");
 }
 
+int dsvt_cast_multi(const float* const* src, void* const* dst, const int64_t* sizes, const int32_t* chunk_tensor,
+                    const int64_t* chunk_start, int64_t nchunks, void* stream) {
+  REQUIRE(src && dst && sizes && chunk_tensor && chunk_start && nchunks > 0, "cast_multi: bad args");
+  hipError_t e = launch_cast_multi(src, dst, sizes, chunk_tensor, chunk_start, nchunks, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "cast_multi");
+}
+
+int dsvt_cast_transpose_multi(const float* const* src, void* const* dst, const int64_t* rows, const int64_t* cols,
+                              const int32_t* tile_tensor, const int32_t* tile_rc, int64_t ntiles, void* stream) {
+  REQUIRE(src && dst && rows && cols && tile_tensor && tile_rc && ntiles > 0, "cast_transpose_multi: bad args");
+  hipError_t e = launch_cast_transpose_multi(src, dst, rows, cols, tile_tensor, tile_rc, ntiles, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "cast_transpose_multi");
+}
+
 int dsvt_embed_bwd(const float* dX, int64_t B, int64_t Np, int64_t T, int64_t C, const int32_t* pos_index,
                    const int32_t* time_index, float* dpos, float* dtime, float* dcls, void* workspace,
                    int64_t workspace_bytes, void* stream) {

@@ -70,6 +70,13 @@ struct RowLnParams {
 };
 hipError_t launch_gemm_rowln(const RowLnParams& p, hipStream_t s);
 
+// multi-tensor bf16 weight copies (backward.hip)
+hipError_t launch_cast_multi(const float* const* src, void* const* dst, const int64_t* sizes, const int32_t* ctensor,
+                             const int64_t* cstart, int64_t nchunks, hipStream_t s);
+hipError_t launch_cast_transpose_multi(const float* const* src, void* const* dst, const int64_t* rows,
+                                       const int64_t* cols, const int32_t* tile_tensor, const int32_t* tile_rc,
+                                       int64_t ntiles, hipStream_t s);
+
 // Weight gradients (wgrad.hip): G[n, k] (+)= sum_m dY[m, n] X[m, k] and optionally
 // db[n] (+)= sum_m dY[m, n], bf16 in, fp32 out
 int64_t wgrad_slices(int64_t M, int64_t N, int64_t K);

@@ -67,6 +67,8 @@ SIGNATURES = {
     "dsvt_rowscale_bias_add": (_i32, [_p, _i64, _i64, _p, _p, _p]),
     "dsvt_cast_transpose": (_i32, [_i32, _p, _p, _i64, _i64, _p]),
     "dsvt_embed_bwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
+    "dsvt_cast_multi": (_i32, [_p, _p, _p, _p, _p, _i64, _p]),
+    "dsvt_cast_transpose_multi": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),
     "dsvt_ema": (_i32, [_p, _p, _p, _p, _p, _i64, _f32, _p]),
     "dsvt_clip_grads": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _f32, _p, _p, _i64, _p]),
     "dsvt_wgrad_bwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i32, _p, _i64, _p]),

@@ -293,8 +293,7 @@ class VisionTransformer(nn.Module):
         if not self.pos_embed.is_cuda:
             return
         mode = self.dsvt_dtype
-        w = self._wcache.getter(mode)
-        w(self.patch_embed.proj.weight, flat=True)
+        ws = [self.patch_embed.proj.weight]
         for blk in self.blocks:
             lins = [blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2]
             if blk.attention_type == 'divided_space_time':
@@ -303,8 +302,8 @@ class VisionTransformer(nn.Module):
                     self._wcache.folded(mode, blk.temporal_fc, blk.temporal_attn.proj)
                 else:
                     lins += [blk.temporal_attn.proj, blk.temporal_fc]
-            for lin in lins:
-                w(lin.weight)
+            ws += [lin.weight for lin in lins]
+        self._wcache.refresh(ws, mode, flat={id(self.patch_embed.proj.weight)})   # one launch
 
     def _indices(self, Hp, Wp, T, device):
         key = (Hp, Wp, T, device)

@@ -160,6 +160,16 @@ class BackboneFn(torch.autograd.Function):
         return tuple(out)
 
 
+def _block_weights(model):
+    """The Linear weights of every divided block the training path multiplies by."""
+    ws = []
+    for blk in model.blocks:
+        ta = blk.temporal_attn
+        ws += [ta.qkv.weight, ta.proj.weight, blk.temporal_fc.weight, blk.attn.qkv.weight, blk.attn.proj.weight,
+               blk.mlp.fc1.weight, blk.mlp.fc2.weight]
+    return ws
+
+
 def _masks(model, nblk, B, Np, T, L, device):
     """DropPath scales for each block (None when inactive): temporal [B*Np], spatial [B*T]
     (+ per-X-row bias scale [B*L]), MLP [B] (+ [B*L])."""
@@ -188,6 +198,8 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
         raise NotImplementedError("dsvt backward is implemented for divided space-time attention (the DINO-SVT "
                                   "path); got %s" % model.attention_type)
     mode = model.dsvt_dtype
+    model._wcache.refresh(_block_weights(model) + [model.patch_embed.proj.weight], mode,
+                          flat={id(model.patch_embed.proj.weight)})       # all stale bf16 copies, one launch
     w = model._wcache.getter(mode)
     Hp, Wp = H // 16, W // 16
     Np, C = Hp * Wp, model.embed_dim
@@ -283,6 +295,7 @@ def _backbone_backward(model, st, dfeat, G):
     mode, B, T, Np, L, C = st.mode, st.B, st.T, st.Np, st.L, st.C
     rows, R = B * L, B * Np * T
     dev = dfeat.device
+    model._wcache.refresh(_block_weights(model), mode, transposed=True)   # all stale W^T copies, one launch
     wt = model._wcache.transposed(mode)
     patch_map = (Np * T, L, 1)
     # final norm on the CLS rows (timesformer.py:342-345)

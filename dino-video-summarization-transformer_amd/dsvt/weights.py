@@ -19,6 +19,7 @@ from ._lib import DsvtError
 class WeightCache:
     def __init__(self):
         self._c = {}
+        self._tables = {}          # multi-tensor pointer / chunk tables of refresh(), by (src, dst) list
 
     @staticmethod
     def _sync(ent):
@@ -133,5 +134,72 @@ class WeightCache:
         self._c[key] = (stamp, (w, b32)) + self._event()
         return w, b32
 
+    def refresh(self, params, mode, transposed=False, flat=()):
+        """Bring the storage-dtype copies (transposed: the W^T copies) of many parameters up to
+        date in ONE multi-tensor launch instead of one cast per weight -- after every optimizer
+        / EMA step all of a model's copies are stale at once.  `flat`: ids of parameters used
+        flattened to [rows, -1] (the patch-embedding conv).  Stale copies are rewritten in
+        place (their previous readers are ordered before this stream's current position: the
+        step's side streams joined it before the optimizer ran)."""
+        if mode == torch.float32 or not params:
+            return
+        stale = []
+        for p in params:
+            fl = id(p) in flat
+            key = (id(p), "T", mode) if transposed else (id(p), fl)
+            ent = self._c.get(key)
+            if ent is not None and ent[0] == p._version and ent[1] == p.data_ptr():
+                continue
+            t = p.detach()
+            if fl:
+                t = t.reshape(t.shape[0], -1)
+            if t.dtype != torch.float32 or not t.is_contiguous() or (transposed and t.dim() != 2):
+                raise TypeError("dsvt expects contiguous fp32 master weights, got %s %s" % (t.dtype, tuple(t.shape)))
+            shape = (t.shape[1], t.shape[0]) if transposed else tuple(t.shape)
+            out = ent[2] if (ent is not None and tuple(ent[2].shape) == shape and ent[2].dtype == mode) else \
+                torch.empty(shape, device=t.device, dtype=mode)
+            stale.append((key, p, t, out))
+        if not stale:
+            return
+        from ._lib import call
+        tkey = (transposed,) + tuple((t.data_ptr(), o.data_ptr(), tuple(t.shape)) for _, _, t, o in stale)
+        tables = self._tables.get(tkey)
+        dev = stale[0][2].device
+        if tables is None:
+            src = torch.tensor([t.data_ptr() for _, _, t, _ in stale], dtype=torch.int64, device=dev)
+            dst = torch.tensor([o.data_ptr() for _, _, _, o in stale], dtype=torch.int64, device=dev)
+            if transposed:
+                rows = [t.shape[0] for _, _, t, _ in stale]
+                cols = [t.shape[1] for _, _, t, _ in stale]
+                tt, rc = [], []
+                for i, (r, c) in enumerate(zip(rows, cols)):
+                    for a in range((r + 63) // 64):
+                        for b in range((c + 63) // 64):
+                            tt.append(i)
+                            rc.append((a << 16) | b)
+                tables = (src, dst, torch.tensor(rows, dtype=torch.int64, device=dev),
+                          torch.tensor(cols, dtype=torch.int64, device=dev),
+                          torch.tensor(tt, dtype=torch.int32, device=dev),
+                          torch.tensor(rc, dtype=torch.int32, device=dev), len(tt))
+            else:
+                from .training import TensorList
+                tl = TensorList([t for _, _, t, _ in stale], dev)
+                tables = (src, dst, tl.sizes, tl.ctensor, tl.cstart, tl.nchunks)
+            if len(self._tables) > 16:
+                self._tables.pop(next(iter(self._tables)))
+            self._tables[tkey] = tables
+        if transposed:
+            src, dst, rows, cols, tt, rc, n = tables
+            call("dsvt_cast_transpose_multi", src.data_ptr(), dst.data_ptr(), rows.data_ptr(), cols.data_ptr(),
+                 tt.data_ptr(), rc.data_ptr(), n, ops._stream())
+        else:
+            src, dst, sizes, ct, cs, n = tables
+            call("dsvt_cast_multi", src.data_ptr(), dst.data_ptr(), sizes.data_ptr(), ct.data_ptr(), cs.data_ptr(),
+                 n, ops._stream())
+        ev = self._event()
+        for key, p, _, out in stale:
+            self._c[key] = (p._version, p.data_ptr(), out) + ev
+
     def clear(self):
         self._c.clear()
+        self._tables.clear()

@@ -296,6 +296,16 @@ int dsvt_embed_bwd(const float *dX, int64_t B, int64_t Np, int64_t T, int64_t C,
  * EMA: teacher = m*teacher + (1-m)*student (train_ssl.py:555-558).  clip: per-tensor L2 norms
  * (norms[ntensors]), grads *= clip/(norm+1e-6) where that is < 1 (utils/utils.py:102-111;
  * clip <= 0: norms only); first_chunk[ntensors+1] = chunk ranges; workspace >= nchunks*4 B. */
+/* bf16 copies of a list of fp32 tensors in one launch (the weight cache's refresh after an
+ * optimizer / EMA step): dst[i][j] = bf16(src[i][j]); chunk tables as dsvt_ema. */
+int dsvt_cast_multi(const float *const *src, void *const *dst, const int64_t *sizes,
+                    const int32_t *chunk_tensor, const int64_t *chunk_start, int64_t nchunks, void *stream);
+/* bf16 transposed copies W^T [cols, rows] of fp32 matrices [rows, cols] in one launch (the B
+ * operands of the backward's dX = dY . W GEMMs): one 64 x 64 tile per entry of
+ * (tile_tensor[t], tile_rc[t] = row_tile << 16 | col_tile). */
+int dsvt_cast_transpose_multi(const float *const *src, void *const *dst, const int64_t *rows,
+                              const int64_t *cols, const int32_t *tile_tensor, const int32_t *tile_rc,
+                              int64_t ntiles, void *stream);
 int dsvt_ema(float *const *teacher, const float *const *student, const int64_t *sizes,
              const int32_t *chunk_tensor, const int64_t *chunk_start, int64_t nchunks, float momentum,
              void *stream);

@@ -203,6 +203,41 @@ def test_gemm_rowscale(M, group, epi):
         assert torch.equal(aux, aux_ref)
 
 
+def test_weight_cache_refresh_multi():
+    """WeightCache.refresh (one multi-tensor launch) makes the same bf16 copies and W^T copies as
+    the per-weight cast / cast-transpose kernels, refreshes only stale entries, and rewrites a
+    stale copy in place."""
+    from dsvt import ops
+    from dsvt.weights import WeightCache
+    shapes = [(768, 768), (2304, 768), (3072, 768), (768, 3072), (40, 72), (768, 3, 16, 16)]
+    ps = [torch.nn.Parameter(to(rnd(sh, 30 + i), torch.float32)) for i, sh in enumerate(shapes)]
+    flat = {id(ps[-1])}
+    wc = WeightCache()
+    wc.refresh(ps, torch.bfloat16, flat=flat)
+    mats = [p for p in ps if p.dim() == 2]
+    wc.refresh(mats, torch.bfloat16, transposed=True)
+    get, get_t = wc.getter(torch.bfloat16), wc.transposed(torch.bfloat16)
+    for p in ps:
+        t = p.detach().reshape(p.shape[0], -1)
+        ref = torch.empty(t.shape, device="cuda", dtype=torch.bfloat16)
+        ops.cast(t.contiguous(), ref)
+        assert torch.equal(get(p, flat=id(p) in flat), ref)
+    for p in mats:
+        ref = torch.empty(p.shape[1], p.shape[0], device="cuda", dtype=torch.bfloat16)
+        ops.cast_transpose(p.detach(), ref)
+        assert torch.equal(get_t(p), ref)
+    old = get(ps[0])
+    with torch.no_grad():
+        ps[0].mul_(0.5)                       # bumps the version: stale
+    wc.refresh(ps, torch.bfloat16, flat=flat)
+    new = get(ps[0])
+    assert new.data_ptr() == old.data_ptr()   # rewritten in place
+    ref = torch.empty(ps[0].shape, device="cuda", dtype=torch.bfloat16)
+    ops.cast(ps[0].detach(), ref)
+    torch.cuda.synchronize()
+    assert torch.equal(new, ref)
+
+
 # ------------------------------------------------------------------ LayerNorm
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("C", [192, 384, 768])
