@@ -215,8 +215,10 @@ def train_bench(args, device, rank, world, steps, warmup):
     teacher.eval()          # the reference never sets eval on the teacher (SURVEY §5 defect 2); dsvt does
     ddp = None
     if world > 1:
-        ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[device.index],
-                                                        gradient_as_bucket_view=True, broadcast_buffers=False)
+        # the head on DDP's reducer, the backbone's gradients in per-block buckets all-reduced
+        # under its own backward (dist.BlockGradReducer)
+        ddp = ddist.wrap_ddp(student, device, overlap=getattr(args, "grad_overlap", True),
+                             gradient_as_bucket_view=True)
     # the reference's defaults (train_ssl.py:50-151): lr 5e-4 scaled by clips * world / 256
     trainer = DINOTrainer(student, teacher, dino_loss, ddp=ddp, niter_per_ep=1000, epochs=100,
                           batch_size_per_gpu=args.clips, world_size=world,
@@ -249,8 +251,10 @@ def train_bench(args, device, rank, world, steps, warmup):
             "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3), "gflop_per_clip": round(clip_gf, 1),
             "tflops_per_gpu": round(value * clip_gf / 1e3 / world, 1), "loss": round(loss_val, 5),
-            "parallelism": ("dp%d (DDP, %s bucketed all-reduce)" % (world, "RCCL" if ddist.backend() == "nccl"
-                                                                      else ddist.backend())) if world > 1 else "dp1",
+            "parallelism": ("dp%d (%s bucketed all-reduce, %s)" % (
+                world, "RCCL" if ddist.backend() == "nccl" else ddist.backend(),
+                "backbone per-block buckets overlapped with its backward + DDP head"
+                if getattr(args, "grad_overlap", True) else "DDP")) if world > 1 else "dp1",
             "optimizer": "dsvt AdamW (multi-tensor HIP kernel)",
             "drop_path": 0.1, "teacher_mode": "eval"}
 
@@ -383,6 +387,8 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
     ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--no-grad-overlap", dest="grad_overlap", action="store_false",
+                    help="train leg at N>1: plain DDP over the whole student (no per-block backbone buckets)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' only to rehearse "
                          "several ranks on one GPU with --shared-gpu)")

@@ -73,3 +73,100 @@ def shard_range(n, rank, world):
     q, r = divmod(n, world)
     lo = rank * q + min(rank, r)
     return lo, lo + q + (1 if rank < r else 0)
+
+
+class BlockGradReducer:
+    """Bucketed gradient all-reduce of the dsvt backbone, overlapped with its backward.
+
+    The reference wraps the whole student in DDP (train_ssl.py:329), whose reducer all-reduces
+    25 MB buckets as AccumulateGrad hooks fire during the backward.  The dsvt backbone backward
+    is ONE autograd node (training.BackboneFn: all resolution groups, all blocks), so under plain
+    DDP every backbone gradient becomes ready at once, at the very end, and ~86 M fp32 gradients
+    are all-reduced after the compute instead of under it.  This reducer takes the backbone's
+    parameters away from DDP (wrap_ddp: DDP keeps the DINO head) and lays their gradients out
+    in one flat fp32 arena, one bucket per divided block (7.1 M values = 28 MB at ViT-B, DDP's
+    bucket size) plus one for the embeddings and the final norm.  The backbone backward hands
+    the arena views out as its gradient buffers and calls `launch(k)` as soon as block k's
+    gradients are final (after the LAST resolution group's pass over it); the bucket's
+    all-reduce is issued on the weight-gradient stream, so RCCL runs it while the dX chain of
+    the blocks below continues.  `finish()` waits for all buckets (the averaging is RCCL's AVG;
+    gloo sums and the arena is divided once).  Gradients equal DDP's: the bucket-wise average
+    of the same fp32 per-rank gradients."""
+
+    def __init__(self, backbone, group=None, ddp=None):
+        self.bb, self.group, self.ddp = backbone, group, ddp
+        self.world = dist.get_world_size(group)
+        self.avg = dist.get_backend(group) == "nccl"
+        self._works, self._arena = [], None
+        backbone.dsvt_grad_reducer = self
+
+    def params(self):
+        """Backbone parameters that take gradients, per bucket: blocks 0..depth-1, then the rest."""
+        buckets = [[p for p in blk.parameters() if p.requires_grad] for blk in self.bb.blocks]
+        seen = {id(p) for b in buckets for p in b}
+        buckets.append([p for p in self.bb.parameters() if p.requires_grad and id(p) not in seen])
+        return buckets
+
+    def active(self):
+        """False inside DDP's no_sync() (gradient accumulation without communication)."""
+        return self.ddp is None or getattr(self.ddp, "require_backward_grad_sync", True)
+
+    def arena(self, device):
+        """A fresh flat fp32 arena for this backward (the returned views become p.grad) and the
+        id(p) -> view map the gradient buffers come from.  Offsets are 256-byte aligned."""
+        buckets = self.params()
+        sizes = [[(p.numel() + 63) // 64 * 64 for p in b] for b in buckets]
+        flat = torch.empty(sum(sum(s) for s in sizes), device=device, dtype=torch.float32)
+        views, self._slices, off = {}, [], 0
+        for b, s in zip(buckets, sizes):
+            start = off
+            for p, n in zip(b, s):
+                views[id(p)] = flat[off:off + p.numel()].view(p.shape)
+                off += n
+            self._slices.append(flat[start:off])
+        self._arena, self._works = flat, []
+        return views
+
+    def launch(self, k, side=None):
+        """Start bucket k's all-reduce once everything queued so far (on the current stream and on
+        `side`) has produced it; issued on `side` when given, so it overlaps the current stream."""
+        buf = self._slices[k]
+        if buf.numel() == 0:
+            return
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        if side is None:
+            self._works.append(dist.all_reduce(buf, op=op, group=self.group, async_op=True))
+            return
+        side.wait_stream(torch.cuda.current_stream(buf.device))
+        with torch.cuda.stream(side):
+            self._works.append(dist.all_reduce(buf, op=op, group=self.group, async_op=True))
+
+    def finish(self):
+        """The current stream waits for every bucket; gloo's sums become averages."""
+        for w in self._works:
+            w.wait()
+        if not self.avg and self._arena is not None:
+            self._arena.div_(self.world)
+        self._works, self._arena, self._slices = [], None, []
+
+
+def wrap_ddp(student, device, overlap=True, **ddp_kw):
+    """DDP over a MultiCropWrapper(dsvt backbone, head) the way train_ssl.py:329 does, with the
+    backbone's gradients all-reduced bucket by bucket under its own backward (BlockGradReducer)
+    when `overlap`; DDP then owns only the head's parameters.  The backbone's parameters and
+    buffers are broadcast from rank 0 like DDP's own initial sync."""
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    ddp_kw.setdefault("broadcast_buffers", False)
+    if device is not None and torch.device(device).type == "cuda":
+        ddp_kw.setdefault("device_ids", [torch.device(device).index])
+    bb = getattr(student, "backbone", None)
+    if not overlap or bb is None or not hasattr(bb, "blocks"):
+        return DDP(student, **ddp_kw)
+    names = ["backbone." + n for n, _ in bb.named_parameters()] + ["backbone." + n for n, _ in bb.named_buffers()]
+    DDP._set_params_and_buffers_to_ignore_for_model(student, names)
+    with torch.no_grad():
+        for t in list(bb.parameters()) + list(bb.buffers()):
+            dist.broadcast(t.data, 0)
+    ddp = DDP(student, **ddp_kw)
+    BlockGradReducer(bb, ddp=ddp)
+    return ddp

@@ -61,9 +61,10 @@ class _Grads:
     buffer and whether it already holds a partial sum (False on the first write: the kernels
     then overwrite instead of accumulating, so no zero fill is needed)."""
 
-    def __init__(self, side=None):
+    def __init__(self, side=None, arena=None):
         self.g = {}
         self.side = side               # weight gradients on this stream (None: the current one)
+        self.arena = arena or {}       # id(p) -> preassigned buffer (dist.BlockGradReducer buckets)
         self._main = None
 
     def run_side(self, fn, inputs):
@@ -89,7 +90,10 @@ class _Grads:
     def acc(self, p):
         buf = self.g.get(id(p))
         if buf is None:
-            buf = self.g[id(p)] = torch.empty(p.shape, device=p.device, dtype=torch.float32)
+            buf = self.arena.get(id(p))
+            if buf is None:
+                buf = torch.empty(p.shape, device=p.device, dtype=torch.float32)
+            self.g[id(p)] = buf
             return buf, False
         return buf, True
 
@@ -147,11 +151,20 @@ class BackboneFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dfeat):
         model, dfeat = ctx.model, dfeat.float().contiguous()
-        G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None)
+        red = getattr(model, "dsvt_grad_reducer", None)         # data-parallel: dist.BlockGradReducer
+        if red is not None and not red.active():
+            red = None
+        G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None,
+                   arena=red.arena(dfeat.device) if red is not None else None)
         offs = np.cumsum([0] + ctx.rows)
         for i in reversed(range(len(ctx.states))):
-            _backbone_backward(model, ctx.states[i], dfeat[offs[i]:offs[i + 1]], G)
+            # a block's gradients are final after the last group's pass over it: its bucket's
+            # all-reduce starts then, under the backward of the blocks below
+            ready = (lambda k: red.launch(k, G.side)) if (red is not None and i == 0) else None
+            _backbone_backward(model, ctx.states[i], dfeat[offs[i]:offs[i + 1]], G, ready)
             ctx.states[i] = None
+        if red is not None:
+            red.finish()
         G.join()
         out = [None, None]
         for p in ctx.params:
@@ -287,11 +300,12 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
     return feats, st
 
 
-def _backbone_backward(model, st, dfeat, G):
+def _backbone_backward(model, st, dfeat, G, ready=None):
     """One group's backward into the gradient buffers G (written on first use, accumulated
     after).  The weight gradients depend only on (dY, X) and nothing reads them before the
     optimizer step: G runs them on a second stream, overlapping the dX chain (GEMM tails,
-    LayerNorm and attention backward, casts, the split-K reductions)."""
+    LayerNorm and attention backward, casts, the split-K reductions).  `ready(k)` is called when
+    block k's gradients are complete (k = depth: the embeddings and the final norm)."""
     mode, B, T, Np, L, C = st.mode, st.B, st.T, st.Np, st.L, st.C
     rows, R = B * L, B * Np * T
     dev = dfeat.device
@@ -301,7 +315,9 @@ def _backbone_backward(model, st, dfeat, G):
     # final norm on the CLS rows (timesformer.py:342-345)
     dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
     _ln_bwd(st.X, dfeat, model.norm, dX, B, G, rowmap=(1, L, 0))
-    for blk, S, mk in zip(reversed(model.blocks), reversed(st.blocks), reversed(st.masks)):
+    depth = len(model.blocks)
+    for bi, blk, S, mk in zip(range(depth - 1, -1, -1), reversed(model.blocks), reversed(st.blocks),
+                              reversed(st.masks)):
         heads = blk.attn.num_heads
         ta = blk.temporal_attn
         # ---- MLP
@@ -323,7 +339,9 @@ def _backbone_backward(model, st, dfeat, G):
         ops.gemm(dpre, wt(fc1.weight), None, da)
         del dpre
         _ln_bwd(S.X2, da, blk.norm2, dX, rows, G)
-        # ---- spatial
+        # ---- spatial: a fresh buffer, not dXb again -- the fc2 weight gradient may still be
+        # reading dXb on the side stream (record_stream guards reuse after free, not rewrites)
+        dXb = torch.empty(rows, C, device=dev, dtype=mode)
         ops.cast_rows(dX, dXb, rows)
         wgrad(dXb, S.o_s, G, blk.attn.proj.weight)
         _colsum(dX, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_rows)
@@ -356,6 +374,8 @@ def _backbone_backward(model, st, dfeat, G):
         _ln_bwd(S.X0, da_t, blk.temporal_norm1, dX, R, G, rowmap=patch_map)
         for k in list(vars(S)):
             setattr(S, k, None)        # free this block's activations as soon as it is done
+        if ready is not None:
+            ready(bi)
     # ---- patch embedding + token embeddings (timesformer.py:201-209, 288-323)
     dP = torch.empty(R, C, device=dev, dtype=mode)
     ops.cast_rows(dX, dP, R, rowmap=patch_map)
@@ -365,6 +385,8 @@ def _backbone_backward(model, st, dfeat, G):
         wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
     ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
                   G.zeros(model.cls_token))
+    if ready is not None:
+        ready(depth)
     return G
 
 

@@ -7,7 +7,8 @@ on its half of the clips.  RCCL refuses two ranks on one GPU, so the two ranks s
 GPU over gloo (same DDP reducer, same bucketed all-reduce code path; only the transport
 differs).  Rank 0 then re-runs the same step in one process on the WHOLE batch and checks the
 all-reduced gradients, the loss and the center against it (fp32 parity mode, 1e-3 relative
-to max |ref| per tensor), and both ranks check they hold bitwise-identical gradients.  A second
+to max |ref| per tensor) -- once with the backbone's gradients on DDP's own reducer and once on
+dsvt.dist.wrap_ddp's per-block buckets overlapped with the backbone backward -- and both ranks check they hold bitwise-identical gradients.  A second
 phase runs dsvt.trainer.DINOTrainer.step (clip + AdamW + EMA) under DDP and checks the student
 and teacher parameters stay identical across the ranks.
 
@@ -96,36 +97,45 @@ def main():
     lo, hi = ddist.shard_range(B_ALL, rank, world)
     mine = [torch.from_numpy(c[lo:hi].copy()).to(dev) for c in full]
 
-    # ---- phase 1: DDP gradients + center vs the single-process whole batch
-    student = build(4101, 4102).train()
-    teacher = build(4201, 4202).eval()
-    for p in teacher.parameters():
-        p.requires_grad_(False)
-    log("models built")
-    ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[0], broadcast_buffers=False)
-    log("ddp wrapped")
-    loss_fn = make_loss(center0)
-    s_out = ddp(mine)                                   # train_ssl.py:523
-    with torch.no_grad():
-        t_out = teacher(mine[:2])                       # :527
-    loss = loss_fn(s_out, t_out, 0)                     # center all-reduce inside (update_center)
-    log("forward + loss done")
-    loss.backward()                                     # DDP bucketed gradient all-reduce
-    log("backward done")
-    torch.cuda.synchronize()
-    names = [n for n, p in student.named_parameters() if p.requires_grad]
-    grads = {n: p.grad.detach().float().cpu().numpy() for n, p in student.named_parameters() if p.requires_grad}
-    missing = [n for n in names if student.get_parameter(n).grad is None]
-    assert not missing, "no gradient for %s" % missing
-    flat = torch.cat([torch.from_numpy(grads[n]).reshape(-1) for n in names])
-    peers = [torch.empty_like(flat) for _ in range(world)]
-    dist.all_gather(peers, flat)
-    assert all(torch.equal(peers[0], x) for x in peers[1:]), "ranks hold different averaged gradients"
-    loss_sum = torch.tensor([float(loss.item())], dtype=torch.float64)
-    dist.all_reduce(loss_sum)
-    center_dp = loss_fn.center.detach().cpu().numpy()
-    info["n_params"] = len(names)
-
+    # ---- phase 1: DDP gradients + center vs the single-process whole batch, with the backbone's
+    # gradients on DDP's reducer (plain DDP) and on the overlapped per-block buckets (wrap_ddp)
+    results = {}
+    for mode in ("ddp", "overlap", "overlap_1stream"):
+        student = build(4101, 4102).train()
+        teacher = build(4201, 4202).eval()
+        for p in teacher.parameters():
+            p.requires_grad_(False)
+        log("models built (%s)" % mode)
+        if mode == "ddp":
+            ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[0], broadcast_buffers=False)
+        else:
+            ddp = ddist.wrap_ddp(student, dev)
+            assert student.backbone.dsvt_grad_reducer is not None
+            if mode == "overlap_1stream":                  # weight gradients and buckets on one stream
+                student.backbone.dsvt_wgrad_stream = False
+        log("ddp wrapped")
+        loss_fn = make_loss(center0)
+        s_out = ddp(mine)                                   # train_ssl.py:523
+        with torch.no_grad():
+            t_out = teacher(mine[:2])                       # :527
+        loss = loss_fn(s_out, t_out, 0)                     # center all-reduce inside (update_center)
+        log("forward + loss done")
+        loss.backward()                                     # bucketed gradient all-reduce
+        log("backward done")
+        torch.cuda.synchronize()
+        names = [n for n, p in student.named_parameters() if p.requires_grad]
+        grads = {n: p.grad.detach().float().cpu().numpy() for n, p in student.named_parameters() if p.requires_grad}
+        missing = [n for n in names if student.get_parameter(n).grad is None]
+        assert not missing, "no gradient for %s (%s)" % (missing, mode)
+        flat = torch.cat([torch.from_numpy(grads[n]).reshape(-1) for n in names])
+        peers = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(peers, flat)
+        assert all(torch.equal(peers[0], x) for x in peers[1:]), "ranks hold different averaged gradients (%s)" % mode
+        loss_sum = torch.tensor([float(loss.item())], dtype=torch.float64)
+        dist.all_reduce(loss_sum)
+        results[mode] = (grads, loss_sum, loss_fn.center.detach().cpu().numpy())
+        info["n_params"] = len(names)
+        del ddp, student
     log("phase 1 collectives done")
     if rank == 0:
         from dsvt import ops
@@ -141,28 +151,34 @@ def main():
         ops.center_ema(lf.center, colsum, lf.center_momentum, 1.0 / rows)
         l_ref.backward()
         torch.cuda.synchronize()
-        errs = {}
-        for n, p in ref.named_parameters():
-            if p.requires_grad:
-                errs[n] = rel(grads[n], p.grad.cpu().numpy())
-        worst = max(errs, key=errs.get)
-        info["worst_grad"] = [worst, errs[worst]]
-        assert errs[worst] < TOL, "DDP grad %s rel err %.3g vs single-process full batch" % (worst, errs[worst])
-        l_mean = float(loss_sum.item()) / world
-        info["loss"] = [l_mean, float(l_ref.item())]
-        assert abs(l_mean - float(l_ref.item())) < TOL * abs(float(l_ref.item())), info["loss"]
-        ec = rel(center_dp, lf.center.cpu().numpy())
-        info["center_err"] = ec
-        assert ec < 1e-5, "center after the all-reduced update differs: %.3g" % ec
+        for mode, (grads, loss_sum, center_dp) in results.items():
+            errs = {}
+            for n, p in ref.named_parameters():
+                if p.requires_grad:
+                    errs[n] = rel(grads[n], p.grad.cpu().numpy())
+            worst = max(errs, key=errs.get)
+            info["worst_grad_" + mode] = [worst, errs[worst]]
+            info["top_" + mode] = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
+            if mode != "ddp":
+                info["vs_ddp_" + mode] = max(rel(grads[n], results["ddp"][0][n]) for n in grads)
+        for mode, (grads, loss_sum, center_dp) in results.items():
+            worst = info["worst_grad_" + mode][0]
+            assert info["worst_grad_" + mode][1] < TOL, "%s grad %s rel err %.3g vs single-process full batch: %s" % (
+                mode, worst, info["worst_grad_" + mode][1], info)
+            l_mean = float(loss_sum.item()) / world
+            info["loss_" + mode] = [l_mean, float(l_ref.item())]
+            assert abs(l_mean - float(l_ref.item())) < TOL * abs(float(l_ref.item())), info["loss_" + mode]
+            ec = rel(center_dp, lf.center.cpu().numpy())
+            info["center_err_" + mode] = ec
+            assert ec < 1e-5, "center after the all-reduced update differs (%s): %.3g" % (mode, ec)
         del ref, lf
     dist.barrier()
-    del ddp, student
 
     # ---- phase 2: whole training steps under DDP stay in sync across ranks
     from dsvt.trainer import DINOTrainer
     student = build(4101, 4102).train()
     teacher = build(4101, 4102).eval()
-    ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[0], broadcast_buffers=False)
+    ddp = ddist.wrap_ddp(student, dev)                 # the bench's wrapping (overlapped backbone buckets)
     tr = DINOTrainer(student, teacher, make_loss(center0), ddp=ddp, epochs=2, niter_per_ep=4, warmup_epochs=1,
                      batch_size_per_gpu=hi - lo, world_size=world)
     for it in (3, 4):                                  # it 3: last layer frozen (epoch 0); it 4: epoch 1

@@ -1,5 +1,6 @@
 """N > 1 data-parallel path on the CPU: gloo, world_size 2, one process per rank (the GPU runs
-the same code over RCCL).  Covers dsvt.dist and the product's dsvt.loss.DINOLoss.update_center
+the same code over RCCL).  Covers dsvt.dist (incl. the overlapped per-block gradient buckets
+of wrap_ddp / BlockGradReducer) and the product's dsvt.loss.DINOLoss.update_center
 (the center column-sum all-reduce of train_ssl.py:673-691), the trainer's world-size lr
 scaling, the bench's max-over-ranks timing, and the video sharding of frame scoring.
 The GPU leg (DDP gradients through the HIP backward) is tests/test_gpu_dist.py."""
@@ -78,6 +79,56 @@ def _worker(rank, world, port, errq):
         dist.all_gather(got, torch.from_numpy(c_dp))
         for g in got[1:]:
             assert torch.equal(g, got[0])
+
+        # dist.wrap_ddp + BlockGradReducer (the overlapped per-block gradient buckets): initial
+        # weights broadcast from rank 0, the backbone's parameters kept from DDP, buckets laid out
+        # per block in one 256-B aligned arena and averaged bucket by bucket in any launch order
+        class _Blk(torch.nn.Module):
+            def __init__(self, seed):
+                super().__init__()
+                g = torch.Generator().manual_seed(seed)
+                self.fc = torch.nn.Linear(6, 5)
+                self.norm = torch.nn.LayerNorm(5)
+                with torch.no_grad():
+                    self.fc.weight.copy_(torch.randn(5, 6, generator=g))
+
+        class _BB(torch.nn.Module):
+            def __init__(self, seed):
+                super().__init__()
+                self.blocks = torch.nn.ModuleList([_Blk(seed + i) for i in range(3)])
+                self.cls_token = torch.nn.Parameter(torch.full((1, 1, 5), float(seed)))
+
+        class _MC(torch.nn.Module):
+            def __init__(self, seed):
+                super().__init__()
+                self.backbone, self.head = _BB(seed), torch.nn.Linear(5, 3)
+
+            def forward(self, x):
+                return self.head(x)
+
+        mc = _MC(100 + 10 * rank)                          # ranks start from different weights
+        ddp = ddist.wrap_ddp(mc, None)
+        red = mc.backbone.dsvt_grad_reducer
+        assert red.ddp is ddp and red.active()
+        assert torch.all(mc.backbone.cls_token == 100.0)    # rank 0's weights everywhere
+        assert "backbone.blocks.0.fc.weight" in mc._ddp_params_and_buffers_to_ignore
+        assert "head.weight" not in mc._ddp_params_and_buffers_to_ignore
+        buckets = red.params()
+        assert [len(b) for b in buckets] == [4, 4, 4, 1]
+        views = red.arena(torch.device("cpu"))
+        for i, b in enumerate(buckets):
+            for p in b:
+                v = views[id(p)]
+                assert v.shape == p.shape and (v.data_ptr() - red._arena.data_ptr()) % 256 == 0
+                v.fill_(float(rank + 1) * (1 + i))
+        for k in (3, 1, 0, 2):
+            red.launch(k)
+        red.finish()
+        for i, b in enumerate(buckets):
+            for p in b:                                   # mean over ranks of (rank + 1) * (i + 1)
+                assert torch.allclose(views[id(p)], torch.full(p.shape, (i + 1) * (world + 1) / 2.0))
+        ddp.require_backward_grad_sync = False             # DDP.no_sync(): no bucket traffic
+        assert not red.active()
 
         # bench: elapsed = MAX over ranks
         assert ddist.max_over_ranks(1.5 + rank) == pytest.approx(1.5 + world - 1)

@@ -141,6 +141,42 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
+@pytest.mark.parametrize("variant", [1, 10])
+@pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8), (16, 196, 8)])
+def test_gemm_residual_k768(variant, B, Np, T):
+    """The K = 768, N = 768 residual GEMM (attn.proj / folded temporal fc shape) at the bench's
+    row counts on the 128x128 kernel and the 256x256 one: through the temporal row map (CLS rows
+    untouched) and on all rows, in place and out of place, against float64."""
+    from dsvt import ops
+    from dsvt._lib import EPI_BIAS_RESID
+    C = 768
+    L, R = 1 + Np * T, B * Np * T
+    w, b = rnd((C, C), 45, 0.03), rnd((C,), 46)
+    x0 = rnd((B * L, C), 47)
+    W, bias = to(w, torch.bfloat16), to(b, torch.float32)
+    _lib_set = __import__("dsvt._lib", fromlist=["call"]).call
+    _lib_set("dsvt_set_gemm_variant", variant)
+    try:
+        for rowmap, M, seed in (((Np * T, L, 1), R, 48), (None, B * L, 49)):
+            A = to(rnd((M, C), seed), torch.bfloat16)
+            X = to(x0, torch.float32)
+            ops.gemm(A, W, bias, X, epilogue=EPI_BIAS_RESID, rowmap=rowmap, M=M)
+            Xo = torch.full_like(X, 3.0)
+            ops.gemm_resid(A, W, bias, to(x0, torch.float32), Xo, rowmap=rowmap, M=M)
+            torch.cuda.synchronize()
+            ref = x0.astype(np.float64).copy()
+            rows = np.arange(M) if rowmap is None else (np.arange(M) // (Np * T)) * L + 1 + np.arange(M) % (Np * T)
+            ref[rows] += back(A) @ back(W).T + b
+            err = np.abs(back(X) - ref).max() / np.abs(ref).max()
+            assert err < 1e-5, err
+            np.testing.assert_array_equal(back(Xo)[rows], back(X)[rows])
+            if rowmap is not None:
+                np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
+                assert np.all(back(Xo)[np.arange(B) * L] == 3.0)
+    finally:
+        _lib_set("dsvt_set_gemm_variant", 0)
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8)])
 def test_gemm_resid_out_of_place(dtype, B, Np, T, gemm_variant):

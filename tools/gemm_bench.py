@@ -34,7 +34,7 @@ SHAPES = [  # (name, M, N, K, epilogue)
 
 
 def set_variant(v):
-    _lib.lib().dsvt_set_gemm_variant(int(v))
+    _lib.call("dsvt_set_gemm_variant", int(v))      # raises for an unknown variant
 
 
 def run(M, N, K, epi, reps=20):
