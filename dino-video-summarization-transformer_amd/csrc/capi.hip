@@ -434,9 +434,9 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 }
 
 int dsvt_set_gemm_variant(int variant) {
-  REQUIRE(variant == 0 || variant == 1 || (variant >= 3 && variant <= 6) || (variant >= 9 && variant <= 13) ||
+  REQUIRE(variant == 0 || variant == 1 || variant == 2 || (variant >= 3 && variant <= 6) || (variant >= 9 && variant <= 13) ||
               (variant >= 20 && variant <= 29 && variant != 24) || variant == 14 || variant == 24 || variant == 34,
-          "gemm variant must be 0, 1, 3-6, 9-13 or 20 (14/24/34: ablation builds)");
+          "gemm variant must be 0-6, 9-13 or 20 (14/24/34: ablation builds)");
   set_gemm_variant(variant);
   return 0;
 }

@@ -243,6 +243,134 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   else epilogue_128<T, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
 }
 
+// ---- variant 2: the same 128x128 bf16 tile on a 4-deep LDS-DMA ring with counted waits.
+// One MFMA k-step (64 B of K) per stage, 16 KB per stage, 64 KB per workgroup (2 per CU).
+// Stage kt+3 is issued right after the barrier that retires stage kt-1, so three stages are
+// in flight and each wave waits only for its own oldest stage (vmcnt 8 / 4 / 0) -- no
+// vmcnt(0) drain per K step.  The k-steps run in the same order as variant 1's, so the two
+// produce bitwise-identical results.  Row r of a stage holds its four 16-B K chunks at
+// slot = chunk ^ pswz(r), pswz(r) = -(r >> 2) mod 4: the 16 lanes of every ds_read_b128
+// lane group then cover all 64 banks.
+// Measured on MI355X (tools/gemm_bench.py, same box, interleaved): 10-17 % SLOWER than
+// variant 1 on every hot-path shape (proj 62.7 vs 58.3 us, fc2 160 vs 138 us): twice the
+// barriers per K and 64-B row segments per load cost more than the drain they remove, since
+// variant 1's second resident workgroup already covers it.  Kept opt-in (DSVT_GEMM_VARIANT=2).
+constexpr int PB = 64;                        // K bytes per stage
+constexpr int P_TILE = BM * PB;               // 8 KB per operand per stage
+constexpr int P_STAGE = 2 * P_TILE;
+constexpr int P_NST = 4;
+
+__device__ __forceinline__ int pswz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
+
+__device__ __forceinline__ void stage_tile64(const char* __restrict__ g, int64_t ld_bytes, int64_t row0, int64_t rows,
+                                             int64_t kbyte0, char* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;           // 8 pieces of 16 rows x 64 B, lane-linear in LDS
+    const int r = piece * 16 + (lane >> 2), cl = lane & 3;
+    int64_t gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const char* src = g + gr * ld_bytes + kbyte0 + ((cl ^ pswz(r)) << 4);
+    __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void p_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(256, 2) void gemm_pipe_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[P_NST * P_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1, r16 = lane & 15, g = lane >> 4;
+  const int tilesN = (int)((p.N + BN - 1) / BN);
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int64_t m0 = (int64_t)(wg / tilesN) * BM;
+  const int64_t n0 = (int64_t)(wg % tilesN) * BN;
+  const char* A = (const char*)p.A;
+  const char* W = (const char*)p.W;
+  const int64_t lda_b = p.lda * 2, ldw_b = p.ldw * 2;
+  const int nk = (int)(p.K * 2 / PB);
+
+  fv4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < P_NST - 1; ++st) {
+    if (st < nk) {
+      stage_tile64(A, lda_b, m0, p.M, (int64_t)st * PB, smem + st * P_STAGE, wave, lane);
+      stage_tile64(W, ldw_b, n0, p.N, (int64_t)st * PB, smem + st * P_STAGE + P_TILE, wave, lane);
+    }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int later = nk - 1 - kt;            // stages issued beyond kt (at most 2 here)
+    if (later >= 2) p_vm_wait<8>();
+    else if (later == 1) p_vm_wait<4>();
+    else p_vm_wait<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();             // stage kt landed for all waves; stage kt-1 read by all
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + P_NST - 1 < nk) {
+      char* nxt = smem + ((kt + P_NST - 1) & (P_NST - 1)) * P_STAGE;
+      stage_tile64(A, lda_b, m0, p.M, (int64_t)(kt + P_NST - 1) * PB, nxt, wave, lane);
+      stage_tile64(W, ldw_b, n0, p.N, (int64_t)(kt + P_NST - 1) * PB, nxt + P_TILE, wave, lane);
+    }
+    const char* At = smem + (kt & (P_NST - 1)) * P_STAGE;
+    const char* Wt = At + P_TILE;
+    sv8 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + r16;
+      a[i] = *reinterpret_cast<const sv8*>(At + row * PB + ((g ^ pswz(row)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wn * 64 + j * 16 + r16;
+      b[j] = *reinterpret_cast<const sv8*>(Wt + row * PB + ((g ^ pswz(row)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+  }
+  mfma_result_fence();
+  if (m0 + BM <= p.M && n0 + BN <= p.N) epilogue_128<bf16_t, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
+  else epilogue_128<bf16_t, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
+}
+
+static bool gemm_pipe_ok(const GemmParams& p) { return p.K % 32 == 0 && p.K >= 32; }
+
+static hipError_t launch_pipe(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
+  const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  dim3 grid((unsigned)tiles), block(256);
+  switch (epi) {
+    case EPI_BIAS:
+      if (out_f32) gemm_pipe_kernel<EPI_BIAS, true><<<grid, block, 0, s>>>(p);
+      else gemm_pipe_kernel<EPI_BIAS, false><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_GELU:
+      if (out_f32) gemm_pipe_kernel<EPI_GELU, true><<<grid, block, 0, s>>>(p);
+      else gemm_pipe_kernel<EPI_GELU, false><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_RESID: gemm_pipe_kernel<EPI_RESID, true><<<grid, block, 0, s>>>(p); break;
+    case EPI_GELU_SAVE: gemm_pipe_kernel<EPI_GELU_SAVE, false><<<grid, block, 0, s>>>(p); break;
+    case EPI_DGELU:
+      if (out_f32) gemm_pipe_kernel<EPI_DGELU, true><<<grid, block, 0, s>>>(p);
+      else gemm_pipe_kernel<EPI_DGELU, false><<<grid, block, 0, s>>>(p);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 template <typename T>
 static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
   const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -284,6 +412,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
     return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (g_gemm_variant >= 20 && g_gemm_variant <= 29) return gemm_8ph_ok(p, epi) ? g_gemm_variant : 1;
+  if (g_gemm_variant == 2) return (gemm_pipe_ok(p) && epi != EPI_PATCH) ? 2 : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
     if (g_gemm_variant == 1 || g_gemm_variant == 9 || g_gemm_variant == 10) return g_gemm_variant;
     return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
@@ -302,6 +431,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
+  if (v == 2) return launch_pipe(p, epi, out_f32, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);
   return launch_t<float>(p, epi, out_f32, s);

@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -141,7 +141,7 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
-@pytest.mark.parametrize("variant", [1, 10])
+@pytest.mark.parametrize("variant", [1, 2, 10])
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8), (16, 196, 8)])
 def test_gemm_residual_k768(variant, B, Np, T):
     """The K = 768, N = 768 residual GEMM (attn.proj / folded temporal fc shape) at the bench's
