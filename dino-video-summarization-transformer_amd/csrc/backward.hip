@@ -34,7 +34,7 @@ namespace dsvt {
 // One wave per row (grid-stride).  VEC (C % 256 == 0): lane owns columns i*256 + 4*lane + e
 // (16-B x / dx accesses); else columns i*64 + lane.  dgamma / dbeta are accumulated in
 // registers, reduced over the 4 waves in LDS and written per block.
-template <typename DyT, bool VEC, int NI = 4>
+template <typename DyT, bool VEC, int NI = 4, bool FAST = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
                                                      const float* __restrict__ gamma, float* __restrict__ dx,
                                                      int64_t rows, int C, int64_t rpg, int64_t gstride, int64_t goff,
@@ -74,12 +74,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
 #pragma unroll
       for (int k = 0; k < NK; ++k)
         s += cx[k];
-      const float mean = wave_sum(s) / C;
+      const float inv_c = 1.0f / (float)C;
+      const float mean = FAST ? wave_sum_dpp(s) * inv_c : wave_sum(s) / C;
       float q = 0.f;
 #pragma unroll
       for (int k = 0; k < NK; ++k)
         { cx[k] -= mean; q += cx[k] * cx[k]; }
-      const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+      const float rstd = FAST ? __builtin_amdgcn_rsqf(wave_sum_dpp(q) * inv_c + eps) : 1.0f / sqrtf(wave_sum(q) / C + eps);
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int k = 0; k < NK; ++k)
@@ -91,8 +92,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
           dg[k] += cd[k] * xh;
           db[k] += cd[k];
         }
-      s1 = wave_sum(s1) / C;
-      s2 = wave_sum(s2) / C;
+      if (FAST) {
+        s1 = wave_sum_dpp(s1) * inv_c;
+        s2 = wave_sum_dpp(s2) * inv_c;
+      } else {
+        s1 = wave_sum(s1) / C;
+        s2 = wave_sum(s2) / C;
+      }
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
           float4 o;
@@ -190,7 +196,15 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
                                                              goff, eps, partial)
 #define DSVT_LNB3(T) ln_bwd_kernel<T, true, 3><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, \
                                                                   gstride, goff, eps, partial)
-  if (C == 768) {                      // ViT-B: 3 float4 chunks per lane, a tighter register file
+  static const int lnb_v = getenv("DSVT_LNB_VARIANT") ? atoi(getenv("DSVT_LNB_VARIANT")) : 1;   // tuning only
+  if (C == 768 && lnb_v == 1) {        // DPP reductions, reciprocal multiplies
+    if (dy_dtype == 0)
+      ln_bwd_kernel<bf16_t, true, 3, true><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, (int)C, rpg,
+                                                              gstride, goff, eps, partial);
+    else
+      ln_bwd_kernel<float, true, 3, true><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, (int)C, rpg,
+                                                             gstride, goff, eps, partial);
+  } else if (C == 768) {               // ViT-B: 3 float4 chunks per lane, a tighter register file
     if (dy_dtype == 0) DSVT_LNB3(bf16_t); else DSVT_LNB3(float);
   } else if (C % 256 == 0 && C <= 1024) {
     if (dy_dtype == 0) DSVT_LNB(bf16_t, true); else DSVT_LNB(float, true);

@@ -107,7 +107,11 @@ def ln_gemm(x, in_rowmap, M, ln_w, ln_b, eps, w, bias, out, ws, epilogue=_lib.EP
 
 def layernorm(x, rows, C, ln_w, ln_b, eps, out, rowmap=None, out_f32=True):
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
-    mode = out.dtype if out.dtype in (torch.bfloat16, torch.float32) else torch.float32
+    if out.dtype not in (torch.bfloat16, torch.float32):
+        raise _lib.DsvtError("layernorm: output must be bf16 or fp32 (got %s)" % out.dtype)
+    if (int(out_f32) & 1) and out.dtype != torch.float32:
+        raise _lib.DsvtError("layernorm: out_f32 writes fp32 rows, the output is %s" % out.dtype)
+    mode = out.dtype
     call("dsvt_layernorm_fwd", _dt(mode), int(out_f32), _ptr(x), _ptr(out), _ptr(ln_w), _ptr(ln_b), rows, C,
          rpg, gs, go, float(eps), _stream())
     return out

@@ -33,6 +33,12 @@ SHAPES = [  # (name, M, N, K, epilogue)
 ]
 
 
+if os.environ.get("DSVT_CUSTOM"):    # "name:M:N:K:epi,...": extra shapes (epi = the EPI_* number)
+    for item in os.environ["DSVT_CUSTOM"].split(","):
+        nm, m, n, k, e = item.split(":")
+        SHAPES.append((nm, int(m), int(n), int(k), int(e)))
+
+
 def set_variant(v):
     _lib.call("dsvt_set_gemm_variant", int(v))      # raises for an unknown variant
 

@@ -1,7 +1,8 @@
-"""LayerNorm forward micro-benchmark at the bench's shapes (fp32 X -> bf16), identity and
-temporal patch-row map.  DSVT_LN_GRID (read once per process) picks the kernel: 0 = one row
-per wave, N > 0 = the C = 768 grid-stride kernel with at most N workgroups.
-usage: DSVT_LN_GRID=N python tools/ln_bench.py [out.pt]   (out.pt: save outputs for a bitwise diff)"""
+"""LayerNorm forward / backward micro-benchmark at the training step's shapes (ViT-B, C = 768).
+
+python tools/ln_bench.py       prints us and GB/s (algorithmic bytes: fp32 x read, bf16 dy read,
+fp32 dx read+write for the backward; fp32 x read + bf16 out write for the forward) for the
+global (16 clips x 1569 tokens) and local (48 x 289) rows and the temporal row map."""
 import os
 import sys
 
@@ -13,38 +14,39 @@ import torch  # noqa: E402
 from dsvt import ops  # noqa: E402
 
 
-def run(B, L, T, rowmap, reps=50):
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(0)
-    C = 768
-    X = torch.randn(B * L, C, device=dev, generator=g) * 2 + 0.5
-    w = torch.randn(C, device=dev, generator=g)
-    b = torch.randn(C, device=dev, generator=g)
-    rows = B * (L - 1) if rowmap else B * L
-    rm = (L - 1, L, 1) if rowmap else None
-    out = torch.empty(rows, C, device=dev, dtype=torch.bfloat16)
-    ops.layernorm(X, rows, C, w, b, 1e-6, out, rowmap=rm, out_f32=False)
+def timed(fn, reps=20):
+    fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        ops.layernorm(X, rows, C, w, b, 1e-6, out, rowmap=rm, out_f32=False)
+        fn()
     e1.record()
     torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / reps * 1e3
-    print("grid=%s rows=%6d map=%d: %6.1f us  %.2f TB/s" % (os.environ.get("DSVT_LN_GRID", "default"), rows,
-          int(rowmap), us, rows * C * 6 / us / 1e6), flush=True)
-    return out
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    dev = torch.device("cuda")
+    C = 768
+    g = torch.Generator(device=dev).manual_seed(0)
+    w = torch.randn(C, device=dev, generator=g) * 0.1 + 1
+    b = torch.randn(C, device=dev, generator=g) * 0.1
+    for name, B, L, Np, T in (("global", 16, 1569, 196, 8), ("local", 48, 289, 36, 8)):
+        rows = B * L
+        x = torch.randn(rows, C, device=dev, generator=g)
+        dy = torch.randn(rows, C, device=dev, generator=g).to(torch.bfloat16)
+        dx = torch.zeros(rows, C, device=dev)
+        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        out = torch.empty(rows, C, device=dev, dtype=torch.bfloat16)
+        us = timed(lambda: ops.layernorm_bwd(x, dy, w, 1e-6, dx, rows, dg, db))
+        print("%-7s ln_bwd   rows %6d  %7.1f us  %6.0f GB/s" % (name, rows, us, rows * C * 14 / us / 1e3), flush=True)
+        R = B * Np * T
+        us = timed(lambda: ops.layernorm_bwd(x, dy[:R], w, 1e-6, dx, R, dg, db, rowmap=(Np * T, L, 1)))
+        print("%-7s ln_bwd_t rows %6d  %7.1f us  %6.0f GB/s" % (name, R, us, R * C * 14 / us / 1e3), flush=True)
+        us = timed(lambda: ops.layernorm(x, rows, C, w, b, 1e-6, out, out_f32=False))
+        print("%-7s ln_fwd   rows %6d  %7.1f us  %6.0f GB/s" % (name, rows, us, rows * C * 6 / us / 1e3), flush=True)
 
 
 if __name__ == "__main__":
-    outs = [run(16, 1569, 8, False), run(16, 1569, 8, True), run(48, 289, 8, False), run(48, 289, 8, True),
-            run(3, 5, 1, False)]
-    if len(sys.argv) > 1:
-        torch.save([o.cpu() for o in outs], sys.argv[1])
-    if len(sys.argv) > 2:
-        ref = torch.load(sys.argv[2], weights_only=True)
-        print("bitwise equal to %s: %s; max |diff| %s; differing elements %s" % (
-            sys.argv[2], all(torch.equal(a.cpu(), r) for a, r in zip(outs, ref)),
-            ["%.3g" % (a.cpu().float() - r.float()).abs().max().item() for a, r in zip(outs, ref)],
-            [int((a.cpu() != r).sum()) for a, r in zip(outs, ref)]))
+    main()
