@@ -99,9 +99,23 @@ template <> struct TileMMA<float> {
   }
 };
 
-template <typename T, int EPI, bool OUT_F32, bool CHECK>
+// The fp32 residual tile of one wave (full tiles): 16 float4 loads, issued by gemm_kernel two
+// K steps before the end of its main loop (PREF) so their latency runs under the last MFMAs.
+__device__ __forceinline__ void resid_load(const GemmParams& p, int64_t m0, int64_t n0, int wm, int wn, int lane,
+                                           float4 (&add)[4][4]) {
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t orow = map_row(m0 + wm * 64 + i * 16 + r16, p.rpg, p.gstride, p.goff);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      add[i][j] = *reinterpret_cast<const float4*>(resid_src(p) + orow * p.ldo + n0 + wn * 64 + j * 16 + 4 * g);
+  }
+}
+
+template <typename T, int EPI, bool OUT_F32, bool CHECK, bool PRE = false>
 __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][4], int64_t m0, int64_t n0, int wm,
-                                             int wn, int lane) {
+                                             int wn, int lane, const float4 (*pre)[4] = nullptr) {
   const int r16 = lane & 15, g = lane >> 4;
   int64_t orow[4];
   bool vrow[4];
@@ -122,7 +136,12 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
     }
   }
   float4 add[4][4];                    // residual / embedding addend per fragment
-  if constexpr (EPI == EPI_RESID || EPI == EPI_PATCH) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) add[i][j] = pre[i][j];
+  } else if constexpr (EPI == EPI_RESID || EPI == EPI_PATCH) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t m = m0 + wm * 64 + i * 16 + r16;
@@ -190,8 +209,8 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
   }
 }
 
-template <typename T, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
+template <typename T, int EPI, bool OUT_F32, bool PREF = false>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -220,7 +239,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
+  // PREF (fp32 residual, full tiles): the last two K steps are peeled; the residual tile's 16
+  // loads are issued right after the last stage's loads, and that step waits with vmcnt(16) --
+  // for the stage, not for them -- so their latency runs under the last two steps' MFMAs.
+  const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
+  const bool peel = PREF && full && nk >= 2;
+  const int nmain = peel ? nk - 2 : nk;
+  for (int kt = 0; kt < nmain; ++kt) {
     char* cur = smem + (kt & 1) * STAGE_BYTES;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
@@ -231,6 +256,25 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  if constexpr (PREF) {
+    if (peel) {
+      char* cur = smem + ((nk - 2) & 1) * STAGE_BYTES;
+      char* nxt = smem + ((nk - 1) & 1) * STAGE_BYTES;
+      stage_tile(A, lda_b, m0, p.M, (int64_t)(nk - 1) * BKB, nxt, wave, lane);
+      stage_tile(W, ldw_b, n0, p.N, (int64_t)(nk - 1) * BKB, nxt + TILE_BYTES, wave, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      float4 xpre[4][4];
+      resid_load(p, m0, n0, wm, wn, lane, xpre);
+      __builtin_amdgcn_sched_barrier(0);
+      TileMMA<T>::run(cur, cur + TILE_BYTES, acc, wm, wn, lane);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      __syncthreads();
+      TileMMA<T>::run(nxt, nxt + TILE_BYTES, acc, wm, wn, lane);
+      mfma_result_fence();
+      epilogue_128<T, EPI, OUT_F32, false, true>(p, acc, m0, n0, wm, wn, lane, xpre);
+      return;
+    }
+  }
 
   // ---- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + 0..3]
   // Every global load of the epilogue (bias, residual X, pos/time embeddings) is issued
@@ -239,7 +283,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
   // Full tiles (uniform per workgroup) take a branch-free path: no per-lane bounds branches,
   // so the compiler's vmcnt waits stay exact instead of draining after every store.
   mfma_result_fence();   // acc is read under the branches below
-  if (m0 + BM <= p.M && n0 + BN <= p.N) epilogue_128<T, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
+  if (full) epilogue_128<T, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
   else epilogue_128<T, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
 }
 
@@ -384,7 +428,12 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
       if (out_f32) gemm_kernel<T, EPI_GELU, true><<<grid, block, 0, s>>>(p);
       else gemm_kernel<T, EPI_GELU, false><<<grid, block, 0, s>>>(p);
       break;
-    case EPI_RESID: gemm_kernel<T, EPI_RESID, true><<<grid, block, 0, s>>>(p); break;
+    case EPI_RESID: {
+      static const int pref = getenv("DSVT_RESID_PREF") ? atoi(getenv("DSVT_RESID_PREF")) : 1;   // tuning only
+      if (pref && sizeof(T) == 2) gemm_kernel<T, EPI_RESID, true, true><<<grid, block, 0, s>>>(p);
+      else gemm_kernel<T, EPI_RESID, true><<<grid, block, 0, s>>>(p);
+      break;
+    }
     case EPI_PATCH: gemm_kernel<T, EPI_PATCH, true><<<grid, block, 0, s>>>(p); break;
     case EPI_GELU_SAVE: gemm_kernel<T, EPI_GELU_SAVE, false><<<grid, block, 0, s>>>(p); break;
     case EPI_DGELU:
