@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void rownorm_kernel(const float* __restrict__ 
     const float4 f = *reinterpret_cast<const float4*>(xr + c);
     s += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
   }
-  const float nrm = sqrtf(wave_sum(s));
+  const float nrm = sqrtf(wave_sum_dpp(s));
   const float sc = MODE == 0 ? 1.0f / fmaxf(nrm, eps) : g[r] / nrm;
   for (int c = lane * 4; c < D; c += 256) {
     const float4 f = *reinterpret_cast<const float4*>(xr + c);
@@ -184,7 +184,34 @@ __global__ __launch_bounds__(256) void rownorm_kernel(const float* __restrict__ 
   }
 }
 
+// D == 256, many rows (the DINO head's last-layer weight rows): one float4 per lane per row, 4 rows per
+// wave with their loads issued together (one row per wave left 65536 single-load waves at
+// 2.9 TB/s on the last layer's weight norm).
+template <typename OutT, int MODE>
+__global__ __launch_bounds__(256) void rownorm256_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                         OutT* __restrict__ y, int64_t rows, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 4;
+  float4 f[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    f[i] = r0 + i < rows ? *reinterpret_cast<const float4*>(x + (r0 + i) * 256 + lane * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (r0 + i >= rows) break;
+    const float nrm = sqrtf(wave_sum_dpp(f[i].x * f[i].x + f[i].y * f[i].y + f[i].z * f[i].z + f[i].w * f[i].w));
+    const float sc = MODE == 0 ? 1.0f / fmaxf(nrm, eps) : g[r0 + i] / nrm;
+    store4(y + (r0 + i) * 256 + lane * 4, f[i].x * sc, f[i].y * sc, f[i].z * sc, f[i].w * sc);
+  }
+}
+
 hipError_t launch_l2norm(int dtype, const float* x, void* y, int64_t rows, int64_t D, float eps, hipStream_t s) {
+  if (D == 256 && rows >= 4096) {          // few rows (the head's 16-64 crop rows): one row per wave
+    dim3 grid((unsigned)((rows + 15) / 16)), block(256);
+    if (dtype == 0) rownorm256_kernel<bf16_t, 0><<<grid, block, 0, s>>>(x, nullptr, (bf16_t*)y, rows, eps);
+    else rownorm256_kernel<float, 0><<<grid, block, 0, s>>>(x, nullptr, (float*)y, rows, eps);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   if (dtype == 0) rownorm_kernel<bf16_t, 0><<<grid, block, 0, s>>>(x, nullptr, (bf16_t*)y, rows, (int)D, eps);
   else rownorm_kernel<float, 0><<<grid, block, 0, s>>>(x, nullptr, (float*)y, rows, (int)D, eps);
@@ -193,6 +220,12 @@ hipError_t launch_l2norm(int dtype, const float* x, void* y, int64_t rows, int64
 
 hipError_t launch_weight_norm(int dtype, const float* v, const float* g, void* w, int64_t rows, int64_t D,
                               hipStream_t s) {
+  if (D == 256 && rows >= 4096) {
+    dim3 grid((unsigned)((rows + 15) / 16)), block(256);
+    if (dtype == 0) rownorm256_kernel<bf16_t, 1><<<grid, block, 0, s>>>(v, g, (bf16_t*)w, rows, 0.f);
+    else rownorm256_kernel<float, 1><<<grid, block, 0, s>>>(v, g, (float*)w, rows, 0.f);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   if (dtype == 0) rownorm_kernel<bf16_t, 1><<<grid, block, 0, s>>>(v, g, (bf16_t*)w, rows, (int)D, 0.f);
   else rownorm_kernel<float, 1><<<grid, block, 0, s>>>(v, g, (float*)w, rows, (int)D, 0.f);
