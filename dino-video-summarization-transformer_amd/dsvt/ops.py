@@ -4,6 +4,8 @@ current HIP stream; every computation is a libdsvt.so kernel.
 Storage dtype ("mode"): torch.bfloat16 (perf) or torch.float32 (parity).  The token
 tensor X, LayerNorm/softmax statistics and losses are always fp32.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -422,7 +424,10 @@ def gemm_kernel_name(tag):
     if variant == 0:
         return "void dsvt::gemm_kernel<float, %d, %s>" % (epi, f32)
     if variant == 1:
-        return "void dsvt::gemm_kernel<unsigned short, %d, %s>" % (epi, f32)
+        # the fp32-residual launches use the instantiation with the residual-tile prefetch
+        # (csrc/gemm.hip PREF) unless DSVT_RESID_PREF=0
+        pref = epi == _lib.EPI_BIAS_RESID and os.environ.get("DSVT_RESID_PREF", "1") != "0"
+        return "void dsvt::gemm_kernel<unsigned short, %d, %s%s>" % (epi, f32, ", true" if pref else "")
     persist = {9: "256, 128, 2, 2, 3, %d, %s, false", 10: "256, 128, 2, 2, 3, %d, %s, true"}
     if variant in persist:
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"

@@ -2,7 +2,7 @@
 # One GPU-box session: each stage under its own time limit; stop at the first crash, abort,
 # fault or timeout (exit status other than 0 = pass / 1 = test failures or Python error).
 # usage: tools/gpu_session.sh stage [stage ...]
-#   stages: kernels model smoke bench prof pmc
+#   stages: kernels model gputests smoke bench prof graphprof trainprof pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
@@ -23,9 +23,13 @@ for stage in "$@"; do
     model)   run model 1200 python -m pytest tests/test_gpu_model.py -q -rf -s ;;
     gputests) run gputests 1500 python -m pytest tests -m gpu -q -rf ;;
     smoke)   run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench)   run bench 900 python bench.py ;;
+    bench)   run bench 900 python bench.py && tail -n 1 "$OUT/bench.log" > "$OUT/bench.json" ;;
     prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --serial --no-graph --no-train --no-other &&
-             python tools/prof_summary.py "$OUT/prof" 7 > "$OUT/prof_summary.txt" ;;
+             python tools/prof_summary.py "$OUT/prof" --step-kernel loss_reduce > "$OUT/prof_summary.txt" ;;
+    graphprof) run graphprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gprof" -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-probe --no-train --no-other &&
+             python tools/prof_summary.py "$OUT/gprof" --step-kernel loss_reduce > "$OUT/gprof_summary.txt" ;;
+    trainprof) run trainprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tprof" -o run -- python3 tools/train_step.py --steps 5 --warmup 2 &&
+             python tools/prof_summary.py "$OUT/tprof" --step-kernel ema_kernel --per-step 2 > "$OUT/tprof_summary.txt" ;;
     pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
              run pmc2 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
              python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" > "$OUT/pmc_summary.txt" ;;
