@@ -169,6 +169,23 @@ int dsvt_gemm_resid_fwd(int dtype, const void* A, int64_t lda, const void* W, in
                 gemm_tag(p, dtype, EPI_RESID, 1), gemm_bytes(dtype, EPI_RESID, 1, M, N, K));
 }
 
+int dsvt_gemm_resid_scaled_fwd(int dtype, const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                               const float* bias_row_scale, const float* x_in, float* x_out, int64_t ldx, int64_t M,
+                               int64_t N, int64_t K, void* stream) {
+  if (int e = check_gemm(dtype, EPI_RESID, A, lda, W, ldw, bias, x_out, ldx, M, N, K)) return e;
+  REQUIRE(x_in && aligned16(x_in), "gemm_resid_scaled: x_in must be a 16-byte aligned fp32 tensor");
+  REQUIRE(bias_row_scale, "gemm_resid_scaled: bias_row_scale is null");
+  int64_t rpg = 0, gstride = 0, goff = 0;
+  norm_map(rpg, gstride, goff);                  // identity row map
+  GemmParams p{A, lda, W, ldw, bias, x_out, ldx, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.resid = x_in;
+  p.row_scale = bias_row_scale;
+  p.rs_group = 1;
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_resid_scaled_fwd",
+                [&] { return launch_gemm(p, dtype, EPI_RESID, 1, (hipStream_t)stream); },
+                gemm_tag(p, dtype, EPI_RESID, 1), gemm_bytes(dtype, EPI_RESID, 1, M, N, K));
+}
+
 int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const float* gamma, const float* beta,
                        int64_t rows, int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "layernorm: bad dtype");

@@ -165,11 +165,11 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
       }
     }
   }
-  float rsc[4];                        // DropPath row scales (EPI_BIAS / EPI_GELU_SAVE)
-#pragma unroll
+  float rsc[4];                        // DropPath row scales (EPI_BIAS / EPI_GELU_SAVE: the output;
+#pragma unroll                         // EPI_RESID: the bias term only)
   for (int i = 0; i < 4; ++i) {
     rsc[i] = 1.0f;
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE)
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE || EPI == EPI_RESID)
       if (p.row_scale) rsc[i] = row_scale_of(p, m0 + wm * 64 + i * 16 + r16);
   }
 #pragma unroll
@@ -179,7 +179,10 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
     for (int j = 0; j < 4; ++j) {
       const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
       if (CHECK && n >= p.N) continue;
-      const float4 bb = bias4[j];
+      float4 bb = bias4[j];
+      if constexpr (EPI == EPI_RESID) {  // x + A.W^T + s[m] * bias (A already carries the scale)
+        bb.x *= rsc[i]; bb.y *= rsc[i]; bb.z *= rsc[i]; bb.w *= rsc[i];
+      }
       float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y, v2 = acc[i][j][2] + bb.z, v3 = acc[i][j][3] + bb.w;
       if constexpr (EPI == EPI_GELU_SAVE) {
         store4((T*)p.aux + orow[i] * p.ld_aux + n, v0, v1, v2, v3);
@@ -459,7 +462,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
   if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
-    return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
+    return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (g_gemm_variant >= 20 && g_gemm_variant <= 29) return gemm_8ph_ok(p, epi) ? g_gemm_variant : 1;
   if (g_gemm_variant == 2) return (gemm_pipe_ok(p) && epi != EPI_PATCH) ? 2 : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only

@@ -65,6 +65,7 @@ SIGNATURES = {
     "dsvt_cast_rows": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvt_row_scale": (_i32, [_i32, _p, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvt_rowscale_bias_add": (_i32, [_p, _i64, _i64, _p, _p, _p]),
+    "dsvt_gemm_resid_scaled_fwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "dsvt_cast_transpose": (_i32, [_i32, _p, _p, _i64, _i64, _p]),
     "dsvt_embed_bwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "dsvt_cast_multi": (_i32, [_p, _p, _p, _p, _p, _i64, _p]),

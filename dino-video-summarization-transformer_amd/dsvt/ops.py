@@ -57,8 +57,10 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     return out
 
 
-def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None):
-    """x_out[row(m)] = x_in[row(m)] + a[m] . w^T + bias (fp32 token rows; out of place)."""
+def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None, bias_row_scale=None):
+    """x_out[row(m)] = x_in[row(m)] + a[m] . w^T + bias (fp32 token rows; out of place).
+    bias_row_scale (fp32 [M], identity row map only): the bias term of row m is scaled by it
+    (training DropPath: a already carries the scale)."""
     mode = w.dtype
     _check(a, mode, "A")
     _check(w, mode, "W")
@@ -68,6 +70,15 @@ def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None):
         raise _lib.DsvtError("gemm_resid: x_in %s and x_out %s differ" % (tuple(x_in.shape), tuple(x_out.shape)))
     M = a.shape[0] if M is None else M
     K = a.shape[-1]
+    if bias_row_scale is not None:
+        if rowmap is not None:
+            raise _lib.DsvtError("gemm_resid: bias_row_scale needs the identity row map")
+        _check(bias_row_scale, torch.float32, "bias_row_scale")
+        if bias_row_scale.numel() < M:
+            raise _lib.DsvtError("gemm_resid: %d bias row scales < %d rows" % (bias_row_scale.numel(), M))
+        call("dsvt_gemm_resid_scaled_fwd", _dt(mode), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
+             _ptr(bias_row_scale), _ptr(x_in), _ptr(x_out), x_out.shape[-1], M, w.shape[0], K, _stream())
+        return x_out
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
     call("dsvt_gemm_resid_fwd", _dt(mode), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias), _ptr(x_in), _ptr(x_out),
          x_out.shape[-1], M, w.shape[0], K, rpg, gs, go, _stream())

@@ -275,8 +275,7 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
             ops.gemm_resid(S.o_s, w(blk.attn.proj.weight), blk.attn.proj.bias, S.X1, X)
         else:
             ops.attn_spatial_scaled(S.qkv_s, S.o_s, mk.s, B, T, L, heads, blk.attn.scale, cls_ws)
-            ops.gemm_resid(S.o_s, w(blk.attn.proj.weight), None, S.X1, X)
-            ops.rowscale_bias_add(X, mk.s_rows, blk.attn.proj.bias)
+            ops.gemm_resid(S.o_s, w(blk.attn.proj.weight), blk.attn.proj.bias, S.X1, X, bias_row_scale=mk.s_rows)
         # ---- MLP (:184)
         S.X2 = X
         S.a_m = torch.empty(rows, C, device=dev, dtype=mode)
@@ -291,8 +290,7 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
         else:                       # drop_path of the MLP branch: h scaled per sample (fc2 is linear)
             ops.gemm_rowscale(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, mk.m, L, aux=S.pre,
                               epilogue=EPI_GELU_SAVE)
-            ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), None, S.X2, X)
-            ops.rowscale_bias_add(X, mk.m_rows, blk.mlp.fc2.bias)
+            ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, S.X2, X, bias_row_scale=mk.m_rows)
         st.blocks.append(S)
     st.X = X
     feats = torch.empty(B, C, device=dev, dtype=torch.float32)

@@ -92,6 +92,15 @@ int dsvt_gemm_resid_fwd(int dtype, const void *A, int64_t lda, const void *W, in
                         const float *x_in, float *x_out, int64_t ldx, int64_t M, int64_t N, int64_t K,
                         int64_t rpg, int64_t gstride, int64_t goff, void *stream);
 
+/* Training-mode DropPath form of dsvt_gemm_resid_fwd (identity row map):
+ *   x_out[m] = x_in[m] + A[m] . W^T + bias_row_scale[m] * bias
+ * A already carries the per-sample DropPath scale (models/vit_utils.py:152-167: drop_path of
+ * attn / mlp, timesformer.py:181, 184 -- the scaled branch is linear in A), so only the bias
+ * term takes the row scale; replaces a GEMM without bias + a separate scaled-bias pass. */
+int dsvt_gemm_resid_scaled_fwd(int dtype, const void *A, int64_t lda, const void *W, int64_t ldw, const float *bias,
+                               const float *bias_row_scale, const float *x_in, float *x_out, int64_t ldx, int64_t M,
+                               int64_t N, int64_t K, void *stream);
+
 /* K7 + K3 fused, bf16 only, N = 768 (ViT-B): the residual projections attn.proj / temporal_fc /
  * mlp.fc2 with their residual add (models/timesformer.py:133-135, 181, 184) and the LayerNorm
  * that reads the updated rows next (norm1 :105, norm2 :112/184, the next block's
