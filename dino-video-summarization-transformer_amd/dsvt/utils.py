@@ -182,22 +182,30 @@ class MultiCropWrapper(nn.Module):
 
 
 # ---------------------------------------------------------------- training-step utilities
-_TLISTS = {}
+_TLISTS = {}      # tensor-list shape (device, numels) -> TensorList (size / chunk tables)
+_TPTRS = {}       # (device, data pointers) -> device pointer table
 
 
 def _tensor_list(tensors):
-    """Cached device tables (pointers, sizes, chunks) for a list of fp32 GPU tensors."""
+    """Cached device tables for a list of fp32 GPU tensors: (TensorList of its shape, pointer
+    table).  Gradients are new buffers every step, so only their pointer table is rebuilt (one
+    pinned, non-blocking copy); the shape tables are built once."""
     from .training import TensorList, check_fp32_contiguous
     check_fp32_contiguous(tensors, "multi-tensor op")
-    key = tuple((t.data_ptr(), t.numel()) for t in tensors)
-    ent = _TLISTS.get(key)
-    if ent is None:
-        dev = tensors[0].device
-        tl = TensorList(tensors, dev)
-        ent = _TLISTS[key] = (tl, TensorList.ptrs(tensors, dev))
+    dev = tensors[0].device
+    skey = (dev, tuple(t.numel() for t in tensors))
+    tl = _TLISTS.get(skey)
+    if tl is None:
+        tl = _TLISTS[skey] = TensorList(tensors, dev)
         if len(_TLISTS) > 64:
             _TLISTS.pop(next(iter(_TLISTS)))
-    return ent
+    pkey = (dev, tuple(t.data_ptr() for t in tensors))
+    ptr = _TPTRS.get(pkey)
+    if ptr is None:
+        ptr = _TPTRS[pkey] = TensorList.ptrs(tensors, dev)
+        if len(_TPTRS) > 64:
+            _TPTRS.pop(next(iter(_TPTRS)))
+    return tl, ptr
 
 
 def ema_update_(teacher_tensors, student_tensors, momentum):
@@ -221,10 +229,10 @@ def clip_gradients_(grads, clip):
     from ._lib import call
     grads = list(grads)
     tl, gptr = _tensor_list(grads)
-    norms = torch.empty(len(tl.tensors), device=tl.sizes.device, dtype=torch.float32)
+    norms = torch.empty(tl.ntensors, device=tl.sizes.device, dtype=torch.float32)
     ws = torch.empty(tl.nchunks, device=tl.sizes.device, dtype=torch.float32)
     call("dsvt_clip_grads", gptr.data_ptr(), tl.sizes.data_ptr(), tl.ctensor.data_ptr(), tl.cstart.data_ptr(),
-         tl.first.data_ptr(), tl.nchunks, len(tl.tensors), float(clip), norms.data_ptr(), ws.data_ptr(),
+         tl.first.data_ptr(), tl.nchunks, tl.ntensors, float(clip), norms.data_ptr(), ws.data_ptr(),
          ws.numel() * 4, ops._stream())
     return norms
 

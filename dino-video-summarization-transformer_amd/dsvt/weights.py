@@ -166,8 +166,9 @@ class WeightCache:
         tables = self._tables.get(tkey)
         dev = stale[0][2].device
         if tables is None:
-            src = torch.tensor([t.data_ptr() for _, _, t, _ in stale], dtype=torch.int64, device=dev)
-            dst = torch.tensor([o.data_ptr() for _, _, _, o in stale], dtype=torch.int64, device=dev)
+            from .training import dev_table
+            src = dev_table([t.data_ptr() for _, _, t, _ in stale], torch.int64, dev)
+            dst = dev_table([o.data_ptr() for _, _, _, o in stale], torch.int64, dev)
             if transposed:
                 rows = [t.shape[0] for _, _, t, _ in stale]
                 cols = [t.shape[1] for _, _, t, _ in stale]
@@ -177,10 +178,8 @@ class WeightCache:
                         for b in range((c + 63) // 64):
                             tt.append(i)
                             rc.append((a << 16) | b)
-                tables = (src, dst, torch.tensor(rows, dtype=torch.int64, device=dev),
-                          torch.tensor(cols, dtype=torch.int64, device=dev),
-                          torch.tensor(tt, dtype=torch.int32, device=dev),
-                          torch.tensor(rc, dtype=torch.int32, device=dev), len(tt))
+                tables = (src, dst, dev_table(rows, torch.int64, dev), dev_table(cols, torch.int64, dev),
+                          dev_table(tt, torch.int32, dev), dev_table(rc, torch.int32, dev), len(tt))
             else:
                 from .training import TensorList
                 tl = TensorList([t for _, _, t, _ in stale], dev)
