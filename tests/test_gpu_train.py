@@ -443,3 +443,54 @@ def test_wgrad_vs_fp64(M, N, K, accumulate):
     ref_b = dy.double().sum(0) + (b0.double() if accumulate else 0)
     err_b = ((outs[0][1].double() - ref_b).abs().max() / ref_b.abs().max()).item()
     assert err_b < 1e-5, err_b
+
+
+def test_train_step_bitwise_repeatable_bf16():
+    """Two runs of the bf16 training step (ViT-B width and heads, depth 2, 2 clips of 2 global
+    8x224^2 + 2 local 8x96^2 crops, DropPath 0.1, concurrent teacher, weight gradients on the
+    side stream) from identical weights, crops and seeds end with BITWISE identical student and
+    teacher parameters.  Every kernel reduces in a fixed order, so a difference can only come
+    from a stream race -- e.g. the side-stream weight-gradient read of a buffer the main stream
+    rewrites (the dXb race of r02, exposed only when the side stream lagged)."""
+    from dsvt.loss import DINOLoss
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.trainer import DINOTrainer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+
+    def nets():
+        out = []
+        for _ in range(2):
+            torch.manual_seed(7)
+            bb = VisionTransformer(img_size=224, patch_size=16, num_classes=0, embed_dim=768, depth=2, num_heads=12,
+                                   mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                                   drop_path_rate=0.1, num_frames=8, attention_type="divided_space_time")
+            hd = DINOHead(768, 4096, hidden_dim=2048, bottleneck_dim=256)
+            bb.dsvt_dtype = hd.dsvt_dtype = torch.bfloat16
+            out.append(MultiCropWrapper(bb, hd).cuda())
+        out[1].load_state_dict(out[0].state_dict())
+        return out
+
+    g = torch.Generator().manual_seed(11)
+    crops = [(torch.randn(2, 3, 8, 224, 224, generator=g)).cuda() for _ in range(2)] + \
+            [(torch.randn(2, 3, 8, 96, 96, generator=g)).cuda() for _ in range(2)]
+    finals = []
+    for run in range(2):
+        student, teacher = nets()
+        student.train()
+        teacher.eval()
+        for p in student.parameters():
+            p.requires_grad_(True)
+        tr = DINOTrainer(student, teacher, DINOLoss(4096, 4, 0.04, 0.04, 0, 2).cuda(), epochs=2, niter_per_ep=4,
+                         warmup_epochs=1, batch_size_per_gpu=2, world_size=1)
+        torch.manual_seed(123)
+        torch.cuda.manual_seed(123)
+        losses = [float(tr.step(crops, it).item()) for it in (4, 5)]
+        torch.cuda.synchronize()
+        finals.append((losses, torch.cat([p.detach().reshape(-1) for p in student.parameters()]),
+                       torch.cat([p.detach().reshape(-1) for p in teacher.parameters()])))
+        del tr, student, teacher
+    assert all(np.isfinite(finals[0][0])), finals[0][0]
+    assert finals[0][0] == finals[1][0], (finals[0][0], finals[1][0])
+    assert torch.equal(finals[0][1], finals[1][1]), "student parameters differ between identical runs"
+    assert torch.equal(finals[0][2], finals[1][2]), "teacher parameters differ between identical runs"
