@@ -287,8 +287,9 @@ def swin_t_flops(T=8, S=224, C=96, depths=(2, 2, 6, 2), window=(2, 7, 7), patch=
 
 def other_configs(args, device):
     """Forward clips/s of the config-2 backbone alone (16 divided-attention 8x224^2 clips) and of
-    BASELINE.json configs 4 (ViT-B/16 joint space-time, 16x224^2) and 5 (Video Swin-T, 8x224^2)
-    on one GPU, random init, synthetic normalized frames."""
+    BASELINE.json configs 4 (ViT-B/16 joint space-time, 16x224^2) and 5 (Video Swin-T, 8x224^2),
+    and frames/s of the frame-scoring path (64 frames, local 3 / global 30), on one GPU, random
+    init, synthetic normalized frames."""
     from functools import partial
 
     import torch.nn as nn
@@ -348,6 +349,22 @@ def other_configs(args, device):
     res["config5_swin_t"] = {"value": round(8 / t, 2), "unit": "clips/s", "clips_per_step": 8,
                              "gflop_per_clip": round(swin_t_flops() / 1e9, 2),
                              "tflops": round(8 * swin_t_flops() / t / 1e12, 1)}
+    del sm, xs
+    # frame scoring (a18 / a19): one F = 64-frame 224^2 video, local 3 / global 30
+    # views per frame (dino_similarity.py:66-93), pairwise DINO loss per frame
+    from dsvt.scoring import FrameScorer
+    torch.manual_seed(2)
+    fm = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
+                           norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=8,
+                           attention_type="divided_space_time").to(device).eval()
+    fm.dsvt_dtype = dtype
+    scorer = FrameScorer(fm, local_clip_size=3, global_clip_size=30)
+    video = torch.randn(64, 3, 224, 224, device=device)
+    with torch.no_grad():
+        t = timed(lambda: scorer.score(video), reps=2, warm=1)
+    gf = (vit_fwd_flops(3, 224) + vit_fwd_flops(30, 224)) / 1e9
+    res["frame_score"] = {"value": round(64 / t, 2), "unit": "frames/s", "frames": 64, "views": "local 3 / global 30",
+                          "gflop_per_frame": round(gf, 1), "tflops": round(64 * gf / t / 1e3, 1)}
     return res
 
 
