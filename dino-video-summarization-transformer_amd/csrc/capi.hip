@@ -200,6 +200,29 @@ int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const fl
   });
 }
 
+int dsvt_add_layernorm_fwd(int d_dtype, int y_dtype, float* x, const void* d, void* y, const float* gamma,
+                           const float* beta, int64_t rows, int64_t C, int64_t L, int dmode, int ymode, float eps,
+                           void* stream) {
+  REQUIRE(d_dtype == DSVT_BF16 || d_dtype == DSVT_F32, "add_layernorm: bad d dtype");
+  REQUIRE(y_dtype == DSVT_BF16 || y_dtype == DSVT_F32, "add_layernorm: bad y dtype");
+  REQUIRE(dmode >= 0 && dmode <= 2 && ymode >= 0 && ymode <= 2, "add_layernorm: dmode / ymode must be in [0, 2]");
+  REQUIRE(dmode != 0 || ymode != 0, "add_layernorm: nothing to do (dmode = ymode = 0)");
+  REQUIRE(C == 768, "add_layernorm: C must be 768 (got %lld)", (long long)C);
+  REQUIRE(rows > 0 && L >= 1 && rows % L == 0, "add_layernorm: rows must be a positive multiple of L");
+  REQUIRE(dmode != 2 || L >= 2, "add_layernorm: the patch layout needs L >= 2");
+  REQUIRE(ymode != 2 || L >= 2, "add_layernorm: the patch layout needs L >= 2");
+  REQUIRE(x && (dmode == 0 || d) && (ymode == 0 || (y && gamma && beta)), "add_layernorm: null pointer");
+  REQUIRE(aligned16(x) && (dmode == 0 || aligned16(d)) && (ymode == 0 || (aligned16(y) && aligned16(gamma) && aligned16(beta))),
+          "add_layernorm: pointers must be 16-byte aligned");
+  const double drows = dmode == 2 ? (double)rows / L * (L - 1) : dmode == 1 ? (double)rows : 0.0;
+  const double yrows = ymode == 2 ? (double)rows / L * (L - 1) : ymode == 1 ? (double)rows : 0.0;
+  const double bytes = (double)C * (4.0 * rows + 4.0 * drows + drows * esize(d_dtype) + yrows * esize(y_dtype));
+  return probed(DSVT_PROBE_NORM, bytes, (hipStream_t)stream, "dsvt_add_layernorm_fwd", [&] {
+    return launch_add_layernorm(d_dtype == DSVT_F32, y_dtype == DSVT_F32, x, d, y, gamma, beta, rows, L, dmode, ymode,
+                                eps, (hipStream_t)stream);
+  });
+}
+
 int dsvt_gemm_resid_ln_fwd(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, float* X,
                            int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
                            const float* gamma, const float* beta, float eps, void* Y, int ymode, int64_t L,

@@ -84,6 +84,9 @@ int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
 hipError_t launch_wgrad(const unsigned short* dy, int64_t ldy, const unsigned short* x, int64_t ldx, float* G,
                         float* db, int64_t M, int64_t N, int64_t K, int accumulate, float* partial, hipStream_t s);
 
+hipError_t launch_add_layernorm(int d_f32, int y_f32, float* x, const void* d, void* y, const float* g,
+                                const float* b, int64_t rows, int64_t L, int dmode, int ymode, float eps,
+                                hipStream_t s);
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
                             int64_t goff, float eps, hipStream_t s);

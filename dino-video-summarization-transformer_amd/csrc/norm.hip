@@ -126,6 +126,127 @@ __global__ __launch_bounds__(256) void layernorm768_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------- residual add + LayerNorm
+// x = x + d ; y = LayerNorm(x)   (timesformer.py:133-135 / :181 / :184 `x + f(x)` followed by the
+// next sub-layer's norm), C = 768.  The sub-layer GEMM writes d = f(x) (storage dtype) with a
+// plain bias epilogue -- the MFMA kernel then never touches the fp32 token rows -- and this
+// streaming pass does the fp32 residual read-modify-write together with the LayerNorm that
+// re-reads the same rows anyway.  Per X row r of a clip (L rows, row 0 = CLS):
+//   DMODE 0: no d (y = LN(x) only), 1: d row r, 2: d row of the compact patch layout
+//            (b * (L - 1) + j - 1; the CLS row j = 0 has none: the temporal branch);
+//   YMODE 0: no LN output, 1: y row r, 2: y row of the compact patch layout (CLS rows skipped).
+// Same summation order as layernorm768_kernel (a row's result does not depend on the grid).
+template <typename DT, typename OutT, int DMODE, int YMODE>
+__global__ __launch_bounds__(256) void add_layernorm768_kernel(float* __restrict__ x, const DT* __restrict__ d,
+                                                               OutT* __restrict__ y, const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, int64_t rows,
+                                                               int64_t L, float eps) {
+  constexpr int C = 768;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float4 gg[3], bb[3];
+  if constexpr (YMODE != 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      gg[i] = *reinterpret_cast<const float4*>(gamma + i * 256 + lane * 4);
+      bb[i] = *reinterpret_cast<const float4*>(beta + i * 256 + lane * 4);
+    }
+  }
+  // compact patch row of X row rr (-1 for a CLS row)
+  auto patch_row = [&](int64_t rr) -> int64_t {
+    const int64_t b = rr / L, j = rr - b * L;
+    return j == 0 ? -1 : b * (L - 1) + j - 1;
+  };
+  auto d_row = [&](int64_t rr) -> int64_t { return DMODE == 1 ? rr : DMODE == 2 ? patch_row(rr) : -1; };
+  float4 cur[3], curd[3];
+  auto load_row = [&](int64_t rr, float4 (&xv)[3], float4 (&dv)[3]) {
+    const float* xr = x + rr * C;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xv[i] = *reinterpret_cast<const float4*>(xr + i * 256 + lane * 4);
+    const int64_t dr = d_row(rr);                    // wave-uniform
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      if (DMODE != 0 && dr >= 0) load4(d + dr * C + i * 256 + lane * 4, t);
+      dv[i] = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  };
+  load_row(r, cur, curd);
+  while (true) {
+    const int64_t rn = r + nw;
+    float4 nxt[3], nxtd[3];
+    load_row(rn < rows ? rn : r, nxt, nxtd);        // clamped: branch-free prefetch
+    float v[12];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float4 f = cur[i], e = curd[i];
+      v[4 * i] = f.x + e.x; v[4 * i + 1] = f.y + e.y; v[4 * i + 2] = f.z + e.z; v[4 * i + 3] = f.w + e.w;
+      s += (v[4 * i] + v[4 * i + 1]) + (v[4 * i + 2] + v[4 * i + 3]);
+    }
+    if (DMODE != 0 && d_row(r) >= 0) {
+      float* xr = x + r * C;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        *reinterpret_cast<float4*>(xr + i * 256 + lane * 4) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    }
+    if constexpr (YMODE != 0) {
+      const int64_t yrow = YMODE == 1 ? r : patch_row(r);
+      if (yrow >= 0) {
+        const float mean = wave_sum(s) / C;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { v[i] -= mean; q += v[i] * v[i]; }
+        const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+        OutT* yr = y + yrow * C;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const float4 g4 = gg[i], b4 = bb[i];
+          store4(yr + i * 256 + lane * 4, v[4 * i] * rstd * g4.x + b4.x, v[4 * i + 1] * rstd * g4.y + b4.y,
+                 v[4 * i + 2] * rstd * g4.z + b4.z, v[4 * i + 3] * rstd * g4.w + b4.w);
+        }
+      }
+    }
+    if (rn >= rows) break;
+    r = rn;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { cur[i] = nxt[i]; curd[i] = nxtd[i]; }
+  }
+}
+
+// d_f32: d is fp32 (else bf16); y_f32: y is fp32 (else bf16)
+hipError_t launch_add_layernorm(int d_f32, int y_f32, float* x, const void* d, void* y, const float* g,
+                                const float* b, int64_t rows, int64_t L, int dmode, int ymode, float eps,
+                                hipStream_t s) {
+  if (dmode < 0 || dmode > 2 || ymode < 0 || ymode > 2) return hipErrorInvalidValue;
+  const int64_t nblk = (rows + 3) / 4;
+  dim3 grid((unsigned)(nblk < 1024 ? nblk : 1024)), block(256);
+#define DSVT_ALN(DT, YT, DM, YM) \
+  add_layernorm768_kernel<DT, YT, DM, YM><<<grid, block, 0, s>>>(x, (const DT*)d, (YT*)y, g, b, rows, L, eps)
+#define DSVT_ALN_Y(DT, YT, DM)                         \
+  switch (ymode) {                                     \
+    case 0: DSVT_ALN(DT, YT, DM, 0); break;            \
+    case 1: DSVT_ALN(DT, YT, DM, 1); break;            \
+    default: DSVT_ALN(DT, YT, DM, 2); break;           \
+  }
+#define DSVT_ALN_D(DT, YT)                             \
+  switch (dmode) {                                     \
+    case 0: DSVT_ALN_Y(DT, YT, 0); break;              \
+    case 1: DSVT_ALN_Y(DT, YT, 1); break;              \
+    default: DSVT_ALN_Y(DT, YT, 2); break;             \
+  }
+  if (d_f32 && y_f32) { DSVT_ALN_D(float, float); }
+  else if (d_f32) { DSVT_ALN_D(float, bf16_t); }
+  else if (y_f32) { DSVT_ALN_D(bf16_t, float); }
+  else { DSVT_ALN_D(bf16_t, bf16_t); }
+#undef DSVT_ALN_D
+#undef DSVT_ALN_Y
+#undef DSVT_ALN
+  return hipGetLastError();
+}
+
 static int ln_grid_cap() {   // workgroups of the C = 768 kernel (0: the one-row-per-wave kernel)
   static const int cap = [] {
     const char* e = getenv("DSVT_LN_GRID");

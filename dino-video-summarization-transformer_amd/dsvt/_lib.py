@@ -31,6 +31,7 @@ SIGNATURES = {
     "dsvt_gemm_resid_ln_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _f32,
                                       _p, _i32, _i64, _p]),
     "dsvt_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_add_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _i32, _f32, _p]),
     "dsvt_ln_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _i64, _i64, _p, _p, _f32, _p, _p, _p, _i64,
                                 _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvt_patch_embed_fwd": (_i32, [_i32, _i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p,

@@ -109,6 +109,8 @@ class Block(nn.Module):
         eps1, eps2 = self.norm1.eps, self.norm2.eps
         if getattr(ctx, "fuse_ln", False) and self.attention_type == "divided_space_time":
             return self._run_fused(X, ctx, probs)
+        if getattr(ctx, "split_resid", False) and self.attention_type == "divided_space_time":
+            return self._run_split(X, ctx, probs)
         if self.attention_type == 'divided_space_time':
             B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
             R = B * Np * T
@@ -144,6 +146,43 @@ class Block(nn.Module):
                     self.mlp.fc1.bias, ctx.hid, ctx.ws, epilogue=EPI_BIAS_GELU)
         ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
 
+
+    def _run_split(self, X, ctx, probs):
+        """Divided block with each residual sub-layer as GEMM (d = f(x), bias epilogue, storage
+        dtype) + one add-LayerNorm pass (x += d; the next norm of the updated rows): ctx.a enters
+        holding temporal_norm1 of the patch rows (compact) and leaves holding the NEXT block's
+        (ctx.next_ln; after the last block X is only updated).  timesformer.py:127-184."""
+        w = ctx.w
+        B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
+        heads = self.attn.num_heads
+        R, rows = B * Np * T, ctx.rows
+        ta = self.temporal_attn
+        a, d = ctx.a, ctx.d
+        # temporal (:127-135): qkv (LN already applied) -> attention -> proj . temporal_fc
+        ops.gemm(a[:R], w(ta.qkv.weight), ta.qkv.bias, ctx.qkv[:R])
+        ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
+        if ctx.fold_temporal:
+            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
+            ops.gemm(ctx.o[:R], wf, bf, d[:R])
+        else:
+            ops.gemm(ctx.o[:R], w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
+            ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, d[:R])
+        # x[patch rows] += d ; a = norm1(x) on every row (CLS rows unchanged by the temporal branch)
+        ops.add_layernorm(X, d, L, ROWLN_COMPACT, ln=self.norm1, y=a, ymode=ROWLN_X)
+        # spatial with CLS replicate / mean (:139-181)
+        ops.gemm(a, w(self.attn.qkv.weight), self.attn.qkv.bias, ctx.qkv)
+        if probs is not None:
+            ops.attn_spatial_probs(ctx.qkv, ctx.o, probs, B, T, L, heads, self.attn.scale, ctx.cls_ws)
+            return
+        ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
+        ops.gemm(ctx.o, w(self.attn.proj.weight), self.attn.proj.bias, d, M=rows)
+        ops.add_layernorm(X, d, L, ROWLN_X, ln=self.norm2, y=a, ymode=ROWLN_X)
+        # MLP (:184): fc1 + GELU, fc2, x += d and the next block's temporal_norm1 (patch rows)
+        ops.gemm(a, w(self.mlp.fc1.weight), self.mlp.fc1.bias, ctx.hid, epilogue=EPI_BIAS_GELU)
+        ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, d, M=rows)
+        nxt = ctx.next_ln
+        ops.add_layernorm(X, d, L, ROWLN_X, ln=nxt, y=a if nxt is not None else None,
+                          ymode=ROWLN_COMPACT if nxt is not None else ROWLN_NONE)
 
     def _run_fused(self, X, ctx, probs):
         """Divided block with every residual projection fused with the LayerNorm that follows
@@ -258,6 +297,12 @@ class VisionTransformer(nn.Module):
         # at K = 768, 210 vs 185 us at K = 3072, 25k rows) -- a full-row workgroup must pull all of
         # W through LDS-DMA for only ~100 rows, which caps it at ~20-25 GB/s per CU
         self.fuse_ln = os.environ.get("DSVT_FUSE_LN", "0") == "1"
+        # divided, C = 768, inference: every residual projection (temporal_fc, attn.proj, mlp.fc2)
+        # writes its output d = f(x) with a plain bias epilogue (the MFMA kernel never touches the
+        # fp32 token rows) and one streaming pass does x += d together with the LayerNorm the next
+        # GEMM reads (dsvt_add_layernorm_fwd).  DSVT_SPLIT_RESID=0 keeps the fp32 residual
+        # epilogue inside the GEMM followed by a separate LayerNorm.
+        self.split_resid = os.environ.get("DSVT_SPLIT_RESID", "1") == "1"
         # inference: split a batch into this many clip chunks on concurrent HIP streams (each
         # kernel's last partly-filled wave of tiles then runs beside the other chunk's kernels);
         # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
@@ -470,7 +515,11 @@ class VisionTransformer(nn.Module):
                 ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
             nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
             ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
-        if ctx.fuse_ln:      # block 0's temporal_norm1 on the patch rows (compact) into ctx.a
+        ctx.split_resid = (not ctx.fuse_ln and self.split_resid and C == 768
+                           and self.attention_type == 'divided_space_time')
+        if ctx.split_resid:
+            ctx.d = torch.empty(ctx.rows, C, device=dev, dtype=mode)
+        if ctx.fuse_ln or ctx.split_resid:   # block 0's temporal_norm1 on the patch rows (compact) into ctx.a
             ctx.a = torch.empty(ctx.rows, C, device=dev, dtype=mode)
             tn = self.blocks[0].temporal_norm1
             ops.layernorm(X, B * Np * T, C, tn.weight, tn.bias, tn.eps, ctx.a, rowmap=(Np * T, ctx.L, 1),
@@ -478,7 +527,7 @@ class VisionTransformer(nn.Module):
         nblk = len(self.blocks)
         if get_attn:            # timesformer.py:325-331: the last block's attention instead of features
             for i, blk in enumerate(self.blocks[:-1]):
-                ctx.next_ln = self.blocks[i + 1].temporal_norm1 if ctx.fuse_ln else None
+                ctx.next_ln = self.blocks[i + 1].temporal_norm1 if (ctx.fuse_ln or ctx.split_resid) else None
                 blk.run(X, ctx)
             if self.attention_type == 'divided_space_time':
                 heads = self.blocks[-1].attn.num_heads
@@ -490,7 +539,8 @@ class VisionTransformer(nn.Module):
             self.blocks[-1].run(X, ctx)
             return X.view(ctx.nb, ctx.L, C)
         for i, blk in enumerate(self.blocks):
-            ctx.next_ln = self.blocks[i + 1].temporal_norm1 if (ctx.fuse_ln and i + 1 < nblk) else None
+            ctx.next_ln = (self.blocks[i + 1].temporal_norm1
+                           if ((ctx.fuse_ln or ctx.split_resid) and i + 1 < nblk) else None)
             blk.run(X, ctx)
         L = ctx.L
         if self.attention_type == 'space_only':      # mean over frames (:338-340)

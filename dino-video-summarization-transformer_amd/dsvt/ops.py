@@ -85,6 +85,36 @@ def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None, bias_row_scale=None
     return x_out
 
 
+def add_layernorm(X, d, L, dmode, ln=None, y=None, ymode=_lib.ROWLN_NONE):
+    """X[r] += d[drow(r)] (fp32 X [rows, 768], clips of L rows), then y[yrow(r)] = ln(X[r]).
+    dmode / ymode: 0 none, ROWLN_X the row itself, ROWLN_COMPACT the patch-row layout of the
+    temporal branch (CLS rows have no d / y row).  One streaming pass: the sub-layer GEMM before
+    it writes d with a plain bias epilogue."""
+    _check(X, torch.float32, "X")
+    rows, C = X.shape
+    if dmode != _lib.ROWLN_NONE and d.dtype not in (torch.bfloat16, torch.float32):
+        raise _lib.DsvtError("add_layernorm: d must be bf16 or fp32 (got %s)" % d.dtype)
+    if dmode != _lib.ROWLN_NONE:
+        _check(d, d.dtype, "d")
+        need = rows if dmode == _lib.ROWLN_X else rows // L * (L - 1)
+        if d.numel() < need * C:
+            raise _lib.DsvtError("add_layernorm: d holds %d rows, %d needed" % (d.numel() // C, need))
+    if ymode != _lib.ROWLN_NONE:
+        if y.dtype not in (torch.bfloat16, torch.float32):
+            raise _lib.DsvtError("add_layernorm: y must be bf16 or fp32 (got %s)" % y.dtype)
+        _check(y, y.dtype, "y")
+        need = rows if ymode == _lib.ROWLN_X else rows // L * (L - 1)
+        if y.numel() < need * C:
+            raise _lib.DsvtError("add_layernorm: y holds %d rows, %d needed" % (y.numel() // C, need))
+    g = ln.weight if ln is not None else None
+    b = ln.bias if ln is not None else None
+    eps = ln.eps if ln is not None else 0.0
+    call("dsvt_add_layernorm_fwd", _dt(d.dtype) if d is not None else _lib.BF16,
+         _dt(y.dtype) if y is not None else _lib.BF16, _ptr(X), _ptr(d), _ptr(y), _ptr(g), _ptr(b), rows, C, L,
+         int(dmode), int(ymode), float(eps), _stream())
+    return X
+
+
 def gemm_resid_ln(a, w, bias, X, M=None, rowmap=None, ln=None, Y=None, ymode=_lib.ROWLN_NONE, L=0):
     """X[row(m)] += a[m] . w^T + bias (fp32 X, N = 768), then (ymode != NONE) Y[yrow] =
     LayerNorm(X[row(m)]) in bf16 -- one full-row kernel (csrc/gemm_rowln.hip).  ln = the

@@ -101,6 +101,20 @@ int dsvt_gemm_resid_scaled_fwd(int dtype, const void *A, int64_t lda, const void
                                const float *bias_row_scale, const float *x_in, float *x_out, int64_t ldx, int64_t M,
                                int64_t N, int64_t K, void *stream);
 
+/* The residual add of a sub-layer and the LayerNorm that reads the updated rows next, as one
+ * streaming pass (models/timesformer.py:133-135, 181, 184 `x = x + f(x)`, then norm1 :105,
+ * norm2 :112/184 or the next block's temporal_norm1 :99), C = 768.  The sub-layer GEMM writes
+ * d = f(x) with a plain bias epilogue (dsvt_gemm_fwd, DSVT_EPI_BIAS); per X row r (clips of L
+ * rows, row 0 of a clip = CLS):
+ *   X[r] += d[drow(r)]                 dmode 0: none; DSVT_ROWLN_X: drow = r;
+ *                                      DSVT_ROWLN_COMPACT: the patch-row index (r/L)*(L-1) + r%L - 1
+ *                                      (CLS rows have none: the temporal branch)
+ *   y[yrow(r)] = LayerNorm(X[r])*gamma + beta   ymode, same three layouts (0: no y)
+ * x fp32 [rows, 768]; d / y in d_dtype / y_dtype (DSVT_BF16 / DSVT_F32); rows a multiple of L. */
+int dsvt_add_layernorm_fwd(int d_dtype, int y_dtype, float *x, const void *d, void *y, const float *gamma,
+                           const float *beta, int64_t rows, int64_t C, int64_t L, int dmode, int ymode,
+                           float eps, void *stream);
+
 /* K7 + K3 fused, bf16 only, N = 768 (ViT-B): the residual projections attn.proj / temporal_fc /
  * mlp.fc2 with their residual add (models/timesformer.py:133-135, 181, 184) and the LayerNorm
  * that reads the updated rows next (norm1 :105, norm2 :112/184, the next block's

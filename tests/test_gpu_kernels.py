@@ -582,6 +582,52 @@ def test_layernorm_c768_multirow(rows, out_dtype, mapped):
     check(back(out), O.layer_norm(x[idx], g, bb), out_dtype, "ln768")
 
 
+@pytest.mark.parametrize("L,nclip", [(1569, 16), (289, 3), (5, 1)])
+@pytest.mark.parametrize("dmode,ymode", [(1, 1), (2, 1), (1, 2), (1, 0), (0, 2)])
+@pytest.mark.parametrize("dtype", DT)
+def test_add_layernorm(L, nclip, dmode, ymode, dtype):
+    """dsvt_add_layernorm_fwd (x += d; y = LayerNorm(x)) for every d / y row layout (the
+    identity rows, the compact patch rows of the temporal branch, none) at the bench's 16 global
+    clips (grid-stride path) and ragged small shapes, d / y in the storage dtype, vs float64:
+    X exactly x + d (fp32 add of the stored d), untouched rows (CLS under the compact d layout)
+    bit-identical, y rows that are not written left alone."""
+    from dsvt import _lib, ops
+    C = 768
+    rows = nclip * L
+    prow = (np.arange(rows) // L) * (L - 1) + np.arange(rows) % L - 1
+    prow[np.arange(rows) % L == 0] = -1
+    x = rnd((rows, C), 40, 2.0) + 0.25
+    nd = rows if dmode == 1 else nclip * (L - 1)
+    dd = rnd((max(nd, 1), C), 41, 1.0)
+    g, bb = 1 + rnd((C,), 42, 0.1), rnd((C,), 43, 0.1)
+    X = to(x, torch.float32)
+    D = to(dd, dtype)
+    ny = rows if ymode == 1 else nclip * (L - 1)
+    Y = torch.full((max(ny, 1), C), 7.0, device=dev(), dtype=dtype)
+    ln = torch.nn.LayerNorm(C, eps=1e-6).to(dev())
+    with torch.no_grad():
+        ln.weight.copy_(torch.from_numpy(g))
+        ln.bias.copy_(torch.from_numpy(bb))
+    ops.add_layernorm(X, D if dmode else None, L, dmode, ln=ln, y=Y if ymode else None, ymode=ymode)
+    torch.cuda.synchronize()
+    dq = back(D).astype(np.float32)
+    want = x.copy()
+    if dmode == 1:
+        want = (x + dq[:rows]).astype(np.float32)
+    elif dmode == 2:
+        m = prow >= 0
+        want[m] = (x[m] + dq[prow[m]]).astype(np.float32)
+    got = X.cpu().numpy()
+    assert np.array_equal(got, want), "X after the residual add"
+    if ymode:
+        ref = O.layer_norm(want.astype(np.float64), g, bb)
+        sel = np.arange(rows) if ymode == 1 else np.where(prow >= 0)[0]
+        ysel = sel if ymode == 1 else prow[sel]
+        check(back(Y)[ysel], ref[sel], dtype, "add_ln y")
+    with pytest.raises(_lib.DsvtError):
+        ops.add_layernorm(X, None, L, 0, ln=None, y=None, ymode=0)      # nothing to do
+
+
 @pytest.mark.parametrize("variant", [0, 7])
 def test_attn_spatial_short_local_shape(variant):
     """The 96^2 local-crop spatial shape (1 + 36 keys, B=6 clips x 8 frames, 12 heads): the
