@@ -154,6 +154,26 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * one_plus_erf;
 }
 
+// GELU for a bf16 OUTPUT (inference fc1 epilogue): x * sigmoid(x * P(x^2)) with P a quadratic in
+// x^2 fitted minimax to the exact erf GELU on [-10, 10] (x^2 clamped at 100 outside, where the
+// sigmoid has saturated): |error| <= 2.6e-5 absolute -- below half a bf16 ulp of the output for
+// |GELU(x)| >= 0.013, and far below the 2^-9 relative rounding of the stored value elsewhere.
+// 7 VALU + 2 transcendental ops against ~16 + 2 for gelu_erf: the fc1 epilogue is VALU-bound
+// and runs with no MFMA beside it.  fp32 outputs (parity mode) and the training epilogues (whose
+// backward differentiates gelu_erf) keep gelu_erf.  Coefficients pre-scaled by -log2(e).
+__device__ __forceinline__ float gelu_bf16out(float x) {
+  const float x2 = fminf(x * x, 100.0f);
+  const float p = fmaf(fmaf(1.01426306e-03f, x2, -1.06775724e-01f), x2, -2.30112134e+00f);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * p));
+}
+
+// the inference GELU epilogue by output type: the fast form only when the result is stored in bf16
+template <bool BF16_OUT>
+__device__ __forceinline__ float gelu_out(float x) {
+  if constexpr (BF16_OUT) return gelu_bf16out(x);
+  else return gelu_erf(x);
+}
+
 // d GELU / dx = Phi(x) + x phi(x) (same A&S 7.1.26 erf as gelu_erf): the Mlp.fc1 backward.
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float z = fabsf(x) * 0.70710678118654752f;

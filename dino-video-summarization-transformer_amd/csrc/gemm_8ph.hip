@@ -33,6 +33,10 @@
 
 #include "gemm_epi.h"
 
+#ifndef DSVT_8PH_GELU_NOFAST
+#define DSVT_8PH_GELU_NOFAST 1   // the 16-byte pair-store path spills (201 VGPRs with the fast GELU too)
+#endif
+
 namespace dsvt {
 
 namespace {
@@ -81,6 +85,13 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   const int ntl = (t_end - t_first + per_x - 1) / per_x;
   const int nk = (int)(p.K >> 6);
   const int J = ntl * nk;                 // K-tiles in this workgroup's stream
+  // a workgroup with fewer tiles than the longest has slack: it starts late so its epilogue
+  // store bursts do not coincide with the others' (every CU storing a 128 KB tile at once is
+  // what stalls the next K-tile's waits); wave-uniform scalar clock reads only
+  if (p.stagger_cycles > 0 && ntl < (tpx + per_x - 1) / per_x) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)p.stagger_cycles) __builtin_amdgcn_s_sleep(8);
+  }
 
   const char* A = (const char*)p.A;
   const char* W = (const char*)p.W;
@@ -277,7 +288,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(acc[i][jj]));
       } else {
-        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC, EPI == EPI_GELU>(p, acc, rbase, cbase,
+        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST)>(p, acc, rbase, cbase,
                                                                                           r16, g);
       }
       post = S_EPI > 0 && rbase + 128 <= p.M && cbase + 64 <= p.N;
@@ -315,6 +326,7 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
   dim3 grid((unsigned)G), block(512);
   GemmParams q = p;
   if (const char* e = getenv("DSVT_TILE_GROUP")) q.tile_group = atoi(e);
+  if (const char* e = getenv("DSVT_8PH_STAGGER")) q.stagger_cycles = atoll(e);
 #define DSVT_K(E, F) gemm_8ph_kernel<E, F><<<grid, block, 0, s>>>(q)
   if (abl) {                                          // diagnostic builds: EPI_BIAS, bf16 out
     if (epi != EPI_BIAS || out_f32) return hipErrorInvalidValue;

@@ -233,7 +233,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_big_kernel(GemmParams p)
           v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
         }
         if constexpr (EPI == EPI_GELU) {
-          v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+          constexpr bool BO = std::is_same<OutT, bf16_t>::value;
+          v0 = gelu_out<BO>(v0); v1 = gelu_out<BO>(v1); v2 = gelu_out<BO>(v2); v3 = gelu_out<BO>(v3);
         }
         const int byte = col * ES;
         const int chunk = (byte >> 4) ^ ((R >> 1) & 7 & (CPR - 1));

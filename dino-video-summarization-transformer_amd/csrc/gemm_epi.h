@@ -108,7 +108,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           }
           if constexpr (EPI == EPI_GELU) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_out<true>(acc[i][j][e]);   // bf16 output
           }
           if constexpr (RS) {
             if (scaled) {
@@ -162,7 +162,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
       acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
       if constexpr (EPI == EPI_GELU) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_out<!OUT_F32>(acc[i][j][e]);
       }
       if constexpr (RS) {
 #pragma unroll

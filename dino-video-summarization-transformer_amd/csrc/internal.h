@@ -28,6 +28,9 @@ struct GemmParams {
   // is not scaled.  Only the 128x128 and persistent kernels take it (gemm_variant_for).
   const float* row_scale = nullptr;
   int64_t rs_group = 1;
+  // persistent 256x256 kernel: workgroups with fewer tiles than the longest start this many
+  // shader cycles late (their epilogue store bursts then fall between the others')
+  int64_t stagger_cycles = 0;
 };
 
 // the DropPath scale of GEMM row m (1 when none)

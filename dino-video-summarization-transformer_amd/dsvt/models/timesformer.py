@@ -297,12 +297,13 @@ class VisionTransformer(nn.Module):
         # at K = 768, 210 vs 185 us at K = 3072, 25k rows) -- a full-row workgroup must pull all of
         # W through LDS-DMA for only ~100 rows, which caps it at ~20-25 GB/s per CU
         self.fuse_ln = os.environ.get("DSVT_FUSE_LN", "0") == "1"
-        # divided, C = 768, inference: every residual projection (temporal_fc, attn.proj, mlp.fc2)
-        # writes its output d = f(x) with a plain bias epilogue (the MFMA kernel never touches the
-        # fp32 token rows) and one streaming pass does x += d together with the LayerNorm the next
-        # GEMM reads (dsvt_add_layernorm_fwd).  DSVT_SPLIT_RESID=0 keeps the fp32 residual
-        # epilogue inside the GEMM followed by a separate LayerNorm.
-        self.split_resid = os.environ.get("DSVT_SPLIT_RESID", "1") == "1"
+        # opt-in (divided, C = 768, inference): every residual projection (temporal_fc, attn.proj,
+        # mlp.fc2) writes d = f(x) with a plain bias epilogue and one streaming pass does x += d
+        # together with the LayerNorm the next GEMM reads (dsvt_add_layernorm_fwd).  Off by
+        # default: measured slower (serial step 26.6 vs 26.0 ms, graph bench 347 vs 356 clips/s):
+        # the bias-only GEMM saves ~9 us per launch over the fp32 residual epilogue, the add-LN
+        # pass (231 MB at 6.3 TB/s, 35 us) costs ~19 us more than the LayerNorm it replaces
+        self.split_resid = os.environ.get("DSVT_SPLIT_RESID", "0") == "1"
         # inference: split a batch into this many clip chunks on concurrent HIP streams (each
         # kernel's last partly-filled wave of tiles then runs beside the other chunk's kernels);
         # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
