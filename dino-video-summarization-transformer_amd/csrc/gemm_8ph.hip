@@ -65,10 +65,13 @@ __device__ __forceinline__ void p8_barrier() {
 // loads after the prologue (stale tiles), bit 2 no MFMA (reads kept live), bit 3 no setprio,
 // bit 4 no epilogue (accumulators kept live), bit 5 non-temporal output stores, bit 6 epilogue
 // without its stores
-template <int EPI, bool OUT_F32, int ABL = 0>
+// NFULL: N % 256 == 0 (every tile full in N), bias / GELU with a bf16 output -- the epilogue is
+// the 16-byte store path alone for every tile (rows past M clamped, gemm_epi.h)
+template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
+  constexpr bool CLAMPED = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32;
   // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores
-  constexpr int S_EPI = (EPI == EPI_BIAS && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
+  constexpr int S_EPI = ((EPI == EPI_BIAS || CLAMPED) && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
   __shared__ __attribute__((aligned(16))) char smem[2 * P8_BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -288,10 +291,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(acc[i][jj]));
       } else {
-        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST)>(p, acc, rbase, cbase,
+        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), false, NFULL>(p, acc, rbase, cbase,
                                                                                           r16, g);
       }
-      post = S_EPI > 0 && rbase + 128 <= p.M && cbase + 64 <= p.N;
+      post = S_EPI > 0 && (CLAMPED || (rbase + 128 <= p.M && cbase + 64 <= p.N));
       kc = 0;
       ++tlc;
       __builtin_amdgcn_sched_barrier(0);   // keep the next tile's bias loads after the stores
@@ -343,10 +346,19 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
     }
     return hipGetLastError();
   }
+  const bool nfull = p.N % 256 == 0 && !out_f32 && !getenv("DSVT_8PH_NO_NFULL");
   switch (epi) {
-    case EPI_BIAS: if (out_f32) DSVT_K(EPI_BIAS, true); else DSVT_K(EPI_BIAS, false); break;
+    case EPI_BIAS:
+      if (out_f32) DSVT_K(EPI_BIAS, true);
+      else if (nfull) gemm_8ph_kernel<EPI_BIAS, false, 0, true><<<grid, block, 0, s>>>(q);
+      else DSVT_K(EPI_BIAS, false);
+      break;
     case EPI_RESID: DSVT_K(EPI_RESID, true); break;
-    case EPI_GELU: if (out_f32) DSVT_K(EPI_GELU, true); else DSVT_K(EPI_GELU, false); break;
+    case EPI_GELU:
+      if (out_f32) DSVT_K(EPI_GELU, true);
+      else if (nfull) gemm_8ph_kernel<EPI_GELU, false, 0, true><<<grid, block, 0, s>>>(q);
+      else DSVT_K(EPI_GELU, false);
+      break;
     case EPI_GELU_SAVE: DSVT_K(EPI_GELU_SAVE, false); break;
     case EPI_DGELU: if (out_f32) DSVT_K(EPI_DGELU, true); else DSVT_K(EPI_DGELU, false); break;
     default: return hipErrorInvalidValue;

@@ -27,8 +27,12 @@ __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int 
 // NOFAST: skip the full-tile 16-byte pair-store path (its cross-lane packing keeps more values
 // live; gemm_8ph.hip's GELU instantiation spills with it)
 // ROWSCALE: honour p.row_scale (EPI_BIAS / EPI_GELU_SAVE; the persistent kernel's instantiation)
+// NFULL (bias / GELU, bf16 output; the caller guarantees cbase + NJ*16 <= N for every tile): the
+// 16-byte store path only, rows past M clamped to M - 1 -- their accumulators ARE row M - 1's
+// (the A loads of those rows are clamped to it), so the extra stores rewrite identical bytes,
+// and no per-lane bounds branch around the stores (which makes the compiler drain vmcnt)
 template <int MI, int NJ, int EPI, bool OUT_F32, bool NT = false, bool NOSTORE = false, bool BIAS_IN_ACC = false,
-          bool NOFAST = false, bool ROWSCALE = false>
+          bool NOFAST = false, bool ROWSCALE = false, bool NFULL = false>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
@@ -94,11 +98,13 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
   const bool ident = p.rpg >= p.M;   // wave-uniform: no per-lane row-map division
   // full wave tile (uniform): branch-free bias / GELU / 16-B stores, so the compiler's vmcnt
   // waits stay exact (a per-lane bounds branch around each store makes it drain every time)
-  if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0 && !NOFAST) {
-    if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
+  constexpr bool CLAMP = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0;
+  if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0 && (!NOFAST || CLAMP)) {
+    if (CLAMP || (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N)) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int64_t m = rbase + i * 16 + r16;
+        int64_t m = rbase + i * 16 + r16;
+        if constexpr (CLAMP) m = m < p.M ? m : p.M - 1;
         const int64_t orow = ident ? m : map_row(m, p.rpg, p.gstride, p.goff);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -106,24 +112,29 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
             const float4 bb = bias4[j];
             acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
           }
-          if constexpr (EPI == EPI_GELU) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_out<true>(acc[i][j][e]);   // bf16 output
-          }
           if constexpr (RS) {
-            if (scaled) {
+            if (scaled && EPI != EPI_GELU) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) acc[i][j][e] *= rsc[i];
             }
           }
         }
 #pragma unroll
-        for (int j = 0; j < NJ; j += 2)
+        for (int j = 0; j < NJ; j += 2) {
+          if constexpr (EPI == EPI_GELU) {     // one fragment pair's GELUs live at a time (bf16 output)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[i][j + jj][e] = gelu_out<true>(acc[i][j + jj][e]);
+          }
           store_pair_bf16<NT, NOSTORE>((bf16_t*)p.out + orow * p.ldo + cbase + j * 16, acc[i][j], acc[i][j + 1], g);
+        }
       }
       return;
     }
   }
+  if constexpr (CLAMP) return;
   // full wave tile, fp32 residual add into X: the X fragments of two rows are loaded before
   // their stores (one HBM round trip per row pair instead of per fragment), branch-free
   if constexpr (EPI == EPI_RESID && MI % 2 == 0) {

@@ -122,17 +122,18 @@ def test_gelu_epilogue_accuracy():
 def test_gelu_epilogue_bf16(variant):
     """The bf16-output GELU epilogue (gelu_bf16out: x * sigmoid(x * P(x^2)), every kernel that
     takes EPI_BIAS_GELU) against the exact erf GELU of the bf16-rounded input, x in [-12, 12]
-    plus extremes: within half a bf16 ulp of the result + 3e-5 (the approximation's fitted
+    plus extremes: within half a bf16 ulp of the result (<= 2^-8 relative) + 3e-5 (the approximation's fitted
     2.6e-5 bound)."""
     from dsvt import _lib, ops
     from dsvt._lib import EPI_BIAS_GELU
     n = 64 * 256
-    x = np.concatenate([np.linspace(-12, 12, 4096 * 64 - 8), [0.0, 1e-6, -1e-6, 1e-3, -1e-3, 60.0, -60.0, -0.5]])
-    x = x.astype(np.float32).reshape(4096, 64)
+    M = 4096 + 40                      # a ragged last 256-row tile (clamped rows in the 256x256 kernel)
+    x = np.concatenate([np.linspace(-12, 12, M * 64 - 8), [0.0, 1e-6, -1e-6, 1e-3, -1e-3, 60.0, -60.0, -0.5]])
+    x = x.astype(np.float32).reshape(M, 64)
     A = to(x, torch.bfloat16)
     W = torch.eye(64, device=dev(), dtype=torch.bfloat16)
     W = torch.cat([W, W, W, W], 0).repeat(n // 256, 1).contiguous()      # N = n: 256 copies of x's columns
-    out = torch.empty(4096, n, device=dev(), dtype=torch.bfloat16)
+    out = torch.empty(M, n, device=dev(), dtype=torch.bfloat16)
     _lib.call("dsvt_set_gemm_variant", variant)
     try:
         ops.gemm(A, W, torch.zeros(n, device=dev()), out, epilogue=EPI_BIAS_GELU)
@@ -144,7 +145,7 @@ def test_gelu_epilogue_bf16(variant):
     got = back(out)
     for c0 in (0, n - 64):
         err = np.abs(got[:, c0:c0 + 64] - ref)
-        assert (err <= np.abs(ref) * 2.0 ** -9 + 3e-5).all(), err.max()
+        assert (err <= np.abs(ref) * 2.0 ** -8 + 3e-5).all(), err.max()
 
 
 @pytest.mark.parametrize("dtype", DT)
