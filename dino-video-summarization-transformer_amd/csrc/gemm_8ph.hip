@@ -63,7 +63,8 @@ __device__ __forceinline__ void p8_barrier() {
 
 // ABL (diagnostic builds, benchmarking only; 0 = normal): bit 0 no wave-row stagger, bit 1 no
 // loads after the prologue (stale tiles), bit 2 no MFMA (reads kept live), bit 3 no setprio,
-// bit 4 no epilogue (accumulators kept live), bit 5 non-temporal output stores, bit 6 epilogue
+// bit 4 no epilogue (accumulators kept live), bit 5 non-temporal output stores, bit 7 sc1 output
+// stores (DSVT_8PH_SC1, full-N bias / GELU), bit 6 epilogue
 // without its stores
 // NFULL: N % 256 == 0 (every tile full in N), bias / GELU with a bf16 output -- the epilogue is
 // the 16-byte store path alone for every tile (rows past M clamped, gemm_epi.h)
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(acc[i][jj]));
       } else {
-        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) != 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), false, NFULL>(p, acc, rbase, cbase,
+        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), false, NFULL>(p, acc, rbase, cbase,
                                                                                           r16, g);
       }
       post = S_EPI > 0 && (CLAMPED || (rbase + 128 <= p.M && cbase + 64 <= p.N));
@@ -347,6 +348,11 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
     return hipGetLastError();
   }
   const bool nfull = p.N % 256 == 0 && !out_f32 && !getenv("DSVT_8PH_NO_NFULL");
+  if (nfull && getenv("DSVT_8PH_SC1") && (epi == EPI_BIAS || epi == EPI_GELU)) {   // sc1 output stores
+    if (epi == EPI_BIAS) gemm_8ph_kernel<EPI_BIAS, false, 128, true><<<grid, block, 0, s>>>(q);
+    else gemm_8ph_kernel<EPI_GELU, false, 128, true><<<grid, block, 0, s>>>(q);
+    return hipGetLastError();
+  }
   switch (epi) {
     case EPI_BIAS:
       if (out_f32) DSVT_K(EPI_BIAS, true);
