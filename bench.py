@@ -491,8 +491,14 @@ def main():
     graph = None
     if not args.no_graph:
         graph = torch.cuda.CUDAGraph()
+        # capture on a stream of our own that has run the step eagerly once: its per-stream
+        # scratch (the stream-K GEMM workspace, dsvt.ops) then exists before capture
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            forward_loss()
         torch.cuda.synchronize()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, stream=cap):
             g_loss = forward_loss()
         torch.cuda.synchronize()
 

@@ -139,6 +139,7 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_SELECT: return up(select_frames_ws_bytes(M, N));                    // M = scores, N = unsampled
     case DSVT_WS_AUGMENT: return up(augment_ws_bytes(M, N));                          // M = frames, N = size
     case DSVT_WS_WGRAD: return up(wgrad_workspace_floats(M, N, K) * 4);              // M = rows, N, K: G [N, K]
+    case DSVT_WS_GEMM_SK: return SK_WS_BYTES;                                        // any shape
     default: return -1;
   }
 }
@@ -152,6 +153,24 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t l
   norm_map(rpg, gstride, goff);
   GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
+                [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
+                gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
+}
+
+int dsvt_gemm_sk_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, const void* W, int64_t ldw,
+                     const float* bias, void* out, int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg,
+                     int64_t gstride, int64_t goff, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
+  REQUIRE(epilogue <= 2, "gemm_sk: epilogue %d is reachable only through dsvt_patch_embed_fwd / dsvt_gemm_aux_fwd",
+          epilogue);
+  REQUIRE(workspace && workspace_bytes >= SK_WS_BYTES && ((uintptr_t)workspace & 255) == 0,
+          "gemm_sk: workspace must be >= %lld bytes (dsvt_workspace_bytes(DSVT_WS_GEMM_SK)), 256-byte aligned",
+          (long long)SK_WS_BYTES);
+  norm_map(rpg, gstride, goff);
+  GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.sk_cnt = (int*)workspace;
+  p.sk_part = (float*)((char*)workspace + SK_CNT_BYTES);
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_sk_fwd",
                 [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
                 gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
 }
@@ -475,8 +494,9 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 
 int dsvt_set_gemm_variant(int variant) {
   REQUIRE(variant == 0 || variant == 1 || variant == 2 || (variant >= 3 && variant <= 6) || (variant >= 9 && variant <= 13) ||
-              (variant >= 20 && variant <= 29 && variant != 24) || variant == 14 || variant == 24 || variant == 34,
-          "gemm variant must be 0-6, 9-13 or 20 (14/24/34: ablation builds)");
+              (variant >= 20 && variant <= 29 && variant != 24) || variant == 14 || variant == 24 || variant == 34 ||
+              variant == 40,
+          "gemm variant must be 0-6, 9-13, 20 or 40 (stream-K; 14/24/34: ablation builds)");
   set_gemm_variant(variant);
   return 0;
 }

@@ -462,18 +462,34 @@ void set_gemm_variant(int v) { g_gemm_variant = v; }
 // N=2304, fc1 N=3072, proj / folded temporal fc N=768) -> persistent staggered 256x128 (v10:
 // 2 WGs/CU, the epilogue of one overlaps the MFMA loop of the other, the next tile's loads fly
 // under the store tail); K = 3072 (fc2), small M (DINO head) and the patch GEMM -> 128x128.
+// Stream-K (variant 40) for the calls that pass a workspace (dsvt_gemm_sk_fwd): DSVT_SK = 0
+// (default) never, 1 bias / GELU projections, 2 also the fp32 residual ones.  Opt-in: measured
+// slower than the data-parallel kernels on every hot-path shape (qkv 118 vs 104 us, fc2 172 vs
+// 137 us): writing and re-reading 256 KB fp32 partial tiles costs more than the tail round.
+static bool sk_auto(int epi) {
+  static const int mode = [] {
+    const char* e = getenv("DSVT_SK");
+    return e ? atoi(e) : 0;
+  }();
+  return mode >= 2 || (mode == 1 && epi != EPI_RESID);
+}
+
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
+  if (p.sk_part && !p.row_scale && gemm_sk_ok(p, epi, out_f32) &&
+      (g_gemm_variant == 40 || (g_gemm_variant == 0 && sk_auto(epi))))
+    return 40;
+  const int gv = g_gemm_variant == 40 ? 0 : g_gemm_variant;   // forced stream-K, ineligible shape: auto
   if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
-  if (g_gemm_variant >= 20 && g_gemm_variant <= 29) return gemm_8ph_ok(p, epi) ? g_gemm_variant : 1;
-  if (g_gemm_variant == 2) return (gemm_pipe_ok(p) && epi != EPI_PATCH) ? 2 : 1;
+  if (gv >= 20 && gv <= 29) return gemm_8ph_ok(p, epi) ? gv : 1;
+  if (gv == 2) return (gemm_pipe_ok(p) && epi != EPI_PATCH) ? 2 : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
-    if (g_gemm_variant == 1 || g_gemm_variant == 9 || g_gemm_variant == 10) return g_gemm_variant;
+    if (gv == 1 || gv == 9 || gv == 10) return gv;
     return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   }
-  if (g_gemm_variant) return g_gemm_variant;
+  if (gv) return gv;
   // wide bias-only projections with a bf16 output (qkv, N = 2304): the 256x256 phase-interleaved
   // kernel (v20) -- measured 895 vs 828 TF/s (global crops) and 933 vs 786 (local crops)
   // fc1 + GELU likewise (728 vs 709 TF/s global crops; its epilogue uses the general store path)
@@ -490,6 +506,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
+  if (v == 40) return launch_gemm_sk(p, epi, out_f32, s);
   if (v == 2) return launch_pipe(p, epi, out_f32, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);

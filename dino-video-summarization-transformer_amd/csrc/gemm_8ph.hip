@@ -68,12 +68,20 @@ __device__ __forceinline__ void p8_barrier() {
 // without its stores
 // NFULL: N % 256 == 0 (every tile full in N), bias / GELU with a bf16 output -- the epilogue is
 // the 16-byte store path alone for every tile (rows past M clamped, gemm_epi.h)
-template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false>
+// SK (stream-K): the tiles x nk K-tiles form ONE iteration space split evenly over the grid
+// (logical workgroup order XCD-major, so an XCD's workgroups walk adjacent tiles and share their
+// A panels in L2); a range may start and end inside a tile.  Every partial segment of a tile
+// stores its fp32 sums to its slot and counts itself in on the tile's counter; the workgroup
+// that arrives last adds all slots in segment order (run-to-run deterministic) and runs the
+// epilogue -- nobody waits on another workgroup, so concurrent launches on other streams cannot
+// deadlock it.  No quantization tail: qkv at 25 104 rows is 891 tiles = 3.48 rounds of 256.
+template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false, bool SK = false>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   constexpr bool CLAMPED = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32;
   // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores
   constexpr int S_EPI = ((EPI == EPI_BIAS || CLAMPED) && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
   __shared__ __attribute__((aligned(16))) char smem[2 * P8_BUF];
+  __shared__ int sk_flag;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -83,19 +91,42 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   const int tiles = (int)((p.M + 255) >> 8) * tilesN;
   // XCD-contiguous tile ranges (block b runs on XCD b % 8; the grid is a multiple of 8)
   const int G = gridDim.x, b = blockIdx.x, xcd = b & 7, li = b >> 3, per_x = G >> 3;
-  const int tpx = (tiles + 7) >> 3;
-  const int t_first = xcd * tpx + li, t_end = min(tiles, xcd * tpx + tpx);
-  if (t_first >= t_end) return;
-  const int ntl = (t_end - t_first + per_x - 1) / per_x;
   const int nk = (int)(p.K >> 6);
-  const int J = ntl * nk;                 // K-tiles in this workgroup's stream
-  // a workgroup with fewer tiles than the longest has slack: it starts late so its epilogue
-  // store bursts do not coincide with the others' (every CU storing a 128 KB tile at once is
-  // what stalls the next K-tile's waits); wave-uniform scalar clock reads only
-  if (p.stagger_cycles > 0 && ntl < (tpx + per_x - 1) / per_x) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)p.stagger_cycles) __builtin_amdgcn_s_sleep(8);
+  // This workgroup's K-tile stream runs over VIRTUAL tiles tl = 0 .. tl_end-1.  Plain: its
+  // strided share of the tiles (XCD-contiguous ranges).  SK: the full rounds of tiles
+  // [0, T0 = tiles / G * G) stay data-parallel with that mapping, and the last partial round --
+  // the quantization tail -- is one iteration space of (tiles - T0) * nk K-tiles split evenly
+  // over the grid; a workgroup streams its tail range FIRST (virtual tiles 0 .. n_tail-1, the
+  // first starting at K-tile k0, the last ending at ke) and then its T0 / G whole tiles.
+  int t_first, k0 = 0, ke = nk, n_tail = 0, tail_t0 = 0, tl_end, J, wl = 0;
+  int64_t I_tail = 1, tail_base = 0;
+  if constexpr (SK) {
+    wl = xcd * per_x + li;
+    const int T0 = tiles / G * G, ndp = T0 / G;
+    t_first = xcd * (T0 >> 3) + li;
+    I_tail = (int64_t)(tiles - T0) * nk;                 // >= G (host-checked): no empty range
+    tail_base = (int64_t)T0 * nk;
+    const int64_t a = tail_base + (int64_t)wl * I_tail / G, b = tail_base + (int64_t)(wl + 1) * I_tail / G;
+    tail_t0 = (int)(a / nk);
+    k0 = (int)(a % nk);
+    ke = (int)((b - 1) % nk) + 1;
+    n_tail = (int)((b - 1) / nk) - tail_t0 + 1;
+    J = (int)(b - a) + ndp * nk;
+    tl_end = n_tail + ndp;
+  } else {
+    const int tpx = (tiles + 7) >> 3;
+    t_first = xcd * tpx + li;
+    const int t_end = min(tiles, xcd * tpx + tpx);
+    if (t_first >= t_end) return;
+    tl_end = (t_end - t_first + per_x - 1) / per_x;
+    J = tl_end * nk;
   }
+  // K-tile range [seg_k0, seg_k1) of virtual tile tl, and the stream advance
+  auto seg_k0 = [&](int tl) { return tl == 0 ? k0 : 0; };
+  auto seg_k1 = [&](int tl) { return tl == n_tail - 1 ? ke : nk; };
+  auto adv = [&](int& tl, int& k) {
+    if (++k == seg_k1(tl)) { k = 0; ++tl; }
+  };
 
   const char* A = (const char*)p.A;
   const char* W = (const char*)p.W;
@@ -107,7 +138,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   uint32_t oAT[2], oAB[2], oBL[2], oBR[2];
   const int tilesM = (int)((p.M + 255) >> 8), GM = p.tile_group;
   auto tile_mn = [&](int tl, int64_t& m0, int64_t& n0) {
-    const int t = t_first + tl * per_x;
+    const int t = tl < n_tail ? tail_t0 + tl : t_first + (tl - n_tail) * per_x;
     if (GM <= 0) {
       m0 = (int64_t)(t / tilesN) * 256;
       n0 = (int64_t)(t % tilesN) * 256;
@@ -203,12 +234,14 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   bool prologue_ = true;
   set_atbl(0);
   set_brab(0);
-  P8_STAGE(H_AT, oAT, A, 0, 0);
-  P8_STAGE(H_BL, oBL, W, 0, 0);
-  P8_STAGE(H_BR, oBR, W, 0, 0);
-  P8_STAGE(H_AB, oAB, A, 0, 0);
-  tl1 = 1 / nk; k1 = 1 % nk;
-  tl2 = 2 / nk; k2 = 2 % nk;
+  P8_STAGE(H_AT, oAT, A, 0, k0 * P8_ROWB);
+  P8_STAGE(H_BL, oBL, W, 0, k0 * P8_ROWB);
+  P8_STAGE(H_BR, oBR, W, 0, k0 * P8_ROWB);
+  P8_STAGE(H_AB, oAB, A, 0, k0 * P8_ROWB);
+  tl1 = 0; k1 = k0;
+  adv(tl1, k1);
+  tl2 = tl1; k2 = k1;
+  adv(tl2, k2);
   if (J > 1) {
     set_atbl(tl1);
     P8_STAGE(H_AT, oAT, A, P8_BUF, k1 * P8_ROWB);
@@ -225,9 +258,9 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   // accumulators start from the bias of their columns (the epilogue adds none)
   constexpr bool BIAS_IN_ACC = EPI != EPI_DGELU;
   fv4 acc[8][4];
-  auto init_acc = [&](int tl) {
+  auto init_acc = [&](int tl, bool with_bias) {   // SK: only a tile's k = 0 segment carries the bias
     float4 b4[4];
-    if (BIAS_IN_ACC && p.bias) {
+    if (BIAS_IN_ACC && p.bias && with_bias) {
       int64_t m0, n0;
       tile_mn(tl, m0, n0);
       const int64_t cbase = n0 + wc * 64;
@@ -249,10 +282,63 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = fv4{b4[j].x, b4[j].y, b4[j].z, b4[j].w};
   };
-  init_acc(0);
+  init_acc(0, k0 == 0);
   prologue_ = false;
-  int tlc = 0, kc = 0;                  // compute position
+  int tlc = 0, kc = k0;                 // compute position
   bool post = false;                    // previous K-tile ended with a full-tile epilogue
+
+  // SK: a partial segment of tail tile t (this workgroup's slot: 0 for its first tail tile, 1
+  // for its last).  Returns true in the workgroup that arrives last, with the tile's full sums
+  // in acc.  owner(it) = the workgroup whose tail range holds iteration it.
+  auto owner = [&](int64_t it) -> int { return (int)(((it - tail_base + 1) * G - 1) / I_tail); };
+  auto sk_combine = [&](int t, int slot) -> bool {
+    if (!(ABL & 1) && wr == 0) p8_barrier();   // unstagger: the barriers below pair up in place
+    // Hand-off without L2 write-back / invalidate fences (MI355X_MICROARCH.md, Valid forms, the
+    // first table row): the slot is written by `sc1` (write-through) 16-B stores -- one wave
+    // instruction covers 8 whole 128-B lines -- drained by every wave before the workgroup
+    // barrier and the counter add; the workgroup whose add returns last reads the slots with
+    // `sc1` loads after a barrier.  Inline-asm memory ops are invisible to the compiler's waits:
+    // expcnt(0) after each store (its data VGPRs are read out after issue), and every load's
+    // result passes through the vmcnt(0) below before use.
+    const int64_t lane_off = (int64_t)wave * 32 * 64 + lane;
+    fv4* mine = reinterpret_cast<fv4*>(p.sk_part) + (int64_t)(wl * 2 + slot) * 8 * 32 * 64 + lane_off;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_waitcnt expcnt(0)" ::"v"(mine + (i * 4 + jj) * 64),
+                     "v"(acc[i][jj])
+                     : "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) sk_flag = __hip_atomic_fetch_add(p.sk_cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int wa = owner((int64_t)t * nk), wb = owner((int64_t)(t + 1) * nk - 1);
+    const bool last = sk_flag == wb - wa;            // workgroup-uniform
+    if (last) {
+      if (tid == 0) __hip_atomic_store(p.sk_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = fv4{0.f, 0.f, 0.f, 0.f};
+      for (int w = wa; w <= wb; ++w) {             // segment order: deterministic sums
+        const int first_t = (int)((tail_base + (int64_t)w * I_tail / G) / nk);
+        const fv4* src = reinterpret_cast<const fv4*>(p.sk_part) + (int64_t)(w * 2 + (t == first_t ? 0 : 1)) * 8 * 32 * 64 + lane_off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          fv4 v[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[jj]) : "v"(src + (i * 4 + jj) * 64) : "memory");
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[i][jj] += v[jj];
+        }
+      }
+    }
+    if (!(ABL & 1) && wr == 1) p8_barrier();   // re-stagger
+    return last;
+  };
 
   for (int j = 0; j < J; ++j) {
     const int cb = (j & 1) * P8_BUF, sb1 = cb ^ P8_BUF, sb2 = cb;
@@ -281,12 +367,17 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     P8_COMPUTE(P8_MFMA(4, 0, fbl));
 
     post = false;
-    if (++kc == nk) {                   // tile done: register epilogue
+    if (++kc == seg_k1(tlc)) {            // tile (or SK tail segment) done: register epilogue
       int64_t m0, n0;
       tile_mn(tlc, m0, n0);
       const int64_t rbase = m0 + wr * 128, cbase = n0 + wc * 64;
       mfma_result_fence();
-      if constexpr ((ABL & 16) != 0) {
+      bool whole = true;
+      if constexpr (SK) {
+        if (tlc < n_tail && (seg_k0(tlc) != 0 || kc != nk)) whole = sk_combine(tail_t0 + tlc, tlc == 0 ? 0 : 1);
+      }
+      if (!whole) {
+      } else if constexpr ((ABL & 16) != 0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -295,15 +386,15 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
         epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), false, NFULL>(p, acc, rbase, cbase,
                                                                                           r16, g);
       }
-      post = S_EPI > 0 && (CLAMPED || (rbase + 128 <= p.M && cbase + 64 <= p.N));
+      post = whole && S_EPI > 0 && (CLAMPED || (rbase + 128 <= p.M && cbase + 64 <= p.N));
       kc = 0;
       ++tlc;
       __builtin_amdgcn_sched_barrier(0);   // keep the next tile's bias loads after the stores
-      if (tlc < ntl) init_acc(tlc);
+      if (tlc < tl_end) init_acc(tlc, true);
     }
     // advance the stagers
-    if (++k1 == nk) { k1 = 0; ++tl1; if (tl1 < ntl) set_brab(tl1); }
-    if (++k2 == nk) { k2 = 0; ++tl2; if (tl2 < ntl) set_atbl(tl2); }
+    { const int o = tl1; adv(tl1, k1); if (tl1 != o && tl1 < tl_end) set_brab(tl1); }
+    { const int o = tl2; adv(tl2, k2); if (tl2 != o && tl2 < tl_end) set_atbl(tl2); }
   }
   if (!(ABL & 1) && wr == 0) p8_barrier();  // balance the stagger barrier
 #undef P8_STAGE
@@ -330,7 +421,6 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
   dim3 grid((unsigned)G), block(512);
   GemmParams q = p;
   if (const char* e = getenv("DSVT_TILE_GROUP")) q.tile_group = atoi(e);
-  if (const char* e = getenv("DSVT_8PH_STAGGER")) q.stagger_cycles = atoll(e);
 #define DSVT_K(E, F) gemm_8ph_kernel<E, F><<<grid, block, 0, s>>>(q)
   if (abl) {                                          // diagnostic builds: EPI_BIAS, bf16 out
     if (epi != EPI_BIAS || out_f32) return hipErrorInvalidValue;
@@ -370,6 +460,33 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
     default: return hipErrorInvalidValue;
   }
 #undef DSVT_K
+  return hipGetLastError();
+}
+
+}  // namespace dsvt
+
+namespace dsvt {
+
+// ---- stream-K launch (variant 40): the kernel above with SK = true.  p.sk_part / p.sk_cnt point
+// into the caller's workspace (gemm_sk_workspace_bytes; counters zero on entry, left zero).
+bool gemm_sk_ok(const GemmParams& p, int epi, int out_f32) {
+  if (!gemm_8ph_ok(p, epi)) return false;
+  const int64_t tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  // a quantization tail to split, at least one tail K-tile per workgroup
+  if (tiles > SK_MAX_TILES || tiles % 256 == 0 || (tiles % 256) * (p.K / 64) < 256) return false;
+  if (epi == EPI_RESID) return true;                   // fp32 token rows whatever out_f32 says
+  return (epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.N % 256 == 0;
+}
+
+hipError_t launch_gemm_sk(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
+  if (!gemm_sk_ok(p, epi, out_f32) || !p.sk_part || !p.sk_cnt) return hipErrorInvalidValue;
+  dim3 grid(256), block(512);
+  switch (epi) {
+    case EPI_BIAS: gemm_8ph_kernel<EPI_BIAS, false, 0, true, true><<<grid, block, 0, s>>>(p); break;
+    case EPI_GELU: gemm_8ph_kernel<EPI_GELU, false, 0, true, true><<<grid, block, 0, s>>>(p); break;
+    case EPI_RESID: gemm_8ph_kernel<EPI_RESID, true, 0, false, true><<<grid, block, 0, s>>>(p); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

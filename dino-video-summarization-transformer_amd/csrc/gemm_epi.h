@@ -11,6 +11,7 @@ namespace dsvt {
 // NT = 2: `sc1` store -- the line is written through and dropped from the XCD's L2 (MI355X_MICROARCH
 // §Workgroup dispatch, stores table), leaving L2 to the re-read operand panels.  The inline-asm
 // store is invisible to the compiler's vmcnt bookkeeping; its own waits only get more conservative.
+// (Without the expcnt wait the outputs came out as garbage: measured.)
 template <int NT = 0, bool NOSTORE = false>
 __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int g) {
   const uint4 v = pack_pair_bf16(a, b);
@@ -19,7 +20,10 @@ __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int 
   } else if constexpr (NT == 2) {
     typedef unsigned int uv4 __attribute__((ext_vector_type(4)));
     const uv4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(span + pair_off(g)), "v"(w) : "memory");
+    // expcnt(0): the store's data VGPRs are read out after issue; the compiler, blind to the asm,
+    // would reuse them at once
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_waitcnt expcnt(0)" ::"v"(span + pair_off(g)), "v"(w)
+                 : "memory");
   } else if constexpr (NT == 1) {
     typedef unsigned int uv4 __attribute__((ext_vector_type(4)));
     const uv4 w = {v.x, v.y, v.z, v.w};

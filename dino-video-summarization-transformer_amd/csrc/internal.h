@@ -28,9 +28,10 @@ struct GemmParams {
   // is not scaled.  Only the 128x128 and persistent kernels take it (gemm_variant_for).
   const float* row_scale = nullptr;
   int64_t rs_group = 1;
-  // persistent 256x256 kernel: workgroups with fewer tiles than the longest start this many
-  // shader cycles late (their epilogue store bursts then fall between the others')
-  int64_t stagger_cycles = 0;
+  // stream-K 256x256 kernel: partial-sum slots ([2 * grid][256 x 256] fp32) and one arrival
+  // counter per output tile (zero on entry, left zero on exit)
+  float* sk_part = nullptr;
+  int* sk_cnt = nullptr;
 };
 
 // the DropPath scale of GEMM row m (1 when none)
@@ -54,6 +55,13 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // 
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
 bool gemm_8ph_ok(const GemmParams& p, int epi);
+// stream-K 256x256 GEMM (variant 40): workspace = [SK_MAX_TILES int32 counters][2 x 256 slots of
+// 256 x 256 fp32 partial sums]
+constexpr int64_t SK_MAX_TILES = 65536;
+constexpr int64_t SK_CNT_BYTES = SK_MAX_TILES * 4;
+constexpr int64_t SK_WS_BYTES = SK_CNT_BYTES + 2 * 256 * 256 * 256 * 4;
+bool gemm_sk_ok(const GemmParams& p, int epi, int out_f32);
+hipError_t launch_gemm_sk(const GemmParams& p, int epi, int out_f32, hipStream_t s);
 void set_gemm_variant(int v);
 
 // Full-row residual GEMM + fused LayerNorm (gemm_rowln.hip), bf16, N = 768:

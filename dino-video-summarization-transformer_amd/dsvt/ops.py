@@ -43,6 +43,25 @@ def workspace_bytes(op, mode, M, N, K):
     return int(_lib.lib().dsvt_workspace_bytes(op, _dt(mode), M, N, K))
 
 
+_SK_WS = {}          # (device index, stream handle) -> zero-filled stream-K scratch (dsvt_gemm_sk_fwd)
+
+
+def _sk_workspace(dev):
+    """The stream-K GEMM scratch of the current stream: allocated (zero-filled) on first use
+    outside graph capture and kept; the kernels leave it zero.  One per stream, so GEMMs on
+    concurrent streams never share counters.  None while capturing a stream that has none (the
+    plain kernels run then) and unless DSVT_SK=1 / 2 (opt-in: measured slower than the
+    data-parallel kernels on every hot-path shape)."""
+    if os.environ.get("DSVT_SK", "0") == "0":
+        return None
+    key = (dev.index, _stream())
+    ws = _SK_WS.get(key)
+    if ws is None and not torch.cuda.is_current_stream_capturing():
+        nbytes = int(_lib.lib().dsvt_workspace_bytes(_lib.WS_GEMM_SK, _lib.BF16, 1, 1, 1))
+        ws = _SK_WS[key] = torch.zeros(nbytes // 4, device=dev, dtype=torch.int32)
+    return ws
+
+
 def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=None):
     """out[row(m)] (op)= a[m] . w^T (+bias ...); a [M,K] mode, w [N,K] mode."""
     mode = w.dtype
@@ -52,8 +71,13 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     K = a.shape[-1]
     N = w.shape[0]
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
-    call("dsvt_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
-         _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _stream())
+    ws = _sk_workspace(a.device) if mode == torch.bfloat16 else None
+    if ws is not None:
+        call("dsvt_gemm_sk_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
+             _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _ptr(ws), ws.numel() * 4, _stream())
+    else:
+        call("dsvt_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
+             _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _stream())
     return out
 
 

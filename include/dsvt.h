@@ -64,6 +64,7 @@ extern "C" {
 #define DSVT_WS_SELECT 10      /* M = number of scores, N = frames of the unsampled video */
 #define DSVT_WS_AUGMENT 11     /* M = output frames T, N = output size S */
 #define DSVT_WS_WGRAD 12       /* M = rows, N, K: the weight gradient is [N, K] */
+#define DSVT_WS_GEMM_SK 13     /* stream-K GEMM scratch (any shape) */
 
 int dsvt_version(void);
 const char *dsvt_last_error(void);
@@ -83,6 +84,19 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
 int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
                   int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N,
                   int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void *stream);
+/* dsvt_gemm_fwd with a caller-owned scratch: bf16 projections whose 256 x 256 tiles leave a
+ * partly filled last round of workgroups run stream-K -- the tiles x K-steps are split evenly
+ * over the grid, partial tiles meet in the workspace and the last workgroup to finish one runs
+ * its epilogue (deterministic: partial sums added in a fixed order).  Other shapes / dtypes
+ * take the dsvt_gemm_fwd kernels.  workspace >= dsvt_workspace_bytes(DSVT_WS_GEMM_SK, ...),
+ * 256-byte aligned, ZERO-FILLED before its first use (the calls leave it that way); calls that
+ * may run concurrently need separate workspaces.  Replaces the same nn.Linear calls as
+ * dsvt_gemm_fwd (models/timesformer.py:63, 71, 41-52, 127-135). */
+int dsvt_gemm_sk_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
+                     int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N, int64_t K,
+                     int64_t rpg, int64_t gstride, int64_t goff, void *workspace, int64_t workspace_bytes,
+                     void *stream);
+
 /* Out-of-place residual GEMM (training forward): x_out[row(m)] = x_in[row(m)] + A[m] . W^T +
  * bias, fp32 x_in / x_out with the same row map and row stride ldx, rows of x_out outside the
  * map untouched.  The reference's `x = x + drop_path(sublayer(norm(x)))`

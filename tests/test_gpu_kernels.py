@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20, 40])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -69,7 +69,7 @@ def test_gemm_bias_gelu(dtype, M, N, K, gemm_variant):
             check(back(out), f(ref), dtype, "gemm epi=%d f32out=%d" % (epi, out_f32))
 
 
-@pytest.mark.parametrize("variant", [10, 20])
+@pytest.mark.parametrize("variant", [10, 20, 40])
 @pytest.mark.parametrize("M,N,K", [(8200, 2304, 768), (8200, 2304, 64), (6000, 3072, 128), (25104, 768, 3072)])
 def test_gemm_persistent_stream(M, N, K, variant):
     """Persistent kernels with several output tiles per workgroup (the K-tile stream crosses
@@ -118,7 +118,48 @@ def test_gelu_epilogue_accuracy():
     assert err.max() < 3e-7, err.max()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 10, 20])
+@pytest.mark.parametrize("M,N,K", [(768, 768, 3072), (25104, 2304, 768), (13872, 768, 3072), (1000, 512, 4096),
+                                   (4136, 3072, 768), (25104, 768, 768)])
+def test_gemm_stream_k(M, N, K, monkeypatch):
+    """Stream-K 256x256 kernel (variant 40): full rounds of tiles data-parallel, the last
+    partial round's tiles x K-steps split evenly over 256 workgroups, so a tail tile's partial
+    sums may come from 2 (the bench shapes) up to ~30 workgroups (768^2 x 3072: 9 tiles = 432
+    K-tiles over 256 workgroups).  Bias, GELU (bf16 out) and the fp32 residual
+    epilogue against torch fp32 of the bf16 operands; three launches bitwise equal (the last
+    arriver adds the slots in a fixed order); the workspace counters left zero."""
+    from dsvt import _lib, ops
+    monkeypatch.setenv("DSVT_SK", "1")           # ops.gemm passes the per-stream workspace
+    g = torch.Generator(device=dev()).manual_seed(M + N + K)
+    A = (torch.randn(M, K, device=dev(), generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev(), generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=dev(), generator=g)
+    ref = torch.addmm(b, A.float(), W.float().t())
+    _lib.call("dsvt_set_gemm_variant", 40)
+    try:
+        for epi in (_lib.EPI_BIAS, _lib.EPI_BIAS_GELU, _lib.EPI_BIAS_RESID):
+            want = torch.nn.functional.gelu(ref) if epi == _lib.EPI_BIAS_GELU else ref
+            x0 = torch.randn(M, N, device=dev(), generator=g) if epi == _lib.EPI_BIAS_RESID else None
+            outs = []
+            for _ in range(3):
+                if x0 is not None:
+                    out = x0.clone()
+                else:
+                    out = torch.full((M, N), float("nan"), device=dev(), dtype=torch.bfloat16)
+                ops.gemm(A, W, b, out, epilogue=epi)
+                outs.append(out)
+            torch.cuda.synchronize()
+            want_e = want + x0 if x0 is not None else want
+            err = ((outs[0].float() - want_e).abs().max() / want_e.abs().max()).item()
+            assert err < (2e-2 if outs[0].dtype == torch.bfloat16 else 2e-3), (epi, err)
+            for o in outs[1:]:
+                assert torch.equal(o, outs[0]), "stream-K launches differ (epi %d)" % epi
+        ws = ops._SK_WS[(dev().index, torch.cuda.current_stream().cuda_stream)]
+        assert int(ws[:65536].abs().sum().item()) == 0, "arrival counters not reset"
+    finally:
+        _lib.call("dsvt_set_gemm_variant", 0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 10, 20, 40])
 def test_gelu_epilogue_bf16(variant):
     """The bf16-output GELU epilogue (gelu_bf16out: x * sigmoid(x * P(x^2)), every kernel that
     takes EPI_BIAS_GELU) against the exact erf GELU of the bf16-rounded input, x in [-12, 12]
