@@ -438,7 +438,11 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
     return hipGetLastError();
   }
   const bool nfull = p.N % 256 == 0 && !out_f32 && !getenv("DSVT_8PH_NO_NFULL");
-  if (nfull && getenv("DSVT_8PH_SC1") && (epi == EPI_BIAS || epi == EPI_GELU)) {   // sc1 output stores
+  static const bool sc1 = [] {
+    const char* e = getenv("DSVT_8PH_SC1");
+    return e && atoi(e) == 1;
+  }();
+  if (nfull && sc1 && (epi == EPI_BIAS || epi == EPI_GELU)) {   // sc1 output stores
     if (epi == EPI_BIAS) gemm_8ph_kernel<EPI_BIAS, false, 128, true><<<grid, block, 0, s>>>(q);
     else gemm_8ph_kernel<EPI_GELU, false, 128, true><<<grid, block, 0, s>>>(q);
     return hipGetLastError();

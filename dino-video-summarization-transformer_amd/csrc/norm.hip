@@ -484,8 +484,35 @@ __global__ void cls_mean_kernel(const float* __restrict__ aux, T* __restrict__ o
   }
 }
 
+// T = 8 (the hot path): one thread per (clip, 4 channels), the 8 frame rows' float4 loads issued
+// together and summed in the order of the generic kernel (t = 0..7) -- bit-identical to it; the
+// generic kernel's 16 workgroups of a 16-clip call each walked 768 channels x 8 dependent loads.
+template <typename T>
+__global__ __launch_bounds__(64) void cls_mean8_kernel(const float* __restrict__ aux, T* __restrict__ out, int64_t B,
+                                                       int64_t L, int C) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;      // (clip, channel quad)
+  const int cq = C >> 2;
+  if (i >= B * cq) return;
+  const int64_t b = i / cq;
+  const int c = (int)(i - b * cq) * 4;
+  float4 v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] = *reinterpret_cast<const float4*>(aux + (b * 8 + t) * C + c);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) { s.x += v[t].x; s.y += v[t].y; s.z += v[t].z; s.w += v[t].w; }
+  const float inv = 1.0f / 8;
+  store4(out + b * L * C + c, s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+}
+
 hipError_t launch_cls_mean(int dtype, const float* aux, void* out, int64_t B, int64_t T, int64_t L, int64_t C,
                            hipStream_t s) {
+  if (T == 8 && C % 4 == 0) {
+    const unsigned grid = (unsigned)((B * (C / 4) + 63) / 64);
+    if (dtype == 0) cls_mean8_kernel<bf16_t><<<grid, 64, 0, s>>>(aux, (bf16_t*)out, B, L, (int)C);
+    else cls_mean8_kernel<float><<<grid, 64, 0, s>>>(aux, (float*)out, B, L, (int)C);
+    return hipGetLastError();
+  }
   if (dtype == 0) cls_mean_kernel<bf16_t><<<(unsigned)B, 256, 0, s>>>(aux, (bf16_t*)out, (int)T, L, (int)C);
   else cls_mean_kernel<float><<<(unsigned)B, 256, 0, s>>>(aux, (float*)out, (int)T, L, (int)C);
   return hipGetLastError();
