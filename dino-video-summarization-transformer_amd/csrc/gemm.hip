@@ -481,6 +481,12 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
       (g_gemm_variant == 40 || (g_gemm_variant == 0 && sk_auto(epi))))
     return 40;
   const int gv = g_gemm_variant == 40 ? 0 : g_gemm_variant;   // forced stream-K, ineligible shape: auto
+  // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
+  // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
+  // 195 vs 254 us (persistent 256x128) and 215 vs 231 us at 25104 x 3072 x 768 (tools/aux_bench.py)
+  if ((epi == EPI_GELU_SAVE || epi == EPI_DGELU) && (gv == 0 || gv == 20) && p.M >= 4096 && p.N % 256 == 0 &&
+      gemm_8ph_ok(p, epi))
+    return 20;
   if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (gv >= 20 && gv <= 29) return gemm_8ph_ok(p, epi) ? gv : 1;
