@@ -503,7 +503,11 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
     return 20;
   // fp32 residual GEMMs (N = 768: proj / temporal fc / fc2): the 128x128 kernel, whose epilogue
   // issues every X load before its first store (527 vs 505 TF/s proj, 871 vs 752 fc2)
-  if (epi == EPI_RESID) return 1;
+  if (epi == EPI_RESID) {
+    static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 0;   // A/B knob
+    if (r8 && p.M >= 4096 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return 20;
+    return 1;
+  }
   // N = 768 bias-only (the split residual path's proj / temporal fc, the backward's dX of proj):
   // the 128x128 kernel -- 43.4 vs 53.8 us (persistent 256x128) at 25104 x 768 x 768
   if (epi == EPI_BIAS && p.N < 1024) return 1;
