@@ -501,16 +501,25 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // fc1 + GELU likewise (728 vs 709 TF/s global crops; its epilogue uses the general store path)
   if ((epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.M >= 4096 && p.N >= 1024 && gemm_8ph_ok(p, epi))
     return 20;
-  // fp32 residual GEMMs (N = 768: proj / temporal fc / fc2): the 128x128 kernel, whose epilogue
-  // issues every X load before its first store (527 vs 505 TF/s proj, 871 vs 752 fc2)
+  // fp32 residual GEMMs (N = 768: proj / temporal fc / fc2): the 256x256 kernel.  ALONE it is
+  // the slower one (proj 73.6 vs 57.6 us, fc2 165 vs 138 us against the 128x128 kernel: 297
+  // tiles on 256 CUs leave a 1.16-round tail), but the forward runs three backbone calls on
+  // concurrent streams whose kernels fill that tail, and there its higher per-tile rate wins:
+  // 379.7 / 380.0 vs 360.6 / 359.7 clips/s on the bench line (same box, two interleaved rounds;
+  // DSVT_RESID_8PH = 0 -> 128x128, 1 -> only K >= 2048, 2 -> all, the default).
   if (epi == EPI_RESID) {
-    static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 0;   // A/B knob
+    static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 2;
     if (r8 && p.M >= 4096 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return 20;
     return 1;
   }
-  // N = 768 bias-only (the split residual path's proj / temporal fc, the backward's dX of proj):
-  // the 128x128 kernel -- 43.4 vs 53.8 us (persistent 256x128) at 25104 x 768 x 768
-  if (epi == EPI_BIAS && p.N < 1024) return 1;
+  // N = 768 bias-only (the split residual path's proj / temporal fc, the backward's dX GEMMs):
+  // the 128x128 kernel -- 43.4 vs 53.8 us (persistent 256x128) at 25104 x 768 x 768 alone;
+  // DSVT_N768_8PH = 1 (A/B knob) puts them on the 256x256 kernel like the residual GEMMs.
+  if (epi == EPI_BIAS && p.N < 1024) {
+    static const int n8 = getenv("DSVT_N768_8PH") ? atoi(getenv("DSVT_N768_8PH")) : 1;
+    if (n8 && p.M >= 4096 && gemm_8ph_ok(p, epi)) return 20;
+    return 1;
+  }
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }
 
