@@ -507,9 +507,13 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // concurrent streams whose kernels fill that tail, and there its higher per-tile rate wins:
   // 379.7 / 380.0 vs 360.6 / 359.7 clips/s on the bench line (same box, two interleaved rounds;
   // DSVT_RESID_8PH = 0 -> 128x128, 1 -> only K >= 2048, 2 -> all, the default).
+  // Below ~half a round of 256x256 tiles (config 4's single 2-clip call: 75 tiles) the 128x128
+  // kernel's 4x more tiles win even with other streams beside it (DSVT_8PH_MIN_TILES).
+  static const int64_t min_t = getenv("DSVT_8PH_MIN_TILES") ? atoll(getenv("DSVT_8PH_MIN_TILES")) : 128;
+  const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= min_t;
   if (epi == EPI_RESID) {
     static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 2;
-    if (r8 && p.M >= 4096 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return 20;
+    if (r8 && big8 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return 20;
     return 1;
   }
   // N = 768 bias-only (the split residual path's proj / temporal fc, the backward's dX GEMMs):
@@ -517,7 +521,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // DSVT_N768_8PH = 1 (A/B knob) puts them on the 256x256 kernel like the residual GEMMs.
   if (epi == EPI_BIAS && p.N < 1024) {
     static const int n8 = getenv("DSVT_N768_8PH") ? atoi(getenv("DSVT_N768_8PH")) : 1;
-    if (n8 && p.M >= 4096 && gemm_8ph_ok(p, epi)) return 20;
+    if (n8 && big8 && gemm_8ph_ok(p, epi)) return 20;
     return 1;
   }
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;

@@ -497,7 +497,7 @@ def gemm_kernel_name(tag):
     if variant in persist:
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
     if variant == 20:
-        return "void dsvt::gemm_8ph_kernel<%d, %s, 0>" % (epi, f32)
+        return "void dsvt::gemm_8ph_kernel<%d, %s, 0, " % (epi, f32)
     if variant == 30:
         return "void dsvt::gemm_rowln_kernel<"
     if variant == 31:
