@@ -487,6 +487,17 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if ((epi == EPI_GELU_SAVE || epi == EPI_DGELU) && (gv == 0 || gv == 20) && p.M >= 4096 && p.N % 256 == 0 &&
       gemm_8ph_ok(p, epi))
     return 20;
+  // 256x256 kernel for the big N = 768 GEMMs: see the residual / N = 768 rules below
+  static const int64_t min_t = getenv("DSVT_8PH_MIN_TILES") ? atoll(getenv("DSVT_8PH_MIN_TILES")) : 128;
+  const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= min_t;
+  static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 2;
+  // training DropPath residual GEMMs (s[m] * bias in the epilogue) likewise
+  // (the row-scaled ones are opt-in, DSVT_RESID_RS_8PH=1: 117.1 / 117.2 vs 117.4 / 117.6 train
+  // clips/s on the same box -- no gain, the 128x128 kernel stays their default)
+  static const int rs8 = getenv("DSVT_RESID_RS_8PH") ? atoi(getenv("DSVT_RESID_RS_8PH")) : 0;
+  if (epi == EPI_RESID && p.row_scale && gemm_8ph_ok(p, epi) &&
+      (gv == 20 || (gv == 0 && rs8 && r8 && big8 && (r8 >= 2 || p.K >= 2048))))
+    return 20;
   if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (gv >= 20 && gv <= 29) return gemm_8ph_ok(p, epi) ? gv : 1;
@@ -509,10 +520,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // DSVT_RESID_8PH = 0 -> 128x128, 1 -> only K >= 2048, 2 -> all, the default).
   // Below ~half a round of 256x256 tiles (config 4's single 2-clip call: 75 tiles) the 128x128
   // kernel's 4x more tiles win even with other streams beside it (DSVT_8PH_MIN_TILES).
-  static const int64_t min_t = getenv("DSVT_8PH_MIN_TILES") ? atoll(getenv("DSVT_8PH_MIN_TILES")) : 128;
-  const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= min_t;
   if (epi == EPI_RESID) {
-    static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 2;
     if (r8 && big8 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return 20;
     return 1;
   }

@@ -260,7 +260,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   fv4 acc[8][4];
   auto init_acc = [&](int tl, bool with_bias) {   // SK: only a tile's k = 0 segment carries the bias
     float4 b4[4];
-    if (BIAS_IN_ACC && p.bias && with_bias) {
+    // (EPI_RESID with DropPath row scales: the epilogue adds s[m] * bias instead)
+    if (BIAS_IN_ACC && p.bias && with_bias && !(EPI == EPI_RESID && p.row_scale)) {
       int64_t m0, n0;
       tile_mn(tl, m0, n0);
       const int64_t cbase = n0 + wc * 64;

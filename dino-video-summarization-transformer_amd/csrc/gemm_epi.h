@@ -57,7 +57,10 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
   // bias: scalar loads for a full 64-column wave slab (no vmcnt wait behind the in-flight
   // prefetch of the next tile); per-lane vector loads only at a ragged N edge
   float4 bias4[NJ];
-  if (BIAS_IN_ACC) {
+  // EPI_RESID with DropPath row scales (training): the bias is NOT in the accumulators (the
+  // kernel leaves it out), it is added here as s[m] * bias like the 128x128 kernel does
+  const bool rres = EPI == EPI_RESID && p.row_scale != nullptr;   // workgroup-uniform
+  if (BIAS_IN_ACC && !rres) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) bias4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   } else if (NJ == 4 && cbase + 64 <= p.N) {
@@ -198,11 +201,17 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
 #pragma unroll
           for (int j = 0; j < NJ; ++j) x[ii][j] = *reinterpret_cast<const float4*>(resid_src(p) + off + j * 16);
         }
+        float rs2[2] = {1.0f, 1.0f};
+        if (rres) {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) rs2[ii] = row_scale_of(p, rbase + (i + ii) * 16 + r16);
+        }
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            const float4 bb = bias4[j];
+            float4 bb = bias4[j];
+            bb.x *= rs2[ii]; bb.y *= rs2[ii]; bb.z *= rs2[ii]; bb.w *= rs2[ii];
             const fv4 a = acc[i + ii][j];
             *reinterpret_cast<float4*>(xr[ii] + j * 16) =
                 make_float4(x[ii][j].x + a[0] + bb.x, x[ii][j].y + a[1] + bb.y, x[ii][j].z + a[2] + bb.z,
@@ -215,9 +224,11 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int64_t m = rbase + i * 16 + r16;
+    const float rsr = rres ? row_scale_of(p, m) : 1.0f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const float4 bb = bias4[j];
+      float4 bb = bias4[j];
+      if constexpr (EPI == EPI_RESID) { bb.x *= rsr; bb.y *= rsr; bb.z *= rsr; bb.w *= rsr; }
       acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
       if constexpr (EPI == EPI_GELU) {
 #pragma unroll

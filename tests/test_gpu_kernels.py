@@ -281,11 +281,13 @@ def test_gemm_resid_out_of_place(dtype, B, Np, T, gemm_variant):
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("M,K", [(300, 192), (4624, 768), (3000, 3072)])
+@pytest.mark.parametrize("M,K", [(300, 192), (4624, 768), (3000, 3072), (13872, 768), (11000, 3072)])
 def test_gemm_resid_scaled_bias(dtype, M, K):
     """dsvt_gemm_resid_scaled_fwd (training DropPath): x_out = x_in + A.W^T + s[m] * bias with
-    A already scaled, against float64; s includes dropped rows (0) and 1/keep rows; x_in intact."""
-    from dsvt import ops
+    A already scaled, against float64; s includes dropped rows (0) and 1/keep rows; x_in intact.
+    The last two shapes (>= 128 tiles of 256x256, the last one ragged) also run the 256x256
+    kernel's row-scaled residual epilogue in bf16 (variant 20, opt-in in the product)."""
+    from dsvt import _lib, ops
     N = 768 if K != 192 else 192
     a, w, b = rnd((M, K), 31), rnd((N, K), 32, 0.03), rnd((N,), 33)
     x0 = rnd((M, N), 34)
@@ -294,12 +296,18 @@ def test_gemm_resid_scaled_bias(dtype, M, K):
     A, W, bias, S = to(a, dtype), to(w, dtype), to(b, torch.float32), to(s, torch.float32)
     X_in = to(x0, torch.float32)
     X_out = torch.full_like(X_in, 7.0)
-    ops.gemm_resid(A, W, bias, X_in, X_out, bias_row_scale=S)
-    torch.cuda.synchronize()
     ref = x0.astype(np.float64) + back(A).astype(np.float64) @ back(W).astype(np.float64).T + s[:, None] * b
-    np.testing.assert_array_equal(back(X_in), x0)
-    err = np.abs(back(X_out) - ref).max() / np.abs(ref).max()
-    assert err < 1e-5, err
+    for v in ([0, 20] if M > 10000 and dtype == torch.bfloat16 else [0]):
+        X_out.fill_(7.0)
+        _lib.call("dsvt_set_gemm_variant", v)
+        try:
+            ops.gemm_resid(A, W, bias, X_in, X_out, bias_row_scale=S)
+        finally:
+            _lib.call("dsvt_set_gemm_variant", 0)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(back(X_in), x0)
+        err = np.abs(back(X_out) - ref).max() / np.abs(ref).max()
+        assert err < 1e-5, (v, err)
     with pytest.raises(Exception):
         ops.gemm_resid(A, W, bias, X_in, X_out, rowmap=(M, M, 0), bias_row_scale=S)
 
