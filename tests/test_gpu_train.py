@@ -149,6 +149,52 @@ def test_attn_spatial_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled, attn_bwd_
     assert rel(outs[0].float().cpu(), q32.grad.cpu()) < tol
 
 
+def test_attn_bwd_bench_shape_repeatable():
+    """The two attention backward kernels of the train step at the bench's global group (16 clips x
+    8 x 224^2, 12 heads, bf16): spatial attn_bwd_short_bf16 (128 frame sequences of 197 tokens,
+    DropPath sequence scales) and temporal attn_temporal_bwd_reg<8> (3136 patch sequences of 8):
+    three launches each bitwise identical and finite (the MFMA-hazard class of DESIGN §3 at the
+    occupancy the step runs them at), and against torch fp32 autograd."""
+    from dsvt import ops
+    B, T, Np, H = 16, 8, 196, 12
+    C, L = H * 64, 1 + Np * T
+    g = torch.Generator(device="cuda").manual_seed(11)
+    qkv = torch.randn(B * L, 3 * C, device="cuda", generator=g).to(torch.bfloat16)
+    dout = torch.randn(B * L, C, device="cuda", generator=g).to(torch.bfloat16)
+    ss = torch.rand(B * T, device="cuda", generator=g) + 0.5
+    outs = []
+    for _ in range(3):
+        dq = torch.full_like(qkv, 7.0)
+        ops.attn_spatial_bwd(qkv, dout, dq, B, T, L, H, 0.125, seq_scale=ss)
+        outs.append(dq)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "spatial backward launches differ at the bench shape"
+    q32 = qkv.float().requires_grad_(True)
+    _ref_spatial(q32, B, T, Np, H, 0.125, ss).backward(dout.float())
+    assert rel(outs[0].float().cpu(), q32.grad.cpu()) < 3e-2
+    del q32, outs
+    nseq = B * Np
+    qt = qkv[: nseq * T].contiguous()
+    dt = dout[: nseq * T].contiguous()
+    outs = []
+    for _ in range(3):
+        dq = torch.full_like(qt, 7.0)
+        ops.attn_temporal_bwd(qt, dt, dq, nseq, T, H, 0.125)
+        outs.append(dq)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "temporal backward launches differ at the bench shape"
+    q32 = qt.float().requires_grad_(True)
+    x = q32.view(nseq, T, 3, H, 64)
+    o = F.scaled_dot_product_attention(x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2),
+                                       x[:, :, 2].transpose(1, 2), scale=0.125)
+    o.transpose(1, 2).reshape(nseq * T, C).backward(dt.float())
+    assert rel(outs[0].float().cpu(), q32.grad.cpu()) < 3e-2
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
 @pytest.mark.parametrize("T,H", [(1, 1), (2, 3), (3, 2), (4, 2), (5, 4), (7, 3), (8, 12), (30, 1)])
 def test_attn_temporal_bwd_vs_autograd(dtype, tol, T, H, attn_bwd_variant):
