@@ -75,13 +75,28 @@ __device__ __forceinline__ void p8_barrier() {
 // that arrives last adds all slots in segment order (run-to-run deterministic) and runs the
 // epilogue -- nobody waits on another workgroup, so concurrent launches on other streams cannot
 // deadlock it.  No quantization tail: qkv at 25 104 rows is 891 tiles = 3.48 rounds of 256.
-template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false, bool SK = false>
+// XS (X stream, EPI_RESID only; N % 256 == 0, K >= 640, no row scales): the fp32 residual tile
+// is NOT read in the epilogue.  It is streamed into the accumulators during the tile's K loop:
+// in K-tiles [KS, KS + 8) (KS = nk - 9) every phase issues ONE LDS-DMA of a 16 x 16 fp32 X
+// fragment (1 KiB per wave: lane = (row r16, 4 columns 4g), exactly the accumulator layout)
+// into a per-wave 4-slot ring (32 KiB beside the 128 KiB K ring = the CU's 160 KiB), and the
+// same phase of the next K-tile reads it back (ds_read_b128, conflict-free) and adds it into
+// the accumulator -- of the quadrant two phases away, so the add never waits on an in-flight
+// MFMA.  The stage waits count those DMAs (vm_wait<8 + c>, c = X DMAs of the three previous
+// phases).  The epilogue is then 32 plain 16-B stores per lane, left in flight under the next
+// tile's first K-tile (vm_wait<8 + 32>): no load -> wait -> store round trips, and the X reads
+// overlap the MFMA loop instead of following it.
+template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false, bool SK = false, bool XS = false>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
+  static_assert(!XS || (EPI == EPI_RESID && !SK && ABL == 0), "X stream: residual epilogue only");
   constexpr bool CLAMPED = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32;
-  // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores
-  constexpr int S_EPI = ((EPI == EPI_BIAS || CLAMPED) && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[2 * P8_BUF];
-  __shared__ int sk_flag;
+  // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores,
+  // X-streamed residual -> 32 fp32 fragment stores
+  constexpr int S_EPI = XS ? 32 : ((EPI == EPI_BIAS || CLAMPED) && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
+  constexpr int XS_BYTES = XS ? 8 * 4096 : 0;           // 8 waves x 4 slots x 1 KiB
+  constexpr int SMEM_BYTES = 2 * P8_BUF + XS_BYTES + (SK ? 16 : 0);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  int& sk_flag = *reinterpret_cast<int*>(smem + 2 * P8_BUF + XS_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -214,16 +229,29 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 // wait for the half-tile the NEXT phase reads; VALID = this phase issued a stage.  After a
 // full-tile epilogue its S_EPI stores sit between the awaited half-tile and the four younger
 // stages (issue order), for the four phases of the next K-tile.
-#define P8_WAIT(VALID)                                     \
+// XS: xc = X DMAs issued in the three phases before this one (the DMA of a phase is issued after
+// its wait), so the half-tile four phases back -- and the X fragment of that phase -- are done.
+#define P8_WAIT(VALID, PH)                                 \
   {                                                        \
     if (!(VALID)) vm_wait<0>();                            \
     else if (S_EPI > 0 && post) vm_wait<8 + S_EPI>();      \
-    else vm_wait<8>();                                     \
+    else if constexpr (XS) {                               \
+      const int xc_ = xs_prev(PH);                         \
+      if (xc_ == 3) vm_wait<11>();                         \
+      else if (xc_ == 2) vm_wait<10>();                    \
+      else if (xc_ == 1) vm_wait<9>();                     \
+      else vm_wait<8>();                                   \
+    } else vm_wait<8>();                                   \
   }
-#define P8_COMPUTE(MFMA_STMT)                              \
+#define P8_COMPUTE(MFMA_STMT, PH)                          \
   {                                                        \
     p8_barrier();                                          \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
+    __builtin_amdgcn_sched_barrier(0);                     \
+    if constexpr (XS) {                                    \
+      xs_add_rt(std::integral_constant<int, PH>{});        \
+      xs_issue_rt(std::integral_constant<int, PH>{});      \
+    }                                                      \
     __builtin_amdgcn_sched_barrier(0);                     \
     MFMA_STMT;                                             \
     p8_barrier();                                          \
@@ -288,6 +316,59 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   int tlc = 0, kc = k0;                 // compute position
   bool post = false;                    // previous K-tile ended with a full-tile epilogue
 
+  // ---- X stream (XS): see the template comment.  Phase PH adds into the quadrant that phase
+  // (PH + 2) % 4 computes: PH 0 -> (4, 2), 1 -> (4, 0), 2 -> (0, 0), 3 -> (0, 2); K-tile kx of
+  // the window supplies its fragment (kx >> 1, kx & 1).
+  const int KS = nk - 9;
+  int64_t xrow0 = 0, xcol0 = 0;         // this wave's 128 x 64 block of the compute tile
+  fv4 xv = {0.f, 0.f, 0.f, 0.f};
+  char* const xslots = smem + 2 * P8_BUF + wave * 4096;
+  auto xs_tile = [&](int tl) {
+    int64_t m0, n0;
+    tile_mn(tl, m0, n0);
+    xrow0 = m0 + wr * 128;
+    xcol0 = n0 + wc * 64;
+  };
+  auto xs_prev = [&](int ph) -> int {   // X DMAs in the three phases before phase ph of K-tile kc
+    const int kx = kc - KS;
+    return (kx >= 1 && kx <= 7) ? 3 : kx == 0 ? ph : kx == 8 ? 3 - ph : 0;
+  };
+#define XS_READ(PH)                                                                   \
+  if constexpr (XS) {                                                                 \
+    const int kx_ = kc - KS;                                                          \
+    asm volatile("" ::: "memory");                                                    \
+    if (kx_ >= 1 && kx_ <= 8) xv = *reinterpret_cast<const fv4*>(xslots + (PH) * 1024 + lane * 16); \
+  }
+  // (XI, XJ) of phase PH; the add targets acc[XI + (kk >> 1)][XJ + (kk & 1)]
+// (the distinct asm tail keeps SimplifyCFG from sinking the eight adds into one dynamically
+// indexed add, which would put acc in scratch)
+#define XS_CASE(PH, KK)                                                                            \
+  case KK:                                                                                         \
+    acc[((PH) < 2 ? 4 : 0) + ((KK) >> 1)][(((PH) == 0 || (PH) == 3) ? 2 : 0) + ((KK) & 1)] += xv;  \
+    asm volatile("; xs add " #PH " " #KK);                                                         \
+    break;
+  auto xs_add_rt = [&](auto ph_c) {
+    constexpr int PH = decltype(ph_c)::value;
+    const int kx = kc - KS;
+    if (kx >= 1 && kx <= 8) {
+      switch (kx - 1) { XS_CASE(PH, 0) XS_CASE(PH, 1) XS_CASE(PH, 2) XS_CASE(PH, 3)
+                        XS_CASE(PH, 4) XS_CASE(PH, 5) XS_CASE(PH, 6) XS_CASE(PH, 7) }
+    }
+  };
+  auto xs_issue_rt = [&](auto ph_c) {
+    constexpr int PH = decltype(ph_c)::value;
+    const int kx = kc - KS;
+    if (kx >= 0 && kx <= 7) {
+      const int fi = (PH < 2 ? 4 : 0) + (kx >> 1), fj = ((PH == 0 || PH == 3) ? 2 : 0) + (kx & 1);
+      int64_t m = xrow0 + fi * 16 + r16;
+      m = m < p.M ? m : p.M - 1;        // rows past M: row M - 1's X (never stored)
+      const int64_t orow = p.rpg >= p.M ? m : map_row(m, p.rpg, p.gstride, p.goff);
+      const float* src = resid_src(p) + orow * p.ldo + xcol0 + fj * 16 + 4 * g;
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(xslots + PH * 1024), 16, 0, 0);
+    }
+  };
+  if constexpr (XS) xs_tile(0);
+
   // SK: a partial segment of tail tile t (this workgroup's slot: 0 for its first tail tile, 1
   // for its last).  Returns true in the workgroup that arrives last, with the tile's full sums
   // in acc.  owner(it) = the workgroup whose tail range holds iteration it.
@@ -350,22 +431,26 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     __builtin_amdgcn_sched_barrier(0);
     P8_RD(fa, H_AT, rdA, cb, 4);
     if (v1) P8_STAGE(H_BR, oBR, W, sb1, kb1);
-    P8_WAIT(v1);
-    P8_COMPUTE(P8_MFMA(0, 0, fbl));
+    P8_WAIT(v1, 0);
+    XS_READ(0);
+    P8_COMPUTE(P8_MFMA(0, 0, fbl), 0);
     // phase 1: read BR, stage AB(j+1), quadrant (AT, BR)
     P8_RD(fbr, H_BR, rdB, cb, 2);
     if (v1) P8_STAGE(H_AB, oAB, A, sb1, kb1);
-    P8_WAIT(v1);
-    P8_COMPUTE(P8_MFMA(0, 2, fbr));
+    P8_WAIT(v1, 1);
+    XS_READ(1);
+    P8_COMPUTE(P8_MFMA(0, 2, fbr), 1);
     // phase 2: read AB, stage AT(j+2), quadrant (AB, BR)
     P8_RD(fa, H_AB, rdA, cb, 4);
     if (v2) P8_STAGE(H_AT, oAT, A, sb2, kb2);
-    P8_WAIT(v2);
-    P8_COMPUTE(P8_MFMA(4, 2, fbr));
+    P8_WAIT(v2, 2);
+    XS_READ(2);
+    P8_COMPUTE(P8_MFMA(4, 2, fbr), 2);
     // phase 3: no reads, stage BL(j+2), quadrant (AB, BL)
     if (v2) P8_STAGE(H_BL, oBL, W, sb2, kb2);
-    P8_WAIT(v2);
-    P8_COMPUTE(P8_MFMA(4, 0, fbl));
+    P8_WAIT(v2, 3);
+    XS_READ(3);
+    P8_COMPUTE(P8_MFMA(4, 0, fbl), 3);
 
     post = false;
     if (++kc == seg_k1(tlc)) {            // tile (or SK tail segment) done: register epilogue
@@ -378,6 +463,27 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
         if (tlc < n_tail && (seg_k0(tlc) != 0 || kc != nk)) whole = sk_combine(tail_t0 + tlc, tlc == 0 ? 0 : 1);
       }
       if (!whole) {
+      } else if constexpr (XS) {          // X already in the accumulators: stores only
+        const bool ident = p.rpg >= p.M;
+        float* const out = (float*)p.out;
+        if (rbase + 128 <= p.M) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int64_t m = rbase + i * 16 + r16;
+            float* o = out + (ident ? m : map_row(m, p.rpg, p.gstride, p.goff)) * p.ldo + cbase + 4 * g;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) *reinterpret_cast<fv4*>(o + jj * 16) = acc[i][jj];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int64_t m = rbase + i * 16 + r16;
+            if (m >= p.M) continue;
+            float* o = out + map_row(m, p.rpg, p.gstride, p.goff) * p.ldo + cbase + 4 * g;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) *reinterpret_cast<fv4*>(o + jj * 16) = acc[i][jj];
+          }
+        }
       } else if constexpr ((ABL & 16) != 0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -391,13 +497,18 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
       kc = 0;
       ++tlc;
       __builtin_amdgcn_sched_barrier(0);   // keep the next tile's bias loads after the stores
-      if (tlc < tl_end) init_acc(tlc, true);
+      if (tlc < tl_end) {
+        init_acc(tlc, true);
+        if constexpr (XS) xs_tile(tlc);
+      }
     }
     // advance the stagers
     { const int o = tl1; adv(tl1, k1); if (tl1 != o && tl1 < tl_end) set_brab(tl1); }
     { const int o = tl2; adv(tl2, k2); if (tl2 != o && tl2 < tl_end) set_atbl(tl2); }
   }
   if (!(ABL & 1) && wr == 0) p8_barrier();  // balance the stagger barrier
+#undef XS_READ
+#undef XS_CASE
 #undef P8_STAGE
 #undef P8_RD
 #undef P8_MFMA
@@ -465,6 +576,24 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
     default: return hipErrorInvalidValue;
   }
 #undef DSVT_K
+  return hipGetLastError();
+}
+
+// ---- X-streamed residual GEMM (variant 30): EPI_RESID, whole 256-column tiles, K-window of 8
+// K-tiles after at least one more (nk >= 10), no DropPath row scales
+bool gemm_8ph_xs_ok(const GemmParams& p, int epi) {
+  return epi == EPI_RESID && gemm_8ph_ok(p, epi) && p.N % 256 == 0 && p.K / 64 >= 10 && !p.row_scale;
+}
+
+hipError_t launch_gemm_8ph_xs(const GemmParams& p, int epi, hipStream_t s) {
+  if (!gemm_8ph_xs_ok(p, epi)) return hipErrorInvalidValue;
+  const int64_t tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  int64_t G = 256;
+  const int64_t per_x = (tiles + 7) / 8;
+  if (per_x * 8 < G) G = per_x * 8;
+  GemmParams q = p;
+  if (const char* e = getenv("DSVT_TILE_GROUP")) q.tile_group = atoi(e);
+  gemm_8ph_kernel<EPI_RESID, true, 0, false, false, true><<<dim3((unsigned)G), dim3(512), 0, s>>>(q);
   return hipGetLastError();
 }
 

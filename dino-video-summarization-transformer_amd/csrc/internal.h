@@ -55,6 +55,9 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // 
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
 bool gemm_8ph_ok(const GemmParams& p, int epi);
+// the 256x256 kernel with the residual tile streamed into the accumulators (variant 30)
+bool gemm_8ph_xs_ok(const GemmParams& p, int epi);
+hipError_t launch_gemm_8ph_xs(const GemmParams& p, int epi, hipStream_t s);
 // stream-K 256x256 GEMM (variant 40): workspace = [SK_MAX_TILES int32 counters][2 x 256 slots of
 // 256 x 256 fp32 partial sums]
 constexpr int64_t SK_MAX_TILES = 65536;

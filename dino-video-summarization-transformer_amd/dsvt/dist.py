@@ -97,7 +97,7 @@ class BlockGradReducer:
         self.bb, self.group, self.ddp = backbone, group, ddp
         self.world = dist.get_world_size(group)
         self.avg = dist.get_backend(group) == "nccl"
-        self._works, self._arena = [], None
+        self._works, self._arena, self._seeded = [], None, []
         backbone.dsvt_grad_reducer = self
 
     def params(self):
@@ -112,20 +112,39 @@ class BlockGradReducer:
         return self.ddp is None or getattr(self.ddp, "require_backward_grad_sync", True)
 
     def arena(self, device):
-        """A fresh flat fp32 arena for this backward (the returned views become p.grad) and the
-        id(p) -> view map the gradient buffers come from.  Offsets are 256-byte aligned."""
+        """A fresh flat fp32 arena for this backward (the returned views become p.grad), the
+        id(p) -> view map the gradient buffers come from, and the ids of the views SEEDED with
+        an existing p.grad.  Offsets are 256-byte aligned.
+
+        Gradient accumulation (DDP.no_sync() micro-steps, then one synchronised step): the
+        no_sync backwards leave LOCAL sums in p.grad.  DDP all-reduces the whole accumulated
+        gradient on the sync step, so the arena starts from those sums (the backward then
+        accumulates onto them) and the caller must REPLACE p.grad with the reduced view instead
+        of letting autograd add it (`take_seeded`)."""
         buckets = self.params()
         sizes = [[(p.numel() + 63) // 64 * 64 for p in b] for b in buckets]
         flat = torch.empty(sum(sum(s) for s in sizes), device=device, dtype=torch.float32)
         views, self._slices, off = {}, [], 0
+        self._seeded = []
         for b, s in zip(buckets, sizes):
             start = off
             for p, n in zip(b, s):
-                views[id(p)] = flat[off:off + p.numel()].view(p.shape)
+                v = flat[off:off + p.numel()].view(p.shape)
+                views[id(p)] = v
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                    self._seeded.append(p)
                 off += n
             self._slices.append(flat[start:off])
         self._arena, self._works = flat, []
-        return views
+        return views, {id(p) for p in self._seeded}
+
+    def take_seeded(self):
+        """Drop the accumulated p.grad of every seeded parameter (its sum is in the reduced
+        arena view the backward returns, which autograd then installs as p.grad)."""
+        for p in self._seeded:
+            p.grad = None
+        self._seeded = []
 
     def launch(self, k, side=None):
         """Start bucket k's all-reduce once everything queued so far (on the current stream and on

@@ -61,10 +61,11 @@ class _Grads:
     buffer and whether it already holds a partial sum (False on the first write: the kernels
     then overwrite instead of accumulating, so no zero fill is needed)."""
 
-    def __init__(self, side=None, arena=None):
+    def __init__(self, side=None, arena=None, seeded=()):
         self.g = {}
         self.side = side               # weight gradients on this stream (None: the current one)
         self.arena = arena or {}       # id(p) -> preassigned buffer (dist.BlockGradReducer buckets)
+        self.seeded = set(seeded)      # arena buffers that already hold a partial sum (no_sync steps)
         self._main = None
 
     def run_side(self, fn, inputs):
@@ -94,7 +95,7 @@ class _Grads:
             if buf is None:
                 buf = torch.empty(p.shape, device=p.device, dtype=torch.float32)
             self.g[id(p)] = buf
-            return buf, False
+            return buf, id(p) in self.seeded
         return buf, True
 
     def zeros(self, p):
@@ -154,8 +155,9 @@ class BackboneFn(torch.autograd.Function):
         red = getattr(model, "dsvt_grad_reducer", None)         # data-parallel: dist.BlockGradReducer
         if red is not None and not red.active():
             red = None
+        arena, seeded = red.arena(dfeat.device) if red is not None else (None, ())
         G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None,
-                   arena=red.arena(dfeat.device) if red is not None else None)
+                   arena=arena, seeded=seeded)
         offs = np.cumsum([0] + ctx.rows)
         for i in reversed(range(len(ctx.states))):
             # a block's gradients are final after the last group's pass over it: its bucket's
@@ -165,6 +167,7 @@ class BackboneFn(torch.autograd.Function):
             ctx.states[i] = None
         if red is not None:
             red.finish()
+            red.take_seeded()          # the reduced arena views replace the local no_sync sums
         G.join()
         out = [None, None]
         for p in ctx.params:

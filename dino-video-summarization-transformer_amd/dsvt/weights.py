@@ -27,8 +27,8 @@ class WeightCache:
         ev, waited = ent[-2], ent[-1]
         if ev is None:
             return
-        sid = torch.cuda.current_stream().cuda_stream
-        if sid in waited:
+        cur = torch.cuda.current_stream()
+        if cur.cuda_stream in waited:
             return
         if torch.cuda.is_current_stream_capturing():
             # cross-capture waits are illegal; a copy made before the capture must be finished
@@ -36,16 +36,33 @@ class WeightCache:
                 raise DsvtError("weight cache entry still in flight at HIP-graph capture: run one eager "
                                 "forward (and synchronize) before capturing")
         else:
-            torch.cuda.current_stream().wait_event(ev)
-        waited.add(sid)
+            cur.wait_event(ev)
+        waited[cur.cuda_stream] = cur      # a reader: refresh() orders its in-place rewrite after it
 
     @staticmethod
     def _event():
+        """(event after the producer, {stream id: stream} of the streams that use the entry)."""
         if torch.cuda.is_current_stream_capturing():
-            return None, set()
+            return None, {}
         ev = torch.cuda.Event()
         ev.record()
-        return ev, {torch.cuda.current_stream().cuda_stream}
+        cur = torch.cuda.current_stream()
+        return ev, {cur.cuda_stream: cur}
+
+    @staticmethod
+    def _after_readers(ents):
+        """Order the current stream after everything queued so far on every OTHER stream that
+        has read one of `ents` (the write-after-read hazard of an in-place rewrite): one event
+        per such stream, recorded at its current tail."""
+        cur = torch.cuda.current_stream()
+        seen = {cur.cuda_stream}
+        for ent in ents:
+            for sid, s in ent[-1].items():
+                if sid not in seen:
+                    seen.add(sid)
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                    cur.wait_event(ev)
 
     def getter(self, mode):
         def get(p, flat=False):
@@ -139,11 +156,12 @@ class WeightCache:
         date in ONE multi-tensor launch instead of one cast per weight -- after every optimizer
         / EMA step all of a model's copies are stale at once.  `flat`: ids of parameters used
         flattened to [rows, -1] (the patch-embedding conv).  Stale copies are rewritten in
-        place (their previous readers are ordered before this stream's current position: the
-        step's side streams joined it before the optimizer ran)."""
+        place, after every other stream that has read them (`_after_readers`); under HIP-graph
+        capture (no cross-stream ordering to the past) they get fresh buffers instead."""
         if mode == torch.float32 or not params:
             return
-        stale = []
+        capturing = torch.cuda.is_current_stream_capturing()
+        stale, reused = [], []
         for p in params:
             fl = id(p) in flat
             key = (id(p), "T", mode) if transposed else (id(p), fl)
@@ -156,11 +174,15 @@ class WeightCache:
             if t.dtype != torch.float32 or not t.is_contiguous() or (transposed and t.dim() != 2):
                 raise TypeError("dsvt expects contiguous fp32 master weights, got %s %s" % (t.dtype, tuple(t.shape)))
             shape = (t.shape[1], t.shape[0]) if transposed else tuple(t.shape)
-            out = ent[2] if (ent is not None and tuple(ent[2].shape) == shape and ent[2].dtype == mode) else \
-                torch.empty(shape, device=t.device, dtype=mode)
+            if (not capturing and ent is not None and tuple(ent[2].shape) == shape and ent[2].dtype == mode):
+                out = ent[2]
+                reused.append(ent)
+            else:
+                out = torch.empty(shape, device=t.device, dtype=mode)
             stale.append((key, p, t, out))
         if not stale:
             return
+        self._after_readers(reused)
         from ._lib import call
         tkey = (transposed,) + tuple((t.data_ptr(), o.data_ptr(), tuple(t.shape)) for _, _, t, o in stale)
         tables = self._tables.get(tkey)

@@ -115,7 +115,8 @@ def _worker(rank, world, port, errq):
         assert "head.weight" not in mc._ddp_params_and_buffers_to_ignore
         buckets = red.params()
         assert [len(b) for b in buckets] == [4, 4, 4, 1]
-        views = red.arena(torch.device("cpu"))
+        views, seeded = red.arena(torch.device("cpu"))
+        assert not seeded                                  # no accumulated p.grad yet
         for i, b in enumerate(buckets):
             for p in b:
                 v = views[id(p)]
@@ -129,6 +130,27 @@ def _worker(rank, world, port, errq):
                 assert torch.allclose(views[id(p)], torch.full(p.shape, (i + 1) * (world + 1) / 2.0))
         ddp.require_backward_grad_sync = False             # DDP.no_sync(): no bucket traffic
         assert not red.active()
+        # gradient accumulation: a no_sync micro-step leaves LOCAL sums in p.grad; the next
+        # synchronised backward must all-reduce the accumulated total (DDP's semantics), so the
+        # arena starts from p.grad and the reduced view replaces it (take_seeded)
+        for i, b in enumerate(buckets):
+            for p in b:
+                p.grad = torch.full(p.shape, 10.0 * (rank + 1) + i)
+        ddp.require_backward_grad_sync = True
+        views, seeded = red.arena(torch.device("cpu"))
+        assert seeded == {id(p) for b in buckets for p in b}
+        for i, b in enumerate(buckets):
+            for p in b:
+                views[id(p)].add_(float(rank + 1))         # this micro-step's local gradient
+        for k in range(len(buckets)):
+            red.launch(k)
+        red.finish()
+        red.take_seeded()
+        for i, b in enumerate(buckets):
+            for p in b:                                   # mean over ranks of 11 (rank + 1) + i
+                assert p.grad is None
+                want = 11.0 * (world + 1) / 2.0 + i
+                assert torch.allclose(views[id(p)], torch.full(p.shape, want)), (views[id(p)].flatten()[0], want)
 
         # bench: elapsed = MAX over ranks
         assert ddist.max_over_ranks(1.5 + rank) == pytest.approx(1.5 + world - 1)
