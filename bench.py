@@ -241,6 +241,22 @@ def train_bench(args, device, rank, world, steps, warmup):
     loss_val = float(loss.item())
     if not np.isfinite(loss_val):
         raise SystemExit("bench: non-finite training loss %r" % loss_val)
+    # the reference's own configuration: the teacher left in train mode (DropPath 0.1 active,
+    # never .eval()'d: train_ssl.py:330-333), run under no_grad after the student -- the masked
+    # training forward without saved activations (training.backbone_forward_nosave)
+    teacher.train()
+    trainer.step(crops, 2000 + warmup + steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for i in range(steps):
+        trainer.step(crops, 2001 + warmup + steps + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_tt = ddist.max_over_ranks(time.perf_counter() - t1, device)
+    teacher.eval()
     g, l = vit_fwd_flops(8, 224), vit_fwd_flops(8, 96)
     fwd_s = 2 * g + 6 * l + 8 * head_flops()
     clip_gf = (2 * g + 2 * head_flops() + 3 * fwd_s) / 1e9      # teacher fwd + student fwd + 2x-fwd backward
@@ -256,7 +272,11 @@ def train_bench(args, device, rank, world, steps, warmup):
                 "backbone per-block buckets overlapped with its backward + DDP head"
                 if getattr(args, "grad_overlap", True) else "DDP")) if world > 1 else "dp1",
             "optimizer": "dsvt AdamW (multi-tensor HIP kernel)",
-            "drop_path": 0.1, "teacher_mode": "eval"}
+            "drop_path": 0.1, "teacher_mode": "eval",
+            "teacher_train_mode": {"value": round(world * args.clips * steps / elapsed_tt, 3),
+                                   "ms_per_step": round(elapsed_tt / steps * 1e3, 3),
+                                   "note": "the reference's teacher: train mode, DropPath 0.1, no_grad, "
+                                           "sequential after the student (RNG order)"}}
 
 
 # ----------------------------------------------------------------- configs 4 / 5: other backbones

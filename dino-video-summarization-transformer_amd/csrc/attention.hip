@@ -466,6 +466,9 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
     else attn_short_bf16<16, 4><<<grid, 256, 0, s>>>(p);
     return hipGetLastError();
   }
+  // contiguous sequences (joint space-time, space-only): the LDS-DMA flash kernel
+  // (attn_flash.hip); variant 8 keeps the register-staged kernel below (A/B, tests)
+  if (v != 8 && attn_flash_ok(dtype, p)) return launch_attn_flash(p, s);
   dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)(p.nb * p.tin));
   if (dtype == 0) attn_seq_bf16<<<grid, 256, 0, s>>>(p);
   else attn_seq_f32<<<grid, 64, 0, s>>>(p);

@@ -502,7 +502,7 @@ int dsvt_set_gemm_variant(int variant) {
 }
 
 int dsvt_set_attn_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 7, "attention variant must be 0-7");
+  REQUIRE(variant >= 0 && variant <= 8, "attention variant must be 0-8");
   set_attn_variant(variant);
   return 0;
 }

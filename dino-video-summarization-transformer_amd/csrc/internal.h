@@ -133,6 +133,9 @@ struct AttnParams {
   const float* seq_scale;  // optional: per-sequence output scale (training DropPath over (b, t), timesformer.py:159)
 };
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s);
+// flash attention over contiguous sequences (attn_flash.hip): joint space-time / space-only
+bool attn_flash_ok(int dtype, const AttnParams& p);
+hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s);
 void set_attn_variant(int v);
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T,
                                 int64_t heads, int64_t C, float scale, hipStream_t s);

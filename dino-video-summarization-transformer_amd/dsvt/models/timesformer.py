@@ -406,7 +406,7 @@ class VisionTransformer(nn.Module):
             k = max(1, min(3, rows // SPLIT_ROWS))
         k = min(int(k), B)
         if k > 1 and not get_attn and clips[0].is_cuda and not self._grad_path() \
-                and not torch.cuda.is_current_stream_capturing():     # (nested forks crash HIP capture)
+                and (not torch.cuda.is_current_stream_capturing() or os.environ.get("DSVT_CAPTURE_SPLIT") == "1"):
             return self._forward_split(clips, B, k, shape, get_all, out)
         srcs = [(c, None, c.shape[0]) for c in clips]
         return self._forward_sources(srcs, B, shape[1], shape[2], shape[3], shape[0], get_all, get_attn, out)
@@ -470,6 +470,15 @@ class VisionTransformer(nn.Module):
         if self._grad_path():
             if get_all or get_attn:
                 raise NotImplementedError("get_all / get_attn are inference exports (no backward)")
+            if not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+                # train mode with DropPath but nothing to differentiate (the reference's teacher
+                # under no_grad): the masked training forward without saved activations
+                from ..training import backbone_forward_nosave
+                feats = backbone_forward_nosave(self, srcs, B, T, H, W, Cin)
+                if out is not None:
+                    out.copy_(feats)
+                    return out
+                return feats
             from ..training import BackboneFn
             feats = BackboneFn.apply(self, [(srcs, B, T, H, W, Cin)], *self.parameters())
             if out is not None:

@@ -25,6 +25,20 @@ from .training import np_cosine_scheduler
 from .utils import cancel_gradients_last_layer, clip_gradients, ema_update_, get_params_groups
 
 
+def _draws_rng(model):
+    """True when a forward of `model` draws random numbers: train mode with an active DropPath
+    or dropout.  Such a teacher must run AFTER the student, as in the reference
+    (train_ssl.py:523-527), so a seeded run draws the masks in the same order."""
+    if not model.training:
+        return False
+    for m in model.modules():
+        if m.training and (getattr(m, "drop_prob", 0.0) or 0.0) > 0.0:
+            return True
+        if isinstance(m, torch.nn.Dropout) and m.training and m.p > 0.0:
+            return True
+    return False
+
+
 class DINOTrainer:
     def __init__(self, student, teacher, dino_loss, lr=5e-4, min_lr=1e-6, weight_decay=0.04, weight_decay_end=0.4,
                  momentum_teacher=0.996, clip_grad=3.0, freeze_last_layer=1, epochs=100, niter_per_ep=1000,
@@ -74,9 +88,9 @@ class DINOTrainer:
             pg["lr"] = float(self.lr_schedule[it])
             if i == 0:
                 pg["weight_decay"] = float(self.wd_schedule[it])
-        if self.concurrent_teacher and images[0].is_cuda:
-            # the teacher forward (no grad, no RNG draws) is independent of the student's: it runs
-            # on its own stream, overlapping the student forward's GEMM tails and short kernels
+        if self.concurrent_teacher and images[0].is_cuda and not _draws_rng(self.teacher):
+            # the teacher forward (no grad, no RNG draws: checked above) is independent of the
+            # student's: it runs on its own stream, overlapping the student forward's GEMM tails
             from .utils import side_stream
             main = torch.cuda.current_stream(images[0].device)
             side = side_stream(images[0].device, "teacher")

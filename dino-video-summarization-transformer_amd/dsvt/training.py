@@ -209,7 +209,17 @@ def _masks(model, nblk, B, Np, T, L, device):
     return out
 
 
-def _backbone_forward(model, srcs, B, T, H, W, Cin):
+def backbone_forward_nosave(model, srcs, B, T, H, W, Cin):
+    """The training-mode forward WITHOUT autograd: DropPath masks drawn and applied exactly as
+    the autograd path does (same kernels, same RNG calls in the same order, same features),
+    but every block's activations are dropped as soon as the next block has consumed them.
+    This is the reference's teacher: it stays in train mode (train_ssl.py:330-333, SURVEY §5
+    defect 2) and runs under torch.no_grad() (:527), so nothing is ever differentiated."""
+    feats, _ = _backbone_forward(model, srcs, B, T, H, W, Cin, save=False)
+    return feats
+
+
+def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
     if model.attention_type != 'divided_space_time':
         raise NotImplementedError("dsvt backward is implemented for divided space-time attention (the DINO-SVT "
                                   "path); got %s" % model.attention_type)
@@ -294,8 +304,12 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin):
             ops.gemm_rowscale(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, mk.m, L, aux=S.pre,
                               epilogue=EPI_GELU_SAVE)
             ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, S.X2, X, bias_row_scale=mk.m_rows)
-        st.blocks.append(S)
-    st.X = X
+        if save:
+            st.blocks.append(S)
+        # (save=False: S and its buffers go out of scope here; the caching allocator reuses them
+        # for the next block once the queued kernels that read them have run on this stream)
+    if save:
+        st.X = X
     feats = torch.empty(B, C, device=dev, dtype=torch.float32)
     ops.layernorm(X, B, C, model.norm.weight, model.norm.bias, model.norm.eps, feats, rowmap=(1, L, 0))
     return feats, st

@@ -407,7 +407,21 @@ def step_crops(it):
            [P.clip(1505 + 10 * it + i, (2, 3, 2, 32, 32)) for i in range(2)]
 
 
-def train_step_cases():
+def train_step_fp16_cases():
+    """train_step_cases with the reference's DEFAULT flag `--use_fp16 True` (train_ssl.py:87):
+    `fp16_scaler = torch.cuda.amp.GradScaler()` (:390-392) is passed to train_one_epoch, so its
+    fp16 branch runs -- autocast (:507), scaler.scale(loss).backward(), unscale_ before the
+    per-parameter clip, scaler.step / update (:545-552).  On this CPU-only host torch disables
+    both the CUDA GradScaler and the CUDA autocast (with a warning), so the branch's control flow
+    runs with fp32 numerics; the recorded trajectory is compared against train_step.npz (the
+    fp32 branch) and stored as `same_as_fp32` plus the per-step loss / center."""
+    out = train_step_cases(use_fp16=True)
+    ref = dict(np.load(os.path.join(HERE, "train_step.npz")))
+    same = all(np.array_equal(out[k], ref[k]) for k in out)
+    return {"same_as_fp32": np.array(int(same)), "loss": out["loss"], "center": out["center"]}
+
+
+def train_step_cases(use_fp16=False):
     """Whole SSL training steps (train_ssl.py:466-573): the reference's own `train_one_epoch`,
     extracted with `ast` and run as written for 2 epochs x 2 iterations on a tiny divided
     TimeSformer student / teacher (drop_path 0: both nets deterministic) with DINOHead and
@@ -420,7 +434,8 @@ def train_step_cases():
 
     import torch.distributed as dist
     from utils import utils as ref_utils
-    A = argparse.Namespace(**STEP_ARGS)
+    A = argparse.Namespace(**dict(STEP_ARGS, use_fp16=use_fp16))
+    scaler = torch.cuda.amp.GradScaler() if use_fp16 else None          # train_ssl.py:390-392
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -481,7 +496,7 @@ def train_step_cases():
         for epoch in range(A.epochs):
             loader = [([torch.from_numpy(c) for c in step_crops(epoch * STEP_ITERS + i)], None, None, {})
                       for i in range(STEP_ITERS)]
-            train_one_epoch(student, teacher, teacher, loss_fn, loader, optimizer, lr_s, wd_s, mom_s, epoch, None,
+            train_one_epoch(student, teacher, teacher, loss_fn, loader, optimizer, lr_s, wd_s, mom_s, epoch, scaler,
                             A, cfg=cfg)
     finally:
         for o, n, v in saved:
@@ -540,6 +555,7 @@ def views_edge_cases():
 
 
 GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases,
+          "train_step_fp16": train_step_fp16_cases,
           "views_edge": views_edge_cases}
 
 if __name__ == "__main__":

@@ -485,18 +485,27 @@ def test_attn_spatial_variants_repeatable(variant):
     check(back(outs[0])[:2 * L], ref, torch.bfloat16, "spatial variant %d" % variant)
 
 
+@pytest.mark.parametrize("variant", [0, 8])
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("nb,L,heads", [(2, 5, 3), (1, 16, 2), (1, 17, 2), (1, 64, 2), (1, 65, 12), (2, 197, 3),
                                         (1, 208, 2), (1, 209, 2), (1, 256, 2), (1, 257, 2), (1, 300, 2),
-                                        (1, 1569, 1)])
-def test_attn_joint(dtype, nb, L, heads):
-    """L <= 256: whole-sequence LDS kernel (attn_short_bf16 in bf16); longer: flash kernel."""
-    from dsvt import ops
+                                        (3, 320, 2), (2, 449, 3), (1, 1569, 1)])
+def test_attn_joint(dtype, nb, L, heads, variant):
+    """L <= 256: whole-sequence LDS kernel (attn_short_bf16 in bf16); longer: the LDS-DMA flash
+    kernel (attn_flash_bf16, variant 0: last partial key tile first -- 1, 44, 64, 1 valid keys
+    at L = 257, 300, 320, 449) or the register-staged one (variant 8)."""
+    from dsvt import _lib, ops
+    if variant and (dtype == torch.float32 or L <= 256):
+        pytest.skip("variant 8 is the bf16 long-sequence kernel")
     C = heads * 64
     qkv = rnd((nb * L, 3 * C), 13, 1.5)
     Q = to(qkv, dtype)
     out = torch.empty(nb * L, C, device=dev(), dtype=dtype)
-    ops.attn_joint(Q, out, nb, L, heads, 0.125)
+    _lib.call("dsvt_set_attn_variant", variant)
+    try:
+        ops.attn_joint(Q, out, nb, L, heads, 0.125)
+    finally:
+        _lib.call("dsvt_set_attn_variant", 0)
     torch.cuda.synchronize()
     q3 = back(Q)
     ref = np.zeros((nb * L, C))
@@ -508,10 +517,11 @@ def test_attn_joint(dtype, nb, L, heads):
     check(back(out), ref, dtype, "joint")
 
 
-@pytest.mark.parametrize("L,hot", [(200, 190), (400, 390)])
+@pytest.mark.parametrize("L,hot", [(200, 190), (400, 390), (400, 10), (3137, 3000)])
 def test_attn_softmax_spike(L, hot):
-    """One key far above the rest in a LATE chunk: the online-softmax rescale branch of the
-    flash kernel (L=400) and the two-pass softmax of the short kernel (L=200)."""
+    """One key far above the rest: the two-pass softmax of the short kernel (L=200); in the flash
+    kernel a spike in the partial last key tile (processed first: L=400 hot=390) and in a later
+    tile (hot=10, 3000: the online-softmax rescale of everything accumulated before it)."""
     from dsvt import ops
     nb, heads = 1, 1
     qkv = rnd((L, 192), 14, 0.5)

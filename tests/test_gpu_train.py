@@ -543,3 +543,107 @@ def test_train_step_bitwise_repeatable_bf16():
     assert finals[0][0] == finals[1][0], (finals[0][0], finals[1][0])
     assert torch.equal(finals[0][1], finals[1][1]), "student parameters differ between identical runs"
     assert torch.equal(finals[0][2], finals[1][2]), "teacher parameters differ between identical runs"
+
+
+@pytest.mark.parametrize("optim", ["torch", "dsvt"])
+def test_train_steps_fp16_scaler_loop_body(optim):
+    """The reference's DEFAULT loop (`--use_fp16 True`, train_ssl.py:87, 390-392): the fp16
+    branch of train_one_epoch (:507 autocast, :545-552 scaler.scale(loss).backward() ->
+    unscale_ -> clip_gradients -> cancel_gradients_last_layer -> scaler.step -> update), written
+    out statement by statement around the dsvt modules, with a REAL torch.cuda.amp.GradScaler
+    (loss scale 65536) and autocast enabled on the GPU, fp32 parity mode, the reference's
+    torch.optim.AdamW or dsvt's.  Against the reference's own run of that branch
+    (tests/golden/train_step_fp16.npz: on the CPU host torch disables the CUDA scaler and
+    autocast, and the recorded trajectory is bit-identical to the fp32 branch's, train_step.npz,
+    whose parameters this test compares).  Power-of-two loss scaling is exact in fp32, so the
+    bar is train_step's."""
+    from dsvt import utils as U
+    from dsvt.loss import DINOLoss
+    from dsvt.optim import AdamW
+    fp16 = dict(np.load("tests/golden/train_step_fp16.npz"))
+    assert int(fp16["same_as_fp32"]) == 1
+    gold = dict(np.load("tests/golden/train_step.npz"))
+    np.testing.assert_array_equal(fp16["loss"], gold["loss"])
+    student, teacher = _step_nets()
+    teacher.load_state_dict(student.state_dict())                        # :330-333
+    for p in teacher.parameters():
+        p.requires_grad = False
+    loss_fn = DINOLoss(128, 4, 0.04, 0.04, 0, 2).cuda()
+    groups = U.get_params_groups(student)                                # :377-384
+    optimizer = torch.optim.AdamW(groups) if optim == "torch" else AdamW(groups)
+    scaler = torch.cuda.amp.GradScaler()                                 # :390-392
+    lr_s, wd_s, mom_s = gold["lr"], gold["wd"], gold["momentum"]
+    epochs, niter = 2, 2
+    for it in range(epochs * niter):
+        epoch = it // niter
+        for i, pg in enumerate(optimizer.param_groups):                 # :486-490
+            pg["lr"] = lr_s[it]
+            if i == 0:
+                pg["weight_decay"] = wd_s[it]
+        images = [torch.from_numpy(P.clip(1500 + 10 * it + i, (2, 3, 2, 48, 48))).cuda() for i in range(2)] + \
+                 [torch.from_numpy(P.clip(1505 + 10 * it + i, (2, 3, 2, 32, 32))).cuda() for i in range(2)]
+        with torch.cuda.amp.autocast(scaler is not None):                # :507
+            student_output = student(images)
+            teacher_output = teacher(images[:2])
+            loss = loss_fn(student_output, teacher_output, epoch)
+        assert np.isfinite(loss.item())                                  # :530-532
+        optimizer.zero_grad()
+        scaler.scale(loss).backward()                                    # :545
+        scaler.unscale_(optimizer)                                       # :547
+        U.clip_gradients(student, 3.0)                                   # :548
+        U.cancel_gradients_last_layer(epoch, student, 1)                 # :549-550
+        scaler.step(optimizer)                                           # :551
+        scaler.update()                                                  # :552
+        with torch.no_grad():                                            # :555-558
+            m = mom_s[it]
+            for param_q, param_k in zip(student.parameters(), teacher.parameters()):
+                param_k.data.mul_(m).add_((1 - m) * param_q.detach().data)
+        torch.cuda.synchronize()
+        assert abs(loss.item() - gold["loss"][it]) < 1e-3 * abs(gold["loss"][it]), (it, loss.item(), gold["loss"][it])
+        assert rel(loss_fn.center.cpu().numpy(), fp16["center"][it]) < 1e-3, it
+    assert scaler.get_scale() == 65536.0                                 # no overflow step was skipped
+    lr_step = float(max(gold["lr"]))
+    for tag, net in (("student", student), ("teacher", teacher)):
+        for k, p in net.named_parameters():
+            ref = gold["%s.%s" % (tag, k)]
+            err = np.abs(p.detach().cpu().numpy().astype(np.float64) - ref)
+            scale = max(np.max(np.abs(ref)), 1e-12)
+            assert float(np.mean(err <= 1e-3 * scale)) >= 0.999, (tag, k)
+            assert err.max() <= 2 * lr_step + 1e-3 * scale, (tag, k)
+            assert float(np.linalg.norm(err) / max(np.linalg.norm(ref), 1e-12)) < 1e-3, (tag, k)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_train_mode_teacher_nosave_matches_autograd_forward(dtype):
+    """The reference's teacher stays in train mode with DropPath (train_ssl.py:330-333, SURVEY §5
+    defect 2) and runs under no_grad.  dsvt then takes the masked training forward WITHOUT saved
+    activations (training.backbone_forward_nosave): its features must be BITWISE those of the
+    autograd training forward on the same RNG state (same kernels, same mask draws in the same
+    order), and it must hold far less memory than the saving forward (ViT-B width, 4 clips)."""
+    from dsvt.models.timesformer import VisionTransformer
+    torch.manual_seed(5)
+    bb = VisionTransformer(img_size=224, patch_size=16, num_classes=0, embed_dim=768, depth=4, num_heads=12,
+                           mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                           drop_path_rate=0.3, num_frames=8, attention_type="divided_space_time").cuda().train()
+    bb.dsvt_dtype = dtype
+    x = torch.randn(4, 3, 8, 224, 224, device="cuda", generator=torch.Generator(device="cuda").manual_seed(9))
+    outs, peaks = [], []
+    for grad in (True, False):
+        for p in bb.parameters():
+            p.requires_grad_(grad)
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.manual_seed(77)
+        with torch.set_grad_enabled(grad):
+            f = bb(x)
+        torch.cuda.synchronize()
+        peaks.append(torch.cuda.max_memory_allocated() - base)
+        outs.append(f.detach().clone())
+        del f
+    assert torch.equal(outs[0], outs[1]), "no-save train-mode forward differs from the autograd forward"
+    assert peaks[1] < 0.5 * peaks[0], peaks
+    torch.cuda.manual_seed(78)
+    with torch.no_grad():
+        other = bb(x)
+    assert not torch.equal(other, outs[1]), "DropPath masks not drawn in the no-save forward"
