@@ -370,17 +370,10 @@ class VisionTransformer(nn.Module):
         if not getattr(x, "is_cuda", False) or not self.pos_embed.is_cuda:
             raise DsvtError("dsvt VisionTransformer runs only on the GPU (no CPU fallback): move model and input "
                             "to cuda")
-        divided = self.attention_type == 'divided_space_time'
         if self.training:
             if any(r > 0 for r in self._drop_rates):
                 raise NotImplementedError("dropout > 0 is not supported by the dsvt forward (the reference's "
                                           "drop_rate / attn_drop_rate are 0)")
-            if not divided and any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0
-                                   for b in self.blocks):
-                raise NotImplementedError("training-mode DropPath is implemented for divided space-time "
-                                          "attention only; call .eval() for %s" % self.attention_type)
-        if self._grad_path() and not divided:
-            raise NotImplementedError("dsvt backward is implemented for divided space-time attention only")
 
     def _grad_path(self):
         """Training path: autograd through dsvt.training.BackboneFn (saved activations +

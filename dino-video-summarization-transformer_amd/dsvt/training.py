@@ -221,8 +221,7 @@ def backbone_forward_nosave(model, srcs, B, T, H, W, Cin):
 
 def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
     if model.attention_type != 'divided_space_time':
-        raise NotImplementedError("dsvt backward is implemented for divided space-time attention (the DINO-SVT "
-                                  "path); got %s" % model.attention_type)
+        return _plain_forward(model, srcs, B, T, H, W, Cin, save)
     mode = model.dsvt_dtype
     model._wcache.refresh(_block_weights(model) + [model.patch_embed.proj.weight], mode,
                           flat={id(model.patch_embed.proj.weight)})       # all stale bf16 copies, one launch
@@ -316,6 +315,12 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
 
 
 def _backbone_backward(model, st, dfeat, G, ready=None):
+    if model.attention_type != 'divided_space_time':
+        return _plain_backward(model, st, dfeat, G, ready)
+    return _divided_backward(model, st, dfeat, G, ready)
+
+
+def _divided_backward(model, st, dfeat, G, ready=None):
     """One group's backward into the gradient buffers G (written on first use, accumulated
     after).  The weight gradients depend only on (dY, X) and nothing reads them before the
     optimizer step: G runs them on a second stream, overlapping the dX chain (GEMM tails,
@@ -400,6 +405,194 @@ def _backbone_backward(model, st, dfeat, G, ready=None):
         wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
     ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
                   G.zeros(model.cls_token))
+    if ready is not None:
+        ready(depth)
+    return G
+
+
+# ======================================================================= joint / space-only
+def _plain_weights(model):
+    ws = []
+    for blk in model.blocks:
+        ws += [blk.attn.qkv.weight, blk.attn.proj.weight, blk.mlp.fc1.weight, blk.mlp.fc2.weight]
+    return ws
+
+
+def _plain_masks(model, nb, L, device):
+    """DropPath scales of the joint / space-only block (timesformer.py:116-123, 184): x is
+    [nb, L, C] -- nb = B clips (joint) or B*T frames (space-only) -- and each of the two
+    residual branches draws one scale per sequence, attention first."""
+    out = []
+    for blk in model.blocks:
+        dp = getattr(blk.drop_path, "drop_prob", 0.0)
+        if not model.training or dp <= 0.0:
+            out.append(None)
+            continue
+        m = _S()
+        m.a = _keep_scale(nb, dp, device)
+        m.m = _keep_scale(nb, dp, device)
+        m.a_rows = m.a.view(nb, 1).expand(nb, L).reshape(-1).contiguous()
+        m.m_rows = m.m.view(nb, 1).expand(nb, L).reshape(-1).contiguous()
+        out.append(m)
+    return out
+
+
+def _plain_forward(model, srcs, B, T, H, W, Cin, save=True):
+    """Training forward of the joint space-time / space-only VisionTransformer
+    (timesformer.py:285-345 with Block.forward :116-123, 184): patch + token embedding, then per
+    block x += drop_path(attn(norm1(x))); x += drop_path(mlp(norm2(x))) on the [nb, L, C] token
+    tensor (contiguous sequences: the LDS-DMA flash / joint attention kernels), the space-only
+    frame mean (:338-340) and the final norm of the CLS rows."""
+    from ._lib import TOKENS_FRAME
+    mode = model.dsvt_dtype
+    space = model.attention_type == 'space_only'
+    model._wcache.refresh(_plain_weights(model) + [model.patch_embed.proj.weight], mode,
+                          flat={id(model.patch_embed.proj.weight)})
+    w = model._wcache.getter(mode)
+    Hp, Wp = H // 16, W // 16
+    Np, C = Hp * Wp, model.embed_dim
+    if space:
+        nb, L, order, per_clip = B * T, 1 + Np, TOKENS_FRAME, T * (1 + Np)
+    else:
+        nb, L, order, per_clip = B, 1 + Np * T, TOKENS_NT, 1 + Np * T
+    rows = nb * L
+    dev = srcs[0][0].device
+    pidx, tidx = model._indices(Hp, Wp, T, dev)
+    st = _S()
+    st.mode, st.B, st.T, st.Np, st.L, st.C, st.nb, st.space = mode, B, T, Np, L, C, nb, space
+    st.pidx, st.tidx = pidx, tidx
+    X = torch.empty(rows, C, device=dev, dtype=torch.float32)
+    st.im2col = []
+    row0 = 0
+    for src, fidx, nbs in srcs:
+        K = Cin * 256
+        ws = torch.empty(ops.workspace_bytes(WS_PATCH_EMBED, mode, nbs * T * Np, C, K) // 2, device=dev,
+                         dtype=torch.bfloat16)
+        ops.patch_embed(src.float().contiguous(), w(model.patch_embed.proj.weight, flat=True),
+                        model.patch_embed.proj.bias, model.cls_token, model.pos_embed, pidx,
+                        None if space else model.time_embed, tidx, X[row0 * per_clip:(row0 + nbs) * per_clip], ws,
+                        order, frame_index=fidx, clip_shape=(nbs, T))
+        st.im2col.append((row0, nbs, ws.view(mode)[:nbs * T * Np * K].view(nbs * T * Np, K)))
+        row0 += nbs
+    masks = _plain_masks(model, nb, L, dev)
+    st.masks = masks
+    st.blocks = []
+    for blk, mk in zip(model.blocks, masks):
+        S = _S()
+        heads = blk.attn.num_heads
+        S.X0 = X
+        S.a = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.layernorm(X, rows, C, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, S.a, out_f32=False)
+        S.qkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
+        ops.gemm(S.a, w(blk.attn.qkv.weight), blk.attn.qkv.bias, S.qkv)
+        S.o = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.attn_joint(S.qkv, S.o, nb, L, heads, blk.attn.scale)
+        X = torch.empty_like(X)
+        if mk is None:
+            ops.gemm_resid(S.o, w(blk.attn.proj.weight), blk.attn.proj.bias, S.X0, X)
+        else:                            # drop_path(proj(o)): o scaled per sequence, s * bias
+            ops.row_scale(S.o, mk.a, L)
+            ops.gemm_resid(S.o, w(blk.attn.proj.weight), blk.attn.proj.bias, S.X0, X, bias_row_scale=mk.a_rows)
+        S.X2 = X
+        S.a_m = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.layernorm(X, rows, C, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, S.a_m, out_f32=False)
+        hid = blk.mlp.fc1.out_features
+        S.pre = torch.empty(rows, hid, device=dev, dtype=mode)
+        S.h = torch.empty(rows, hid, device=dev, dtype=mode)
+        X = torch.empty_like(X)
+        if mk is None:
+            ops.gemm_aux(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, S.pre, EPI_GELU_SAVE)
+            ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, S.X2, X)
+        else:
+            ops.gemm_rowscale(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, mk.m, L, aux=S.pre,
+                              epilogue=EPI_GELU_SAVE)
+            ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, S.X2, X, bias_row_scale=mk.m_rows)
+        if save:
+            st.blocks.append(S)
+    if space:                            # x.view(B, T, L, C).mean(1)  (:338-340)
+        Xm = torch.empty(B * L, C, device=dev, dtype=torch.float32)
+        ops.frame_mean(X, Xm, B, T, L * C)
+        X = Xm
+    if save:
+        st.X = X
+    feats = torch.empty(B, C, device=dev, dtype=torch.float32)
+    ops.layernorm(X, B, C, model.norm.weight, model.norm.bias, model.norm.eps, feats, rowmap=(1, L, 0))
+    return feats, st
+
+
+def _plain_backward(model, st, dfeat, G, ready=None):
+    """Backward of _plain_forward into the gradient buffers G (see _divided_backward)."""
+    mode, B, T, Np, L, C, nb, space = st.mode, st.B, st.T, st.Np, st.L, st.C, st.nb, st.space
+    rows = nb * L
+    dev = dfeat.device
+    model._wcache.refresh(_plain_weights(model), mode, transposed=True)
+    wt = model._wcache.transposed(mode)
+    if space:
+        # final norm of the frame-mean CLS rows, then d(mean over frames) = dXm / T on every frame
+        dXm = torch.zeros(B * L, C, device=dev, dtype=torch.float32)
+        _ln_bwd(st.X, dfeat, model.norm, dXm, B, G, rowmap=(1, L, 0))
+        dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
+        dX.view(B, T, L, C)[:, :, 0].copy_((dXm.view(B, L, C)[:, 0] * (1.0 / T)).unsqueeze(1).expand(B, T, C))
+    else:
+        dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
+        _ln_bwd(st.X, dfeat, model.norm, dX, B, G, rowmap=(1, L, 0))
+    depth = len(model.blocks)
+    for bi, blk, S, mk in zip(range(depth - 1, -1, -1), reversed(model.blocks), reversed(st.blocks),
+                              reversed(st.masks)):
+        heads = blk.attn.num_heads
+        fc1, fc2 = blk.mlp.fc1, blk.mlp.fc2
+        # ---- MLP (identical to the divided block's)
+        dXb = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.cast_rows(dX, dXb, rows)
+        if mk is None:
+            dXs = dXb
+            _colsum(dX, G, fc2.bias)
+        else:
+            dXs = torch.empty(rows, C, device=dev, dtype=mode)
+            ops.cast_rows(dX, dXs, rows, row_scale=mk.m, group=L)
+            _colsum(dX, G, fc2.bias, row_scale=mk.m_rows)
+        wgrad(dXb, S.h, G, fc2.weight)
+        dpre = torch.empty(rows, fc1.out_features, device=dev, dtype=mode)
+        ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
+        wgrad(dpre, S.a_m, G, fc1.weight, bias=fc1.bias)
+        da = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.gemm(dpre, wt(fc1.weight), None, da)
+        del dpre
+        _ln_bwd(S.X2, da, blk.norm2, dX, rows, G)
+        # ---- attention: proj (its input o carries the DropPath scale), joint attention, qkv, norm1
+        dXb = torch.empty(rows, C, device=dev, dtype=mode)
+        ops.cast_rows(dX, dXb, rows)
+        wgrad(dXb, S.o, G, blk.attn.proj.weight)
+        _colsum(dX, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.a_rows)
+        do = torch.empty(rows, C, device=dev, dtype=mode)
+        if mk is None:
+            ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)
+        else:
+            ops.gemm_rowscale(dXb, wt(blk.attn.proj.weight), None, do, mk.a, L)
+        dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
+        ops.attn_joint_bwd(S.qkv, do, dqkv, nb, L, heads, blk.attn.scale)
+        wgrad(dqkv, S.a, G, blk.attn.qkv.weight, bias=blk.attn.qkv.bias)
+        ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da)
+        del dqkv, do
+        _ln_bwd(S.X0, da, blk.norm1, dX, rows, G)
+        for k in list(vars(S)):
+            setattr(S, k, None)
+        if ready is not None:
+            ready(bi)
+    # ---- patch embedding + token embeddings
+    R = nb * Np
+    patch_map = (Np, L, 1) if space else (Np * T, L, 1)
+    dP = torch.empty(R, C, device=dev, dtype=mode)
+    ops.cast_rows(dX, dP, R, rowmap=patch_map)
+    conv = model.patch_embed.proj
+    for row0, nbs, a in st.im2col:
+        r0 = row0 * Np * T
+        wgrad(dP[r0:r0 + nbs * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
+    if space:                            # frame-major rows: the NT map with T = 1 over B*T sequences
+        ops.embed_bwd(dX, nb, Np, 1, st.pidx, None, G.zeros(model.pos_embed), None, G.zeros(model.cls_token))
+    else:
+        ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
+                      G.zeros(model.cls_token))
     if ready is not None:
         ready(depth)
     return G

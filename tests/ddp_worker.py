@@ -32,8 +32,20 @@ import torch.nn as nn  # noqa: E402
 
 from oracle import params as P  # noqa: E402
 
-CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
-OUT_DIM, B_ALL, NCROPS = 512, 4, 4
+# DSVT_DDP_CFG=tiny (default): a 64-wide depth-2 model, 4 clips of 2 x 4x64^2 + 2 x 4x32^2 crops.
+# DSVT_DDP_CFG=vitb: ViT-B widths (embed 768, 12 heads, depth 2) on 2 clips of 2 x 8x224^2 +
+# 2 x 8x96^2 crops, DINOHead(768 -> 2048 -> 256 -> 4096): the per-block gradient buckets of
+# dist.BlockGradReducer at their real sizes (7.1 M values = 28 MB per block) and launch order
+# under the real backward.
+SIZE = os.environ.get("DSVT_DDP_CFG", "tiny")
+if SIZE == "vitb":
+    CFG = dict(embed_dim=768, num_heads=12, depth=2, img_size=224, num_frames=8)
+    HEAD = dict(hidden_dim=2048, bottleneck_dim=256)
+    OUT_DIM, B_ALL, NCROPS, T, G_SZ, L_SZ = 4096, 2, 4, 8, 224, 96
+else:
+    CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
+    HEAD = dict(hidden_dim=128, bottleneck_dim=64)
+    OUT_DIM, B_ALL, NCROPS, T, G_SZ, L_SZ = 512, 4, 4, 4, 64, 32
 TOL = 1e-3
 
 
@@ -41,21 +53,22 @@ def build(seed_bb, seed_hd):
     from dsvt.models.timesformer import VisionTransformer
     from dsvt.utils import MultiCropWrapper
     from dsvt.vision_transformer import DINOHead
-    bb = VisionTransformer(img_size=64, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
-                           qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_path_rate=0.0,
-                           num_frames=4, attention_type="divided_space_time")
+    E = CFG["embed_dim"]
+    bb = VisionTransformer(img_size=CFG["img_size"], patch_size=16, num_classes=0, embed_dim=E, depth=CFG["depth"],
+                           num_heads=CFG["num_heads"], mlp_ratio=4, qkv_bias=True,
+                           norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_path_rate=0.0,
+                           num_frames=CFG["num_frames"], attention_type="divided_space_time")
     bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(seed_bb, **CFG).items()})
-    hd = DINOHead(64, OUT_DIM, hidden_dim=128, bottleneck_dim=64)
-    hd.load_state_dict({k: torch.from_numpy(v) for k, v in
-                        P.dino_head_state(seed_hd, 64, OUT_DIM, hidden_dim=128, bottleneck_dim=64).items()})
+    hd = DINOHead(E, OUT_DIM, **HEAD)
+    hd.load_state_dict({k: torch.from_numpy(v) for k, v in P.dino_head_state(seed_hd, E, OUT_DIM, **HEAD).items()})
     bb.dsvt_dtype = hd.dsvt_dtype = torch.float32
     return MultiCropWrapper(bb, hd).cuda()
 
 
 def crops_all():
-    """The whole batch: 2 global 4x64^2 and 2 local 4x32^2 crops of B_ALL clips."""
-    return [P.clip(3100 + i, (B_ALL, 3, 4, 64, 64)) for i in range(2)] + \
-           [P.clip(3110 + i, (B_ALL, 3, 4, 32, 32)) for i in range(2)]
+    """The whole batch: 2 global and 2 local crops of B_ALL clips."""
+    return [P.clip(3100 + i, (B_ALL, 3, T, G_SZ, G_SZ)) for i in range(2)] + \
+           [P.clip(3110 + i, (B_ALL, 3, T, L_SZ, L_SZ)) for i in range(2)]
 
 
 def make_loss(center0):
@@ -100,13 +113,17 @@ def main():
     # ---- phase 1: DDP gradients + center vs the single-process whole batch, with the backbone's
     # gradients on DDP's reducer (plain DDP) and on the overlapped per-block buckets (wrap_ddp)
     results = {}
-    for mode in ("ddp", "overlap", "overlap_1stream"):
+    # *_accum: gradient accumulation -- one micro-step under DDP.no_sync() (local sums only),
+    # then a synchronised one; DDP averages the ACCUMULATED gradient (the overlapped
+    # buckets must reduce the no_sync sums too, dist.BlockGradReducer.arena seeding)
+    modes = ("ddp", "overlap", "overlap_1stream", "ddp_accum", "overlap_accum")
+    for mode in modes:
         student = build(4101, 4102).train()
         teacher = build(4201, 4202).eval()
         for p in teacher.parameters():
             p.requires_grad_(False)
         log("models built (%s)" % mode)
-        if mode == "ddp":
+        if mode.startswith("ddp"):
             ddp = torch.nn.parallel.DistributedDataParallel(student, device_ids=[0], broadcast_buffers=False)
         else:
             ddp = ddist.wrap_ddp(student, dev)
@@ -115,6 +132,13 @@ def main():
                 student.backbone.dsvt_wgrad_stream = False
         log("ddp wrapped")
         loss_fn = make_loss(center0)
+        if mode.endswith("_accum"):                         # micro-step 1: no gradient traffic
+            with ddp.no_sync():
+                s0 = ddp(mine)
+                with torch.no_grad():
+                    t0 = teacher(mine[:2])
+                loss_fn(s0, t0, 0).backward()
+            log("no_sync micro-step done")
         s_out = ddp(mine)                                   # train_ssl.py:523
         with torch.no_grad():
             t_out = teacher(mine[:2])                       # :527
@@ -143,38 +167,53 @@ def main():
         lf = make_loss(center0)
         lf.defer_center_update = True      # a single process: its center update has no all-reduce
         allc = [torch.from_numpy(c).to(dev) for c in full]
-        so = ref(allc)
-        with torch.no_grad():
-            to = teacher(allc[:2])
-        l_ref = lf(so, to, 0)
-        colsum, rows = lf.last_colsum
-        ops.center_ema(lf.center, colsum, lf.center_momentum, 1.0 / rows)
-        l_ref.backward()
+
+        def ref_step():
+            so = ref(allc)
+            with torch.no_grad():
+                to = teacher(allc[:2])
+            loss_r = lf(so, to, 0)
+            colsum, rows = lf.last_colsum
+            ops.center_ema(lf.center, colsum, lf.center_momentum, 1.0 / rows)
+            loss_r.backward()
+            return loss_r
+        l_ref = ref_step()
         torch.cuda.synchronize()
+        g_one = {n: p.grad.cpu().numpy().copy() for n, p in ref.named_parameters() if p.requires_grad}
+        c_one = lf.center.cpu().numpy().copy()
+        l_acc = ref_step()                 # accumulated onto the first step's gradients
+        torch.cuda.synchronize()
+        g_acc = {n: p.grad.cpu().numpy().copy() for n, p in ref.named_parameters() if p.requires_grad}
+        c_acc = lf.center.cpu().numpy().copy()
         for mode, (grads, loss_sum, center_dp) in results.items():
-            errs = {}
-            for n, p in ref.named_parameters():
-                if p.requires_grad:
-                    errs[n] = rel(grads[n], p.grad.cpu().numpy())
+            accum = mode.endswith("_accum")
+            ref_g = g_acc if accum else g_one
+            errs = {n: rel(grads[n], ref_g[n]) for n in ref_g}
             worst = max(errs, key=errs.get)
             info["worst_grad_" + mode] = [worst, errs[worst]]
             info["top_" + mode] = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
-            if mode != "ddp":
-                info["vs_ddp_" + mode] = max(rel(grads[n], results["ddp"][0][n]) for n in grads)
+            base = "ddp_accum" if accum else "ddp"
+            if mode != base:
+                info["vs_ddp_" + mode] = max(rel(grads[n], results[base][0][n]) for n in grads)
         for mode, (grads, loss_sum, center_dp) in results.items():
+            accum = mode.endswith("_accum")
             worst = info["worst_grad_" + mode][0]
             assert info["worst_grad_" + mode][1] < TOL, "%s grad %s rel err %.3g vs single-process full batch: %s" % (
                 mode, worst, info["worst_grad_" + mode][1], info)
             l_mean = float(loss_sum.item()) / world
-            info["loss_" + mode] = [l_mean, float(l_ref.item())]
-            assert abs(l_mean - float(l_ref.item())) < TOL * abs(float(l_ref.item())), info["loss_" + mode]
-            ec = rel(center_dp, lf.center.cpu().numpy())
+            lr_ = l_acc if accum else l_ref
+            info["loss_" + mode] = [l_mean, float(lr_.item())]
+            assert abs(l_mean - float(lr_.item())) < TOL * abs(float(lr_.item())), info["loss_" + mode]
+            ec = rel(center_dp, c_acc if accum else c_one)
             info["center_err_" + mode] = ec
             assert ec < 1e-5, "center after the all-reduced update differs (%s): %.3g" % (mode, ec)
         del ref, lf
     dist.barrier()
 
     # ---- phase 2: whole training steps under DDP stay in sync across ranks
+    if SIZE != "tiny":
+        dist.destroy_process_group()
+        return info
     from dsvt.trainer import DINOTrainer
     student = build(4101, 4102).train()
     teacher = build(4101, 4102).eval()

@@ -80,15 +80,15 @@ def tsf_model(seed, **kw):
 TRAIN_CFG = dict(embed_dim=64, num_heads=1, depth=2, img_size=64, num_frames=4)
 
 
-def train_grads(TL):
+def train_grads(TL, attention_type="divided_space_time"):
     import models.vit_utils as ref_vu
     res = {}
     for tag, dpr in (("eval", 0.0), ("drop", 0.5)):
         bb = ref_tsf.VisionTransformer(img_size=64, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1,
                                        mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
                                        drop_rate=0., attn_drop_rate=0., drop_path_rate=dpr, num_frames=4,
-                                       attention_type="divided_space_time")
-        _load(bb, P.timesformer_state(1201, **TRAIN_CFG))
+                                       attention_type=attention_type)
+        _load(bb, P.timesformer_state(1201, attention_type=attention_type, **TRAIN_CFG))
         hd = ref_vit.DINOHead(64, 512, hidden_dim=128, bottleneck_dim=64)
         _load(hd, P.dino_head_state(1202, 64, 512, hidden_dim=128, bottleneck_dim=64))
         masks = []
@@ -131,6 +131,24 @@ def train_grads(TL):
             res[tag + "_masks"] = np.concatenate(masks)
             res[tag + "_mask_sizes"] = np.array([len(m) for m in masks], np.int32)
     return res
+
+
+def train_grads_plain_cases():
+    """train_grads for the two other attention types the reference trains through autograd
+    (train_ssl.py:205-211 builds the student with cfg.TIMESFORMER.ATTENTION_TYPE;
+    models/timesformer.py:116-123): joint space-time and space-only, eval and DropPath 0.5
+    (masks recorded in call order), keys prefixed 'joint_' / 'space_'."""
+    import torch.distributed as dist
+    if not dist.is_initialized():                  # DINOLoss.update_center all-reduces (world 1)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29534")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    TL = _extract(os.path.join(REF, "train_ssl.py"), ["DINOLoss"])["DINOLoss"]
+    out = {}
+    for pre, at in (("joint_", "joint_space_time"), ("space_", "space_only")):
+        for k, v in train_grads(TL, at).items():
+            out[pre + k] = v
+    return out
 
 
 SWIN_SMALL = dict(embed_dim=64, depths=[2, 2, 2, 2], num_heads=[2, 4, 8, 16])
@@ -555,7 +573,7 @@ def views_edge_cases():
 
 
 GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases,
-          "train_step_fp16": train_step_fp16_cases,
+          "train_step_fp16": train_step_fp16_cases, "train_grads_plain": train_grads_plain_cases,
           "views_edge": views_edge_cases}
 
 if __name__ == "__main__":

@@ -23,13 +23,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_ddp_two_ranks_match_single_process(tmp_path):
+@pytest.mark.parametrize("size", ["tiny", "vitb"])
+def test_ddp_two_ranks_match_single_process(tmp_path, size):
+    """tiny: 64-wide depth-2 model (all phases); vitb: ViT-B widths (768, 12 heads, depth 2, 224^2 /
+    96^2 crops of 8 frames) so the per-block gradient buckets run at their real 28 MB size."""
     world, port = 2, _free_port()
     procs, outs = [], []
     for r in range(world):
         out = tmp_path / ("rank%d.json" % r)
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
-                   WORLD_SIZE=str(world), DSVT_TEST_OUT=str(out),
+                   WORLD_SIZE=str(world), DSVT_TEST_OUT=str(out), DSVT_DDP_CFG=size,
                    DSVT_TEST_LOGDIR=str(LOGDIR if os.path.isdir(LOGDIR) else tmp_path))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ddp_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -49,7 +52,7 @@ def test_ddp_two_ranks_match_single_process(tmp_path):
         assert res["world"] == world and res["backend"] == "gloo"
         if r == 0:
             print("ddp rank0:", res)
-            for mode in ("ddp", "overlap", "overlap_1stream"):     # worker's phase-1 wrappings
+            for mode in ("ddp", "overlap", "overlap_1stream", "ddp_accum", "overlap_accum"):   # phase-1 wrappings
                 assert res["worst_grad_" + mode][1] < 1e-3 and res["center_err_" + mode] < 1e-5, mode
 
 

@@ -31,14 +31,15 @@ def gold():
     return dict(np.load("tests/golden/train_grads.npz"))
 
 
-def _student(dtype, drop):
+def _student(dtype, drop, attention_type="divided_space_time"):
     from dsvt.models.timesformer import VisionTransformer
     from dsvt.utils import MultiCropWrapper
     from dsvt.vision_transformer import DINOHead
     bb = VisionTransformer(img_size=64, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
                            qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
-                           drop_path_rate=0.5 if drop else 0.0, num_frames=4, attention_type="divided_space_time")
-    bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(1201, **CFG).items()})
+                           drop_path_rate=0.5 if drop else 0.0, num_frames=4, attention_type=attention_type)
+    bb.load_state_dict({k: torch.from_numpy(v) for k, v in
+                        P.timesformer_state(1201, attention_type=attention_type, **CFG).items()})
     hd = DINOHead(64, 512, hidden_dim=128, bottleneck_dim=64)
     hd.load_state_dict({k: torch.from_numpy(v) for k, v in
                         P.dino_head_state(1202, 64, 512, hidden_dim=128, bottleneck_dim=64).items()})
@@ -48,6 +49,66 @@ def _student(dtype, drop):
     if not drop:
         bb.eval()
     return net
+
+
+@pytest.fixture(scope="module")
+def gold_plain():
+    return dict(np.load("tests/golden/train_grads_plain.npz"))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tag", ["eval", "drop"])
+@pytest.mark.parametrize("attn", ["joint_space_time", "space_only"])
+def test_student_grads_plain_attention(gold_plain, attn, dtype, tag, monkeypatch):
+    """The training path of the two other attention types (train_ssl.py:205-211 trains
+    cfg.TIMESFORMER.ATTENTION_TYPE; models/timesformer.py:116-123): loss, student logits and
+    every student parameter gradient vs the reference's autograd (tests/golden/
+    train_grads_plain.npz), eval and DropPath 0.5 replaying the reference's per-sequence masks
+    (per clip for joint, per (clip, frame) for space-only; attention branch then MLP)."""
+    from dsvt import training
+    from dsvt.loss import DINOLoss
+    pre = "joint_" if attn == "joint_space_time" else "space_"
+    gold = {k[len(pre):]: v for k, v in gold_plain.items() if k.startswith(pre)}
+    if tag == "drop":
+        masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
+        state = {"off": 0, "i": 0}
+
+        def replay(n, p, device):
+            assert n == sizes[state["i"]], (n, sizes[state["i"]])
+            m = masks[state["off"]:state["off"] + n]
+            state["off"] += n
+            state["i"] += 1
+            return torch.from_numpy(m.copy()).to(device)
+        monkeypatch.setattr(training, "_keep_scale", replay)
+    net = _student(dtype, tag == "drop", attn)
+    crops = [torch.from_numpy(P.clip(1210 + i, (2, 3, 4, 64, 64))).cuda() for i in range(2)] + \
+            [torch.from_numpy(P.clip(1220 + i, (2, 3, 4, 32, 32))).cuda() for i in range(2)]
+    s_out = net(crops)
+    t_out = torch.from_numpy(gold[tag + "_teacher"]).cuda()
+    loss_fn = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    loss = loss_fn(s_out, t_out, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert abs(loss.item() - float(gold[tag + "_loss"])) < tol * abs(float(gold[tag + "_loss"]))
+    assert rel(s_out.detach().cpu().numpy(), gold[tag + "_student"]) < tol
+    named = [("bb." + k, p) for k, p in net.backbone.named_parameters()] + \
+            [("hd." + k, p) for k, p in net.head.named_parameters()]
+    checked, worst = 0, 0.0
+    for k, p in named:
+        key = tag + "_" + k
+        if key not in gold:
+            assert p.grad is None or not p.requires_grad, k
+            continue
+        assert p.grad is not None, k
+        err = rel(p.grad.cpu().numpy(), gold[key])
+        worst = max(worst, err)
+        assert err < tol, "%s grad rel err %.3g" % (k, err)
+        checked += 1
+    if tag == "drop":
+        assert state["i"] == len(sizes), "mask draws %d of %d" % (state["i"], len(sizes))
+    print("train grads", attn, tag, dtype, "worst rel err %.3g" % worst)
+    assert checked >= 28
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
