@@ -76,6 +76,7 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
 // host can name the exact kernel instantiation rocprofv3 reports (dsvt/ops.py gemm_kernel_name)
 constexpr int ROWLN_PROBE_TAG = 30 * 32 + 2 * 2 + 1;   // "variant 30": gemm_rowln_kernel (dsvt/ops.py)
 constexpr int WGRAD_PROBE_TAG = 31 * 32 + 1;            // "variant 31": wgrad_kernel
+constexpr int GROUPED_PROBE_TAG = 50 * 32;               // "variant 50": gemm_8ph_kernel<..., SEG = true>
 
 // algorithmic HBM bytes of one GEMM launch: A and W once, the output once (+ the fp32 residual
 // X read for EPI_RESID, + the aux tensor for the training epilogues), the bias
@@ -155,6 +156,49 @@ int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t l
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
                 [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
                 gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
+}
+
+int dsvt_gemm_grouped_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, int64_t ldw, void* out,
+                          int64_t ldo, int64_t N, int64_t K, int nseg, const dsvt_gemm_seg* segs, void* stream) {
+  REQUIRE(nseg >= 1 && nseg <= GemmParams::MAX_SEG && segs, "gemm_grouped: nseg must be 1..%d",
+          GemmParams::MAX_SEG);
+  REQUIRE(epilogue <= 2, "gemm_grouped: epilogue %d not supported", epilogue);
+  int64_t vrows = 0;
+  double flops = 0, bytes = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const dsvt_gemm_seg& q = segs[i];
+    REQUIRE(q.M >= 1 && q.a_row0 >= 0, "gemm_grouped: segment %d: bad rows", i);
+    if (int e = check_gemm(dtype, epilogue, (const char*)A + q.a_row0 * lda * (dtype == DSVT_BF16 ? 2 : 4), lda,
+                           q.W, ldw, q.bias, out, ldo, q.M, N, K))
+      return e;
+    vrows += (q.M + 255) / 256 * 256;
+    flops += 2.0 * q.M * N * K;
+    bytes += gemm_bytes(dtype, epilogue, out_f32, q.M, N, K);
+  }
+  GemmParams p{A, lda, segs[0].W, ldw, segs[0].bias, out, ldo, vrows, N, K, 0, 0, 0,
+               nullptr, nullptr, nullptr, nullptr, 1};
+  p.nseg = nseg;
+  int64_t mt = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const dsvt_gemm_seg& q = segs[i];
+    int64_t rpg = q.rpg, gs = q.gstride, go = q.goff;
+    if (rpg <= 0) { rpg = INT64_MAX; gs = 0; }
+    p.seg[i] = GemmParams::Seg{q.W, q.bias, q.a_row0, q.M, rpg, gs, go, mt};
+    mt += (q.M + 255) / 256;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const bool grouped = dtype == DSVT_BF16 && gemm_8ph_grouped_ok(p, epilogue, out_f32);
+  return probed(DSVT_PROBE_GEMM, flops, s, "dsvt_gemm_grouped_fwd", [&]() -> hipError_t {
+    if (grouped) return launch_gemm_8ph_grouped(p, epilogue, out_f32, s);
+    for (int i = 0; i < nseg; ++i) {          // one plain launch per segment
+      const dsvt_gemm_seg& q = segs[i];
+      GemmParams g{(const char*)A + q.a_row0 * lda * (dtype == DSVT_BF16 ? 2 : 4), lda, q.W, ldw, q.bias, out, ldo,
+                   q.M, N, K, q.rpg, q.gstride, q.goff, nullptr, nullptr, nullptr, nullptr, 1};
+      norm_map(g.rpg, g.gstride, g.goff);
+      if (hipError_t e = launch_gemm(g, dtype, epilogue, out_f32, s)) return e;
+    }
+    return hipSuccess;
+  }, grouped ? GROUPED_PROBE_TAG + dtype * 16 + epilogue * 2 + (out_f32 || epilogue == EPI_RESID) : 0, bytes);
 }
 
 int dsvt_gemm_sk_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, const void* W, int64_t ldw,

@@ -86,9 +86,15 @@ __device__ __forceinline__ void p8_barrier() {
 // phases).  The epilogue is then 32 plain 16-B stores per lane, left in flight under the next
 // tile's first K-tile (vm_wait<8 + 32>): no load -> wait -> store round trips, and the X reads
 // overlap the MFMA loop instead of following it.
-template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false, bool SK = false, bool XS = false>
+// SEG (grouped launch): the virtual m-tiles belong to up to MAX_SEG row segments of one A /
+// one out buffer, each multiplied by its own W (+ bias) and written through its own row map --
+// e.g. the teacher's and the student's calls of one layer as ONE launch (identical shapes,
+// different weights), so their tiles share the rounds instead of each call paying a
+// partly filled last round.  The stagers and the epilogue look the segment up per tile.
+template <int EPI, bool OUT_F32, int ABL = 0, bool NFULL = false, bool SK = false, bool XS = false, bool SEG = false>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   static_assert(!XS || (EPI == EPI_RESID && !SK && ABL == 0), "X stream: residual epilogue only");
+  static_assert(!SEG || (!SK && !XS && ABL == 0), "grouped launch: plain data-parallel kernel only");
   constexpr bool CLAMPED = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32;
   // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores,
   // X-streamed residual -> 32 fp32 fragment stores
@@ -146,6 +152,23 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   const char* A = (const char*)p.A;
   const char* W = (const char*)p.W;
   const int64_t lda_b = p.lda * 2, ldw_b = p.ldw * 2;
+  // segment of the tile whose first virtual row is m0 (SEG); plain launches: one segment = p
+  struct SegV { const char* W; const float* bias; int64_t vrow0, a_row0, M, rpg, gstride, goff; };
+  auto seg_of = [&](int64_t m0) -> SegV {
+    if constexpr (SEG) {
+      const int64_t mt = m0 >> 8;
+      int s = 0;
+#pragma unroll
+      for (int i = 1; i < GemmParams::MAX_SEG; ++i)
+        if (i < p.nseg && mt >= p.seg[i].mtile0) s = i;
+      const GemmParams::Seg& q = p.seg[s];
+      return SegV{(const char*)q.W, q.bias, q.mtile0 * 256, q.a_row0, q.M, q.rpg, q.gstride, q.goff};
+    } else {
+      return SegV{(const char*)p.W, p.bias, 0, 0, p.M, p.rpg, p.gstride, p.goff};
+    }
+  };
+  const char* Wa = W;                   // the W of the tile the AT / BL stager is on (SEG)
+  const char* Wb = W;                   // ... and of the BR / AB stager's tile
 
   // ---- LDS-DMA source offsets (32-bit, checked on the host) of the four half-tiles
   const int srow = tid >> 3;                                   // half-tile row within a 64-row piece
@@ -164,9 +187,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
       n0 = (int64_t)(w / gm) * 256;
     }
   };
-  auto a_off = [&](int64_t gr) -> uint32_t {
-    gr = gr < p.M ? gr : p.M - 1;
-    return (uint32_t)(gr * lda_b) + schunk;
+  auto a_off = [&](const SegV& sv, int64_t gr) -> uint32_t {   // gr: virtual row of the tile
+    gr -= sv.vrow0;
+    gr = gr < sv.M ? gr : sv.M - 1;
+    return (uint32_t)((sv.a_row0 + gr) * lda_b) + schunk;
   };
   auto b_off = [&](int64_t gr) -> uint32_t {
     gr = gr < p.N ? gr : p.N - 1;
@@ -176,18 +200,22 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   auto set_atbl = [&](int tl) {
     int64_t m0, n0;
     tile_mn(tl, m0, n0);
+    const SegV sv = seg_of(m0);
+    if constexpr (SEG) Wa = sv.W;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      oAT[q] = a_off(m0 + q * 128 + srow);
+      oAT[q] = a_off(sv, m0 + q * 128 + srow);
       oBL[q] = b_off(n0 + (2 * q + (srow >> 5)) * 64 + (srow & 31));
     }
   };
   auto set_brab = [&](int tl) {
     int64_t m0, n0;
     tile_mn(tl, m0, n0);
+    const SegV sv = seg_of(m0);
+    if constexpr (SEG) Wb = sv.W;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      oAB[q] = a_off(m0 + q * 128 + 64 + srow);
+      oAB[q] = a_off(sv, m0 + q * 128 + 64 + srow);
       oBR[q] = b_off(n0 + (2 * q + (srow >> 5)) * 64 + 32 + (srow & 31));
     }
   };
@@ -263,8 +291,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   set_atbl(0);
   set_brab(0);
   P8_STAGE(H_AT, oAT, A, 0, k0 * P8_ROWB);
-  P8_STAGE(H_BL, oBL, W, 0, k0 * P8_ROWB);
-  P8_STAGE(H_BR, oBR, W, 0, k0 * P8_ROWB);
+  P8_STAGE(H_BL, oBL, Wa, 0, k0 * P8_ROWB);
+  P8_STAGE(H_BR, oBR, Wb, 0, k0 * P8_ROWB);
   P8_STAGE(H_AB, oAB, A, 0, k0 * P8_ROWB);
   tl1 = 0; k1 = k0;
   adv(tl1, k1);
@@ -273,7 +301,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   if (J > 1) {
     set_atbl(tl1);
     P8_STAGE(H_AT, oAT, A, P8_BUF, k1 * P8_ROWB);
-    P8_STAGE(H_BL, oBL, W, P8_BUF, k1 * P8_ROWB);
+    P8_STAGE(H_BL, oBL, Wa, P8_BUF, k1 * P8_ROWB);
     vm_wait<8>();                       // AT(0), BL(0) retired
   } else {
     vm_wait<0>();
@@ -289,17 +317,18 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   auto init_acc = [&](int tl, bool with_bias) {   // SK: only a tile's k = 0 segment carries the bias
     float4 b4[4];
     // (EPI_RESID with DropPath row scales: the epilogue adds s[m] * bias instead)
-    if (BIAS_IN_ACC && p.bias && with_bias && !(EPI == EPI_RESID && p.row_scale)) {
-      int64_t m0, n0;
-      tile_mn(tl, m0, n0);
-      const int64_t cbase = n0 + wc * 64;
+    int64_t bm0 = 0, bn0 = 0;
+    tile_mn(tl, bm0, bn0);
+    const float* tbias = seg_of(bm0).bias;
+    if (BIAS_IN_ACC && tbias && with_bias && !(EPI == EPI_RESID && p.row_scale)) {
+      const int64_t cbase = bn0 + wc * 64;
       if (cbase + 64 <= p.N) {
-        bias_frag4(p.bias, cbase, g, b4);
+        bias_frag4(tbias, cbase, g, b4);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int64_t n = cbase + j * 16 + 4 * g;
-          b4[j] = n < p.N ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+          b4[j] = n < p.N ? *reinterpret_cast<const float4*>(tbias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
     } else {
@@ -430,7 +459,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     P8_RD(fbl, H_BL, rdB, cb, 2);
     __builtin_amdgcn_sched_barrier(0);
     P8_RD(fa, H_AT, rdA, cb, 4);
-    if (v1) P8_STAGE(H_BR, oBR, W, sb1, kb1);
+    if (v1) P8_STAGE(H_BR, oBR, Wb, sb1, kb1);
     P8_WAIT(v1, 0);
     XS_READ(0);
     P8_COMPUTE(P8_MFMA(0, 0, fbl), 0);
@@ -447,7 +476,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     XS_READ(2);
     P8_COMPUTE(P8_MFMA(4, 2, fbr), 2);
     // phase 3: no reads, stage BL(j+2), quadrant (AB, BL)
-    if (v2) P8_STAGE(H_BL, oBL, W, sb2, kb2);
+    if (v2) P8_STAGE(H_BL, oBL, Wa, sb2, kb2);
     P8_WAIT(v2, 3);
     XS_READ(3);
     P8_COMPUTE(P8_MFMA(4, 0, fbl), 3);
@@ -456,6 +485,13 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     if (++kc == seg_k1(tlc)) {            // tile (or SK tail segment) done: register epilogue
       int64_t m0, n0;
       tile_mn(tlc, m0, n0);
+      // SEG: the tile's segment as a plain problem (its M, bias, row map) for the epilogue
+      GemmParams pe = p;
+      if constexpr (SEG) {
+        const SegV sv = seg_of(m0);
+        m0 -= sv.vrow0;
+        pe.M = sv.M; pe.bias = sv.bias; pe.rpg = sv.rpg; pe.gstride = sv.gstride; pe.goff = sv.goff;
+      }
       const int64_t rbase = m0 + wr * 128, cbase = n0 + wc * 64;
       mfma_result_fence();
       bool whole = true;
@@ -490,10 +526,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(acc[i][jj]));
       } else {
-        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), EPI == EPI_GELU_SAVE, NFULL>(p, acc, rbase, cbase,
+        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), EPI == EPI_GELU_SAVE, NFULL>(pe, acc, rbase, cbase,
                                                                                           r16, g);
       }
-      post = whole && S_EPI > 0 && (CLAMPED || (rbase + 128 <= p.M && cbase + 64 <= p.N));
+      post = whole && S_EPI > 0 && (CLAMPED || (rbase + 128 <= pe.M && cbase + 64 <= p.N));
       kc = 0;
       ++tlc;
       __builtin_amdgcn_sched_barrier(0);   // keep the next tile's bias loads after the stores
@@ -576,6 +612,45 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
     default: return hipErrorInvalidValue;
   }
 #undef DSVT_K
+  return hipGetLastError();
+}
+
+// ---- grouped launch: segments of rows with their own W / bias / row map (dsvt_gemm_grouped_fwd)
+bool gemm_8ph_grouped_ok(const GemmParams& p, int epi, int out_f32) {
+  if (p.nseg < 1 || p.nseg > GemmParams::MAX_SEG || !gemm_8ph_ok(p, epi) || p.row_scale || p.resid) return false;
+  if (!(epi == EPI_BIAS || epi == EPI_GELU || epi == EPI_RESID)) return false;
+  if (epi != EPI_RESID && out_f32) return false;
+  int64_t mt = 0;
+  for (int i = 0; i < p.nseg; ++i) {
+    const GemmParams::Seg& q = p.seg[i];
+    if (q.mtile0 != mt || q.M < 1 || !q.W) return false;
+    if ((q.a_row0 + q.M - 1) * p.lda * 2 + p.K * 2 > (int64_t)UINT32_MAX) return false;
+    if (((const char*)q.W - (const char*)nullptr) % 16) return false;
+    mt += (q.M + 255) / 256;
+  }
+  return mt * 256 == p.M;
+}
+
+hipError_t launch_gemm_8ph_grouped(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
+  if (!gemm_8ph_grouped_ok(p, epi, out_f32)) return hipErrorInvalidValue;
+  const int64_t tiles = (p.M / 256) * ((p.N + 255) / 256);
+  int64_t G = 256;
+  const int64_t per_x = (tiles + 7) / 8;
+  if (per_x * 8 < G) G = per_x * 8;
+  const bool nfull = p.N % 256 == 0;
+  dim3 grid((unsigned)G), block(512);
+  switch (epi) {
+    case EPI_BIAS:
+      if (nfull) gemm_8ph_kernel<EPI_BIAS, false, 0, true, false, false, true><<<grid, block, 0, s>>>(p);
+      else gemm_8ph_kernel<EPI_BIAS, false, 0, false, false, false, true><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_GELU:
+      if (nfull) gemm_8ph_kernel<EPI_GELU, false, 0, true, false, false, true><<<grid, block, 0, s>>>(p);
+      else gemm_8ph_kernel<EPI_GELU, false, 0, false, false, false, true><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_RESID: gemm_8ph_kernel<EPI_RESID, true, 0, false, false, false, true><<<grid, block, 0, s>>>(p); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

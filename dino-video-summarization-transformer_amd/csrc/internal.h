@@ -32,6 +32,18 @@ struct GemmParams {
   // counter per output tile (zero on entry, left zero on exit)
   float* sk_part = nullptr;
   int* sk_cnt = nullptr;
+  // grouped launch (dsvt_gemm_grouped_fwd, 256x256 kernel): nseg > 0 segments of rows, each with
+  // its own W / bias / output row map; M is then the sum of the segments' 256-row-padded extents
+  // (segment s owns the virtual m-tiles [seg[s].mtile0, seg[s + 1].mtile0))
+  struct Seg {
+    const void* W; const float* bias;
+    int64_t a_row0, M;           // A rows [a_row0, a_row0 + M)
+    int64_t rpg, gstride, goff;  // out row of segment row m (map_row)
+    int64_t mtile0;
+  };
+  static constexpr int MAX_SEG = 4;
+  int nseg = 0;
+  Seg seg[MAX_SEG] = {};
 };
 
 // the DropPath scale of GEMM row m (1 when none)
@@ -58,6 +70,9 @@ bool gemm_8ph_ok(const GemmParams& p, int epi);
 // the 256x256 kernel with the residual tile streamed into the accumulators (variant 30)
 bool gemm_8ph_xs_ok(const GemmParams& p, int epi);
 hipError_t launch_gemm_8ph_xs(const GemmParams& p, int epi, hipStream_t s);
+// grouped (segmented) launch of the 256x256 kernel: bias / GELU / residual epilogues
+bool gemm_8ph_grouped_ok(const GemmParams& p, int epi, int out_f32);
+hipError_t launch_gemm_8ph_grouped(const GemmParams& p, int epi, int out_f32, hipStream_t s);
 // stream-K 256x256 GEMM (variant 40): workspace = [SK_MAX_TILES int32 counters][2 x 256 slots of
 // 256 x 256 fp32 partial sums]
 constexpr int64_t SK_MAX_TILES = 65536;

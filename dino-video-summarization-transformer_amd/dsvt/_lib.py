@@ -20,6 +20,12 @@ WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_GEMM_SK = 10, 11, 12, 13
 
 _i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
+
+class GemmSeg(ctypes.Structure):
+    """dsvt_gemm_seg (include/dsvt.h): one row segment of dsvt_gemm_grouped_fwd."""
+    _fields_ = [("W", _p), ("bias", _p), ("a_row0", _i64), ("M", _i64), ("rpg", _i64), ("gstride", _i64),
+                ("goff", _i64)]
+
 # name -> (restype, argtypes); must mirror include/dsvt.h exactly (tests/test_capi_symbols.py)
 SIGNATURES = {
     "dsvt_version": (_i32, []),
@@ -29,6 +35,8 @@ SIGNATURES = {
                              _i64, _i64, _i64, _p]),
     "dsvt_gemm_sk_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
                                 _i64, _i64, _i64, _p, _i64, _p]),
+    "dsvt_gemm_grouped_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _i64, _p, _i64, _i64, _i64, _i32,
+                                     ctypes.POINTER(GemmSeg), _p]),
     "dsvt_gemm_resid_fwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "dsvt_gemm_resid_ln_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _f32,
                                       _p, _i32, _i64, _p]),

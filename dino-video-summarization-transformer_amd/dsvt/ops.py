@@ -81,6 +81,25 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     return out
 
 
+def gemm_grouped(a, segs, out, epilogue=_lib.EPI_BIAS, out_f32=False):
+    """One launch over row segments of `a` with their own weights: segs = [(w, bias, a_row0, M,
+    rowmap or None, out_row0)], out row of segment row m = out_row0 + map(m) (dsvt_gemm_grouped_fwd)."""
+    mode = a.dtype
+    _check(a, mode, "A")
+    arr = (_lib.GemmSeg * len(segs))()
+    K = a.shape[-1]
+    N = segs[0][0].shape[0]
+    for i, (w, bias, a_row0, M, rowmap, out_row0) in enumerate(segs):
+        _check(w, mode, "W")
+        if w.shape[0] != N or w.shape[1] != K:
+            raise _lib.DsvtError("gemm_grouped: every segment's W must be [%d, %d]" % (N, K))
+        rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
+        arr[i] = _lib.GemmSeg(w.data_ptr(), _ptr(bias), int(a_row0), int(M), int(rpg), int(gs), int(go + out_row0))
+    call("dsvt_gemm_grouped_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, K, _ptr(out), out.shape[-1], N, K,
+         len(segs), arr, _stream())
+    return out
+
+
 def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None, bias_row_scale=None):
     """x_out[row(m)] = x_in[row(m)] + a[m] . w^T + bias (fp32 token rows; out of place).
     bias_row_scale (fp32 [M], identity row map only): the bias term of row m is scaled by it

@@ -59,9 +59,26 @@ def prepare_weights(module):
             fn()
 
 
+def _groupable(student, teacher, images):
+    import os
+    if os.environ.get("DSVT_GROUPED", "1") == "0" or not images[0].is_cuda:
+        return False
+    if not all(isinstance(m, MultiCropWrapper) and not m.vary_fr for m in (student, teacher)):
+        return False
+    if torch.is_grad_enabled() and any(p.requires_grad for m in (student, teacher) for p in m.parameters()):
+        return False
+    from .grouped import eligible
+    return eligible([teacher.backbone, student.backbone])
+
+
 def dino_forward(student, teacher, images, n_global=2, concurrent=True):
     """train_ssl.py:523-527: teacher on the `n_global` global views, student on all views.
-    The two networks are independent, so their backbone calls run concurrently."""
+    dsvt divided-attention backbones in inference: the three backbone calls run GROUPED, every
+    layer's Linear of all calls as one launch (dsvt.grouped; DSVT_GROUPED=0 turns it off).
+    Otherwise the two networks are independent and their calls run on concurrent streams."""
+    if _groupable(student, teacher, images):
+        from .grouped import dino_forward_grouped
+        return dino_forward_grouped(student, teacher, images, n_global)
     if not concurrent:
         return student(images), teacher(images[:n_global])
     for net in (student, teacher):

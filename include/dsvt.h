@@ -84,6 +84,26 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
 int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
                   int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N,
                   int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void *stream);
+/* One row segment of a grouped GEMM: rows [a_row0, a_row0 + M) of A times ITS W [N, K] (+ bias)
+ * into out rows goff + (m / rpg) * gstride + m % rpg (m = 0 .. M-1 within the segment; rpg <= 0:
+ * out row goff + m). */
+typedef struct {
+  const void *W;
+  const float *bias;
+  int64_t a_row0, M;
+  int64_t rpg, gstride, goff;
+} dsvt_gemm_seg;
+
+/* Grouped GEMM: up to 4 row segments of one A and one out buffer, each with its own weights and
+ * output row map, in ONE launch of the 256 x 256 kernel (bf16; EPI_BIAS / EPI_BIAS_GELU with a
+ * bf16 output, EPI_BIAS_RESID in place).  The same Linear of the teacher's and the student's
+ * backbone calls of one DINO step (models/timesformer.py:63-64, 71, 83, 133, 41-52 under
+ * train_ssl.py:523-527; identical shapes, different weights) then share one set of tile
+ * rounds.  `segs` is a HOST array.  Other dtypes / shapes run one dsvt_gemm_fwd per segment
+ * (same results). */
+int dsvt_gemm_grouped_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, int64_t ldw, void *out,
+                          int64_t ldo, int64_t N, int64_t K, int nseg, const dsvt_gemm_seg *segs, void *stream);
+
 /* dsvt_gemm_fwd with a caller-owned scratch: bf16 projections whose 256 x 256 tiles leave a
  * partly filled last round of workgroups run stream-K -- the tiles x K-steps are split evenly
  * over the grid, partial tiles meet in the workspace and the last workgroup to finish one runs

@@ -59,6 +59,16 @@ def test_validation_rejects_before_launch(L):
     # K not a multiple of 64 (bf16)
     rc = L.dsvt_gemm_fwd(_lib.BF16, 0, 0, fake, 100, fake, 100, None, fake, 64, 16, 64, 100, 0, 0, 0, None)
     assert rc == 1 and b"multiple of 64" in L.dsvt_last_error()
+    # grouped GEMM: segment count, per-segment shape checks
+    segs = (_lib.GemmSeg * 2)(_lib.GemmSeg(256, None, 0, 100, 0, 0, 0), _lib.GemmSeg(256, None, 100, 0, 0, 0, 0))
+    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 768, 768, fake, 768, 768, 768, 0, segs, None)
+    assert rc == 1 and b"nseg" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 768, 768, fake, 768, 768, 768, 5, segs, None)
+    assert rc == 1 and b"nseg" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 768, 768, fake, 768, 768, 768, 2, segs, None)
+    assert rc == 1 and b"segment 1" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 100, 100, fake, 768, 768, 100, 1, segs, None)
+    assert rc == 1 and b"multiple of 64" in L.dsvt_last_error()
     # head_dim must be 64
     rc = L.dsvt_attn_temporal_fwd(_lib.BF16, fake, fake, 4, 8, 3, 32, ctypes.c_float(0.1), None)
     assert rc == 1 and b"head_dim" in L.dsvt_last_error()

@@ -421,3 +421,47 @@ def test_joint16_config4_full_size():
     assert eb < BF16_TOL
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
+
+
+@pytest.mark.parametrize("variant", [20, 0])
+def test_grouped_forward_bitwise(variant, monkeypatch):
+    """dsvt.grouped: the three backbone calls of a DINO step (teacher on 2 global crops, student on
+    2 global + 2 local) as one lockstep forward with every Linear a grouped launch
+    (dsvt_gemm_grouped_fwd, a row segment per call with its own weights) against the same calls
+    run separately (DSVT_GROUPED=0).  With the separate calls' GEMMs on the same 256x256 kernel
+    (variant 20) the student / teacher logits are BITWISE equal; with the automatic kernel choice
+    (small separate calls take the 128x128 kernel) within BF16_TOL.  Also fp32 parity mode (the
+    grouped op's per-segment fallback) within 1e-5."""
+    from dsvt import _lib
+    from dsvt.utils import MultiCropWrapper, dino_forward
+    from dsvt.vision_transformer import DINOHead
+    cfg = dict(embed_dim=768, num_heads=12, depth=2, img_size=64, num_frames=8)
+
+    def net(seed, dtype):
+        m = tsf(P.timesformer_state(seed, **cfg), dtype, **cfg)
+        hd = DINOHead(768, 4096)
+        hd.load_state_dict({k: torch.from_numpy(v) for k, v in P.dino_head_state(seed + 1, 768, 4096).items()})
+        hd = hd.cuda()
+        hd.dsvt_dtype = dtype
+        return MultiCropWrapper(m, hd)
+    crops = [cu(P.clip(1601 + i, (3, 3, 8, 64, 64))) for i in range(2)] + \
+            [cu(P.clip(1611 + i, (3, 3, 8, 32, 32))) for i in range(2)]
+    for dtype in (torch.bfloat16, torch.float32):
+        student, teacher = net(1701, dtype), net(1801, dtype)
+        outs = {}
+        _lib.call("dsvt_set_gemm_variant", variant)
+        try:
+            for grouped in ("1", "0"):
+                monkeypatch.setenv("DSVT_GROUPED", grouped)
+                with torch.no_grad():
+                    s, t = dino_forward(student, teacher, crops, concurrent=False)
+                torch.cuda.synchronize()
+                outs[grouped] = (s.clone(), t.clone())
+        finally:
+            _lib.call("dsvt_set_gemm_variant", 0)
+        for a, b in zip(outs["1"], outs["0"]):
+            assert torch.isfinite(a).all()
+            if dtype == torch.bfloat16 and variant == 20:
+                assert torch.equal(a, b), "grouped forward differs from the separate calls"
+            else:
+                assert rel(a.cpu(), b.cpu()) < (BF16_TOL if dtype == torch.bfloat16 else 1e-5)
