@@ -422,6 +422,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
+    ap.add_argument("--no-grouped", action="store_true",
+                    help="run the teacher / student backbone calls separately (DSVT_GROUPED=0; A/B)")
     ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-grad-overlap", dest="grad_overlap", action="store_false",
@@ -432,6 +434,8 @@ def main():
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: allow N ranks on fewer GPUs (rank r uses GPU r %% count; needs --backend gloo)")
     args = ap.parse_args()
+    if args.no_grouped:
+        os.environ["DSVT_GROUPED"] = "0"
 
     from dsvt import dist as ddist
 
@@ -597,6 +601,11 @@ def main():
                                     "/ measured time",
                         "all_gemm_tflops": round(float(np.sum(work)) / (all_ms * 1e-3) / 1e12, 1)}
 
+    from dsvt.utils import _groupable
+    with torch.no_grad():
+        grouped = _groupable(student, teacher, crops)
+    grouped_desc = ("grouped: the teacher / student backbone calls advance in lockstep over one token buffer, every "
+                    "Linear of a layer ONE launch over all calls (dsvt_gemm_grouped_fwd), one stream")
     value = world * args.clips * args.steps / elapsed
     step_ms = elapsed / args.steps * 1e3
     folded = student.backbone.fold_temporal_fc
@@ -613,7 +622,8 @@ def main():
                       "parallelism": "dp%d" % world,
                       "weights": "random init (torch seed 0)",
                       "launch": "eager" if graph is None else "hip_graph (forward+loss captured; center all-reduce eager)",
-                      "streams": "serial" if args.serial else "3 backbone calls on concurrent HIP streams"},
+                      "streams": grouped_desc if grouped else
+                      ("serial" if args.serial else "3 backbone calls on concurrent HIP streams")},
            "step_roofline": {"achieved": round(step_tflops / world, 1), "peak": PEAK_TFLOPS[args.dtype],
                              "unit": "TFLOP/s per GPU", "flops": "executed",
                              "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4),

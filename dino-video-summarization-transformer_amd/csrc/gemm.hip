@@ -474,7 +474,7 @@ static bool sk_auto(int epi) {
   return mode >= 2 || (mode == 1 && epi != EPI_RESID);
 }
 
-// the residual GEMMs' X stream (variant 30) in the auto choice: DSVT_RESID_XS = 1 on, 0 off
+// the residual GEMMs' X stream (variant 33) in the auto choice: DSVT_RESID_XS = 1 on, 0 off
 static bool xs_auto() {
   static const int mode = [] {
     const char* e = getenv("DSVT_RESID_XS");
@@ -510,7 +510,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (gv >= 20 && gv <= 29) return gemm_8ph_ok(p, epi) ? gv : 1;
-  if (gv == 30) return gemm_8ph_xs_ok(p, epi) ? 30 : gemm_8ph_ok(p, epi) ? 20 : 1;
+  if (gv == 33) return gemm_8ph_xs_ok(p, epi) ? 33 : gemm_8ph_ok(p, epi) ? 20 : 1;
   if (gv == 2) return (gemm_pipe_ok(p) && epi != EPI_PATCH) ? 2 : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
     if (gv == 1 || gv == 9 || gv == 10) return gv;
@@ -531,7 +531,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // Below ~half a round of 256x256 tiles (config 4's single 2-clip call: 75 tiles) the 128x128
   // kernel's 4x more tiles win even with other streams beside it (DSVT_8PH_MIN_TILES).
   if (epi == EPI_RESID) {
-    if (r8 && big8 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return xs_auto() && gemm_8ph_xs_ok(p, epi) ? 30 : 20;
+    if (r8 && big8 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return xs_auto() && gemm_8ph_xs_ok(p, epi) ? 33 : 20;
     return 1;
   }
   // N = 768 bias-only (the split residual path's proj / temporal fc, the backward's dX GEMMs):

@@ -654,7 +654,7 @@ hipError_t launch_gemm_8ph_grouped(const GemmParams& p, int epi, int out_f32, hi
   return hipGetLastError();
 }
 
-// ---- X-streamed residual GEMM (variant 30): EPI_RESID, whole 256-column tiles, K-window of 8
+// ---- X-streamed residual GEMM (variant 33): EPI_RESID, whole 256-column tiles, K-window of 8
 // K-tiles after at least one more (nk >= 10), no DropPath row scales
 bool gemm_8ph_xs_ok(const GemmParams& p, int epi) {
   return epi == EPI_RESID && gemm_8ph_ok(p, epi) && p.N % 256 == 0 && p.K / 64 >= 10 && !p.row_scale;

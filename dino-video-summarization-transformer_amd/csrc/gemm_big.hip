@@ -474,7 +474,7 @@ hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f3
     case 27: return launch_gemm_8ph(p, epi, out_f32, s, 18);
     case 28: return launch_gemm_8ph(p, epi, out_f32, s, 32);
     case 29: return launch_gemm_8ph(p, epi, out_f32, s, 64);
-    case 30: return launch_gemm_8ph_xs(p, epi, s);
+    case 33: return launch_gemm_8ph_xs(p, epi, s);
     default: break;
   }
   // ablation builds (EPI_BIAS, bf16 out only) of variant 4: 14 no-MFMA, 24 no-load, 34 no-epilogue

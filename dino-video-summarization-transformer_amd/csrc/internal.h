@@ -67,7 +67,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // 
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
 bool gemm_8ph_ok(const GemmParams& p, int epi);
-// the 256x256 kernel with the residual tile streamed into the accumulators (variant 30)
+// the 256x256 kernel with the residual tile streamed into the accumulators (variant 33)
 bool gemm_8ph_xs_ok(const GemmParams& p, int epi);
 hipError_t launch_gemm_8ph_xs(const GemmParams& p, int epi, hipStream_t s);
 // grouped (segmented) launch of the 256x256 kernel: bias / GELU / residual epilogues

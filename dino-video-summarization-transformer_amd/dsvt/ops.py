@@ -515,8 +515,10 @@ def gemm_kernel_name(tag):
     persist = {9: "256, 128, 2, 2, 3, %d, %s, false", 10: "256, 128, 2, 2, 3, %d, %s, true"}
     if variant in persist:
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
-    if variant == 20:
+    if variant in (20, 50):       # 50: the grouped (segmented) instantiations, same prefix
         return "void dsvt::gemm_8ph_kernel<%d, %s, 0, " % (epi, f32)
+    if variant == 33:
+        return "void dsvt::gemm_8ph_kernel<2, true, 0, false, false, true"
     if variant == 30:
         return "void dsvt::gemm_rowln_kernel<"
     if variant == 31:
