@@ -194,7 +194,7 @@ int dsvt_gemm_grouped_fwd(int dtype, int epilogue, int out_f32, const void* A, i
       const dsvt_gemm_seg& q = segs[i];
       GemmParams g{(const char*)A + q.a_row0 * lda * (dtype == DSVT_BF16 ? 2 : 4), lda, q.W, ldw, q.bias, out, ldo,
                    q.M, N, K, q.rpg, q.gstride, q.goff, nullptr, nullptr, nullptr, nullptr, 1};
-      norm_map(g.rpg, g.gstride, g.goff);
+      if (g.rpg <= 0) { g.rpg = INT64_MAX; g.gstride = 0; }   // identity map, keeping the segment's out row offset
       if (hipError_t e = launch_gemm(g, dtype, epilogue, out_f32, s)) return e;
     }
     return hipSuccess;

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
       const int fi = (PH < 2 ? 4 : 0) + (kx >> 1), fj = ((PH == 0 || PH == 3) ? 2 : 0) + (kx & 1);
       int64_t m = xrow0 + fi * 16 + r16;
       m = m < p.M ? m : p.M - 1;        // rows past M: row M - 1's X (never stored)
-      const int64_t orow = p.rpg >= p.M ? m : map_row(m, p.rpg, p.gstride, p.goff);
+      const int64_t orow = (p.rpg >= p.M && p.goff == 0) ? m : map_row(m, p.rpg, p.gstride, p.goff);
       const float* src = resid_src(p) + orow * p.ldo + xcol0 + fj * 16 + 4 * g;
       __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(xslots + PH * 1024), 16, 0, 0);
     }
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
       }
       if (!whole) {
       } else if constexpr (XS) {          // X already in the accumulators: stores only
-        const bool ident = p.rpg >= p.M;
+        const bool ident = p.rpg >= p.M && p.goff == 0;
         float* const out = (float*)p.out;
         if (rbase + 128 <= p.M) {
 #pragma unroll

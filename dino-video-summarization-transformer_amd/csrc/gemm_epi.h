@@ -83,7 +83,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
     // (Per-lane bounds branches around the stores make the compiler drain vmcnt every time:
     // the GELU'-epilogue dX GEMM ran at 412 TF/s with them.)
     if (cbase + NJ * 16 <= p.N) {
-      const bool ident_t = p.rpg >= p.M;
+      const bool ident_t = p.rpg >= p.M && p.goff == 0;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         int64_t m = rbase + i * 16 + r16;
@@ -146,7 +146,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
     }
     return;
   }
-  const bool ident = p.rpg >= p.M;   // wave-uniform: no per-lane row-map division
+  const bool ident = p.rpg >= p.M && p.goff == 0;   // wave-uniform: no per-lane row-map division
   // full wave tile (uniform): branch-free bias / GELU / 16-B stores, so the compiler's vmcnt
   // waits stay exact (a per-lane bounds branch around each store makes it drain every time)
   constexpr bool CLAMP = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0;

@@ -580,7 +580,7 @@ def _plain_backward(model, st, dfeat, G, ready=None):
         if ready is not None:
             ready(bi)
     # ---- patch embedding + token embeddings
-    R = nb * Np
+    R = nb * (L - 1)                     # patch rows: Np per frame sequence (space-only), Np * T per clip (joint)
     patch_map = (Np, L, 1) if space else (Np * T, L, 1)
     dP = torch.empty(R, C, device=dev, dtype=mode)
     ops.cast_rows(dX, dP, R, rowmap=patch_map)
