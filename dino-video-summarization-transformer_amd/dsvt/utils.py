@@ -61,7 +61,7 @@ def prepare_weights(module):
 
 def _groupable(student, teacher, images):
     import os
-    if os.environ.get("DSVT_GROUPED", "1") == "0" or not images[0].is_cuda:
+    if os.environ.get("DSVT_GROUPED", "0") != "1" or not images[0].is_cuda:
         return False
     if not all(isinstance(m, MultiCropWrapper) and not m.vary_fr for m in (student, teacher)):
         return False
@@ -73,9 +73,11 @@ def _groupable(student, teacher, images):
 
 def dino_forward(student, teacher, images, n_global=2, concurrent=True):
     """train_ssl.py:523-527: teacher on the `n_global` global views, student on all views.
-    dsvt divided-attention backbones in inference: the three backbone calls run GROUPED, every
-    layer's Linear of all calls as one launch (dsvt.grouped; DSVT_GROUPED=0 turns it off).
-    Otherwise the two networks are independent and their calls run on concurrent streams."""
+    The two networks are independent and their backbone calls run on concurrent streams.
+    DSVT_GROUPED=1 (opt-in) runs dsvt divided-attention backbones in inference GROUPED instead,
+    every layer's Linear of all calls as one launch (dsvt.grouped): bitwise the same features,
+    measured slower (354 vs 370 clips/s on the bench line, same box: one stream loses the overlap
+    of the attention / LayerNorm kernels with the other calls' GEMMs)."""
     if _groupable(student, teacher, images):
         from .grouped import dino_forward_grouped
         return dino_forward_grouped(student, teacher, images, n_global)

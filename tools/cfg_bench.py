@@ -1,0 +1,62 @@
+"""One BASELINE config's forward alone, for rocprofv3 / A-B runs: c2bb (the config-2 ViT-B/16
+divided backbone, 16 clips 8x224^2), c4 (joint space-time ViT-B/16, 2 clips 16x224^2) or c5
+(Video Swin-T, 8 clips 8x224^2); bf16, random init, synthetic input.
+
+usage: python tools/cfg_bench.py c4 [--reps 5] [--warm 2] [--streams auto|1|2|3]"""
+import argparse
+import os
+import sys
+import time
+from functools import partial
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dino-video-summarization-transformer_amd"))
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+from bench import PEAK_TFLOPS, joint_flops, swin_t_flops, vit_fwd_flops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cfg", choices=["c2bb", "c4", "c5"])
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--warm", type=int, default=2)
+    ap.add_argument("--streams", default=None)
+    args = ap.parse_args()
+    from dsvt.models import SwinTransformer3D
+    from dsvt.models.timesformer import VisionTransformer
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    if args.cfg == "c5":
+        m = SwinTransformer3D().to(dev).eval()
+        x = torch.randn(8, 3, 8, 224, 224, device=dev)
+        n, gf = 8, swin_t_flops() / 1e9
+    else:
+        T, attn = (8, "divided_space_time") if args.cfg == "c2bb" else (16, "joint_space_time")
+        m = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
+                              norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=T,
+                              attention_type=attn).to(dev).eval()
+        n = 16 if args.cfg == "c2bb" else 2
+        x = torch.randn(n, 3, T, 224, 224, device=dev)
+        gf = (vit_fwd_flops(8, 224, folded=True) if args.cfg == "c2bb" else joint_flops()) / 1e9
+        if args.streams is not None:
+            m.dsvt_streams = args.streams if args.streams == "auto" else int(args.streams)
+    m.dsvt_dtype = torch.bfloat16
+    with torch.no_grad():
+        for _ in range(args.warm):
+            m(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            m(x)
+        torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / args.reps
+    print("%s: %.2f clips/s, %.3f ms per call, %.1f TFLOP/s executed (%.1f %% of the bf16 peak)"
+          % (args.cfg, n / t, t * 1e3, n * gf / t / 1e3, 100 * n * gf / t / 1e3 / PEAK_TFLOPS["bf16"]))
+
+
+if __name__ == "__main__":
+    main()
