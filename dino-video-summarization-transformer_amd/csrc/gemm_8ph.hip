@@ -526,7 +526,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(acc[i][jj]));
       } else {
-        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), EPI == EPI_GELU_SAVE, NFULL>(pe, acc, rbase, cbase,
+        epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), EPI == EPI_GELU_SAVE, NFULL, true>(pe, acc, rbase, cbase,
                                                                                           r16, g);
       }
       post = whole && S_EPI > 0 && (CLAMPED || (rbase + 128 <= pe.M && cbase + 64 <= p.N));

@@ -43,7 +43,7 @@ __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int 
 // (the A loads of those rows are clamped to it), so the extra stores rewrite identical bytes,
 // and no per-lane bounds branch around the stores (which makes the compiler drain vmcnt)
 template <int MI, int NJ, int EPI, bool OUT_F32, int NT = 0, bool NOSTORE = false, bool BIAS_IN_ACC = false,
-          bool NOFAST = false, bool ROWSCALE = false, bool NFULL = false>
+          bool NOFAST = false, bool ROWSCALE = false, bool NFULL = false, bool PAIR_AUX = false>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
@@ -76,6 +76,80 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
     }
   }
   // training epilogues (bf16 aux operand): GELU with the pre-activation saved, and GELU backward
+  // PAIR_AUX (the 256x256 kernel; the persistent 256x128 one spills with it), bf16 output, full
+  // wave tile in N: 16-byte PAIR accesses (pack_pair_bf16's layout: lane group
+  // g owns 8 contiguous columns of each 32-column span) -- one 16-B load / store per fragment pair
+  // instead of two 8-B ones, each wave instruction covering 16 rows x 64 contiguous bytes.
+  // DGELU: the pre-activation pairs of the next PW = 4 rows stay in flight (a rolling window, 8 x
+  // 16 B per lane; all 8 rows up front spill the 256x256 kernel), so the HBM round trip is paid
+  // about twice per tile instead of once per row.
+  if constexpr (PAIR_AUX && (EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) && !OUT_F32 && NJ % 2 == 0) {
+    if (cbase + NJ * 16 <= p.N) {
+      const bool ident_t = p.rpg >= p.M && p.goff == 0;
+      int64_t orow[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        int64_t m = rbase + i * 16 + r16;
+        m = m < p.M ? m : p.M - 1;
+        orow[i] = ident_t ? m : map_row(m, p.rpg, p.gstride, p.goff);
+      }
+      const int po = pair_off(g);
+      constexpr int PW = MI < 4 ? MI : 4;          // DGELU: rows of pre-activations in flight
+      uint4 pre[EPI == EPI_DGELU ? PW : 1][NJ / 2];
+      auto load_pre = [&](int i) {
+#pragma unroll
+        for (int jp = 0; jp < NJ / 2; ++jp)
+          pre[i % PW][jp] = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + orow[i] * p.ld_aux + cbase + jp * 32 + po);
+      };
+      if constexpr (EPI == EPI_DGELU) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) load_pre(i);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        float rs = 1.0f;
+        if constexpr (RS) rs = scaled ? row_scale_of(p, rbase + i * 16 + r16 < p.M ? rbase + i * 16 + r16 : p.M - 1) : 1.0f;
+#pragma unroll
+        for (int jp = 0; jp < NJ / 2; ++jp) {
+          const int j = 2 * jp;
+          bf16_t* const span = (bf16_t*)p.out + orow[i] * p.ldo + cbase + jp * 32 + po;
+          if constexpr (EPI == EPI_GELU_SAVE) {
+            fv4 a = acc[i][j], b = acc[i][j + 1];
+            const float4 ba = bias4[j], bb = bias4[j + 1];
+            a[0] += ba.x; a[1] += ba.y; a[2] += ba.z; a[3] += ba.w;
+            b[0] += bb.x; b[1] += bb.y; b[2] += bb.z; b[3] += bb.w;
+            *reinterpret_cast<uint4*>((bf16_t*)p.aux + orow[i] * p.ld_aux + cbase + jp * 32 + po) = pack_pair_bf16(a, b);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { a[e] = gelu_erf(a[e]) * rs; b[e] = gelu_erf(b[e]) * rs; }
+            *reinterpret_cast<uint4*>(span) = pack_pair_bf16(a, b);
+          } else {
+            // the accumulators in the pair layout: v[k] = column k, v[4 + k] = column 4 + k
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][k]),
+                                                              __float_as_uint(acc[i][j + 1][k]), false, false);
+              v[k] = __uint_as_float(s[0]);
+              v[4 + k] = __uint_as_float(s[1]);
+            }
+            const uint4 u = pre[i % PW][jp];
+            const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[2 * q] *= gelu_erf_grad(__uint_as_float(w[q] << 16));
+              v[2 * q + 1] *= gelu_erf_grad(__uint_as_float(w[q] & 0xffff0000u));
+            }
+            *reinterpret_cast<uint4*>(span) = make_uint4(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]),
+                                                         cvt_pk_bf16(v[4], v[5]), cvt_pk_bf16(v[6], v[7]));
+          }
+        }
+        if constexpr (EPI == EPI_DGELU) {
+          if (i + PW < MI) load_pre(i + PW);
+        }
+      }
+      return;
+    }
+  }
   if constexpr (EPI == EPI_GELU_SAVE || EPI == EPI_DGELU) {
     // full wave tile in N (wave-uniform): branch-free, rows past M clamped to M - 1 (their
     // accumulators are row M - 1's -- the A loads are clamped -- and so are the aux row and the

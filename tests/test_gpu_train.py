@@ -327,12 +327,13 @@ def test_layernorm_bwd_rowmap_vs_autograd(C, dy_dtype):
     assert rel(dg.cpu(), g32.grad.cpu()) < 1e-4 and rel(db.cpu(), b32.grad.cpu()) < 1e-4
 
 
-@pytest.mark.parametrize("M", [300, 4037])
+@pytest.mark.parametrize("M", [300, 4037, 4613])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
 def test_gelu_save_and_dgelu_epilogues(dtype, tol, M):
     """fc1 forward saving the pre-activation, and (dY.W2) * GELU'(pre) -- vs torch autograd.
     M = 4037: the persistent kernel with a ragged last tile (its branch-free epilogue clamps the
-    rows past M to identical rewrites of row M - 1)."""
+    rows past M to identical rewrites of row M - 1); M = 4613: the 256x256 kernel's 16-byte pair
+    epilogue (ragged last tile too)."""
     from dsvt import ops
     from dsvt._lib import EPI_DGELU, EPI_GELU_SAVE
     K, N = 128, 256
