@@ -35,12 +35,15 @@ IMAGENET_STD = (0.225, 0.225, 0.225)
 
 
 # ----------------------------------------------------------------- algorithmic FLOPs
-def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16, folded=False):
+def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16, folded=False, cls_tail=False):
     """2*M*N*K over every matmul of one divided-ST clip forward, counted as the reference
     executes it (CLS replicated T times in the spatial branch).  8x224^2: 391.7 GFLOP,
     8x96^2: 70.7 GFLOP (391.66 / 70.70 from torch.utils.flop_counter).
     folded=True: what dsvt executes -- temporal proj and temporal_fc folded into one GEMM
-    (VisionTransformer.fold_temporal_fc), i.e. one 2*R*C*C GEMM less per block."""
+    (VisionTransformer.fold_temporal_fc), i.e. one 2*R*C*C GEMM less per block.
+    cls_tail=True: also what dsvt executes for a CLS-only forward (VisionTransformer.cls_tail):
+    the last block's spatial attention for the CLS queries only, attn.proj and the MLP on the
+    CLS row only (Block._run_cls_tail)."""
     N = (S // patch) ** 2
     d = C // heads
     R = N * T
@@ -51,16 +54,20 @@ def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16, folded=False
                  + 2 * 2 * L * C * mlp * C)                                                  # MLP
     if folded:
         per_block -= 2 * R * C * C
-    return depth * per_block + 2 * R * (3 * patch * patch) * C
+    tail = 0
+    if cls_tail:   # last block: no patch-row queries, no patch-row proj / MLP
+        tail = 4 * T * heads * (1 + N) * N * d + 2 * (rows_s - 1) * C * C + 2 * 2 * (L - 1) * C * mlp * C
+    return depth * per_block - tail + 2 * R * (3 * patch * patch) * C
 
 
 def head_flops(in_dim=768, hidden=2048, bottleneck=256, out_dim=65536):
     return 2 * (in_dim * hidden + hidden * hidden + hidden * bottleneck + bottleneck * out_dim)
 
 
-def clip_flops(n_global=2, n_local=6, folded=False):
+def clip_flops(n_global=2, n_local=6, folded=False, cls_tail=False):
     """teacher (2 global) + student (2 global + 6 local) + heads on every crop row."""
-    g, l = vit_fwd_flops(8, 224, folded=folded), vit_fwd_flops(8, 96, folded=folded)
+    g = vit_fwd_flops(8, 224, folded=folded, cls_tail=cls_tail)
+    l = vit_fwd_flops(8, 96, folded=folded, cls_tail=cls_tail)
     return 2 * n_global * g + n_local * l + (2 * n_global + n_local) * head_flops()
 
 
@@ -339,7 +346,7 @@ def other_configs(args, device):
     xd = torch.randn(16, 3, 8, 224, 224, device=device)
     with torch.no_grad():
         t = timed(lambda: dm(xd))
-    ref_gf, exe_gf = vit_fwd_flops(8, 224), vit_fwd_flops(8, 224, folded=True)
+    ref_gf, exe_gf = vit_fwd_flops(8, 224), vit_fwd_flops(8, 224, folded=True, cls_tail=dm.cls_tail)
     peak = PEAK_TFLOPS[args.dtype]
     res["config2_backbone_fwd"] = {"value": round(16 / t, 2), "unit": "clips/s", "clips_per_step": 16,
                                    "streams": "batch split over concurrent HIP streams (dsvt_streams=%s)"
@@ -610,7 +617,8 @@ def main():
     value = world * args.clips * args.steps / elapsed
     step_ms = elapsed / args.steps * 1e3
     folded = student.backbone.fold_temporal_fc
-    step_tflops = value * clip_flops(folded=folded) / 1e12        # FLOPs the GPU executed
+    tail = student.backbone.cls_tail and not grouped                 # the grouped forward runs full last blocks
+    step_tflops = value * clip_flops(folded=folded, cls_tail=tail) / 1e12        # FLOPs the GPU executed
     out = {"metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
@@ -619,7 +627,9 @@ def main():
                                   "DINOLoss(ncrops=8) + center all-reduce",
                       "clips_per_gpu": args.clips, "global_batch": world * args.clips,
                       "gflop_per_clip": round(clip_flops() / 1e9, 1),
-                      "executed_gflop_per_clip": round(clip_flops(folded=folded) / 1e9, 1),
+                      "executed_gflop_per_clip": round(clip_flops(folded=folded, cls_tail=tail) / 1e9, 1),
+                      "last_block": ("CLS rows only past the spatial qkv (the reference discards the last block's "
+                                     "patch-row outputs: x[:, 0] after the final norm)") if tail else "full",
                       "parallelism": "dp%d" % world,
                       "weights": "random init (torch seed 0)",
                       "launch": "eager" if graph is None else "hip_graph (forward+loss captured; center all-reduce eager)",

@@ -660,4 +660,131 @@ hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t n
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------- CLS-query spatial attention
+// The spatial attention of the LAST divided block when forward_features returns the CLS token
+// only (timesformer.py:139-167, 341-345): the patch rows' outputs of that block never reach the
+// result, so only the CLS query of each frame sequence (b, t) is evaluated -- one query against
+// CLS + the N patch rows of frame t -- and the T outputs are averaged (the reference's
+// cls_token.mean over frames).  One 256-thread workgroup per (clip, head); wave w takes frames
+// w, w+4, ...; the frame outputs meet in LDS and are summed in frame order (deterministic).
+// Lane layout: 8 groups of 8 lanes; a group owns one key row per step, a lane 8 of its 64 dims
+// (one 16-byte piece of bf16 / two of fp32), so one wave instruction reads 8 whole 128-B rows.
+// Out: out[b * ld_out + h*64 + d] in the storage dtype (compact [B, C] rows for the CLS-row
+// projection GEMM that follows).  seqlen <= ATTN_CLS_MAXSEQ.
+constexpr int ATTN_CLS_MAXSEQ = 1024;
+
+template <typename TI>
+__device__ __forceinline__ void load8f(const TI* p, float (&v)[8]) {
+  if constexpr (sizeof(TI) == 2) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+    v[4] = bf16_lo(u.z); v[5] = bf16_hi(u.z); v[6] = bf16_lo(u.w); v[7] = bf16_hi(u.w);
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restrict__ qkv, TI* __restrict__ out,
+                                                             int64_t ld_out, int64_t L, int T, int seqlen, int heads,
+                                                             float scale) {
+  __shared__ float sc[4][ATTN_CLS_MAXSEQ];     // per-wave scores -> probabilities
+  __shared__ float ot[64][64];                 // frame outputs [t][d], T <= 64
+  const int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int grp = lane >> 3, c = lane & 7;
+  const int64_t C = (int64_t)heads * 64, ld = 3 * C;
+  const TI* base = qkv + (int64_t)b * L * ld;
+  float q[8];
+  load8f(base + h * 64 + c * 8, q);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] *= scale;
+  float* s = sc[w];
+  for (int t = w; t < T; t += 4) {
+    // scores: key j of frame t = CLS row (j = 0) or patch row 1 + (j-1)*T + t
+    float mx = -INFINITY;
+    for (int j0 = 0; j0 < seqlen; j0 += 8) {
+      const int j = j0 + grp;
+      float part = 0.f;
+      if (j < seqlen) {
+        const int64_t row = j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t;
+        float k[8];
+        load8f(base + row * ld + C + h * 64 + c * 8, k);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) part = fmaf(q[i], k[i], part);
+      }
+      part += __shfl_xor(part, 1);
+      part += __shfl_xor(part, 2);
+      part += __shfl_xor(part, 4);
+      if (j < seqlen) {
+        if (c == 0) s[j] = part;
+        mx = fmaxf(mx, part);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    float sum = 0.f;
+    for (int j = lane; j < seqlen; j += 64) {
+      const float e = __expf(s[j] - mx);
+      s[j] = e;
+      sum += e;
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // P.V: group grp takes keys j = grp (mod 8), lane c dims c*8 .. c*8+7
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int j = grp; j < seqlen; j += 8) {
+      const int64_t row = j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t;
+      float v[8];
+      load8f(base + row * ld + 2 * C + h * 64 + c * 8, v);
+      const float pj = s[j];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, v[i], acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[i] += __shfl_xor(acc[i], 8);
+      acc[i] += __shfl_xor(acc[i], 16);
+      acc[i] += __shfl_xor(acc[i], 32);
+    }
+    const float inv = 1.0f / sum;
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ot[t][c * 8 + i] = acc[i] * inv;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float m = 0.f;
+    for (int t = 0; t < T; ++t) m += ot[t][tid];
+    out[(int64_t)b * ld_out + h * 64 + tid] = Elem<TI>::from_f(m / (float)T);
+  }
+}
+
+bool attn_cls_ok(int64_t T, int64_t seqlen) { return T >= 1 && T <= 64 && seqlen >= 1 && seqlen <= ATTN_CLS_MAXSEQ; }
+
+hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
+                           int64_t heads, float scale, hipStream_t s) {
+  const int64_t seqlen = 1 + (L - 1) / T;
+  if (!attn_cls_ok(T, seqlen)) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)(B * heads);
+  if (dtype == 0)
+    attn_cls_query_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, ld_out, L, (int)T,
+                                                       (int)seqlen, (int)heads, scale);
+  else
+    attn_cls_query_kernel<float><<<grid, 256, 0, s>>>((const float*)qkv, (float*)out, ld_out, L, (int)T, (int)seqlen,
+                                                      (int)heads, scale);
+  return hipGetLastError();
+}
+
 }  // namespace dsvt

@@ -402,6 +402,22 @@ int dsvt_attn_spatial_fwd(int dtype, const void* qkv, void* out, int64_t B, int6
   return 0;
 }
 
+int dsvt_attn_spatial_cls_fwd(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
+                              int64_t heads, int64_t head_dim, float scale, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial_cls: bad dtype");
+  REQUIRE(qkv && out && aligned16(qkv), "attn_spatial_cls: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_spatial_cls: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_cls: need (L-1) %% T == 0");
+  REQUIRE(attn_cls_ok(T, 1 + (L - 1) / T), "attn_spatial_cls: need T <= 64 and 1 + (L-1)/T <= 1024");
+  const int64_t C = heads * 64;
+  REQUIRE(ld_out >= C, "attn_spatial_cls: ld_out must be >= C");
+  const int64_t seqlen = 1 + (L - 1) / T;
+  const double flops = 4.0 * B * T * heads * (double)seqlen * 64;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, "dsvt_attn_spatial_cls_fwd", [&] {
+    return launch_attn_cls(dtype, qkv, out, ld_out, B, T, L, heads, scale, (hipStream_t)stream);
+  });
+}
+
 int dsvt_attn_spatial_scaled_fwd(int dtype, const void* qkv, void* out, const float* seq_scale, int64_t B, int64_t T,
                                  int64_t L, int64_t heads, int64_t head_dim, float scale, void* workspace,
                                  int64_t workspace_bytes, void* stream) {

@@ -51,6 +51,7 @@ SIGNATURES = {
     "dsvt_attn_spatial_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
     "dsvt_attn_spatial_probs_fwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
     "dsvt_attn_joint_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_attn_spatial_cls_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_frame_mean_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
     "dsvt_cast_fwd": (_i32, [_i32, _p, _p, _i64, _p]),
     "dsvt_dino_head_norm_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _f32, _p]),

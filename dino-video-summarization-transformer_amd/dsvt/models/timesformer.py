@@ -100,11 +100,16 @@ class Block(nn.Module):
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
 
     # -------------------------------------------------------------- HIP forward
-    def run(self, X, ctx, probs=None):
+    def run(self, X, ctx, probs=None, cls_tail=False):
         """One block on the fp32 token tensor X (in place).  ctx: per-forward buffers.
         probs (divided only): stop after the spatial softmax and write it there -- the
-        return_attn path of timesformer.py:155-157 (X is then left mid-block)."""
+        return_attn path of timesformer.py:155-157 (X is then left mid-block).
+        cls_tail (divided, the LAST block of a CLS-only forward): after the temporal branch and
+        the spatial qkv (the keys / values of every row), only the CLS rows are carried on -- see
+        _run_cls_tail."""
         w = ctx.w
+        if cls_tail:
+            return self._run_cls_tail(X, ctx)
         C, heads = ctx.C, self.attn.num_heads
         eps1, eps2 = self.norm1.eps, self.norm2.eps
         if getattr(ctx, "fuse_ln", False) and self.attention_type == "divided_space_time":
@@ -146,6 +151,45 @@ class Block(nn.Module):
                     self.mlp.fc1.bias, ctx.hid, ctx.ws, epilogue=EPI_BIAS_GELU)
         ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
 
+
+    def _run_cls_tail(self, X, ctx):
+        """The last divided block when forward_features returns the CLS token only
+        (timesformer.py:341-345 `x[:, 0]` after the final norm).  That block's patch-row outputs
+        -- their spatial attention, attn.proj, norm2 and MLP -- never reach the result, so they
+        are not computed: the temporal branch and the spatial qkv run on every row as in run()
+        (the CLS query attends to every frame's patch keys / values), then the CLS query of each
+        frame sequence (dsvt_attn_spatial_cls_fwd, mean over frames, :139-167), attn.proj +
+        residual, norm2, fc1 + GELU and fc2 + residual run on the B CLS rows alone (:181-184).
+        The CLS features are those of the full block (tests/test_gpu_model.py::
+        test_cls_tail_matches_full_block)."""
+        w = ctx.w
+        B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
+        heads = self.attn.num_heads
+        R = B * Np * T
+        patch_map = (Np * T, L, 1)
+        cls_map = (1, L, 0)                 # CLS row b -> X row b*L
+        ta = self.temporal_attn
+        ops.ln_gemm(X, patch_map, R, self.temporal_norm1.weight, self.temporal_norm1.bias,
+                    self.temporal_norm1.eps, w(ta.qkv.weight), ta.qkv.bias, ctx.qkv, ctx.ws)
+        ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
+        if ctx.fold_temporal:
+            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
+            ops.gemm(ctx.o, wf, bf, X, epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)
+        else:
+            ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
+            ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X, epilogue=EPI_BIAS_RESID,
+                     rowmap=patch_map, M=R)
+        ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, w(self.attn.qkv.weight),
+                    self.attn.qkv.bias, ctx.qkv, ctx.ws)
+        o_cls = ctx.o[:B]                   # compact [B, C] rows (ctx.o is free again)
+        ops.attn_spatial_cls(ctx.qkv, o_cls, B, T, L, heads, self.attn.scale)
+        ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,
+                 M=B)
+        h_cls = ctx.hid[:B]
+        ops.ln_gemm(X, cls_map, B, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
+                    self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
+        ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,
+                 M=B)
 
     def _run_split(self, X, ctx, probs):
         """Divided block with each residual sub-layer as GEMM (d = f(x), bias epilogue, storage
@@ -309,6 +353,10 @@ class VisionTransformer(nn.Module):
         # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
         # bit-identical to the unsplit batch at 16 clips (tools/split_bench.py)
         self.dsvt_streams = os.environ.get("DSVT_STREAMS", "auto")
+        # divided, CLS-only forwards (get_all / get_attn off): the last block carries only the CLS
+        # rows past its spatial qkv (Block._run_cls_tail) -- its patch-row outputs are discarded by
+        # the reference (x[:, 0] after the final norm).  DSVT_CLS_TAIL=0 runs the full last block.
+        self.cls_tail = os.environ.get("DSVT_CLS_TAIL", "1") != "0"
         self._wcache = WeightCache()
         self._index_cache = {}
 
@@ -541,10 +589,12 @@ class VisionTransformer(nn.Module):
             # output tokens (un-normed)
             self.blocks[-1].run(X, ctx)
             return X.view(ctx.nb, ctx.L, C)
+        cls_tail = (self.cls_tail and not get_all and self.attention_type == 'divided_space_time'
+                    and not (ctx.fuse_ln or ctx.split_resid) and ops.attn_cls_ok(T, ctx.L))
         for i, blk in enumerate(self.blocks):
             ctx.next_ln = (self.blocks[i + 1].temporal_norm1
                            if ((ctx.fuse_ln or ctx.split_resid) and i + 1 < nblk) else None)
-            blk.run(X, ctx)
+            blk.run(X, ctx, cls_tail=cls_tail and i + 1 == nblk)
         L = ctx.L
         if self.attention_type == 'space_only':      # mean over frames (:338-340)
             Xm = torch.empty(B * L, C, device=dev, dtype=torch.float32)

@@ -245,6 +245,19 @@ def attn_spatial_probs(qkv, out, probs, B, T, L, heads, scale, ws):
     return probs
 
 
+def attn_cls_ok(T, L):
+    """dsvt_attn_spatial_cls_fwd's limits: T <= 64 frames, 1 + N <= 1024 keys per frame sequence."""
+    return 1 <= T <= 64 and L > 1 and (L - 1) % T == 0 and 1 + (L - 1) // T <= 1024
+
+
+def attn_spatial_cls(qkv, out, B, T, L, heads, scale):
+    """CLS output only of attn_spatial (mean over the T frame sequences): out [B, C] rows."""
+    _check(out, qkv.dtype, "out")
+    call("dsvt_attn_spatial_cls_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.stride(0), B, T, L, heads, 64,
+         float(scale), _stream())
+    return out
+
+
 def attn_joint(qkv, out, nb, L, heads, scale):
     call("dsvt_attn_joint_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), nb, L, heads, 64, float(scale), _stream())
     return out

@@ -456,6 +456,36 @@ def test_attn_spatial_cls_mean(dtype, B, T, N, heads):
     check(back(out), spatial_ref(back(Q), B, T, L, heads, 0.125), dtype, "spatial")
 
 
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,T,N,heads", [(2, 1, 4, 3), (2, 3, 36, 12), (3, 8, 196, 12), (2, 4, 49, 3),
+                                         (1, 2, 150, 1), (1, 16, 255, 2), (2, 5, 300, 2)])
+def test_attn_spatial_cls_only(dtype, B, T, N, heads):
+    """dsvt_attn_spatial_cls_fwd (the last block of a CLS-only forward): the CLS row of
+    spatial_ref -- mean over frames of the CLS query's attention over CLS + the frame's patches --
+    into compact [B, C] rows (here with a row stride wider than C), against float64; bitwise
+    repeatable; the rest of the output untouched."""
+    C, L = heads * 64, 1 + N * T
+    qkv = rnd((B * L, 3 * C), 14, 1.5)
+    Q = to(qkv, dtype)
+    outs = []
+    for _ in range(2):
+        out = torch.full((B, C + 64), 3.0, device=dev(), dtype=dtype)
+        _lib_cls(Q, out, B, T, L, heads, 0.125)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), "repeat launches differ"
+    assert (back(outs[0])[:, C:] == 3.0).all()
+    ref = spatial_ref(back(Q), B, T, L, heads, 0.125)[np.arange(B) * L]
+    check(back(outs[0])[:, :C], ref, dtype, "spatial cls-only")
+
+
+def _lib_cls(Q, out, B, T, L, heads, scale):
+    """dsvt_attn_spatial_cls_fwd with ld_out = out.shape[1] (a strided output)."""
+    from dsvt import _lib, ops
+    _lib.call("dsvt_attn_spatial_cls_fwd", ops._dt(Q.dtype), Q.data_ptr(), out.data_ptr(), out.shape[1], B, T, L,
+              heads, 64, float(scale), ops._stream())
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 7])
 def test_attn_spatial_variants_repeatable(variant):
     """Every bf16 short-sequence kernel at a multi-clip global shape (B=4, 8x196 patches, 12 heads,

@@ -87,6 +87,33 @@ def test_base_divided_golden(base_sd, dtype, tol):
     assert max(errs.values()) < tol, errs
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cls_tail_matches_full_block(base_sd, dtype):
+    """VisionTransformer.cls_tail (Block._run_cls_tail): the last block of a CLS-only forward
+    carries only the CLS rows past its spatial qkv (dsvt_attn_spatial_cls_fwd + CLS-row proj /
+    norm2 / MLP).  Its CLS features equal the full last block's: 1e-5 in fp32; in bf16 within
+    1e-2 (the full block's MFMA attention rounds P to bf16, the CLS kernel keeps it fp32), and
+    against the reference goldens (the default path of test_base_divided_golden).  Shapes: the
+    bench clip (8x224^2, 3 clips), 96^2 local crops, T = 3, and a batch split over streams."""
+    m = tsf(base_sd, dtype)
+    cases = [P.clip(211, (3, 3, 8, 224, 224)), P.clip(212, (5, 3, 8, 96, 96)), P.clip(213, (2, 3, 3, 224, 224))]
+    f = g("base_div")
+    with torch.no_grad():
+        for x in cases:
+            xc = cu(x)
+            m.cls_tail = True
+            y_tail = m(xc).clone()
+            m.cls_tail = False
+            y_full = m(xc).clone()
+            e = rel(y_tail.cpu(), y_full.cpu())
+            print("cls_tail", dtype, tuple(x.shape), e)
+            assert torch.isfinite(y_tail).all()
+            assert e < (1e-5 if dtype == torch.float32 else 1e-2), e
+        m.cls_tail = True
+        assert rel(m(cu(P.clip(202, (1, 3, 8, 224, 224)))).cpu(), f["cls_224"]) < (
+            FP32_TOL if dtype == torch.float32 else BF16_TOL)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
 def test_base_divided_unfolded_golden(base_sd, dtype, tol):
     """fold_temporal_fc=False runs temporal proj and temporal_fc as the reference's two
@@ -448,6 +475,8 @@ def test_grouped_forward_bitwise(variant, monkeypatch):
             [cu(P.clip(1611 + i, (3, 3, 8, 32, 32))) for i in range(2)]
     for dtype in (torch.bfloat16, torch.float32):
         student, teacher = net(1701, dtype), net(1801, dtype)
+        for m in (student, teacher):     # the grouped forward runs full last blocks
+            m.backbone.cls_tail = False
         outs = {}
         _lib.call("dsvt_set_gemm_variant", variant)
         try:

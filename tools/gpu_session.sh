@@ -27,7 +27,7 @@ for stage in "$@"; do
     prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --serial --no-graph --no-train --no-other &&
              python tools/prof_summary.py "$OUT/prof" --step-kernel loss_reduce > "$OUT/prof_summary.txt" ;;
     graphprof) run graphprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gprof" -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-probe --no-train --no-other &&
-             python tools/prof_summary.py "$OUT/gprof" --step-kernel loss_reduce --last 15 > "$OUT/gprof_summary.txt" ;;
+             python tools/prof_summary.py "$OUT/gprof" --step-kernel center_ema --last 15 > "$OUT/gprof_summary.txt" ;;
     trainprof) run trainprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tprof" -o run -- python3 tools/train_step.py --steps 5 --warmup 2 &&
              python tools/prof_summary.py "$OUT/tprof" --step-kernel 'dsvt::ema_kernel(' --per-step 1 > "$OUT/tprof_summary.txt" ;;
     pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&

@@ -7,7 +7,8 @@ per-step count.  E.g. the train step launches `ema_kernel` once (teacher EMA) an
 forward+loss step `loss_reduce_kernel` once per DINO loss.
 
 `--last N` (with --step-kernel) keeps only the kernels of the LAST N steps: those that start after
-the end of the step kernel's (N+1)-th-from-last launch.  A bench trace mixes the eager warm-up /
+the end of the step kernel's (N+1)-th-from-last launch and no later than its last launch (name the
+step's LAST kernel, e.g. `center_ema` of the fwd+loss step).  A bench trace mixes the eager warm-up /
 probe passes with the HIP-graph replays that follow them, so whole-trace averages mix two
 launch patterns; the window holds replays only.  Every kernel's call count must then be a
 multiple of N, or the summary refuses ("mixed trace") instead of printing per-step numbers."""
@@ -45,7 +46,8 @@ def main(path, step_kernel=None, per_step=1, last=0):
         if len(ends) < need:
             raise SystemExit("--last %d: only %d launches of '%s'" % (last, len(ends), step_kernel))
         t_start = ends[-need + per_step - 1] if per_step > 1 else ends[-need]
-        rows = [r for r in rows if r[2] > t_start]
+        t_end = ends[-1]                # kernels after the last step's step kernel belong to no step
+        rows = [r for r in rows if t_start < r[2] <= t_end]
         bad = {}
         counts = {}
         for n, _, _, _ in rows:
