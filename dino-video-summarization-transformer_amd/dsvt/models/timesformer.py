@@ -446,8 +446,14 @@ class VisionTransformer(nn.Module):
             rows = B * (1 + (shape[2] // 16) * (shape[3] // 16) * shape[1])
             k = max(1, min(3, rows // SPLIT_ROWS))
         k = min(int(k), B)
+        # Inside a HIP-graph capture the batch is split only when this forward is not already
+        # one of several concurrent calls (dino_forward / MultiCropWrapper forks): the split's
+        # fork would then sit under theirs, and a two-level fork tree crashes capture_end on this
+        # ROCm stack (dsvt.utils.nested_capture_fork; run_concurrent also refuses to nest).  Eager
+        # forwards split either way (bitwise the same features).
+        from ..utils import fork_depth
         if k > 1 and not get_attn and clips[0].is_cuda and not self._grad_path() \
-                and (not torch.cuda.is_current_stream_capturing() or os.environ.get("DSVT_CAPTURE_SPLIT") == "1"):
+                and not (torch.cuda.is_current_stream_capturing() and fork_depth() > 0):
             return self._forward_split(clips, B, k, shape, get_all, out)
         srcs = [(c, None, c.shape[0]) for c in clips]
         return self._forward_sources(srcs, B, shape[1], shape[2], shape[3], shape[0], get_all, get_attn, out)

@@ -1,10 +1,29 @@
 """Drop-in for utils.utils.MultiCropWrapper (utils/utils.py:564-609), plus the concurrent
 teacher/student forward of one DINO step."""
+import threading
+
 import torch
 import torch.nn as nn
 
 _SIDE_STREAMS = {}
 _SLOT_OF = {}          # cuda_stream handle of a side stream -> its slot
+_FORK = threading.local()
+
+
+def fork_depth():
+    """How many run_concurrent forks the calling code runs inside (0 = none)."""
+    return getattr(_FORK, "depth", 0)
+
+
+def nested_capture_fork(device):
+    """True when forking side streams from the current stream would be a NESTED fork inside a
+    HIP-graph capture: the current stream is itself one of our side streams, forked from the
+    capture's origin stream.  On this ROCm 7.2 / torch 2.10 stack a capture whose fork tree is
+    two levels deep (origin -> side A -> side B, joined back B -> A -> origin) dies with a host
+    segfault in capture_end even with no dsvt code in it (tools/capture_nested_min.py: plain
+    torch elementwise ops, with or without allocations on B; one level -- origin -> A -> origin --
+    captures and replays), so such a fork runs its items in order on the current stream instead."""
+    return torch.cuda.is_current_stream_capturing() and torch.cuda.current_stream(device).cuda_stream in _SLOT_OF
 
 
 def side_stream(device, slot):
@@ -30,18 +49,24 @@ def run_concurrent(thunks, device, slot0=0):
     stream's prior work, and the current stream waits for all of them before returning.
     Kernels of the different items then overlap on the chip (one backbone call's last,
     partly-filled wave of tiles runs beside another's full waves)."""
+    if nested_capture_fork(device):         # see nested_capture_fork: in order, no fork
+        return [fn() for fn in thunks]
     cur = torch.cuda.current_stream(device)
     results, used = [None] * len(thunks), []
-    for i, fn in enumerate(thunks):
-        if i == 0:
-            continue
-        st = side_stream(device, slot0 + i - 1 if isinstance(slot0, int) else (slot0, i))
-        st.wait_stream(cur)
-        with torch.cuda.stream(st):
-            results[i] = fn()
-        used.append(st)
-    if thunks:
-        results[0] = thunks[0]()
+    _FORK.depth = fork_depth() + 1
+    try:
+        for i, fn in enumerate(thunks):
+            if i == 0:
+                continue
+            st = side_stream(device, slot0 + i - 1 if isinstance(slot0, int) else (slot0, i))
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                results[i] = fn()
+            used.append(st)
+        if thunks:
+            results[0] = thunks[0]()
+    finally:
+        _FORK.depth -= 1
     for st in used:
         cur.wait_stream(st)
     for r in results:                      # outputs made on side streams are consumed on `cur`

@@ -450,6 +450,51 @@ def test_joint16_config4_full_size():
     assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
 
 
+def test_capture_split_streams():
+    """HIP-graph capture of forwards that ask for a batch split (dsvt_streams = 3): a plain
+    backbone call (a one-level fork from the capture stream: split) and dino_forward (student and
+    teacher already on two streams, the student's resolution groups on a third: the inner splits
+    would be a two-level fork tree, which crashes capture_end on this ROCm stack, so they run
+    unsplit -- dsvt.utils.nested_capture_fork).  Both capture, and replay bitwise equal to the
+    eager (split) forward."""
+    from dsvt.utils import MultiCropWrapper, dino_forward
+    from dsvt.vision_transformer import DINOHead
+    cfg = dict(embed_dim=768, num_heads=12, depth=2, img_size=224, num_frames=8)
+
+    def bb(seed):
+        m = tsf(P.timesformer_state(seed, **cfg), torch.bfloat16, **cfg)
+        m.dsvt_streams = 3
+        return m
+    plain = bb(1901)
+    x = cu(P.clip(1902, (6, 3, 8, 224, 224)))
+    s = MultiCropWrapper(bb(1903), DINOHead(768, 4096)).cuda().eval()
+    t = MultiCropWrapper(bb(1904), DINOHead(768, 4096)).cuda().eval()
+    crops = [cu(P.clip(1905 + i, (3, 3, 8, 224, 224))) for i in range(2)] + \
+            [cu(P.clip(1907 + i, (3, 3, 8, 96, 96))) for i in range(2)]
+
+    def fwd():
+        with torch.no_grad():
+            a, b = dino_forward(s, t, crops)
+            return plain(x), a, b
+    ref = [r.clone() for r in fwd()]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fwd()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        outs = fwd()
+    for o in outs:
+        o.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref):
+        assert torch.isfinite(o).all()
+        assert torch.equal(o, r), (o - r).abs().max().item()
+
+
 @pytest.mark.parametrize("variant", [20, 0])
 def test_grouped_forward_bitwise(variant, monkeypatch):
     """dsvt.grouped: the three backbone calls of a DINO step (teacher on 2 global crops, student on

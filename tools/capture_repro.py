@@ -1,6 +1,9 @@
-"""Reproduce / check HIP-graph capture of a split-batch forward (VisionTransformer.dsvt_streams
-> 1 inside a capture).  usage: DSVT_CAPTURE_SPLIT=1 python tools/capture_repro.py [nested]
-nested: capture dino_forward (student + teacher on two streams, each splitting its batch)."""
+"""Check HIP-graph capture of a split-batch forward (VisionTransformer.dsvt_streams > 1 inside a
+capture).  usage: python tools/capture_repro.py [nested]
+nested: capture dino_forward (student + teacher on two streams, each asking to split its batch).
+Before dsvt.utils.nested_capture_fork the nested case died in capture_end (a two-level fork tree;
+tools/capture_nested_min.py reproduces that with plain torch ops); now the inner splits run
+unsplit inside a capture and both cases replay equal to eager."""
 import faulthandler
 import os
 import sys
@@ -28,15 +31,28 @@ def net(seed):
     return bb
 
 
+# bisection knobs: CAP_SERIAL_NETS=1 (dino_forward without the student/teacher fork), CAP_SERIAL_GROUPS=1
+# (MultiCropWrapper groups in order), CAP_NO_RECORD=1 (Tensor.record_stream a no-op), CAP_K=<k> (chunks)
+if os.environ.get("CAP_NO_RECORD") == "1":
+    torch.Tensor.record_stream = lambda self, s: None
+if os.environ.get("CAP_K"):
+    _net = net
+
+    def net(seed):   # noqa: F811
+        bb = _net(seed)
+        bb.dsvt_streams = int(os.environ["CAP_K"])
+        return bb
 if nested:
     s, t = MultiCropWrapper(net(1), DINOHead(768, 4096)).to(dev).eval(), \
         MultiCropWrapper(net(1), DINOHead(768, 4096)).to(dev).eval()
+    if os.environ.get("CAP_SERIAL_GROUPS") == "1":
+        s.concurrent_groups = t.concurrent_groups = False
     x = [torch.randn(3, 3, 8, 224, 224, device=dev) for _ in range(2)] + \
         [torch.randn(3, 3, 8, 96, 96, device=dev) for _ in range(2)]
 
     def fwd():
         with torch.no_grad():
-            a, b = dino_forward(s, t, x)
+            a, b = dino_forward(s, t, x, concurrent=os.environ.get("CAP_SERIAL_NETS") != "1")
         return torch.cat([a, b])
 else:
     m = net(1)
