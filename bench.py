@@ -429,9 +429,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
-    ap.add_argument("--grouped", action="store_true",
-                    help="run the teacher / student backbone calls as one grouped lockstep forward (DSVT_GROUPED=1; "
-                         "A/B: measured 354 vs 370 clips/s for the concurrent streams)")
+    ap.add_argument("--grouped", nargs="?", const="1", default=None, choices=["1", "2"],
+                    help="1: run the teacher / student backbone calls as one grouped lockstep forward (DSVT_GROUPED=1; "
+                         "A/B: measured 354 vs 370 clips/s for the concurrent streams); 2: group only the "
+                         "global-crop calls, the local-crop call on a concurrent stream")
     ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-grad-overlap", dest="grad_overlap", action="store_false",
@@ -443,7 +444,7 @@ def main():
                     help="rehearsal: allow N ranks on fewer GPUs (rank r uses GPU r %% count; needs --backend gloo)")
     args = ap.parse_args()
     if args.grouped:
-        os.environ["DSVT_GROUPED"] = "1"
+        os.environ["DSVT_GROUPED"] = args.grouped
 
     from dsvt import dist as ddist
 
@@ -614,10 +615,14 @@ def main():
         grouped = _groupable(student, teacher, crops)
     grouped_desc = ("grouped: the teacher / student backbone calls advance in lockstep over one token buffer, every "
                     "Linear of a layer ONE launch over all calls (dsvt_gemm_grouped_fwd), one stream")
+    if os.environ.get("DSVT_GROUPED") == "2":
+        grouped_desc = ("grouped global crops: the teacher's and the student's global-crop calls in lockstep, every "
+                        "Linear of a layer ONE launch over both (dsvt_gemm_grouped_fwd); the local-crop call on a "
+                        "concurrent stream")
     value = world * args.clips * args.steps / elapsed
     step_ms = elapsed / args.steps * 1e3
     folded = student.backbone.fold_temporal_fc
-    tail = student.backbone.cls_tail and not grouped                 # the grouped forward runs full last blocks
+    tail = student.backbone.cls_tail
     step_tflops = value * clip_flops(folded=folded, cls_tail=tail) / 1e12        # FLOPs the GPU executed
     out = {"metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",

@@ -260,6 +260,44 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
     }
   }
   if constexpr (CLAMP) return;
+  // full wave tile, fp32 residual add into X, bias already in the accumulators, MI >= 4: a
+  // rolling window of DSVT_RESID_PIPE rows of X fragments in flight -- the load of row i + W is
+  // issued right after row i's stores, so the HBM round trips overlap instead of running one per
+  // row pair (the stores are younger than the awaited loads and never waited for here).  The
+  // window lives in the registers the K loop's operand fragments held (0 = off).
+#ifndef DSVT_RESID_PIPE
+#define DSVT_RESID_PIPE 3
+#endif
+  if constexpr (EPI == EPI_RESID && MI % 2 == 0 && MI >= 4 && DSVT_RESID_PIPE && BIAS_IN_ACC) {
+    if (!rres && rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {   // the bias is in acc: add X only
+      const bool idm = p.rpg >= p.M && p.goff == 0;
+      auto row_off = [&](int i) -> int64_t {
+        const int64_t m = rbase + i * 16 + r16;
+        return (idm ? m : map_row(m, p.rpg, p.gstride, p.goff)) * p.ldo + cbase + 4 * g;
+      };
+      constexpr int W = DSVT_RESID_PIPE > 0 ? DSVT_RESID_PIPE : 1;   // rows of X in flight (a rolling window)
+      float4 x[W][NJ];
+      auto load_row = [&](int i) {
+        const float* src = resid_src(p) + row_off(i);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) x[i % W][j] = *reinterpret_cast<const float4*>(src + j * 16);
+      };
+#pragma unroll
+      for (int i = 0; i < W; ++i) load_row(i);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        float* dst = (float*)p.out + row_off(i);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const fv4 a = acc[i][j];
+          const float4 xv = x[i % W][j];
+          *reinterpret_cast<float4*>(dst + j * 16) = make_float4(xv.x + a[0], xv.y + a[1], xv.z + a[2], xv.w + a[3]);
+        }
+        if (i + W < MI) load_row(i + W);
+      }
+      return;
+    }
+  }
   // full wave tile, fp32 residual add into X: the X fragments of two rows are loaded before
   // their stores (one HBM round trip per row pair instead of per fragment), branch-free
   if constexpr (EPI == EPI_RESID && MI % 2 == 0) {

@@ -104,6 +104,9 @@ def forward_features_grouped(calls, outs=None):
                                              C, 0) // 4 + 4, device=dev, dtype=torch.float32)
     fold = m0.fold_temporal_fc
     r1 = None if fold else torch.empty(R, C, device=dev, dtype=mode)
+    # CLS-only last block (VisionTransformer.cls_tail, timesformer.Block._run_cls_tail): past the
+    # last spatial qkv only the CLS rows of each call are carried on
+    cls_tail = all(c.m.cls_tail for c in cs) and all(ops.attn_cls_ok(T, c.L) for c in cs)
     for k in range(depth):
         blks = [c.m.blocks[k] for c in cs]
         # ---- temporal (timesformer.py:127-135): LN of the patch rows -> qkv -> attention -> proj.fc
@@ -130,6 +133,19 @@ def forward_features_grouped(calls, outs=None):
             ops.layernorm(X[c.xoff:], c.rows, C, b.norm1.weight, b.norm1.bias, b.norm1.eps, a[c.xoff:], out_f32=False)
         ops.gemm_grouped(a, [(c.w(b.attn.qkv.weight), b.attn.qkv.bias, c.xoff, c.rows, None, c.xoff)
                              for c, b in zip(cs, blks)], qkv)
+        if cls_tail and k == depth - 1:
+            for c, b in zip(cs, blks):
+                cmap = (1, c.L, 0)
+                xc = X[c.xoff:c.xoff + c.rows]
+                o_cls, h_cls = o[c.xoff:c.xoff + c.B], h[c.xoff:c.xoff + c.B]
+                ops.attn_spatial_cls(qkv[c.xoff:c.xoff + c.rows], o_cls, c.B, T, c.L, heads, b.attn.scale)
+                ops.gemm(o_cls, c.w(b.attn.proj.weight), b.attn.proj.bias, xc, epilogue=EPI_BIAS_RESID, rowmap=cmap,
+                         M=c.B)
+                ops.ln_gemm(xc, cmap, c.B, b.norm2.weight, b.norm2.bias, b.norm2.eps, c.w(b.mlp.fc1.weight),
+                            b.mlp.fc1.bias, h_cls, a[c.xoff:], epilogue=EPI_BIAS_GELU)
+                ops.gemm(h_cls, c.w(b.mlp.fc2.weight), b.mlp.fc2.bias, xc, epilogue=EPI_BIAS_RESID, rowmap=cmap,
+                         M=c.B)
+            break
         for run in runs:
             c = run[0]
             ops.attn_spatial(qkv[c.xoff:], o[c.xoff:], sum(x.B for x in run), T, c.L, heads, blks[0].attn.scale,
@@ -163,9 +179,12 @@ def crop_groups(x):
     return out
 
 
-def dino_forward_grouped(student, teacher, images, n_global=2):
+def dino_forward_grouped(student, teacher, images, n_global=2, same_shape_only=False):
     """train_ssl.py:523-527 (student on all crops, teacher on the global crops) with the three
-    backbone calls grouped; the heads run on the features as MultiCropWrapper does."""
+    backbone calls grouped; the heads run on the features as MultiCropWrapper does.
+    same_shape_only (DSVT_GROUPED=2): only the calls of the first call's clip shape (the teacher's
+    and the student's global crops: identical layer shapes) are grouped; the other calls (the
+    student's local crops) run as plain forwards on a concurrent stream beside the group."""
     s_groups = crop_groups(images)
     t_groups = crop_groups(images[:n_global])
     calls = [(teacher.backbone, g) for g in t_groups] + [(student.backbone, g) for g in s_groups]
@@ -183,5 +202,16 @@ def dino_forward_grouped(student, teacher, images, n_global=2):
         n = sum(x.shape[0] for x in g)
         outs.append(s_feats[r:r + n])
         r += n
-    forward_features_grouped(calls, outs)
+    if same_shape_only:
+        from .utils import run_concurrent
+        shp = tuple(calls[0][1][0].shape[1:])
+        grp = [i for i, (_, g) in enumerate(calls) if tuple(g[0].shape[1:]) == shp]
+        rest = [i for i in range(len(calls)) if i not in grp]
+        for m in (teacher.backbone, student.backbone):
+            m.prepare_weights()
+        thunks = [lambda: forward_features_grouped([calls[i] for i in grp], [outs[i] for i in grp])]
+        thunks += [lambda i=i: calls[i][0].forward_features(calls[i][1], out=outs[i]) for i in rest]
+        run_concurrent(thunks, dev, slot0=16)
+    else:
+        forward_features_grouped(calls, outs)
     return student.head(s_feats), teacher.head(t_feats)

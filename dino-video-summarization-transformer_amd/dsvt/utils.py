@@ -86,7 +86,7 @@ def prepare_weights(module):
 
 def _groupable(student, teacher, images):
     import os
-    if os.environ.get("DSVT_GROUPED", "0") != "1" or not images[0].is_cuda:
+    if os.environ.get("DSVT_GROUPED", "0") not in ("1", "2") or not images[0].is_cuda:
         return False
     if not all(isinstance(m, MultiCropWrapper) and not m.vary_fr for m in (student, teacher)):
         return False
@@ -102,10 +102,12 @@ def dino_forward(student, teacher, images, n_global=2, concurrent=True):
     DSVT_GROUPED=1 (opt-in) runs dsvt divided-attention backbones in inference GROUPED instead,
     every layer's Linear of all calls as one launch (dsvt.grouped): bitwise the same features,
     measured slower (354 vs 370 clips/s on the bench line, same box: one stream loses the overlap
-    of the attention / LayerNorm kernels with the other calls' GEMMs)."""
+    of the attention / LayerNorm kernels with the other calls' GEMMs).  DSVT_GROUPED=2 groups only
+    the same-shape calls (teacher and student global crops) and runs the rest beside them."""
     if _groupable(student, teacher, images):
         from .grouped import dino_forward_grouped
-        return dino_forward_grouped(student, teacher, images, n_global)
+        return dino_forward_grouped(student, teacher, images, n_global,
+                                    same_shape_only=os.environ.get("DSVT_GROUPED") == "2")
     if not concurrent:
         return student(images), teacher(images[:n_global])
     for net in (student, teacher):

@@ -495,15 +495,18 @@ def test_capture_split_streams():
         assert torch.equal(o, r), (o - r).abs().max().item()
 
 
-@pytest.mark.parametrize("variant", [20, 0])
-def test_grouped_forward_bitwise(variant, monkeypatch):
+@pytest.mark.parametrize("variant,mode,tail", [(20, "1", False), (0, "1", False), (20, "1", True), (20, "2", True),
+                                               (20, "2", False)])
+def test_grouped_forward_bitwise(variant, mode, tail, monkeypatch):
     """dsvt.grouped: the three backbone calls of a DINO step (teacher on 2 global crops, student on
     2 global + 2 local) as one lockstep forward with every Linear a grouped launch
     (dsvt_gemm_grouped_fwd, a row segment per call with its own weights) against the same calls
     run separately (DSVT_GROUPED=0).  With the separate calls' GEMMs on the same 256x256 kernel
     (variant 20) the student / teacher logits are BITWISE equal; with the automatic kernel choice
     (small separate calls take the 128x128 kernel) within BF16_TOL.  Also fp32 parity mode (the
-    grouped op's per-segment fallback) within 1e-5."""
+    grouped op's per-segment fallback) within 1e-5.  mode "2" (DSVT_GROUPED=2) groups only the
+    global-crop calls and runs the local one beside them; tail: the CLS-only last block on both
+    sides (the per-call CLS kernels are the separate calls' own, so still bitwise)."""
     from dsvt import _lib
     from dsvt.utils import MultiCropWrapper, dino_forward
     from dsvt.vision_transformer import DINOHead
@@ -520,12 +523,12 @@ def test_grouped_forward_bitwise(variant, monkeypatch):
             [cu(P.clip(1611 + i, (3, 3, 8, 32, 32))) for i in range(2)]
     for dtype in (torch.bfloat16, torch.float32):
         student, teacher = net(1701, dtype), net(1801, dtype)
-        for m in (student, teacher):     # the grouped forward runs full last blocks
-            m.backbone.cls_tail = False
+        for m in (student, teacher):
+            m.backbone.cls_tail = tail
         outs = {}
         _lib.call("dsvt_set_gemm_variant", variant)
         try:
-            for grouped in ("1", "0"):
+            for grouped in (mode, "0"):
                 monkeypatch.setenv("DSVT_GROUPED", grouped)
                 with torch.no_grad():
                     s, t = dino_forward(student, teacher, crops, concurrent=False)
@@ -533,7 +536,7 @@ def test_grouped_forward_bitwise(variant, monkeypatch):
                 outs[grouped] = (s.clone(), t.clone())
         finally:
             _lib.call("dsvt_set_gemm_variant", 0)
-        for a, b in zip(outs["1"], outs["0"]):
+        for a, b in zip(outs[mode], outs["0"]):
             assert torch.isfinite(a).all()
             if dtype == torch.bfloat16 and variant == 20:
                 assert torch.equal(a, b), "grouped forward differs from the separate calls"

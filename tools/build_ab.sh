@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build an A/B copy of libdsvt.so with extra compile flags on the GEMM sources, e.g.
+#   tools/build_ab.sh "-DDSVT_RESID_PIPE=0"   -> tools/ab_lib/libdsvt_ab.so (run with DSVT_LIB=...)
+set -e
+cd "$(dirname "$0")/../dino-video-summarization-transformer_amd/csrc"
+make -s
+FLAGS="$1"
+mkdir -p build/ab ../../tools/ab_lib
+for f in gemm gemm_big gemm_8ph; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS -c $f.hip -o build/ab/$f.o
+done
+objs=""
+for f in gemm gemm_rowln wgrad gemm_big gemm_8ph norm attention attn_flash dino_loss backward swin select augment capi; do
+  if [ -f build/ab/$f.o ]; then objs="$objs build/ab/$f.o"; else objs="$objs build/$f.o"; fi
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/ab_lib/libdsvt_ab.so $objs
+echo "built tools/ab_lib/libdsvt_ab.so with $FLAGS"

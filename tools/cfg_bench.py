@@ -41,7 +41,7 @@ def main():
                               attention_type=attn).to(dev).eval()
         n = 16 if args.cfg == "c2bb" else 2
         x = torch.randn(n, 3, T, 224, 224, device=dev)
-        gf = (vit_fwd_flops(8, 224, folded=True) if args.cfg == "c2bb" else joint_flops()) / 1e9
+        gf = (vit_fwd_flops(8, 224, folded=True, cls_tail=m.cls_tail) if args.cfg == "c2bb" else joint_flops()) / 1e9
         if args.streams is not None:
             m.dsvt_streams = args.streams if args.streams == "auto" else int(args.streams)
     m.dsvt_dtype = torch.bfloat16
