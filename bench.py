@@ -287,12 +287,17 @@ def train_bench(args, device, rank, world, steps, warmup):
 
 
 # ----------------------------------------------------------------- configs 4 / 5: other backbones
-def joint_flops(T=16, S=224, C=768, depth=12, heads=12, mlp=4, patch=16):
-    """ViT-B/16 joint space-time forward: 899.35 GFLOP at 16x224^2."""
+def joint_flops(T=16, S=224, C=768, depth=12, heads=12, mlp=4, patch=16, cls_tail=False):
+    """ViT-B/16 joint space-time forward: 899.35 GFLOP at 16x224^2.  cls_tail: what
+    dsvt executes for a CLS-only forward (the last block's attention for the CLS query only, its
+    proj and MLP on the CLS row only)."""
     N = (S // patch) ** 2
     L = 1 + N * T
     per_block = 2 * L * C * 3 * C + 4 * heads * L * L * (C // heads) + 2 * L * C * C + 2 * 2 * L * C * mlp * C
-    return depth * per_block + 2 * N * T * (3 * patch * patch) * C
+    tail = 0
+    if cls_tail:
+        tail = 4 * heads * (L - 1) * L * (C // heads) + 2 * (L - 1) * C * C + 2 * 2 * (L - 1) * C * mlp * C
+    return depth * per_block - tail + 2 * N * T * (3 * patch * patch) * C
 
 
 def swin_t_flops(T=8, S=224, C=96, depths=(2, 2, 6, 2), window=(2, 7, 7), patch=(4, 4, 4)):
@@ -365,7 +370,9 @@ def other_configs(args, device):
         t = timed(lambda: jm(xj))
     res["config4_joint16"] = {"value": round(2 / t, 2), "unit": "clips/s", "clips_per_step": 2,
                               "gflop_per_clip": round(joint_flops() / 1e9, 1),
-                              "tflops": round(2 * joint_flops() / t / 1e12, 1)}
+                              "executed_gflop_per_clip": round(joint_flops(cls_tail=jm.cls_tail) / 1e9, 1),
+                              "tflops": round(2 * joint_flops() / t / 1e12, 1),
+                              "tflops_executed": round(2 * joint_flops(cls_tail=jm.cls_tail) / t / 1e12, 1)}
     del jm, xj
     sm = SwinTransformer3D().to(device)
     sm.eval()

@@ -661,18 +661,23 @@ hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t n
 }
 
 
-// ---------------------------------------------------------------- CLS-query spatial attention
-// The spatial attention of the LAST divided block when forward_features returns the CLS token
-// only (timesformer.py:139-167, 341-345): the patch rows' outputs of that block never reach the
-// result, so only the CLS query of each frame sequence (b, t) is evaluated -- one query against
-// CLS + the N patch rows of frame t -- and the T outputs are averaged (the reference's
-// cls_token.mean over frames).  One 256-thread workgroup per (clip, head); wave w takes frames
-// w, w+4, ...; the frame outputs meet in LDS and are summed in frame order (deterministic).
+// ---------------------------------------------------------------- CLS-query attention
+// The attention of the LAST block when forward_features returns the CLS token only
+// (timesformer.py:139-167, 341-345): the patch rows' outputs of that block never reach the
+// result, so only the CLS query is evaluated.
+//   divided (T frames): sequence (b, t) = CLS row b*L + the N patch rows 1 + n*T + t of frame t;
+//     the T outputs are averaged (the reference's cls_token mean over frames);
+//   joint / space-only (T = 1): sequence b = the L contiguous rows of clip (or frame) b.
+// One 256-thread workgroup per (sequence group b, head).  The work items are (t, key chunk) with
+// chunks of ATTN_CLS_CHUNK keys; wave w takes items w, w+4, ...  Each item leaves its running
+// max m, sum l and unnormalized P.V row in LDS; a frame's chunks are merged with the usual
+// log-sum-exp rescale and the frames summed in order (deterministic).
 // Lane layout: 8 groups of 8 lanes; a group owns one key row per step, a lane 8 of its 64 dims
 // (one 16-byte piece of bf16 / two of fp32), so one wave instruction reads 8 whole 128-B rows.
-// Out: out[b * ld_out + h*64 + d] in the storage dtype (compact [B, C] rows for the CLS-row
-// projection GEMM that follows).  seqlen <= ATTN_CLS_MAXSEQ.
-constexpr int ATTN_CLS_MAXSEQ = 1024;
+// Out: out[b * ld_out + h*64 + d] in the storage dtype (compact [nb, C] rows for the CLS-row
+// projection GEMM that follows).  T * chunks <= ATTN_CLS_ITEMS.
+constexpr int ATTN_CLS_CHUNK = 1024;
+constexpr int ATTN_CLS_ITEMS = 64;
 
 template <typename TI>
 __device__ __forceinline__ void load8f(const TI* p, float (&v)[8]) {
@@ -688,10 +693,11 @@ __device__ __forceinline__ void load8f(const TI* p, float (&v)[8]) {
 
 template <typename TI>
 __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restrict__ qkv, TI* __restrict__ out,
-                                                             int64_t ld_out, int64_t L, int T, int seqlen, int heads,
-                                                             float scale) {
-  __shared__ float sc[4][ATTN_CLS_MAXSEQ];     // per-wave scores -> probabilities
-  __shared__ float ot[64][64];                 // frame outputs [t][d], T <= 64
+                                                             int64_t ld_out, int64_t L, int T, int seqlen, int nchunk,
+                                                             int heads, float scale) {
+  __shared__ float sc[4][ATTN_CLS_CHUNK];            // per-wave scores -> probabilities of one chunk
+  __shared__ float po[ATTN_CLS_ITEMS][64];           // per-item unnormalized P.V
+  __shared__ float pm[ATTN_CLS_ITEMS], pl[ATTN_CLS_ITEMS];
   const int b = blockIdx.x / heads, h = blockIdx.x % heads;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int grp = lane >> 3, c = lane & 7;
@@ -702,13 +708,16 @@ __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restric
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] *= scale;
   float* s = sc[w];
-  for (int t = w; t < T; t += 4) {
-    // scores: key j of frame t = CLS row (j = 0) or patch row 1 + (j-1)*T + t
+  const int items = T * nchunk;
+  for (int it = w; it < items; it += 4) {
+    const int t = it / nchunk, j0c = (it % nchunk) * ATTN_CLS_CHUNK;
+    const int j1c = min(seqlen, j0c + ATTN_CLS_CHUNK);
+    // scores: key j of sequence t = CLS row (j = 0) or row 1 + (j-1)*T + t
     float mx = -INFINITY;
-    for (int j0 = 0; j0 < seqlen; j0 += 8) {
+    for (int j0 = j0c; j0 < j1c; j0 += 8) {
       const int j = j0 + grp;
       float part = 0.f;
-      if (j < seqlen) {
+      if (j < j1c) {
         const int64_t row = j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t;
         float k[8];
         load8f(base + row * ld + C + h * 64 + c * 8, k);
@@ -718,8 +727,8 @@ __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restric
       part += __shfl_xor(part, 1);
       part += __shfl_xor(part, 2);
       part += __shfl_xor(part, 4);
-      if (j < seqlen) {
-        if (c == 0) s[j] = part;
+      if (j < j1c) {
+        if (c == 0) s[j - j0c] = part;
         mx = fmaxf(mx, part);
       }
     }
@@ -728,7 +737,7 @@ __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restric
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     float sum = 0.f;
-    for (int j = lane; j < seqlen; j += 64) {
+    for (int j = lane; j < j1c - j0c; j += 64) {
       const float e = __expf(s[j] - mx);
       s[j] = e;
       sum += e;
@@ -737,15 +746,15 @@ __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restric
     for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // P.V: group grp takes keys j = grp (mod 8), lane c dims c*8 .. c*8+7
+    // P.V: group grp takes keys j = j0c + grp (mod 8), lane c dims c*8 .. c*8+7
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-    for (int j = grp; j < seqlen; j += 8) {
+    for (int j = j0c + grp; j < j1c; j += 8) {
       const int64_t row = j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t;
       float v[8];
       load8f(base + row * ld + 2 * C + h * 64 + c * 8, v);
-      const float pj = s[j];
+      const float pj = s[j - j0c];
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, v[i], acc[i]);
     }
@@ -755,10 +764,13 @@ __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restric
       acc[i] += __shfl_xor(acc[i], 16);
       acc[i] += __shfl_xor(acc[i], 32);
     }
-    const float inv = 1.0f / sum;
     if (grp == 0) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) ot[t][c * 8 + i] = acc[i] * inv;
+      for (int i = 0; i < 8; ++i) po[it][c * 8 + i] = acc[i];
+    }
+    if (lane == 0) {
+      pm[it] = mx;
+      pl[it] = sum;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -766,24 +778,37 @@ __global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restric
   __syncthreads();
   if (tid < 64) {
     float m = 0.f;
-    for (int t = 0; t < T; ++t) m += ot[t][tid];
+    for (int t = 0; t < T; ++t) {
+      float M = -INFINITY;
+      for (int k = 0; k < nchunk; ++k) M = fmaxf(M, pm[t * nchunk + k]);
+      float l = 0.f, o = 0.f;
+      for (int k = 0; k < nchunk; ++k) {
+        const float f = __expf(pm[t * nchunk + k] - M);
+        l = fmaf(pl[t * nchunk + k], f, l);
+        o = fmaf(po[t * nchunk + k][tid], f, o);
+      }
+      m += o / l;
+    }
     out[(int64_t)b * ld_out + h * 64 + tid] = Elem<TI>::from_f(m / (float)T);
   }
 }
 
-bool attn_cls_ok(int64_t T, int64_t seqlen) { return T >= 1 && T <= 64 && seqlen >= 1 && seqlen <= ATTN_CLS_MAXSEQ; }
+bool attn_cls_ok(int64_t T, int64_t seqlen) {
+  return T >= 1 && seqlen >= 1 && T * ((seqlen + ATTN_CLS_CHUNK - 1) / ATTN_CLS_CHUNK) <= ATTN_CLS_ITEMS;
+}
 
 hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
                            int64_t heads, float scale, hipStream_t s) {
   const int64_t seqlen = 1 + (L - 1) / T;
   if (!attn_cls_ok(T, seqlen)) return hipErrorInvalidValue;
+  const int nchunk = (int)((seqlen + ATTN_CLS_CHUNK - 1) / ATTN_CLS_CHUNK);
   const unsigned grid = (unsigned)(B * heads);
   if (dtype == 0)
     attn_cls_query_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, ld_out, L, (int)T,
-                                                       (int)seqlen, (int)heads, scale);
+                                                       (int)seqlen, nchunk, (int)heads, scale);
   else
     attn_cls_query_kernel<float><<<grid, 256, 0, s>>>((const float*)qkv, (float*)out, ld_out, L, (int)T, (int)seqlen,
-                                                      (int)heads, scale);
+                                                      nchunk, (int)heads, scale);
   return hipGetLastError();
 }
 

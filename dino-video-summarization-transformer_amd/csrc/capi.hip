@@ -408,7 +408,7 @@ int dsvt_attn_spatial_cls_fwd(int dtype, const void* qkv, void* out, int64_t ld_
   REQUIRE(qkv && out && aligned16(qkv), "attn_spatial_cls: null/misaligned pointer");
   REQUIRE(head_dim == 64, "attn_spatial_cls: head_dim must be 64");
   REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_cls: need (L-1) %% T == 0");
-  REQUIRE(attn_cls_ok(T, 1 + (L - 1) / T), "attn_spatial_cls: need T <= 64 and 1 + (L-1)/T <= 1024");
+  REQUIRE(attn_cls_ok(T, 1 + (L - 1) / T), "attn_spatial_cls: need T * ceil((1 + (L-1)/T) / 1024) <= 64");
   const int64_t C = heads * 64;
   REQUIRE(ld_out >= C, "attn_spatial_cls: ld_out must be >= C");
   const int64_t seqlen = 1 + (L - 1) / T;

@@ -104,8 +104,8 @@ class Block(nn.Module):
         """One block on the fp32 token tensor X (in place).  ctx: per-forward buffers.
         probs (divided only): stop after the spatial softmax and write it there -- the
         return_attn path of timesformer.py:155-157 (X is then left mid-block).
-        cls_tail (divided, the LAST block of a CLS-only forward): after the temporal branch and
-        the spatial qkv (the keys / values of every row), only the CLS rows are carried on -- see
+        cls_tail (the LAST block of a CLS-only forward): after the temporal branch and the
+        spatial qkv (the keys / values of every row), only the CLS rows are carried on -- see
         _run_cls_tail."""
         w = ctx.w
         if cls_tail:
@@ -163,8 +163,24 @@ class Block(nn.Module):
         The CLS features are those of the full block (tests/test_gpu_model.py::
         test_cls_tail_matches_full_block)."""
         w = ctx.w
-        B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
         heads = self.attn.num_heads
+        if self.attention_type != 'divided_space_time':
+            # joint / space-only (:120-123, 338-340): one contiguous sequence per clip (frame), its CLS
+            # query over all L rows
+            nb, L = ctx.nb, ctx.L
+            cmap = (1, L, 0)
+            ops.ln_gemm(X, None, nb * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, w(self.attn.qkv.weight),
+                        self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            o_cls, h_cls = ctx.o[:nb], ctx.hid[:nb]
+            ops.attn_spatial_cls(ctx.qkv, o_cls, nb, 1, L, heads, self.attn.scale)
+            ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap,
+                     M=nb)
+            ops.ln_gemm(X, cmap, nb, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
+                        self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
+            ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap,
+                     M=nb)
+            return
+        B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
         R = B * Np * T
         patch_map = (Np * T, L, 1)
         cls_map = (1, L, 0)                 # CLS row b -> X row b*L
@@ -353,8 +369,8 @@ class VisionTransformer(nn.Module):
         # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
         # bit-identical to the unsplit batch at 16 clips (tools/split_bench.py)
         self.dsvt_streams = os.environ.get("DSVT_STREAMS", "auto")
-        # divided, CLS-only forwards (get_all / get_attn off): the last block carries only the CLS
-        # rows past its spatial qkv (Block._run_cls_tail) -- its patch-row outputs are discarded by
+        # CLS-only forwards (get_all / get_attn off): the last block carries only the CLS rows past
+        # its (spatial) qkv (Block._run_cls_tail) -- its patch-row outputs are discarded by
         # the reference (x[:, 0] after the final norm).  DSVT_CLS_TAIL=0 runs the full last block.
         self.cls_tail = os.environ.get("DSVT_CLS_TAIL", "1") != "0"
         self._wcache = WeightCache()
@@ -446,14 +462,14 @@ class VisionTransformer(nn.Module):
             rows = B * (1 + (shape[2] // 16) * (shape[3] // 16) * shape[1])
             k = max(1, min(3, rows // SPLIT_ROWS))
         k = min(int(k), B)
-        # Inside a HIP-graph capture the batch is split only when this forward is not already
-        # one of several concurrent calls (dino_forward / MultiCropWrapper forks): the split's
-        # fork would then sit under theirs, and a two-level fork tree crashes capture_end on this
-        # ROCm stack (dsvt.utils.nested_capture_fork; run_concurrent also refuses to nest).  Eager
-        # forwards split either way (bitwise the same features).
+        # The batch is split only when this forward is not already one of several concurrent
+        # calls (dino_forward / MultiCropWrapper forks): their streams already overlap, and under
+        # HIP-graph capture the split's fork would sit under theirs -- a two-level fork tree
+        # crashes capture_end on this ROCm stack (dsvt.utils.nested_capture_fork; run_concurrent
+        # also refuses to nest).  The same rule in eager mode keeps eager and captured forwards
+        # bitwise equal (the split changes the GEMMs' row counts, hence their kernels).
         from ..utils import fork_depth
-        if k > 1 and not get_attn and clips[0].is_cuda and not self._grad_path() \
-                and not (torch.cuda.is_current_stream_capturing() and fork_depth() > 0):
+        if k > 1 and not get_attn and clips[0].is_cuda and not self._grad_path() and fork_depth() == 0:
             return self._forward_split(clips, B, k, shape, get_all, out)
         srcs = [(c, None, c.shape[0]) for c in clips]
         return self._forward_sources(srcs, B, shape[1], shape[2], shape[3], shape[0], get_all, get_attn, out)
@@ -595,8 +611,9 @@ class VisionTransformer(nn.Module):
             # output tokens (un-normed)
             self.blocks[-1].run(X, ctx)
             return X.view(ctx.nb, ctx.L, C)
-        cls_tail = (self.cls_tail and not get_all and self.attention_type == 'divided_space_time'
-                    and not (ctx.fuse_ln or ctx.split_resid) and ops.attn_cls_ok(T, ctx.L))
+        divided = self.attention_type == 'divided_space_time'
+        cls_tail = (self.cls_tail and not get_all and not (ctx.fuse_ln or ctx.split_resid)
+                    and ops.attn_cls_ok(T if divided else 1, ctx.L))
         for i, blk in enumerate(self.blocks):
             ctx.next_ln = (self.blocks[i + 1].temporal_norm1
                            if ((ctx.fuse_ln or ctx.split_resid) and i + 1 < nblk) else None)

@@ -246,8 +246,9 @@ def attn_spatial_probs(qkv, out, probs, B, T, L, heads, scale, ws):
 
 
 def attn_cls_ok(T, L):
-    """dsvt_attn_spatial_cls_fwd's limits: T <= 64 frames, 1 + N <= 1024 keys per frame sequence."""
-    return 1 <= T <= 64 and L > 1 and (L - 1) % T == 0 and 1 + (L - 1) // T <= 1024
+    """dsvt_attn_spatial_cls_fwd's limits: T frame sequences of 1 + (L-1)/T keys, split in chunks of
+    1024 keys, at most 64 (frame, chunk) items."""
+    return T >= 1 and L > 1 and (L - 1) % T == 0 and T * -(-(1 + (L - 1) // T) // 1024) <= 64
 
 
 def attn_spatial_cls(qkv, out, B, T, L, heads, scale):

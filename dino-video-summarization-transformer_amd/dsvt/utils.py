@@ -1,5 +1,6 @@
 """Drop-in for utils.utils.MultiCropWrapper (utils/utils.py:564-609), plus the concurrent
 teacher/student forward of one DINO step."""
+import os
 import threading
 
 import torch
@@ -26,12 +27,26 @@ def nested_capture_fork(device):
     return torch.cuda.is_current_stream_capturing() and torch.cuda.current_stream(device).cuda_stream in _SLOT_OF
 
 
+def _slot_priority(slot):
+    """DSVT_SIDE_PRIO="slot:prio,..." (A/B knob; integer slots only): HIP stream priority of a side
+    stream (lower = higher priority; torch's range on this stack is -1 .. 0)."""
+    import os
+    spec = os.environ.get("DSVT_SIDE_PRIO")
+    if not spec or not isinstance(slot, int):
+        return 0
+    for item in spec.split(","):
+        k, v = item.split(":")
+        if int(k) == slot:
+            return int(v)
+    return 0
+
+
 def side_stream(device, slot):
     """A persistent non-default HIP stream per (device, slot), created on first use."""
     key = (torch.device(device), slot)
     st = _SIDE_STREAMS.get(key)
     if st is None:
-        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=key[0])
+        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=key[0], priority=_slot_priority(slot))
         _SLOT_OF[st.cuda_stream] = slot
     return st
 
@@ -85,7 +100,6 @@ def prepare_weights(module):
 
 
 def _groupable(student, teacher, images):
-    import os
     if os.environ.get("DSVT_GROUPED", "0") not in ("1", "2") or not images[0].is_cuda:
         return False
     if not all(isinstance(m, MultiCropWrapper) and not m.vary_fr for m in (student, teacher)):

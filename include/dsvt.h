@@ -223,10 +223,11 @@ int dsvt_attn_spatial_fwd(int dtype, const void *qkv, void *out, int64_t B, int6
                           int64_t workspace_bytes, void *stream);
 /* The CLS output ONLY of dsvt_attn_spatial_fwd: for every frame sequence (b,t) the attention of
  * the CLS query (row b*L) over CLS + the N patch rows of frame t, averaged over t, written to
- * out[b*ld_out + c] (c < C; compact rows).  Replaces the last divided block's spatial attention
- * when VisionTransformer.forward_features returns the CLS token only (models/timesformer.py:
- * 139-167, 341-345): that block's patch-row outputs never reach the result.  T <= 64,
- * 1 + N <= 1024. */
+ * out[b*ld_out + c] (c < C; compact rows).  Replaces the last block's attention when
+ * VisionTransformer.forward_features returns the CLS token only (models/timesformer.py:139-167,
+ * 341-345): that block's patch-row outputs never reach the result.  T = 1 is the joint /
+ * space-only case: sequence b = the L contiguous rows b*L ... (models/timesformer.py:120-123).
+ * T * ceil((1 + (L-1)/T) / 1024) <= 64. */
 int dsvt_attn_spatial_cls_fwd(int dtype, const void *qkv, void *out, int64_t ld_out, int64_t B, int64_t T,
                               int64_t L, int64_t heads, int64_t head_dim, float scale, void *stream);
 /* dsvt_attn_spatial_fwd with the output of sequence (b,t) scaled by seq_scale[b*T + t] before the

@@ -458,12 +458,14 @@ def test_attn_spatial_cls_mean(dtype, B, T, N, heads):
 
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,T,N,heads", [(2, 1, 4, 3), (2, 3, 36, 12), (3, 8, 196, 12), (2, 4, 49, 3),
-                                         (1, 2, 150, 1), (1, 16, 255, 2), (2, 5, 300, 2)])
+                                         (1, 2, 150, 1), (1, 16, 255, 2), (2, 5, 300, 2), (2, 1, 3136, 2),
+                                         (1, 1, 1500, 3), (1, 3, 1100, 1)])
 def test_attn_spatial_cls_only(dtype, B, T, N, heads):
     """dsvt_attn_spatial_cls_fwd (the last block of a CLS-only forward): the CLS row of
     spatial_ref -- mean over frames of the CLS query's attention over CLS + the frame's patches --
     into compact [B, C] rows (here with a row stride wider than C), against float64; bitwise
-    repeatable; the rest of the output untouched."""
+    repeatable; the rest of the output untouched.  T = 1 with > 1024 keys is the joint case
+    (config 4: 1 + 3136 keys in 4 chunks merged by log-sum-exp)."""
     C, L = heads * 64, 1 + N * T
     qkv = rnd((B * L, 3 * C), 14, 1.5)
     Q = to(qkv, dtype)

@@ -114,6 +114,31 @@ def test_cls_tail_matches_full_block(base_sd, dtype):
             FP32_TOL if dtype == torch.float32 else BF16_TOL)
 
 
+@pytest.mark.parametrize("attn", ["joint_space_time", "space_only"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cls_tail_joint_space_only(attn, dtype):
+    """The CLS-only last block of the joint and space-only models (one contiguous sequence per
+    clip / frame, its CLS query over every row): equal to the full last block -- 1e-5 in fp32,
+    1e-2 in bf16 -- at 4 x 64^2 and T = 8 (joint: 129 keys; space-only: 17 keys per frame, frame
+    mean after) and for joint at 16 x 128^2 (1 + 1024 keys: two key chunks)."""
+    cfg = dict(embed_dim=192, num_heads=3, depth=2, img_size=128, num_frames=16, attention_type=attn)
+    m = tsf(P.timesformer_state(2101, **cfg), dtype, **cfg)
+    cases = [P.clip(2102, (2, 3, 8, 64, 64))]
+    if attn == "joint_space_time":
+        cases.append(P.clip(2103, (1, 3, 16, 128, 128)))
+    with torch.no_grad():
+        for x in cases:
+            xc = cu(x)
+            m.cls_tail = True
+            y_tail = m(xc).clone()
+            m.cls_tail = False
+            y_full = m(xc).clone()
+            e = rel(y_tail.cpu(), y_full.cpu())
+            print("cls_tail", attn, dtype, tuple(x.shape), e)
+            assert torch.isfinite(y_tail).all()
+            assert e < (1e-5 if dtype == torch.float32 else 1e-2), e
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_TOL)])
 def test_base_divided_unfolded_golden(base_sd, dtype, tol):
     """fold_temporal_fc=False runs temporal proj and temporal_fc as the reference's two
@@ -455,8 +480,8 @@ def test_capture_split_streams():
     backbone call (a one-level fork from the capture stream: split) and dino_forward (student and
     teacher already on two streams, the student's resolution groups on a third: the inner splits
     would be a two-level fork tree, which crashes capture_end on this ROCm stack, so they run
-    unsplit -- dsvt.utils.nested_capture_fork).  Both capture, and replay bitwise equal to the
-    eager (split) forward."""
+    unsplit, in eager mode too -- dsvt.utils.nested_capture_fork).  Both capture, and replay
+    bitwise equal to the eager forward."""
     from dsvt.utils import MultiCropWrapper, dino_forward
     from dsvt.vision_transformer import DINOHead
     cfg = dict(embed_dim=768, num_heads=12, depth=2, img_size=224, num_frames=8)
