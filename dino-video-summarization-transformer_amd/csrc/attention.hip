@@ -668,16 +668,16 @@ hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t n
 //   divided (T frames): sequence (b, t) = CLS row b*L + the N patch rows 1 + n*T + t of frame t;
 //     the T outputs are averaged (the reference's cls_token mean over frames);
 //   joint / space-only (T = 1): sequence b = the L contiguous rows of clip (or frame) b.
-// One 256-thread workgroup per (sequence group b, head).  The work items are (t, key chunk) with
-// chunks of ATTN_CLS_CHUNK keys; wave w takes items w, w+4, ...  Each item leaves its running
-// max m, sum l and unnormalized P.V row in LDS; a frame's chunks are merged with the usual
-// log-sum-exp rescale and the frames summed in order (deterministic).
-// Lane layout: 8 groups of 8 lanes; a group owns one key row per step, a lane 8 of its 64 dims
-// (one 16-byte piece of bf16 / two of fp32), so one wave instruction reads 8 whole 128-B rows.
-// Out: out[b * ld_out + h*64 + d] in the storage dtype (compact [nb, C] rows for the CLS-row
-// projection GEMM that follows).  T * chunks <= ATTN_CLS_ITEMS.
-constexpr int ATTN_CLS_CHUNK = 1024;
-constexpr int ATTN_CLS_ITEMS = 64;
+// Split-K over the keys ("flash decoding"), two launches:
+//   attn_cls_part_kernel: one wave per (b, t, head, chunk of ATTN_CLS_CHUNK keys) -- 1536 waves
+//     for the bench's 16 global clips, 312 for config 4's two joint clips -- leaves the chunk's
+//     max m, sum l and unnormalized P.V row (66 floats) in the workspace;
+//   attn_cls_merge_kernel: one thread per (b, channel): a frame's chunks merged with the
+//     log-sum-exp rescale, the frames summed in order (deterministic), / T.
+// Lane layout in a wave: 8 groups of 8 lanes; a group owns one key row per step, a lane 8 of its
+// 64 dims (one 16-byte piece of bf16 / two of fp32), so one wave instruction reads 8 whole 128-B
+// rows; the score loop is unrolled by 2 (16 keys, two rows' loads in flight per lane).
+constexpr int ATTN_CLS_CHUNK = 256;
 
 template <typename TI>
 __device__ __forceinline__ void load8f(const TI* p, float (&v)[8]) {
@@ -692,123 +692,142 @@ __device__ __forceinline__ void load8f(const TI* p, float (&v)[8]) {
 }
 
 template <typename TI>
-__global__ __launch_bounds__(256) void attn_cls_query_kernel(const TI* __restrict__ qkv, TI* __restrict__ out,
-                                                             int64_t ld_out, int64_t L, int T, int seqlen, int nchunk,
-                                                             int heads, float scale) {
-  __shared__ float sc[4][ATTN_CLS_CHUNK];            // per-wave scores -> probabilities of one chunk
-  __shared__ float po[ATTN_CLS_ITEMS][64];           // per-item unnormalized P.V
-  __shared__ float pm[ATTN_CLS_ITEMS], pl[ATTN_CLS_ITEMS];
-  const int b = blockIdx.x / heads, h = blockIdx.x % heads;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+__global__ __launch_bounds__(256) void attn_cls_part_kernel(const TI* __restrict__ qkv, float* __restrict__ part,
+                                                            int64_t items, int64_t L, int T, int seqlen, int nchunk,
+                                                            int heads, float scale) {
+  __shared__ float sc[4][ATTN_CLS_CHUNK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t item = (int64_t)blockIdx.x * 4 + w;       // ((b * T + t) * heads + h) * nchunk + chunk
+  if (item >= items) return;                               // wave-uniform; no block barrier below
+  const int chunk = (int)(item % nchunk);
+  const int64_t bth = item / nchunk;
+  const int h = (int)(bth % heads);
+  const int64_t bt = bth / heads;
+  const int t = (int)(bt % T);
+  const int64_t b = bt / T;
   const int grp = lane >> 3, c = lane & 7;
   const int64_t C = (int64_t)heads * 64, ld = 3 * C;
-  const TI* base = qkv + (int64_t)b * L * ld;
+  const TI* base = qkv + b * L * ld;
+  const int j0c = chunk * ATTN_CLS_CHUNK, nk = min(seqlen - j0c, ATTN_CLS_CHUNK);
+  auto key_row = [&](int j) -> int64_t { return j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t; };
   float q[8];
   load8f(base + h * 64 + c * 8, q);
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] *= scale;
   float* s = sc[w];
-  const int items = T * nchunk;
-  for (int it = w; it < items; it += 4) {
-    const int t = it / nchunk, j0c = (it % nchunk) * ATTN_CLS_CHUNK;
-    const int j1c = min(seqlen, j0c + ATTN_CLS_CHUNK);
-    // scores: key j of sequence t = CLS row (j = 0) or row 1 + (j-1)*T + t
-    float mx = -INFINITY;
-    for (int j0 = j0c; j0 < j1c; j0 += 8) {
-      const int j = j0 + grp;
-      float part = 0.f;
-      if (j < j1c) {
-        const int64_t row = j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t;
-        float k[8];
-        load8f(base + row * ld + C + h * 64 + c * 8, k);
+  float mx = -INFINITY;
+  for (int j0 = 0; j0 < nk; j0 += 16) {
+    float part[2];
+    int jj[2];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) part = fmaf(q[i], k[i], part);
+    for (int u = 0; u < 2; ++u) {
+      jj[u] = j0 + 8 * u + grp;
+      const int jl = jj[u] < nk ? jj[u] : nk - 1;          // clamped: loads stay in bounds
+      float k[8];
+      load8f(base + key_row(j0c + jl) * ld + C + h * 64 + c * 8, k);
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a = fmaf(q[i], k[i], a);
+      part[u] = a;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      part[u] += __shfl_xor(part[u], 1);
+      part[u] += __shfl_xor(part[u], 2);
+      part[u] += __shfl_xor(part[u], 4);
+      if (jj[u] < nk) {
+        if (c == 0) s[jj[u]] = part[u];
+        mx = fmaxf(mx, part[u]);
       }
-      part += __shfl_xor(part, 1);
-      part += __shfl_xor(part, 2);
-      part += __shfl_xor(part, 4);
-      if (j < j1c) {
-        if (c == 0) s[j - j0c] = part;
-        mx = fmaxf(mx, part);
-      }
     }
-#pragma unroll
-    for (int o = 8; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    float sum = 0.f;
-    for (int j = lane; j < j1c - j0c; j += 64) {
-      const float e = __expf(s[j] - mx);
-      s[j] = e;
-      sum += e;
-    }
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // P.V: group grp takes keys j = j0c + grp (mod 8), lane c dims c*8 .. c*8+7
-    float acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-    for (int j = j0c + grp; j < j1c; j += 8) {
-      const int64_t row = j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t;
-      float v[8];
-      load8f(base + row * ld + 2 * C + h * 64 + c * 8, v);
-      const float pj = s[j - j0c];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, v[i], acc[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      acc[i] += __shfl_xor(acc[i], 8);
-      acc[i] += __shfl_xor(acc[i], 16);
-      acc[i] += __shfl_xor(acc[i], 32);
-    }
-    if (grp == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) po[it][c * 8 + i] = acc[i];
-    }
-    if (lane == 0) {
-      pm[it] = mx;
-      pl[it] = sum;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   }
-  __syncthreads();
-  if (tid < 64) {
-    float m = 0.f;
-    for (int t = 0; t < T; ++t) {
-      float M = -INFINITY;
-      for (int k = 0; k < nchunk; ++k) M = fmaxf(M, pm[t * nchunk + k]);
-      float l = 0.f, o = 0.f;
-      for (int k = 0; k < nchunk; ++k) {
-        const float f = __expf(pm[t * nchunk + k] - M);
-        l = fmaf(pl[t * nchunk + k], f, l);
-        o = fmaf(po[t * nchunk + k][tid], f, o);
-      }
-      m += o / l;
-    }
-    out[(int64_t)b * ld_out + h * 64 + tid] = Elem<TI>::from_f(m / (float)T);
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  float sum = 0.f;
+  for (int j = lane; j < nk; j += 64) {
+    const float e = __expf(s[j] - mx);
+    s[j] = e;
+    sum += e;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // P.V: group grp takes keys grp (mod 8) of the chunk, lane c dims c*8 .. c*8+7
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int j = grp; j < nk; j += 16) {
+    const int j2 = j + 8 < nk ? j + 8 : j;
+    float v0[8], v1[8];
+    load8f(base + key_row(j0c + j) * ld + 2 * C + h * 64 + c * 8, v0);
+    load8f(base + key_row(j0c + j2) * ld + 2 * C + h * 64 + c * 8, v1);
+    const float p0 = s[j], p1 = j + 8 < nk ? s[j2] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = fmaf(p1, v1[i], fmaf(p0, v0[i], acc[i]));
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    acc[i] += __shfl_xor(acc[i], 8);
+    acc[i] += __shfl_xor(acc[i], 16);
+    acc[i] += __shfl_xor(acc[i], 32);
+  }
+  float* dst = part + item * 66;
+  if (grp == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dst[c * 8 + i] = acc[i];
+  }
+  if (lane == 0) {
+    dst[64] = mx;
+    dst[65] = sum;
   }
 }
 
-bool attn_cls_ok(int64_t T, int64_t seqlen) {
-  return T >= 1 && seqlen >= 1 && T * ((seqlen + ATTN_CLS_CHUNK - 1) / ATTN_CLS_CHUNK) <= ATTN_CLS_ITEMS;
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_cls_merge_kernel(const float* __restrict__ part, TI* __restrict__ out,
+                                                             int64_t ld_out, int64_t B, int T, int nchunk, int heads) {
+  const int64_t C = (int64_t)heads * 64;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int64_t b = i / C;
+  const int hc = (int)(i % C), h = hc >> 6, d = hc & 63;
+  float m = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float* pp = part + (((b * T + t) * heads + h) * nchunk) * 66;
+    float M = -INFINITY;
+    for (int k = 0; k < nchunk; ++k) M = fmaxf(M, pp[k * 66 + 64]);
+    float l = 0.f, o = 0.f;
+    for (int k = 0; k < nchunk; ++k) {
+      const float f = __expf(pp[k * 66 + 64] - M);
+      l = fmaf(pp[k * 66 + 65], f, l);
+      o = fmaf(pp[k * 66 + d], f, o);
+    }
+    m += o / l;
+  }
+  out[b * ld_out + hc] = Elem<TI>::from_f(m / (float)T);
+}
+
+int64_t attn_cls_ws_bytes(int64_t nseq, int64_t heads, int64_t seqlen) {
+  return nseq * heads * ((seqlen + ATTN_CLS_CHUNK - 1) / ATTN_CLS_CHUNK) * 66 * 4;
 }
 
 hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
-                           int64_t heads, float scale, hipStream_t s) {
+                           int64_t heads, float scale, float* ws, hipStream_t s) {
   const int64_t seqlen = 1 + (L - 1) / T;
-  if (!attn_cls_ok(T, seqlen)) return hipErrorInvalidValue;
   const int nchunk = (int)((seqlen + ATTN_CLS_CHUNK - 1) / ATTN_CLS_CHUNK);
-  const unsigned grid = (unsigned)(B * heads);
-  if (dtype == 0)
-    attn_cls_query_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, ld_out, L, (int)T,
-                                                       (int)seqlen, nchunk, (int)heads, scale);
-  else
-    attn_cls_query_kernel<float><<<grid, 256, 0, s>>>((const float*)qkv, (float*)out, ld_out, L, (int)T, (int)seqlen,
-                                                      nchunk, (int)heads, scale);
+  const int64_t items = B * T * heads * nchunk;
+  const unsigned g1 = (unsigned)((items + 3) / 4), g2 = (unsigned)((B * heads * 64 + 255) / 256);
+  if (dtype == 0) {
+    attn_cls_part_kernel<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)qkv, ws, items, L, (int)T, (int)seqlen, nchunk,
+                                                    (int)heads, scale);
+    attn_cls_merge_kernel<bf16_t><<<g2, 256, 0, s>>>(ws, (bf16_t*)out, ld_out, B, (int)T, nchunk, (int)heads);
+  } else {
+    attn_cls_part_kernel<float><<<g1, 256, 0, s>>>((const float*)qkv, ws, items, L, (int)T, (int)seqlen, nchunk,
+                                                   (int)heads, scale);
+    attn_cls_merge_kernel<float><<<g2, 256, 0, s>>>(ws, (float*)out, ld_out, B, (int)T, nchunk, (int)heads);
+  }
   return hipGetLastError();
 }
 

@@ -141,6 +141,7 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_AUGMENT: return up(augment_ws_bytes(M, N));                          // M = frames, N = size
     case DSVT_WS_WGRAD: return up(wgrad_workspace_floats(M, N, K) * 4);              // M = rows, N, K: G [N, K]
     case DSVT_WS_GEMM_SK: return SK_WS_BYTES;                                        // any shape
+    case DSVT_WS_ATTN_CLS: return up(attn_cls_ws_bytes(M, N, K));                    // M = B*T, N = heads, K = keys
     default: return -1;
   }
 }
@@ -403,18 +404,21 @@ int dsvt_attn_spatial_fwd(int dtype, const void* qkv, void* out, int64_t B, int6
 }
 
 int dsvt_attn_spatial_cls_fwd(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
-                              int64_t heads, int64_t head_dim, float scale, void* stream) {
+                              int64_t heads, int64_t head_dim, float scale, void* workspace, int64_t workspace_bytes,
+                              void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial_cls: bad dtype");
   REQUIRE(qkv && out && aligned16(qkv), "attn_spatial_cls: null/misaligned pointer");
   REQUIRE(head_dim == 64, "attn_spatial_cls: head_dim must be 64");
   REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_cls: need (L-1) %% T == 0");
-  REQUIRE(attn_cls_ok(T, 1 + (L - 1) / T), "attn_spatial_cls: need T * ceil((1 + (L-1)/T) / 1024) <= 64");
   const int64_t C = heads * 64;
-  REQUIRE(ld_out >= C, "attn_spatial_cls: ld_out must be >= C");
+  REQUIRE(heads >= 1 && ld_out >= C, "attn_spatial_cls: need heads >= 1, ld_out >= C");
+  REQUIRE(workspace && aligned16(workspace) &&
+              workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_CLS, dtype, B * T, heads, 1 + (L - 1) / T),
+          "attn_spatial_cls: workspace too small");
   const int64_t seqlen = 1 + (L - 1) / T;
   const double flops = 4.0 * B * T * heads * (double)seqlen * 64;
   return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, "dsvt_attn_spatial_cls_fwd", [&] {
-    return launch_attn_cls(dtype, qkv, out, ld_out, B, T, L, heads, scale, (hipStream_t)stream);
+    return launch_attn_cls(dtype, qkv, out, ld_out, B, T, L, heads, scale, (float*)workspace, (hipStream_t)stream);
   });
 }
 

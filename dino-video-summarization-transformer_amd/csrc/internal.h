@@ -153,9 +153,9 @@ bool attn_flash_ok(int dtype, const AttnParams& p);
 hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s);
 void set_attn_variant(int v);
 // CLS query only of every spatial sequence, mean over frames -> out[b * ld_out + c] (attention.hip)
-bool attn_cls_ok(int64_t T, int64_t seqlen);
+int64_t attn_cls_ws_bytes(int64_t nseq, int64_t heads, int64_t seqlen);   // nseq = B*T
 hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
-                           int64_t heads, float scale, hipStream_t s);
+                           int64_t heads, float scale, float* ws, hipStream_t s);
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T,
                                 int64_t heads, int64_t C, float scale, hipStream_t s);
 

@@ -366,7 +366,8 @@ class VisionTransformer(nn.Module):
         self.split_resid = os.environ.get("DSVT_SPLIT_RESID", "0") == "1"
         # inference: split a batch into this many clip chunks on concurrent HIP streams (each
         # kernel's last partly-filled wave of tiles then runs beside the other chunk's kernels);
-        # "auto" = one chunk per SPLIT_ROWS token rows, at most 3.  Per-clip results are
+        # "auto" = one chunk per SPLIT_ROWS token rows, at most 3 (2 from SPLIT_ROWS / 2 rows and
+        # 2 clips up).  Per-clip results are
         # bit-identical to the unsplit batch at 16 clips (tools/split_bench.py)
         self.dsvt_streams = os.environ.get("DSVT_STREAMS", "auto")
         # CLS-only forwards (get_all / get_attn off): the last block carries only the CLS rows past
@@ -461,6 +462,8 @@ class VisionTransformer(nn.Module):
         if k == "auto":
             rows = B * (1 + (shape[2] // 16) * (shape[3] // 16) * shape[1])
             k = max(1, min(3, rows // SPLIT_ROWS))
+            if k == 1 and B >= 2 and rows >= SPLIT_ROWS // 2:
+                k = 2   # e.g. config 4 (2 joint 16x224^2 clips, 6274 rows): 591-596 vs 580-584 clips/s
         k = min(int(k), B)
         # The batch is split only when this forward is not already one of several concurrent
         # calls (dino_forward / MultiCropWrapper forks): their streams already overlap, and under

@@ -246,16 +246,16 @@ def attn_spatial_probs(qkv, out, probs, B, T, L, heads, scale, ws):
 
 
 def attn_cls_ok(T, L):
-    """dsvt_attn_spatial_cls_fwd's limits: T frame sequences of 1 + (L-1)/T keys, split in chunks of
-    1024 keys, at most 64 (frame, chunk) items."""
-    return T >= 1 and L > 1 and (L - 1) % T == 0 and T * -(-(1 + (L - 1) // T) // 1024) <= 64
+    """dsvt_attn_spatial_cls_fwd's shape rule: T frame sequences of 1 + (L-1)/T keys."""
+    return T >= 1 and L > 1 and (L - 1) % T == 0
 
 
 def attn_spatial_cls(qkv, out, B, T, L, heads, scale):
     """CLS output only of attn_spatial (mean over the T frame sequences): out [B, C] rows."""
     _check(out, qkv.dtype, "out")
+    ws = _ws(_lib.WS_ATTN_CLS, torch.float32, B * T, heads, 1 + (L - 1) // T, qkv.device)
     call("dsvt_attn_spatial_cls_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.stride(0), B, T, L, heads, 64,
-         float(scale), _stream())
+         float(scale), _ptr(ws), ws.numel() * 4, _stream())
     return out
 
 

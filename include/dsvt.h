@@ -65,6 +65,7 @@ extern "C" {
 #define DSVT_WS_AUGMENT 11     /* M = output frames T, N = output size S */
 #define DSVT_WS_WGRAD 12       /* M = rows, N, K: the weight gradient is [N, K] */
 #define DSVT_WS_GEMM_SK 13     /* stream-K GEMM scratch (any shape) */
+#define DSVT_WS_ATTN_CLS 14    /* M = B*T sequences, N = heads, K = keys per sequence 1 + (L-1)/T */
 
 int dsvt_version(void);
 const char *dsvt_last_error(void);
@@ -227,9 +228,11 @@ int dsvt_attn_spatial_fwd(int dtype, const void *qkv, void *out, int64_t B, int6
  * VisionTransformer.forward_features returns the CLS token only (models/timesformer.py:139-167,
  * 341-345): that block's patch-row outputs never reach the result.  T = 1 is the joint /
  * space-only case: sequence b = the L contiguous rows b*L ... (models/timesformer.py:120-123).
- * T * ceil((1 + (L-1)/T) / 1024) <= 64. */
+ * Keys are split in chunks of 256 (one wave each) and merged; workspace >=
+ * dsvt_workspace_bytes(DSVT_WS_ATTN_CLS, ., B*T, heads, 1 + (L-1)/T). */
 int dsvt_attn_spatial_cls_fwd(int dtype, const void *qkv, void *out, int64_t ld_out, int64_t B, int64_t T,
-                              int64_t L, int64_t heads, int64_t head_dim, float scale, void *stream);
+                              int64_t L, int64_t heads, int64_t head_dim, float scale, void *workspace,
+                              int64_t workspace_bytes, void *stream);
 /* dsvt_attn_spatial_fwd with the output of sequence (b,t) scaled by seq_scale[b*T + t] before the
  * CLS mean: training-mode DropPath of the spatial branch, whose mask is per (b,t) sequence
  * (timesformer.py:159 drop_path over the [(B*T), 1+N, C] batch). */

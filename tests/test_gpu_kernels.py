@@ -464,8 +464,8 @@ def test_attn_spatial_cls_only(dtype, B, T, N, heads):
     """dsvt_attn_spatial_cls_fwd (the last block of a CLS-only forward): the CLS row of
     spatial_ref -- mean over frames of the CLS query's attention over CLS + the frame's patches --
     into compact [B, C] rows (here with a row stride wider than C), against float64; bitwise
-    repeatable; the rest of the output untouched.  T = 1 with > 1024 keys is the joint case
-    (config 4: 1 + 3136 keys in 4 chunks merged by log-sum-exp)."""
+    repeatable; the rest of the output untouched.  Keys are split in chunks of 256 merged by
+    log-sum-exp: T = 1 with 1 + 3136 keys is the joint case of config 4 (13 chunks)."""
     C, L = heads * 64, 1 + N * T
     qkv = rnd((B * L, 3 * C), 14, 1.5)
     Q = to(qkv, dtype)
@@ -484,8 +484,9 @@ def test_attn_spatial_cls_only(dtype, B, T, N, heads):
 def _lib_cls(Q, out, B, T, L, heads, scale):
     """dsvt_attn_spatial_cls_fwd with ld_out = out.shape[1] (a strided output)."""
     from dsvt import _lib, ops
+    ws = ops._ws(_lib.WS_ATTN_CLS, torch.float32, B * T, heads, 1 + (L - 1) // T, Q.device)
     _lib.call("dsvt_attn_spatial_cls_fwd", ops._dt(Q.dtype), Q.data_ptr(), out.data_ptr(), out.shape[1], B, T, L,
-              heads, 64, float(scale), ops._stream())
+              heads, 64, float(scale), ws.data_ptr(), ws.numel() * 4, ops._stream())
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 7])
