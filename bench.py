@@ -436,10 +436,12 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
-    ap.add_argument("--grouped", nargs="?", const="1", default=None, choices=["1", "2"],
+    ap.add_argument("--grouped", nargs="?", const="1", default=None, choices=["1", "2", "3", "4"],
                     help="1: run the teacher / student backbone calls as one grouped lockstep forward (DSVT_GROUPED=1; "
                          "A/B: measured 354 vs 370 clips/s for the concurrent streams); 2: group only the "
-                         "global-crop calls, the local-crop call on a concurrent stream")
+                         "global-crop calls, the local-crop call on a concurrent stream; 3: three concurrent "
+                         "grouped forwards, each over a balanced share of every call's clips; 4: the two global "
+                         "calls minus r clips each plain, one grouped call over the rest, all concurrent")
     ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-grad-overlap", dest="grad_overlap", action="store_false",
@@ -622,6 +624,14 @@ def main():
         grouped = _groupable(student, teacher, crops)
     grouped_desc = ("grouped: the teacher / student backbone calls advance in lockstep over one token buffer, every "
                     "Linear of a layer ONE launch over all calls (dsvt_gemm_grouped_fwd), one stream")
+    if os.environ.get("DSVT_GROUPED") == "4":
+        grouped_desc = ("remainder grouped: the teacher's and the student's global-crop calls minus r clips each as "
+                        "plain forwards, one grouped forward over their last r clips and the local crops, three "
+                        "concurrent HIP streams")
+    if os.environ.get("DSVT_GROUPED") == "3":
+        grouped_desc = ("balanced grouped: three concurrent HIP streams, each a lockstep grouped forward over a "
+                        "balanced share of the teacher-global, student-global and student-local clips (every Linear "
+                        "one dsvt_gemm_grouped_fwd launch per stream)")
     if os.environ.get("DSVT_GROUPED") == "2":
         grouped_desc = ("grouped global crops: the teacher's and the student's global-crop calls in lockstep, every "
                         "Linear of a layer ONE launch over both (dsvt_gemm_grouped_fwd); the local-crop call on a "

@@ -179,12 +179,56 @@ def crop_groups(x):
     return out
 
 
-def dino_forward_grouped(student, teacher, images, n_global=2, same_shape_only=False):
+def _clip_slices(tensors, a, b):
+    """The clips [a, b) of the concatenation of `tensors` (batch dim 0) as tensor slices."""
+    out, off = [], 0
+    for x in tensors:
+        n = x.shape[0]
+        lo, hi = max(a, off), min(b, off + n)
+        if lo < hi:
+            out.append(x[lo - off:hi - off])
+        off += n
+    return out
+
+
+def balanced_partition(calls, k):
+    """Split every call's clips into k contiguous ranges, one per stream, so that the streams'
+    token rows are as even as possible: calls with the longest sequences first, each clip counted
+    to the least-loaded stream, ranges then laid out in stream order.  Returns [[(call index, a, b)]
+    per stream]."""
+    load = [0] * k
+    counts = {}
+    order = sorted(range(len(calls)), key=lambda i: -calls[i][2])
+    for i in order:
+        n, L = calls[i][3], calls[i][2]
+        c = [0] * k
+        for _ in range(n):
+            s = min(range(k), key=lambda j: (load[j], j))
+            c[s] += 1
+            load[s] += L
+        counts[i] = c
+    parts = [[] for _ in range(k)]
+    for i in range(len(calls)):
+        a = 0
+        for s in range(k):
+            if counts[i][s]:
+                parts[s].append((i, a, a + counts[i][s]))
+                a += counts[i][s]
+    return parts
+
+
+def dino_forward_grouped(student, teacher, images, n_global=2, same_shape_only=False, balanced=0, remainder=False):
     """train_ssl.py:523-527 (student on all crops, teacher on the global crops) with the three
     backbone calls grouped; the heads run on the features as MultiCropWrapper does.
     same_shape_only (DSVT_GROUPED=2): only the calls of the first call's clip shape (the teacher's
     and the student's global crops: identical layer shapes) are grouped; the other calls (the
-    student's local crops) run as plain forwards on a concurrent stream beside the group."""
+    student's local crops) run as plain forwards on a concurrent stream beside the group.
+    balanced = k > 1 (DSVT_GROUPED=3, k = 3): k concurrent grouped forwards, each over a share of
+    EVERY call's clips (balanced_partition), so the k streams carry equal work and every launch
+    is a grouped one.
+    remainder (DSVT_GROUPED=4): the teacher's and the student's global-crop calls as two plain
+    forwards of n - r clips each, and ONE grouped forward over their last r clips and the local
+    crops, all three concurrent (r balancing the three streams' rows)."""
     s_groups = crop_groups(images)
     t_groups = crop_groups(images[:n_global])
     calls = [(teacher.backbone, g) for g in t_groups] + [(student.backbone, g) for g in s_groups]
@@ -202,7 +246,42 @@ def dino_forward_grouped(student, teacher, images, n_global=2, same_shape_only=F
         n = sum(x.shape[0] for x in g)
         outs.append(s_feats[r:r + n])
         r += n
-    if same_shape_only:
+    if remainder and len(calls) == 3 and tuple(calls[0][1][0].shape[1:]) == tuple(calls[1][1][0].shape[1:]):
+        # two plain calls (teacher / student global crops minus r clips each) + one grouped call
+        # over the rest (their last r clips and the local crops), r balancing the three streams
+        from .utils import run_concurrent
+        for m in (teacher.backbone, student.backbone):
+            m.prepare_weights()
+        g0 = calls[0][1][0]
+        Lg = 1 + (g0.shape[3] // 16) * (g0.shape[4] // 16) * g0.shape[2]
+        l0 = calls[2][1][0]
+        nl = sum(x.shape[0] for x in calls[2][1])
+        rows_l = nl * (1 + (l0.shape[3] // 16) * (l0.shape[4] // 16) * l0.shape[2])
+        nt, ns = (sum(x.shape[0] for x in calls[i][1]) for i in (0, 1))
+        n = min(nt, ns)
+        r = min(range(n), key=lambda q: max((n - q) * Lg, 2 * q * Lg + rows_l))
+        (mt, gt), (ms, gs), (ml, gl) = calls
+        thunks = [lambda: mt.forward_features(_clip_slices(gt, 0, nt - r), out=outs[0][:nt - r]),
+                  lambda: ms.forward_features(_clip_slices(gs, 0, ns - r), out=outs[1][:ns - r])]
+        rest = ([(mt, _clip_slices(gt, nt - r, nt)), (ms, _clip_slices(gs, ns - r, ns))] if r else []) + [(ml, gl)]
+        rest_out = ([outs[0][nt - r:], outs[1][ns - r:]] if r else []) + [outs[2]]
+        thunks.append(lambda: forward_features_grouped(rest, rest_out))
+        run_concurrent(thunks, dev, slot0=24)
+    elif balanced > 1:
+        from .utils import run_concurrent
+        for m in (teacher.backbone, student.backbone):
+            m.prepare_weights()
+        info = []
+        for m, g in calls:
+            Hp, Wp = g[0].shape[3] // 16, g[0].shape[4] // 16
+            info.append((m, g, 1 + Hp * Wp * g[0].shape[2], sum(x.shape[0] for x in g)))
+        parts = balanced_partition(info, balanced)
+
+        def job(part):
+            sub = [(calls[i][0], _clip_slices(calls[i][1], a, b)) for i, a, b in part]
+            return lambda: forward_features_grouped(sub, [outs[i][a:b] for i, a, b in part])
+        run_concurrent([job(p) for p in parts if p], dev, slot0=24)
+    elif same_shape_only:
         from .utils import run_concurrent
         shp = tuple(calls[0][1][0].shape[1:])
         grp = [i for i, (_, g) in enumerate(calls) if tuple(g[0].shape[1:]) == shp]

@@ -100,7 +100,7 @@ def prepare_weights(module):
 
 
 def _groupable(student, teacher, images):
-    if os.environ.get("DSVT_GROUPED", "0") not in ("1", "2") or not images[0].is_cuda:
+    if os.environ.get("DSVT_GROUPED", "0") not in ("1", "2", "3", "4") or not images[0].is_cuda:
         return False
     if not all(isinstance(m, MultiCropWrapper) and not m.vary_fr for m in (student, teacher)):
         return False
@@ -120,8 +120,9 @@ def dino_forward(student, teacher, images, n_global=2, concurrent=True):
     the same-shape calls (teacher and student global crops) and runs the rest beside them."""
     if _groupable(student, teacher, images):
         from .grouped import dino_forward_grouped
-        return dino_forward_grouped(student, teacher, images, n_global,
-                                    same_shape_only=os.environ.get("DSVT_GROUPED") == "2")
+        mode = os.environ.get("DSVT_GROUPED")
+        return dino_forward_grouped(student, teacher, images, n_global, same_shape_only=mode == "2",
+                                    balanced=3 if mode == "3" else 0, remainder=mode == "4")
     if not concurrent:
         return student(images), teacher(images[:n_global])
     for net in (student, teacher):

@@ -521,7 +521,7 @@ def test_capture_split_streams():
 
 
 @pytest.mark.parametrize("variant,mode,tail", [(20, "1", False), (0, "1", False), (20, "1", True), (20, "2", True),
-                                               (20, "2", False)])
+                                               (20, "2", False), (20, "3", True), (20, "4", True)])
 def test_grouped_forward_bitwise(variant, mode, tail, monkeypatch):
     """dsvt.grouped: the three backbone calls of a DINO step (teacher on 2 global crops, student on
     2 global + 2 local) as one lockstep forward with every Linear a grouped launch
@@ -530,7 +530,8 @@ def test_grouped_forward_bitwise(variant, mode, tail, monkeypatch):
     (variant 20) the student / teacher logits are BITWISE equal; with the automatic kernel choice
     (small separate calls take the 128x128 kernel) within BF16_TOL.  Also fp32 parity mode (the
     grouped op's per-segment fallback) within 1e-5.  mode "2" (DSVT_GROUPED=2) groups only the
-    global-crop calls and runs the local one beside them; tail: the CLS-only last block on both
+    global-crop calls and runs the local one beside them, mode "3" runs three concurrent grouped
+    forwards over balanced shares of every call's clips; tail: the CLS-only last block on both
     sides (the per-call CLS kernels are the separate calls' own, so still bitwise)."""
     from dsvt import _lib
     from dsvt.utils import MultiCropWrapper, dino_forward
