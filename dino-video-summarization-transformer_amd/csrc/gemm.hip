@@ -489,7 +489,8 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (p.sk_part && !p.row_scale && gemm_sk_ok(p, epi, out_f32) &&
       (g_gemm_variant == 40 || (g_gemm_variant == 0 && sk_auto(epi))))
     return 40;
-  const int gv = g_gemm_variant == 40 ? 0 : g_gemm_variant;   // forced stream-K, ineligible shape: auto
+  // forced stream-K on an ineligible shape, or 41 (auto + tail split): the automatic choice
+  const int gv = (g_gemm_variant == 40 || g_gemm_variant == 41) ? 0 : g_gemm_variant;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
   // 195 vs 254 us (persistent 256x128) and 215 vs 231 us at 25104 x 3072 x 768 (tools/aux_bench.py)
@@ -545,8 +546,51 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }
 
+// Tail split (DSVT_TAIL_SPLIT=1, opt-in): a 256x256 launch whose last round of tiles is at most
+// half full -- the global-crop residual GEMMs: 297 tiles = one round + 41; qkv: 891 = three
+// rounds + 123 -- runs its full rounds on the 256x256 kernel and the rows of the last round on the
+// 128x128 kernel (4x the tiles for the same rows: the tail round's work spread over more CUs).
+// Alone it is faster (proj 72.4 -> 61.1 us, fc2 163 -> 134 us, qkv unchanged), inside the DINO
+// step slower (374 vs 385 clips/s, three interleaved rounds): the three concurrent backbone
+// calls already fill the tail round, and the second launch waits for the whole first one.
+// Bias / plain residual epilogues only (no row scales, no aux operand); with a row map the split
+// falls on a row-group boundary so the second launch's map is the first's shifted by whole groups.
+// Returns the first launch's row count, 0 = no split.
+static int64_t tail_split_rows(const GemmParams& p, int epi) {
+  static const int on = getenv("DSVT_TAIL_SPLIT") ? atoi(getenv("DSVT_TAIL_SPLIT")) : 0;
+  // variant 41 = the automatic choice with the tail split (tests, A/B on one thread)
+  if (!(g_gemm_variant == 41 || (on && g_gemm_variant == 0)) || p.row_scale || p.nseg || p.sk_part ||
+      !(epi == EPI_BIAS || epi == EPI_RESID))
+    return 0;
+  const int64_t tn = (p.N + 255) / 256, tiles = ((p.M + 255) / 256) * tn, full = tiles / 256;
+  const int64_t rem = tiles - full * 256;
+  if (full < 1 || rem == 0 || rem * 2 > 256) return 0;
+  int64_t rows_a = (full * 256 / tn) * 256;
+  const bool ident = p.rpg >= p.M && p.goff == 0;
+  if (!ident) rows_a = p.rpg > 0 ? rows_a / p.rpg * p.rpg : 0;
+  return (rows_a > 0 && rows_a < p.M) ? rows_a : 0;
+}
+
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
+  if (v == 20) {
+    if (const int64_t ra = tail_split_rows(p, epi)) {
+      GemmParams a = p, b = p;
+      a.M = ra;
+      if (hipError_t e = launch_gemm_8ph(a, epi, out_f32, s)) return e;
+      b.M = p.M - ra;
+      b.A = (const char*)p.A + ra * p.lda * 2;
+      if (p.rpg >= p.M && p.goff == 0) {            // identity map: shift the output rows
+        const int64_t osz = (epi == EPI_RESID || out_f32) ? 4 : 2;
+        b.out = (char*)p.out + ra * p.ldo * osz;
+        if (p.resid) b.resid = p.resid + ra * p.ldo;
+        b.rpg = b.M;
+      } else {                                      // row groups: shift the map by ra / rpg groups
+        b.goff = p.goff + (ra / p.rpg) * p.gstride;
+      }
+      return launch_t<bf16_t>(b, epi, out_f32, s);
+    }
+  }
   if (v == 40) return launch_gemm_sk(p, epi, out_f32, s);
   if (v == 2) return launch_pipe(p, epi, out_f32, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);

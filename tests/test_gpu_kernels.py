@@ -212,12 +212,14 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
-@pytest.mark.parametrize("variant", [1, 2, 10, 20, 33])
+@pytest.mark.parametrize("variant", [0, 41, 1, 2, 10, 20, 33])
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8), (16, 196, 8)])
 def test_gemm_residual_k768(variant, B, Np, T):
     """The K = 768, N = 768 residual GEMM (attn.proj / folded temporal fc shape) at the bench's
     row counts on the 128x128 kernel and the 256x256 one: through the temporal row map (CLS rows
-    untouched) and on all rows, in place and out of place, against float64."""
+    untouched) and on all rows, in place and out of place, against float64.  Variant 41 (the
+    automatic choice with the opt-in tail split) at 16 clips: the first 21 760 rows (20 384
+    through the row map: 13 whole row groups) on the 256x256 kernel, the rest on the 128x128 one."""
     from dsvt import ops
     from dsvt._lib import EPI_BIAS_RESID
     C = 768
@@ -246,6 +248,50 @@ def test_gemm_residual_k768(variant, B, Np, T):
                 assert np.all(back(Xo)[np.arange(B) * L] == 3.0)
     finally:
         _lib_set("dsvt_set_gemm_variant", 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(25104, 2304, 768), (25104, 768, 3072), (21761, 768, 768)])
+def test_gemm_tail_split(M, N, K):
+    """The automatic kernel choice's tail split (gemm.hip tail_split_rows): a 256x256 launch whose
+    last round is at most half full runs its last round's rows on the 128x128 kernel -- qkv at
+    25 104 rows (891 tiles = 3 rounds + 123), the fc2 shape (297 = 1 round + 41), and a ragged
+    split point.  Against torch fp32 on the same bf16 operands, against the unsplit 256x256
+    launch (variant 20 forced: bitwise identical rows before the split, within rounding after), and
+    bitwise repeatable.  (Opt-in in the product: DSVT_TAIL_SPLIT=1; here variant 41 = the automatic
+    choice with the split.)"""
+    from dsvt import _lib, ops
+    from dsvt._lib import EPI_BIAS, EPI_BIAS_RESID
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g)
+    ref = (A.float() @ W.float().t() + b)
+    epi = EPI_BIAS_RESID if N == 768 else EPI_BIAS
+    x0 = torch.randn(M, N, device="cuda", generator=g)
+
+    def run():
+        out = x0.clone() if epi == EPI_BIAS_RESID else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ops.gemm(A, W, b, out, epilogue=epi)
+        return out
+    _lib.call("dsvt_set_gemm_variant", 41)
+    try:
+        outs = [run(), run()]
+    finally:
+        _lib.call("dsvt_set_gemm_variant", 0)
+    assert torch.equal(outs[0], outs[1])
+    got = outs[0].float() - (x0 if epi == EPI_BIAS_RESID else 0)
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (1e-5 if epi == EPI_BIAS_RESID else 8e-3), err
+    _lib.call("dsvt_set_gemm_variant", 20)          # forced 256x256: no split
+    try:
+        whole = run()
+    finally:
+        _lib.call("dsvt_set_gemm_variant", 0)
+    torch.cuda.synchronize()
+    ra = 85 * 256                                    # the first launch's rows for all three shapes
+    assert torch.equal(outs[0][:ra], whole[:ra]), "rows before the split differ from the 256x256 launch"
+    d = (outs[0].float() - whole.float()).abs().max().item() / ref.abs().max().item()
+    assert d < (1e-5 if epi == EPI_BIAS_RESID else 8e-3), d
 
 
 @pytest.mark.parametrize("dtype", DT)
