@@ -2,7 +2,7 @@
 # One GPU-box session: each stage under its own time limit; stop at the first crash, abort,
 # fault or timeout (exit status other than 0 = pass / 1 = test failures or Python error).
 # usage: tools/gpu_session.sh stage [stage ...]
-#   stages: kernels model gputests smoke bench prof graphprof trainprof c4prof pmc
+#   stages: kernels model gputests smoke bench prof graphprof trainprof c4prof c5prof pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
@@ -32,6 +32,8 @@ for stage in "$@"; do
              python tools/prof_summary.py "$OUT/tprof" --step-kernel 'dsvt::ema_kernel(' --per-step 1 > "$OUT/tprof_summary.txt" ;;
     c4prof)  run c4prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c4prof" -o run -- python3 tools/cfg_bench.py c4 --reps 5 --warm 2 &&
              python tools/prof_summary.py "$OUT/c4prof" > "$OUT/c4prof_summary.txt" ;;
+    c5prof)  run c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5prof" -o run -- python3 tools/cfg_bench.py c5 --reps 5 --warm 2 &&
+             python tools/prof_summary.py "$OUT/c5prof" > "$OUT/c5prof_summary.txt" ;;
     pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
              run pmc2 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
              python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" > "$OUT/pmc_summary.txt" ;;
