@@ -98,8 +98,87 @@ __global__ __launch_bounds__(256) void swin_ln_rows_kernel(const float* __restri
   }
 }
 
+// The same for the narrow stages (C = 96 / 192 / 384): LPR lanes per row, 64 / LPR rows per wave,
+// each lane VPL = C / LPR contiguous columns (8-byte loads, 4-byte bf16-pair stores), the row sums
+// over the LPR-lane group by xor shuffles.  One wave per row left 2/3 of the lanes idle at C = 96
+// and made config 5's stage-1 norms (100 352 rows) latency-bound: 24 us per call.
+template <typename T, int C, int LPR>
+__global__ __launch_bounds__(256) void swin_ln_rows_small_kernel(const float* __restrict__ x,
+                                                                 const int32_t* __restrict__ idx,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, T* __restrict__ out,
+                                                                 int64_t rows, int ldo, float eps) {
+  constexpr int VPL = C / LPR, RPW = 64 / LPR;
+  static_assert(C % LPR == 0 && VPL % 2 == 0 && 64 % LPR == 0, "row split");
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t m = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool live = m < rows;
+  const int64_t src = live ? (idx ? (int64_t)idx[m] : m) : -1;
+  float v[VPL];
+  float s = 0.f;
+  if (src >= 0) {
+    const float2* xr = reinterpret_cast<const float2*>(x + src * C + sub * VPL);
+#pragma unroll
+    for (int i = 0; i < VPL / 2; ++i) {
+      const float2 t = xr[i];
+      v[2 * i] = t.x;
+      v[2 * i + 1] = t.y;
+      s += t.x + t.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] = 0.f;
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o);
+  const float mean = s * (1.0f / C);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    v[i] -= mean;
+    q += v[i] * v[i];
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) q += __shfl_xor(q, o);
+  const float rstd = 1.0f / sqrtf(q * (1.0f / C) + eps);
+  if (!live) return;
+  T* o = out + m * ldo;
+  const int c0 = sub * VPL;
+#pragma unroll
+  for (int i = 0; i < VPL; i += 2) {
+    float a = 0.f, b = 0.f;
+    if (src >= 0) {                    // the reference pads with zeros AFTER norm1
+      a = v[i] * rstd * gamma[c0 + i] + beta[c0 + i];
+      b = v[i + 1] * rstd * gamma[c0 + i + 1] + beta[c0 + i + 1];
+    }
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<unsigned*>(o + c0 + i) = pack_bf16x2(a, b);
+    } else {
+      *reinterpret_cast<float2*>(o + c0 + i) = make_float2(a, b);
+    }
+  }
+  for (int c = C + sub; c < ldo; c += LPR) o[c] = Elem<T>::from_f(0.f);   // zero K padding
+}
+
 hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, const float* gamma, const float* beta,
                                void* out, int64_t rows, int64_t C, int64_t ldo, float eps, hipStream_t s) {
+#define DSVT_SLN(CC, LPR)                                                                                      \
+  {                                                                                                             \
+    const unsigned nb = (unsigned)((rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR)));                           \
+    if (dtype == 0)                                                                                             \
+      swin_ln_rows_small_kernel<bf16_t, CC, LPR><<<nb, 256, 0, s>>>(x, idx, gamma, beta, (bf16_t*)out, rows,   \
+                                                                   (int)ldo, eps);                            \
+    else                                                                                                        \
+      swin_ln_rows_small_kernel<float, CC, LPR><<<nb, 256, 0, s>>>(x, idx, gamma, beta, (float*)out, rows,     \
+                                                                  (int)ldo, eps);                             \
+    return hipGetLastError();                                                                                   \
+  }
+  if (((uintptr_t)x & 7) == 0 && ((uintptr_t)out & 3) == 0 && ldo % 2 == 0) {
+    if (C == 96) DSVT_SLN(96, 16)
+    if (C == 192) DSVT_SLN(192, 16)
+    if (C == 384) DSVT_SLN(384, 32)
+  }
+#undef DSVT_SLN
   const unsigned blocks = (unsigned)((rows + 3) / 4);
   if (dtype == 0)
     swin_ln_rows_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, idx, gamma, beta, (bf16_t*)out, rows, (int)C, (int)ldo, eps);

@@ -60,3 +60,31 @@ def test_swin_forward_vs_reference(gold, dtype, tag, kw, shape, seed):
     assert got.shape == ref.shape
     err = np.max(np.abs(got - ref)) / np.max(np.abs(ref))
     assert err < TOL[dtype], err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,ldo", [(96, 128), (192, 192), (384, 384), (768, 768), (64, 64)])
+def test_swin_ln_rows_gather(dtype, C, ldo):
+    """dsvt_swin_ln_rows_fwd (norm1 + window-partition gather, swin_transformer.py:221-237): rows
+    gathered through an index with -1 = the reference's zero padding (applied AFTER the norm),
+    zero K-padding columns C..ldo, against torch.nn.functional.layer_norm -- the narrow-row kernel
+    (C = 96 / 192 / 384) and the one-wave-per-row one (768, 64), 1001 rows (ragged)."""
+    from dsvt import ops
+    g = torch.Generator(device="cuda").manual_seed(C)
+    src_rows, rows = 900, 1001
+    x = torch.randn(src_rows, C, device="cuda", generator=g) * 2 + 0.5
+    idx = torch.randint(-1, src_rows, (rows,), device="cuda", generator=g, dtype=torch.int64).to(torch.int32)
+    ln = torch.nn.LayerNorm(C, eps=1e-5).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(torch.rand(C, device="cuda", generator=g) + 0.5)
+        ln.bias.copy_(torch.randn(C, device="cuda", generator=g) * 0.1)
+    out = torch.full((rows, ldo), 7.0, device="cuda", dtype=dtype)
+    ops.swin_ln_rows(x, idx, ln, out, rows)
+    with torch.no_grad():
+        ref = torch.zeros(rows, ldo, device="cuda")
+        valid = idx >= 0
+        ref[valid, :C] = torch.nn.functional.layer_norm(x[idx[valid].long()], (C,), ln.weight, ln.bias, 1e-5)
+    err = (out.float() - ref).abs().max().item()
+    assert err < (2e-5 if dtype == torch.float32 else 3e-2), err
+    assert (out[~valid].float() == 0).all() and (out[:, C:].float() == 0).all()

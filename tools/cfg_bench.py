@@ -31,7 +31,8 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(1)
     if args.cfg == "c5":
-        m = SwinTransformer3D().to(dev).eval()
+        m = SwinTransformer3D().to(dev)
+        m.eval()                        # returns None, as the reference's (swin_transformer.py:684-687)
         x = torch.randn(8, 3, 8, 224, 224, device=dev)
         n, gf = 8, swin_t_flops() / 1e9
     else:
