@@ -167,6 +167,21 @@ __device__ __forceinline__ float gelu_bf16out(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * p));
 }
 
+// gelu_bf16out on a PAIR of values: the same operations, the non-transcendental ones as packed
+// fp32 VALU (v_pk_mul / v_pk_fma / v_pk_add_f32: two lanes' worth per instruction) -- bitwise the
+// scalar form's results, ~12 instead of 18 instructions per pair in the VALU-bound fc1 epilogue.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v gelu_bf16out2(f2v x) {
+  f2v x2 = x * x;
+  x2.x = fminf(x2.x, 100.0f);
+  x2.y = fminf(x2.y, 100.0f);
+  const f2v c0 = {1.01426306e-03f, 1.01426306e-03f}, c1 = {-1.06775724e-01f, -1.06775724e-01f};
+  const f2v c2 = {-2.30112134e+00f, -2.30112134e+00f}, one = {1.0f, 1.0f};
+  const f2v t = x * __builtin_elementwise_fma(__builtin_elementwise_fma(c0, x2, c1), x2, c2);
+  const f2v d = one + f2v{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  return x * f2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 // the inference GELU epilogue by output type: the fast form only when the result is stored in bf16
 template <bool BF16_OUT>
 __device__ __forceinline__ float gelu_out(float x) {

@@ -248,10 +248,22 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
         for (int j = 0; j < NJ; j += 2) {
           if constexpr (EPI == EPI_GELU) {     // one fragment pair's GELUs live at a time (bf16 output)
             __builtin_amdgcn_sched_barrier(0);
+#ifndef DSVT_GELU_PK
+#define DSVT_GELU_PK 1
+#endif
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[i][j + jj][e] = gelu_out<true>(acc[i][j + jj][e]);
+              for (int e = 0; e < 4; e += 2) {   // packed pairs: bitwise gelu_out<true>
+                if constexpr (DSVT_GELU_PK) {
+                  const f2v v = gelu_bf16out2(f2v{acc[i][j + jj][e], acc[i][j + jj][e + 1]});
+                  acc[i][j + jj][e] = v.x;
+                  acc[i][j + jj][e + 1] = v.y;
+                } else {
+                  acc[i][j + jj][e] = gelu_out<true>(acc[i][j + jj][e]);
+                  acc[i][j + jj][e + 1] = gelu_out<true>(acc[i][j + jj][e + 1]);
+                }
+              }
           }
           store_pair_bf16<NT, NOSTORE>((bf16_t*)p.out + orow * p.ldo + cbase + j * 16, acc[i][j], acc[i][j + 1], g);
         }
