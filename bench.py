@@ -42,8 +42,8 @@ def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16, folded=False
     folded=True: what dsvt executes -- temporal proj and temporal_fc folded into one GEMM
     (VisionTransformer.fold_temporal_fc), i.e. one 2*R*C*C GEMM less per block.
     cls_tail=True: also what dsvt executes for a CLS-only forward (VisionTransformer.cls_tail):
-    the last block's spatial attention for the CLS queries only, attn.proj and the MLP on the
-    CLS row only (Block._run_cls_tail)."""
+    the last block's spatial queries and attention for the CLS rows only, attn.proj and the MLP
+    on the CLS row only (Block._run_cls_tail)."""
     N = (S // patch) ** 2
     d = C // heads
     R = N * T
@@ -56,7 +56,8 @@ def vit_fwd_flops(T, S, C=768, depth=12, heads=12, mlp=4, patch=16, folded=False
         per_block -= 2 * R * C * C
     tail = 0
     if cls_tail:   # last block: no patch-row queries, no patch-row proj / MLP
-        tail = 4 * T * heads * (1 + N) * N * d + 2 * (rows_s - 1) * C * C + 2 * 2 * (L - 1) * C * mlp * C
+        tail = (4 * T * heads * (1 + N) * N * d + 2 * (rows_s - 1) * C * C + 2 * 2 * (L - 1) * C * mlp * C
+                + 2 * (rows_s - 1) * C * C)                                      # + the patch rows' queries
     return depth * per_block - tail + 2 * R * (3 * patch * patch) * C
 
 
@@ -296,7 +297,8 @@ def joint_flops(T=16, S=224, C=768, depth=12, heads=12, mlp=4, patch=16, cls_tai
     per_block = 2 * L * C * 3 * C + 4 * heads * L * L * (C // heads) + 2 * L * C * C + 2 * 2 * L * C * mlp * C
     tail = 0
     if cls_tail:
-        tail = 4 * heads * (L - 1) * L * (C // heads) + 2 * (L - 1) * C * C + 2 * 2 * (L - 1) * C * mlp * C
+        tail = (4 * heads * (L - 1) * L * (C // heads) + 2 * (L - 1) * C * C + 2 * 2 * (L - 1) * C * mlp * C
+                + 2 * (L - 1) * C * C)                                           # + the patch rows' queries
     return depth * per_block - tail + 2 * N * T * (3 * patch * patch) * C
 
 

@@ -156,8 +156,9 @@ class Block(nn.Module):
         """The last divided block when forward_features returns the CLS token only
         (timesformer.py:341-345 `x[:, 0]` after the final norm).  That block's patch-row outputs
         -- their spatial attention, attn.proj, norm2 and MLP -- never reach the result, so they
-        are not computed: the temporal branch and the spatial qkv run on every row as in run()
-        (the CLS query attends to every frame's patch keys / values), then the CLS query of each
+        are not computed: the temporal branch runs on every row as in run(), the spatial keys /
+        values too (the CLS query attends to every frame's patches) but the queries only for the
+        CLS rows; then the CLS query of each
         frame sequence (dsvt_attn_spatial_cls_fwd, mean over frames, :139-167), attn.proj +
         residual, norm2, fc1 + GELU and fc2 + residual run on the B CLS rows alone (:181-184).
         The CLS features are those of the full block (tests/test_gpu_model.py::
@@ -195,8 +196,14 @@ class Block(nn.Module):
             ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
             ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X, epilogue=EPI_BIAS_RESID,
                      rowmap=patch_map, M=R)
-        ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, w(self.attn.qkv.weight),
-                    self.attn.qkv.bias, ctx.qkv, ctx.ws)
+        # spatial qkv: keys / values of every row, queries of the CLS rows only (the patch rows'
+        # queries have no consumer here)
+        C = ctx.C
+        wqkv, bqkv = w(self.attn.qkv.weight), self.attn.qkv.bias
+        ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[C:],
+                    None if bqkv is None else bqkv[C:], ctx.qkv, ctx.ws, col0=C)
+        ops.ln_gemm(X, cls_map, B, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[:C],
+                    None if bqkv is None else bqkv[:C], ctx.qkv, ctx.ws, rowmap=cls_map)
         o_cls = ctx.o[:B]                   # compact [B, C] rows (ctx.o is free again)
         ops.attn_spatial_cls(ctx.qkv, o_cls, B, T, L, heads, self.attn.scale)
         ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,

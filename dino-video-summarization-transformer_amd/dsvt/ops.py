@@ -178,16 +178,19 @@ def gemm_resid_ln(a, w, bias, X, M=None, rowmap=None, ln=None, Y=None, ymode=_li
 
 
 def ln_gemm(x, in_rowmap, M, ln_w, ln_b, eps, w, bias, out, ws, epilogue=_lib.EPI_BIAS, out_f32=False,
-            rowmap=None):
-    """LayerNorm(rows of fp32 x through in_rowmap) -> GEMM with epilogue."""
+            rowmap=None, col0=0):
+    """LayerNorm(rows of fp32 x through in_rowmap) -> GEMM with epilogue.  col0: the GEMM's N
+    columns land in out's columns [col0, col0 + N) (out's row stride kept)."""
     mode = w.dtype
     _check(x, torch.float32, "x")
     K = x.shape[-1]
+    if col0 < 0 or col0 + w.shape[0] > out.shape[-1]:
+        raise _lib.DsvtError("ln_gemm: columns [%d, %d) outside out's %d" % (col0, col0 + w.shape[0], out.shape[-1]))
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
     irpg, igs, igo = in_rowmap if in_rowmap is not None else (0, 0, 0)
     call("dsvt_ln_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(x), irpg, igs, igo, _ptr(ln_w), _ptr(ln_b),
-         float(eps), _ptr(w), _ptr(bias), _ptr(out), out.shape[-1], M, w.shape[0], K, rpg, gs, go, _ptr(ws),
-         ws.numel() * ws.element_size(), _stream())
+         float(eps), _ptr(w), _ptr(bias), out.data_ptr() + col0 * out.element_size(), out.shape[-1], M, w.shape[0],
+         K, rpg, gs, go, _ptr(ws), ws.numel() * ws.element_size(), _stream())
     return out
 
 
