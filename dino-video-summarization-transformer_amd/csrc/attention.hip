@@ -425,18 +425,29 @@ __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnPara
         }
       }
     }
+    // the row's 64 outputs as two 16-byte pieces per lane (fragment pairs packed across the lane
+    // groups by v_permlane16_swap, every lane taking part before the per-lane store branch):
+    // each store instruction writes 16 rows x 64 contiguous bytes instead of 16 rows x 32
+    const float inv = (p.seq_scale ? p.seq_scale[seq] : 1.0f) / rs;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= inv;
+    const uint4 pk0 = pack_pair_bf16(o[0], o[1]), pk1 = pack_pair_bf16(o[2], o[3]);
+#ifndef DSVT_ATTN_PAIRSTORE
+#define DSVT_ATTN_PAIRSTORE 1
+#endif
     if (qo < L) {
-      const float inv = (p.seq_scale ? p.seq_scale[seq] : 1.0f) / rs;
-      if (qo == 0 && p.cls_aux) {
+      if ((qo == 0 && p.cls_aux) || !DSVT_ATTN_PAIRSTORE) {
         float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
+        bf16_t* dsto = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + 4 * g;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+        for (int dt = 0; dt < 4; ++dt) {
+          if (qo == 0 && p.cls_aux) store4(dst + dt * 16, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+          else store4(dsto + dt * 16, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+        }
       } else {
-        bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + 4 * g;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+        bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + pair_off(g);
+        *reinterpret_cast<uint4*>(dst) = pk0;
+        *reinterpret_cast<uint4*>(dst + 32) = pk1;
       }
     }
   }

@@ -1,12 +1,13 @@
 #!/bin/bash
-# Build an A/B copy of libdsvt.so with extra compile flags on the GEMM sources, e.g.
+# Build an A/B copy of libdsvt.so with extra compile flags on the GEMM sources (AB_SRCS="..." to
+# pick other sources), e.g.
 #   tools/build_ab.sh "-DDSVT_RESID_PIPE=0"   -> tools/ab_lib/libdsvt_ab.so (run with DSVT_LIB=...)
 set -e
 cd "$(dirname "$0")/../dino-video-summarization-transformer_amd/csrc"
 make -s
 FLAGS="$1"
 mkdir -p build/ab ../../tools/ab_lib
-for f in gemm gemm_big gemm_8ph; do
+for f in ${AB_SRCS:-gemm gemm_big gemm_8ph}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS -c $f.hip -o build/ab/$f.o
 done
 objs=""
