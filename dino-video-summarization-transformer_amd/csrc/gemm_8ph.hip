@@ -33,6 +33,9 @@
 
 #include "gemm_epi.h"
 
+#ifndef DSVT_RESID_SEPI
+#define DSVT_RESID_SEPI 0   // 55: leave the residual epilogue in flight (measured slower: fc2 171 vs 166 us)
+#endif
 #ifndef DSVT_8PH_GELU_NOFAST
 #define DSVT_8PH_GELU_NOFAST 1   // the 16-byte pair-store path spills (201 VGPRs with the fast GELU too)
 #endif
@@ -98,7 +101,11 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   constexpr bool CLAMPED = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32;
   // VMEM instructions of a full-tile register epilogue: bf16 bias / GELU -> 16 pair stores,
   // X-streamed residual -> 32 fp32 fragment stores
-  constexpr int S_EPI = XS ? 32 : ((EPI == EPI_BIAS || CLAMPED) && !OUT_F32 && !(ABL & 64)) ? 16 : 0;
+  // rolling-window residual (gemm_epi.h) -> 32 X loads + 32 fp32 stores; the waits can skip at
+  // most 63 - 8 of them (a 6-bit vmcnt), so the oldest few still drain before the next K-tile
+  constexpr int S_EPI = XS ? 32
+                      : ((EPI == EPI_BIAS || CLAMPED) && !OUT_F32 && !(ABL & 64)) ? 16
+                      : (EPI == EPI_RESID && ABL == 0 && !SK && DSVT_RESID_PIPE) ? DSVT_RESID_SEPI : 0;
   constexpr int XS_BYTES = XS ? 8 * 4096 : 0;           // 8 waves x 4 slots x 1 KiB
   constexpr int SMEM_BYTES = 2 * P8_BUF + XS_BYTES + (SK ? 16 : 0);
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
@@ -529,7 +536,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
         epilogue_direct<8, 4, EPI, OUT_F32, (ABL & 32) ? 1 : (ABL & 128) ? 2 : 0, (ABL & 64) != 0, BIAS_IN_ACC, (EPI == EPI_GELU && DSVT_8PH_GELU_NOFAST), EPI == EPI_GELU_SAVE, NFULL, true>(pe, acc, rbase, cbase,
                                                                                           r16, g);
       }
-      post = whole && S_EPI > 0 && (CLAMPED || (rbase + 128 <= pe.M && cbase + 64 <= p.N));
+      post = whole && S_EPI > 0 && (CLAMPED || (rbase + 128 <= pe.M && cbase + 64 <= p.N)) &&
+             (EPI != EPI_RESID || XS || !p.row_scale);
       kc = 0;
       ++tlc;
       __builtin_amdgcn_sched_barrier(0);   // keep the next tile's bias loads after the stores
