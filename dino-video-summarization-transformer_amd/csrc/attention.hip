@@ -245,7 +245,8 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
 // MFMA decomposition as attn_seq_bf16: S^T = K.Q^T (lane = one query, 4 keys per tile) and
 // O^T = V^T.P^T with the k-slot permutation and ds_read_b64_tr_b16 V^T fragments.
 // DBG (diagnostic builds only): 1 = drain lgkmcnt before every P.V MFMA, 2 = V^T fragments by
-// scalar LDS reads instead of ds_read_b64_tr_b16.
+// scalar LDS reads instead of ds_read_b64_tr_b16, 3 = the loads, LDS staging and stores alone (no
+// math), 4 = the grid as (sequence, head) instead of (head, sequence).
 // SWZ: LDS rows of exactly 64 bf16 with the 16-B chunks XOR-swizzled by (row & 7) instead of the
 // 72-element padded rows, and only the NKT staged key tiles (an odd last tile finishes with a
 // 16x16x32 P.V step whose second 16-key half is zero in both operands -- one MFMA shape per
@@ -263,8 +264,8 @@ __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnPara
   __shared__ __attribute__((aligned(16))) bf16_t kv[2][LP * ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  const int h = blockIdx.x;
-  const int64_t seq = blockIdx.y, b = seq / p.tin, t = seq % p.tin;
+  const int h = DBG == 4 ? blockIdx.y : blockIdx.x;
+  const int64_t seq = DBG == 4 ? blockIdx.x : blockIdx.y, b = seq / p.tin, t = seq % p.tin;
   const bf16_t* qkv = (const bf16_t*)p.qkv;
   const int64_t C = p.C;
   const int L = (int)p.seqlen;
@@ -310,6 +311,25 @@ __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnPara
   const bf16_t* Ks = kv[0];
   const bf16_t* Vs = kv[1];
   const float sl2 = p.scale * 1.4426950408889634f;
+  if constexpr (DBG == 3) {   // the loads, the LDS staging and the output stores alone (no math)
+#pragma unroll
+    for (int w = 0; w < QT_W; ++w) {
+      const int qt = wave + NW * w;
+      if (qt >= nqt) break;
+      const int qo = qt * 16 + r16;
+      if (qo < L) {
+        sv8 v = qa[w];
+        const sv8 kx = *reinterpret_cast<const sv8*>(Ks + lds(qo, g));
+        const sv8 vx = *reinterpret_cast<const sv8*>(Vs + lds(qo, g));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] ^= kx[e] ^ vx[e] ^ qb[w][e];
+        bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + g * 8;
+        *reinterpret_cast<sv8*>(dst) = v;
+        *reinterpret_cast<sv8*>(dst + 32) = v;
+      }
+    }
+    return;
+  }
 
 #pragma unroll
   for (int w = 0; w < QT_W; ++w) {
@@ -471,6 +491,9 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
     else if (v == 7 && p.seqlen <= 48) attn_short_bf16<3, 4, 0, true><<<grid, 256, 0, s>>>(p);
     else if (p.seqlen <= 64 && v == 0) attn_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
     else if (v == 3 && p.seqlen <= 208) attn_short_bf16<13, 4><<<grid, 256, 0, s>>>(p);   // padded rows
+    else if (v == 9 && p.seqlen <= 208) attn_short_bf16<13, 4, 3, true><<<grid, 256, 0, s>>>(p);   // diagnostic
+    else if (v == 10 && p.seqlen <= 208)                                      // (sequence, head) grid
+      attn_short_bf16<13, 4, 4, true><<<dim3(grid.y, grid.x), 256, 0, s>>>(p);
     // 1 + 196 patches: swizzled exact-tile LDS, 3 workgroups per CU -- 53.4 vs 62.2 us at the
     // bench's global call (16 clips x 8 frames x 12 heads); 25.3 vs 24.5 us at 1 + 36 (kept <4, 4>)
     else if (p.seqlen <= 208) attn_short_bf16<13, 4, 0, true><<<grid, 256, 0, s>>>(p);
