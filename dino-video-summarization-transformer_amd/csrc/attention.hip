@@ -16,6 +16,7 @@
 // attn_temporal_reg (K5, bf16, T <= 8): register-only, 16 lanes per (patch, head), butterfly
 //   reduce-scatter of Q.K^T; HBM-bound.  attn_temporal_kernel: LDS-staged general-T fallback.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -252,6 +253,183 @@ __global__ __launch_bounds__(64) void attn_seq_f32(AttnParams p) {
 // 16x16x32 P.V step whose second 16-key half is zero in both operands -- one MFMA shape per
 // accumulator chain): 2 x 208 x 128 B = 52 KB per workgroup at 1 + 196 keys, so
 // 3 workgroups (12 waves) share a CU instead of 2.
+// ds_read_b64_tr_b16 as inline asm: the compiler does not track it, so it adds no vmcnt wait
+// for in-flight LDS-DMA of OTHER buffers before it (the caller waits lgkmcnt itself)
+__device__ __forceinline__ sv4 ds_read_tr16_asm(const bf16_t* lds_ptr) {
+  sv4 r;
+  const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const bf16_t*)lds_ptr;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+// One 16-query tile of a short sequence against its K / V staged in LDS (`lds` layout below):
+// scores, exact two-pass softmax, P.V and the output stores.  Shared by the one-item kernel
+// and the pipelined persistent one.
+template <int NKT, int DBG, bool SWZ>
+__device__ __forceinline__ void short_tile(const AttnParams& p, const bf16_t* Ks, const bf16_t* Vs, const sv8 qf0,
+                                           const sv8 qf1, const int qt, const int L, const int nkt, const int64_t seq,
+                                           const int64_t b, const int64_t t, const int h, const float sl2, const int r16,
+                                           const int g, const float oscale) {
+  constexpr int NKP = SWZ ? NKT / 2 : (NKT + 1) / 2;   // full 32-key PV steps
+  constexpr bool HALF = SWZ && (NKT & 1);              // + one 16-key step
+  constexpr int SN = SWZ ? NKT : 2 * NKP;    // score tiles held (padded: the last of an odd NKT is 0)
+  auto lds = [](int r, int c) { return SWZ ? r * 64 + ((c ^ (r & 7)) << 3) : r * KV_ROW + c * 8; };
+  const int64_t C = p.C;
+  // scores: s[kt][j] = raw score(query qt*16 + r16, key kt*16 + 4g + j); the row max is taken
+  // on raw scores (scale > 0) and the scale folded into the exponent: exp2(s*c - max*c)
+  // Every tile of the compile-time extent is computed (rows past the sequence are staged
+  // zeros; their scores are masked by a select): the score -> max -> exp -> P.V chain is
+  // straight-line code.  A runtime branch between an MFMA and the VALU reading its result
+  // made the ROCm 7.2 hazard recognizer under-insert wait states on the taken path (stale
+  // scores in the row max: ~1-ulp nondeterminism at 4 waves, NaN at 8).
+  fv4 s[SN];
+#pragma unroll
+  for (int kt = 0; kt < SN; ++kt) {
+    const int kr = kt * 16 + r16;
+    const sv8 k0 = *reinterpret_cast<const sv8*>(Ks + lds(kr, g));
+    const sv8 k1 = *reinterpret_cast<const sv8*>(Ks + lds(kr, g + 4));
+    fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+    z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
+    s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < SN; ++kt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[kt][j] = (kt * 16 + 4 * g + j < L) ? s[kt][j] : -INFINITY;
+    mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float mxs = mx * sl2;
+  float rs = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < SN; ++kt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));   // args <= 0; masked -> 0
+      s[kt][j] = e;
+      rs += e;
+    }
+  }
+  rs += __shfl_xor(rs, 16, 64);
+  rs += __shfl_xor(rs, 32, 64);
+  // O^T += V^T . P^T over 32-key steps; k-slot (g, jj): jj<4 -> key tile 2kp, jj>=4 -> 2kp+1
+  fv4 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = fv4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kp = 0; kp < NKP; ++kp) {
+    sv8 pb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pb[j] = (short)f2bf(s[2 * kp][j]);
+      pb[4 + j] = (short)f2bf(s[2 * kp + 1][j]);
+    }
+    const int vr0 = kp * 32 + 4 * g + (r16 >> 2);
+    const int vr1 = vr0 + 16;
+    sv4 vlo[4], vhi[4];
+    if constexpr (DBG == 5) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        vlo[dt] = ds_read_tr16_asm(Vs + lds(vr0, col >> 3) + (col & 7));
+        vhi[dt] = ds_read_tr16_asm(Vs + lds(vr1, col >> 3) + (col & 7));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[0]), "+v"(vlo[1]), "+v"(vlo[2]), "+v"(vlo[3]), "+v"(vhi[0]),
+                   "+v"(vhi[1]), "+v"(vhi[2]), "+v"(vhi[3]));
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int col = dt * 16 + 4 * (r16 & 3);
+      sv8 vf;
+      if constexpr (DBG == 5) {
+        vf = __builtin_shufflevector(vlo[dt], vhi[dt], 0, 1, 2, 3, 4, 5, 6, 7);
+      } else if constexpr (DBG == 2) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          vf[jj] = (short)Vs[(kp * 32 + 4 * g + jj) * KV_ROW + dt * 16 + r16];
+          vf[4 + jj] = (short)Vs[(kp * 32 + 16 + 4 * g + jj) * KV_ROW + dt * 16 + r16];
+        }
+      } else {
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + lds(vr0, col >> 3) + (col & 7)));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + lds(vr1, col >> 3) + (col & 7)));
+        vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+      if constexpr (DBG == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+    }
+  }
+  if constexpr (HALF) {   // odd last key tile: the same 16x16x32 step with the second key tile's
+    constexpr int kt = 2 * NKP;   // k-slots zero in both operands (one MFMA shape in the chain:
+    sv8 pb;                       // mixing in 16x16x16 left a srcC hazard under 3-WG occupancy)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pb[j] = (short)f2bf(s[kt][j]);
+      pb[4 + j] = 0;
+    }
+    const int vr0 = kt * 16 + 4 * g + (r16 >> 2);
+    sv4 vlo[4];
+    if constexpr (DBG == 5) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) vlo[dt] = ds_read_tr16_asm(Vs + lds(vr0, (dt * 16 + 4 * (r16 & 3)) >> 3) + (4 * (r16 & 3) & 7));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[0]), "+v"(vlo[1]), "+v"(vlo[2]), "+v"(vlo[3]));
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int col = dt * 16 + 4 * (r16 & 3);
+      const sv4 lo = DBG == 5 ? vlo[dt] : __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) sv4*)(Vs + lds(vr0, col >> 3) + (col & 7)));
+      const sv8 vf = __builtin_shufflevector(lo, sv4{0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+    }
+  }
+  mfma_result_fence();     // the stores below are under per-lane branches
+  // lane holds O[query qt*16 + r16][d = dt*16 + 4g + 0..3]
+  const int qo = qt * 16 + r16;
+  if (p.probs && qo < L) {                 // get_attn: normalized probabilities, fp32
+    const float inv = 1.0f / rs;
+    float* prow = p.probs + ((seq * p.heads + h) * (int64_t)L + qo) * L;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = kt * 16 + 4 * g + j;
+          if (key < L) prow[key] = s[kt][j] * inv;
+        }
+      }
+    }
+  }
+  // the row's 64 outputs as two 16-byte pieces per lane (fragment pairs packed across the lane
+  // groups by v_permlane16_swap, every lane taking part before the per-lane store branch):
+  // each store instruction writes 16 rows x 64 contiguous bytes instead of 16 rows x 32
+  const float inv = oscale / rs;   // oscale: the sequence's DropPath scale or 1
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] *= inv;
+  const uint4 pk0 = pack_pair_bf16(o[0], o[1]), pk1 = pack_pair_bf16(o[2], o[3]);
+#ifndef DSVT_ATTN_PAIRSTORE
+#define DSVT_ATTN_PAIRSTORE 1
+#endif
+  if (qo < L) {
+    if ((qo == 0 && p.cls_aux) || !DSVT_ATTN_PAIRSTORE) {
+      float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
+      bf16_t* dsto = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        if (qo == 0 && p.cls_aux) store4(dst + dt * 16, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+        else store4(dsto + dt * 16, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+      }
+    } else {
+      bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + pair_off(g);
+      *reinterpret_cast<uint4*>(dst) = pk0;
+      *reinterpret_cast<uint4*>(dst + 32) = pk1;
+    }
+  }
+}
+
 template <int NKT, int NW, int DBG = 0, bool SWZ = false>
 __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnParams p) {
   constexpr int NKP = SWZ ? NKT / 2 : (NKT + 1) / 2;   // full 32-key PV steps
@@ -335,140 +513,69 @@ __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnPara
   for (int w = 0; w < QT_W; ++w) {
     const int qt = wave + NW * w;
     if (qt >= nqt) break;
-    const sv8 qf0 = qa[w], qf1 = qb[w];
-    // scores: s[kt][j] = raw score(query qt*16 + r16, key kt*16 + 4g + j); the row max is taken
-    // on raw scores (scale > 0) and the scale folded into the exponent: exp2(s*c - max*c)
-    // Every tile of the compile-time extent is computed (rows past the sequence are staged
-    // zeros; their scores are masked by a select): the score -> max -> exp -> P.V chain is
-    // straight-line code.  A runtime branch between an MFMA and the VALU reading its result
-    // made the ROCm 7.2 hazard recognizer under-insert wait states on the taken path (stale
-    // scores in the row max: ~1-ulp nondeterminism at 4 waves, NaN at 8).
-    fv4 s[SN];
-#pragma unroll
-    for (int kt = 0; kt < SN; ++kt) {
-      const int kr = kt * 16 + r16;
-      const sv8 k0 = *reinterpret_cast<const sv8*>(Ks + lds(kr, g));
-      const sv8 k1 = *reinterpret_cast<const sv8*>(Ks + lds(kr, g + 4));
-      fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
-      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, z, 0, 0, 0);
-      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, z, 0, 0, 0);
+    short_tile<NKT, DBG, SWZ>(p, Ks, Vs, qa[w], qb[w], qt, L, nkt, seq, b, t, h, sl2, r16, g,
+                              p.seq_scale ? p.seq_scale[seq] : 1.0f);
+  }
+}
+
+// Pipelined persistent form (1 + 196 keys, the swizzled layout; opt-in, DSVT_ATTN_PIPE=1 or
+// variant 11): one 512-thread workgroup per CU walks the (sequence, head) items with a stride of
+// the grid; Q, K and V of its NEXT item are staged by LDS-DMA into the other half of 156 KB of
+// LDS while the 8 waves run the current item's query tiles.  Bitwise the one-item kernel's
+// results, but SLOWER: 54-57 vs 44-48 us at the bench's global call, and 56.5 us with the overlap
+// defeated (intrinsic V^T reads, before which the compiler waits for every in-flight LDS-DMA) --
+// one 8-wave workgroup per CU computes an item about 3x slower than three co-resident 4-wave
+// ones, which the overlap does not buy back (bench 385 vs 388-389 clips/s).
+// Every staged row is a 128-byte head slice of one token row; a wave DMA instruction moves 8 of
+// them (lane = row (l >> 3), physical 16-B chunk l & 7, loading logical chunk (l & 7) ^ (row & 7)
+// -- the `lds` swizzle).  Rows past L are staged as row L - 1: finite, their keys are masked,
+// their probabilities are 0 and their queries are not stored.
+template <int NKT>
+__global__ __launch_bounds__(512, 1) void attn_short_pipe_bf16(AttnParams p, int64_t items) {
+  constexpr int NW = 8, LP = NKT * 16, BUFE = LP * 64, NI = LP / 8;   // NI: DMA instructions per buffer
+  constexpr int QT_W = (NKT + NW - 1) / NW;
+  __shared__ __attribute__((aligned(16))) bf16_t sm[2][3][BUFE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const bf16_t* qkv = (const bf16_t*)p.qkv;
+  const int64_t C = p.C, heads = p.heads, G = gridDim.x;
+  const int L = (int)p.seqlen, nkt = (L + 15) >> 4, nqt = nkt;
+  const float sl2 = p.scale * 1.4426950408889634f;
+  auto stage = [&](int buf, int64_t item) {
+    const int h = (int)(item % heads);
+    const int64_t seq = item / heads, b = seq / p.tin, t = seq % p.tin;
+    for (int i = wave; i < 3 * NI; i += NW) {   // wave-uniform
+      const int role = i / NI, ri = i - role * NI;
+      const int r = ri * 8 + (lane >> 3), c = (lane & 7) ^ (r & 7);
+      const bf16_t* src = qkv + tok_row(p, b, t, r < L ? r : L - 1) * p.ld_qkv + role * C + h * 64 + c * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(&sm[buf][role][ri * 512]), 16, 0, 0);
     }
-    float mx = -INFINITY;
+  };
+  int64_t item = blockIdx.x;
+  if (item < items) stage(0, item);
+  for (int buf = 0; item < items; item += G, buf ^= 1) {
+    // this wave's DMAs of `item` have landed (vmcnt 0); the barrier: every wave's have, and
+    // every wave is done reading the other buffer (the previous item)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), lgkmcnt / expcnt untouched
+    __syncthreads();
+    const int h = (int)(item % heads);
+    const int64_t seq = item / heads, b = seq / p.tin, t = seq % p.tin;
+    // the DropPath scale is read BEFORE the next item's staging: a global load issued behind the
+    // staging DMAs would make the compiler wait for all of them (vmcnt counts in order)
+    const float oscale = p.seq_scale ? p.seq_scale[seq] : 1.0f;
+    asm volatile("" ::"v"(oscale));
+    if (item + G < items) stage(buf ^ 1, item + G);
+    const bf16_t* Qs = sm[buf][0];
+    const bf16_t* Ks = sm[buf][1];
+    const bf16_t* Vs = sm[buf][2];
 #pragma unroll
-    for (int kt = 0; kt < SN; ++kt) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[kt][j] = (kt * 16 + 4 * g + j < L) ? s[kt][j] : -INFINITY;
-      mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mxs = mx * sl2;
-    float rs = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < SN; ++kt) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));   // args <= 0; masked -> 0
-        s[kt][j] = e;
-        rs += e;
-      }
-    }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    // O^T += V^T . P^T over 32-key steps; k-slot (g, jj): jj<4 -> key tile 2kp, jj>=4 -> 2kp+1
-    fv4 o[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[d] = fv4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kp = 0; kp < NKP; ++kp) {
-      sv8 pb;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[j] = (short)f2bf(s[2 * kp][j]);
-        pb[4 + j] = (short)f2bf(s[2 * kp + 1][j]);
-      }
-      const int vr0 = kp * 32 + 4 * g + (r16 >> 2);
-      const int vr1 = vr0 + 16;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int col = dt * 16 + 4 * (r16 & 3);
-        sv8 vf;
-        if constexpr (DBG == 2) {
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            vf[jj] = (short)Vs[(kp * 32 + 4 * g + jj) * KV_ROW + dt * 16 + r16];
-            vf[4 + jj] = (short)Vs[(kp * 32 + 16 + 4 * g + jj) * KV_ROW + dt * 16 + r16];
-          }
-        } else {
-          const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) sv4*)(Vs + lds(vr0, col >> 3) + (col & 7)));
-          const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) sv4*)(Vs + lds(vr1, col >> 3) + (col & 7)));
-          vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-        if constexpr (DBG == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
-      }
-    }
-    if constexpr (HALF) {   // odd last key tile: the same 16x16x32 step with the second key tile's
-      constexpr int kt = 2 * NKP;   // k-slots zero in both operands (one MFMA shape in the chain:
-      sv8 pb;                       // mixing in 16x16x16 left a srcC hazard under 3-WG occupancy)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[j] = (short)f2bf(s[kt][j]);
-        pb[4 + j] = 0;
-      }
-      const int vr0 = kt * 16 + 4 * g + (r16 >> 2);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int col = dt * 16 + 4 * (r16 & 3);
-        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) sv4*)(Vs + lds(vr0, col >> 3) + (col & 7)));
-        const sv8 vf = __builtin_shufflevector(lo, sv4{0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
-      }
-    }
-    mfma_result_fence();     // the stores below are under per-lane branches
-    // lane holds O[query qt*16 + r16][d = dt*16 + 4g + 0..3]
-    const int qo = qt * 16 + r16;
-    if (p.probs && qo < L) {                 // get_attn: normalized probabilities, fp32
-      const float inv = 1.0f / rs;
-      float* prow = p.probs + ((seq * p.heads + h) * (int64_t)L + qo) * L;
-#pragma unroll
-      for (int kt = 0; kt < SN; ++kt) {
-        if (kt < nkt) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int key = kt * 16 + 4 * g + j;
-            if (key < L) prow[key] = s[kt][j] * inv;
-          }
-        }
-      }
-    }
-    // the row's 64 outputs as two 16-byte pieces per lane (fragment pairs packed across the lane
-    // groups by v_permlane16_swap, every lane taking part before the per-lane store branch):
-    // each store instruction writes 16 rows x 64 contiguous bytes instead of 16 rows x 32
-    const float inv = (p.seq_scale ? p.seq_scale[seq] : 1.0f) / rs;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= inv;
-    const uint4 pk0 = pack_pair_bf16(o[0], o[1]), pk1 = pack_pair_bf16(o[2], o[3]);
-#ifndef DSVT_ATTN_PAIRSTORE
-#define DSVT_ATTN_PAIRSTORE 1
-#endif
-    if (qo < L) {
-      if ((qo == 0 && p.cls_aux) || !DSVT_ATTN_PAIRSTORE) {
-        float* dst = p.cls_aux + seq * C + h * 64 + 4 * g;
-        bf16_t* dsto = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + 4 * g;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          if (qo == 0 && p.cls_aux) store4(dst + dt * 16, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
-          else store4(dsto + dt * 16, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
-        }
-      } else {
-        bf16_t* dst = (bf16_t*)p.out + tok_row(p, b, t, qo) * p.ld_out + h * 64 + pair_off(g);
-        *reinterpret_cast<uint4*>(dst) = pk0;
-        *reinterpret_cast<uint4*>(dst + 32) = pk1;
-      }
+    for (int w = 0; w < QT_W; ++w) {
+      const int qt = wave + NW * w;
+      if (qt >= nqt) break;
+      const int qr = qt * 16 + r16;
+      const sv8 qf0 = *reinterpret_cast<const sv8*>(Qs + qr * 64 + ((g ^ (qr & 7)) << 3));
+      const sv8 qf1 = *reinterpret_cast<const sv8*>(Qs + qr * 64 + (((g + 4) ^ (qr & 7)) << 3));
+      short_tile<NKT, 5, true>(p, Ks, Vs, qf0, qf1, qt, L, nkt, seq, b, t, h, sl2, r16, g, oscale);
     }
   }
 }
@@ -479,7 +586,9 @@ static thread_local int g_attn_variant = 0;
 void set_attn_variant(int v) { g_attn_variant = v; }
 
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
-  const int v = g_attn_variant;
+  // DSVT_ATTN_PIPE=1: the pipelined persistent kernel for 1 + 196 keys (variant 11) by default
+  static const int pipe = getenv("DSVT_ATTN_PIPE") ? atoi(getenv("DSVT_ATTN_PIPE")) : 0;
+  const int v = g_attn_variant ? g_attn_variant : (pipe && p.seqlen > 192 && p.seqlen <= 208) ? 11 : 0;
   if (dtype == 0 && p.seqlen <= 256 && v != 4) {
     dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
     // measured at 1 + 196 keys x 8 frames x 16 clips (tools/attn_bench.py): <13, 4> 60 us,
@@ -494,6 +603,10 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
     else if (v == 9 && p.seqlen <= 208) attn_short_bf16<13, 4, 3, true><<<grid, 256, 0, s>>>(p);   // diagnostic
     else if (v == 10 && p.seqlen <= 208)                                      // (sequence, head) grid
       attn_short_bf16<13, 4, 4, true><<<dim3(grid.y, grid.x), 256, 0, s>>>(p);
+    else if (v == 11 && p.seqlen <= 208 && p.seqlen > 192) {                  // pipelined persistent
+      const int64_t items = (int64_t)grid.x * grid.y;
+      attn_short_pipe_bf16<13><<<dim3((unsigned)(items < 256 ? items : 256)), 512, 0, s>>>(p, items);
+    }
     // 1 + 196 patches: swizzled exact-tile LDS, 3 workgroups per CU -- 53.4 vs 62.2 us at the
     // bench's global call (16 clips x 8 frames x 12 heads); 25.3 vs 24.5 us at 1 + 36 (kept <4, 4>)
     else if (p.seqlen <= 208) attn_short_bf16<13, 4, 0, true><<<grid, 256, 0, s>>>(p);

@@ -567,7 +567,7 @@ int dsvt_set_gemm_variant(int variant) {
 }
 
 int dsvt_set_attn_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 10, "attention variant must be 0-10");
+  REQUIRE(variant >= 0 && variant <= 11, "attention variant must be 0-11");
   set_attn_variant(variant);
   return 0;
 }

@@ -535,7 +535,7 @@ def _lib_cls(Q, out, B, T, L, heads, scale):
               heads, 64, float(scale), ws.data_ptr(), ws.numel() * 4, ops._stream())
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 7, 11])
 def test_attn_spatial_variants_repeatable(variant):
     """Every bf16 short-sequence kernel at a multi-clip global shape (B=4, 8x196 patches, 12 heads,
     N(0,1) q/k/v): finite, within tolerance of the float64 reference, and bitwise identical over
@@ -562,6 +562,34 @@ def test_attn_spatial_variants_repeatable(variant):
         assert torch.equal(o, outs[0]), "repeat launches differ"
     ref = spatial_ref(back(Q)[:2 * L], 2, T, L, heads, 0.125)     # first 2 clips vs float64
     check(back(outs[0])[:2 * L], ref, torch.bfloat16, "spatial variant %d" % variant)
+
+
+@pytest.mark.parametrize("B,T,N,heads", [(4, 8, 196, 12), (1, 8, 196, 12), (3, 1, 196, 12), (40, 1, 196, 12)])
+def test_attn_spatial_pipe_bitwise(B, T, N, heads):
+    """The pipelined persistent kernel (variant 11: LDS-DMA staging of the next (sequence, head)
+    under the current one's math) computes exactly what the one-item kernel does: bitwise equal
+    outputs (CLS rows included) at the bench's global shape, one clip (a grid of 96 items), the
+    T = 1 joint / space-only form, and more items than workgroups with a ragged last round."""
+    from dsvt import _lib, ops
+    from dsvt._lib import WS_ATTN_SPATIAL
+    C, L = heads * 64, 1 + N * T
+    Q = to(rnd((B * L, 3 * C), 23, 1.5), torch.bfloat16)
+    ws = torch.empty(ops.workspace_bytes(WS_ATTN_SPATIAL, torch.bfloat16, B * T, C, 0) // 4, device=dev())
+    outs = {}
+    for v in (0, 11):
+        _lib.call("dsvt_set_attn_variant", v)
+        try:
+            out = torch.full((B * L, C), 7.0, device=dev(), dtype=torch.bfloat16)
+            if T == 1:
+                ops.attn_joint(Q, out, B, L, heads, 0.125)
+            else:
+                ops.attn_spatial(Q, out, B, T, L, heads, 0.125, ws)
+            torch.cuda.synchronize()
+            outs[v] = out
+        finally:
+            _lib.call("dsvt_set_attn_variant", 0)
+    assert torch.isfinite(outs[11].float()).all()
+    assert torch.equal(outs[11], outs[0])
 
 
 @pytest.mark.parametrize("variant", [0, 8])
