@@ -559,10 +559,15 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 int dsvt_set_gemm_variant(int variant) {
   REQUIRE(variant == 0 || variant == 1 || variant == 2 || (variant >= 3 && variant <= 6) || (variant >= 9 && variant <= 13) ||
               (variant >= 20 && variant <= 29 && variant != 24) || variant == 14 || variant == 24 || variant == 34 ||
-              variant == 33 || variant == 40 || variant == 41,
-          "gemm variant must be 0-6, 9-13, 20, 33 (X-streamed residual), 40 (stream-K) or 41 (auto + tail split; "
+              variant == 33 || variant == 40 || variant == 41 || variant == 50,
+          "gemm variant must be 0-6, 9-13, 20, 33 (X-streamed residual), 40 (stream-K), 41 (auto + tail split), 50 (K-split skinny; "
           "14/24/34: ablation builds)");
   set_gemm_variant(variant);
+  return 0;
+}
+
+int dsvt_set_gemm_skinny(int on) {
+  set_gemm_skinny(on ? 1 : 0);
   return 0;
 }
 

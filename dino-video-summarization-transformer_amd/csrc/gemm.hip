@@ -455,6 +455,9 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
 static thread_local int g_gemm_variant = 0; // 0 = auto; otherwise forced (tools/gemm_bench.py, tests)
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
+// call-site scope (dsvt_set_gemm_skinny): the few-row GEMMs of the CLS-only tail and the DINO head
+static thread_local int g_skinny_scope = 0;
+void set_gemm_skinny(int on) { g_skinny_scope = on; }
 
 // Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, >= 2: gemm_big.hip variants, 20:
 // gemm_8ph.hip).
@@ -490,7 +493,14 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
       (g_gemm_variant == 40 || (g_gemm_variant == 0 && sk_auto(epi))))
     return 40;
   // forced stream-K on an ineligible shape, or 41 (auto + tail split): the automatic choice
-  const int gv = (g_gemm_variant == 40 || g_gemm_variant == 41) ? 0 : g_gemm_variant;
+  const int gv = (g_gemm_variant == 40 || g_gemm_variant == 41 || g_gemm_variant == 50) ? 0 : g_gemm_variant;
+  // inside a dsvt_set_gemm_skinny scope (the CLS-only tail's and the DINO head's few-row GEMMs,
+  // chosen by call site so that a batch split over streams picks the same kernel as the whole
+  // batch): the K-split skinny kernel (variant 50 forces it where eligible) -- bench 397.7-398.7
+  // vs 395.1-396.0 clips/s with the 128x128 kernel (same box, three interleaved rounds;
+  // DSVT_SKINNY=0 turns the scopes off for A/B)
+  static const int skinny = getenv("DSVT_SKINNY") ? atoi(getenv("DSVT_SKINNY")) : 1;
+  if ((g_gemm_variant == 50 || (g_gemm_variant == 0 && skinny && g_skinny_scope)) && gemm_skinny_ok(p, epi)) return 50;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
   // 195 vs 254 us (persistent 256x128) and 215 vs 231 us at 25104 x 3072 x 768 (tools/aux_bench.py)
@@ -592,6 +602,7 @@ hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hip
     }
   }
   if (v == 40) return launch_gemm_sk(p, epi, out_f32, s);
+  if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);
   if (v == 2) return launch_pipe(p, epi, out_f32, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);

@@ -488,4 +488,105 @@ hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f3
   return hipGetLastError();
 }
 
+// ---- skinny GEMM (variant 50): a few rows -- the CLS-only last block's Q / proj / fc1 / fc2 over
+// the B clips' CLS rows and the DINO head's layers.  The 128x128 kernel runs these as N / 128
+// workgroups that each walk all of K (6-24 busy CUs, 20-50 us per launch).  Here one 512-thread
+// workgroup owns 32 output columns of a 64-row block and its 8 waves split K eight ways:
+// N / 32 x ceil(M / 64) workgroups, each streaming its 32 rows of W once.  A row's result does
+// not depend on M (the same K-split sums for every row), so a batch split over streams stays
+// bitwise equal to the whole batch as long as the CALL SITE picks this kernel whatever M is
+// (dsvt_set_gemm_skinny scopes, not an M threshold).  Operands go from HBM / L2
+// straight to registers (16-B loads in the MFMA fragment layout; the few A rows are shared by
+// every workgroup), the waves' partial sums are added in a fixed order through LDS (run-to-run
+// deterministic), and wave 0 runs the register epilogue of the other kernels (bias, GELU, fp32
+// residual through the output row map).  Rows past M are clamped on load and never stored.
+constexpr int SKN_NW = 8, SKN_U = 4;
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
+  __shared__ fv4 red[SKN_NW - 1][4][2][64];   // waves 1..7: [m fragment][n fragment][lane], 56 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.x * 32, r0 = (int64_t)blockIdx.y * 64;
+  const int64_t kw = p.K / SKN_NW, k0 = wave * kw;
+  const int ns = (int)(kw / 32);
+  const bf16_t* ar[4];
+  const bf16_t* wr[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = r0 + i * 16 + r16;
+    ar[i] = (const bf16_t*)p.A + (m < p.M ? m : p.M - 1) * p.lda + k0 + g * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t n = n0 + j * 16 + r16;
+    wr[j] = (const bf16_t*)p.W + (n < p.N ? n : p.N - 1) * p.ldw + k0 + g * 8;
+  }
+  fv4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < ns; s0 += SKN_U) {     // SKN_U k-steps of loads in flight, then their MFMAs
+    sv8 a[SKN_U][4], b[SKN_U][2];
+#pragma unroll
+    for (int u = 0; u < SKN_U; ++u) {
+      if (s0 + u < ns) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[u][j] = *reinterpret_cast<const sv8*>(wr[j] + (s0 + u) * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[u][i] = *reinterpret_cast<const sv8*>(ar[i] + (s0 + u) * 32);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SKN_U; ++u) {
+      if (s0 + u < ns) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][j], a[u][i], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  mfma_result_fence();
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[wave - 1][i][j][lane] = acc[i][j];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll 1
+  for (int w = 0; w < SKN_NW - 1; ++w)      // (not unrolled: all 56 partial fragments at once spill)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] += red[w][i][j][lane];
+  epilogue_direct<4, 2, EPI, OUT_F32>(p, acc, r0, n0, r16, g);
+}
+
+bool gemm_skinny_ok(const GemmParams& p, int epi) {
+  return p.M >= 1 && p.K >= 512 && p.K % (SKN_NW * 32) == 0 && p.N % 32 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
+         (epi == EPI_BIAS || epi == EPI_GELU || epi == EPI_RESID) && !p.row_scale && !p.nseg && !p.sk_part &&
+         ((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0;
+}
+
+hipError_t launch_gemm_skinny(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
+  if (!gemm_skinny_ok(p, epi)) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(p.N / 32), (unsigned)((p.M + 63) / 64)), block(512);
+  switch (epi) {
+    case EPI_BIAS:
+      if (out_f32) gemm_skinny_kernel<EPI_BIAS, true><<<grid, block, 0, s>>>(p);
+      else gemm_skinny_kernel<EPI_BIAS, false><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_GELU:
+      if (out_f32) gemm_skinny_kernel<EPI_GELU, true><<<grid, block, 0, s>>>(p);
+      else gemm_skinny_kernel<EPI_GELU, false><<<grid, block, 0, s>>>(p);
+      break;
+    case EPI_RESID: gemm_skinny_kernel<EPI_RESID, true><<<grid, block, 0, s>>>(p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace dsvt

@@ -67,6 +67,10 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // 
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
 bool gemm_8ph_ok(const GemmParams& p, int epi);
+// K split over the 8 waves of a workgroup, 64-row blocks (variant 50, gemm_big.hip)
+bool gemm_skinny_ok(const GemmParams& p, int epi);
+hipError_t launch_gemm_skinny(const GemmParams& p, int epi, int out_f32, hipStream_t s);
+void set_gemm_skinny(int on);   // this thread's launches: the skinny kernel where eligible (gemm.hip)
 // the 256x256 kernel with the residual tile streamed into the accumulators (variant 33)
 bool gemm_8ph_xs_ok(const GemmParams& p, int epi);
 hipError_t launch_gemm_8ph_xs(const GemmParams& p, int epi, hipStream_t s);

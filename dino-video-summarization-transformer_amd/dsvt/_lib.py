@@ -101,6 +101,7 @@ SIGNATURES = {
     "dsvt_video_augment": (_i32, [_p, _i32, _i64, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _i32, _p,
                                   ctypes.c_size_t, _p]),
     "dsvt_set_gemm_variant": (_i32, [_i32]),
+    "dsvt_set_gemm_skinny": (_i32, [_i32]),
     "dsvt_set_attn_variant": (_i32, [_i32]),
     "dsvt_set_attn_bwd_variant": (_i32, [_i32]),
     "dsvt_probe_enable": (_i32, [_i32, _i32]),

@@ -174,12 +174,13 @@ class Block(nn.Module):
                         self.attn.qkv.bias, ctx.qkv, ctx.ws)
             o_cls, h_cls = ctx.o[:nb], ctx.hid[:nb]
             ops.attn_spatial_cls(ctx.qkv, o_cls, nb, 1, L, heads, self.attn.scale)
-            ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap,
-                     M=nb)
-            ops.ln_gemm(X, cmap, nb, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
-                        self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
-            ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap,
-                     M=nb)
+            with ops.skinny():              # the CLS rows' GEMMs: K-split skinny kernel
+                ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID,
+                         rowmap=cmap, M=nb)
+                ops.ln_gemm(X, cmap, nb, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
+                            self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
+                ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap,
+                         M=nb)
             return
         B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
         R = B * Np * T
@@ -202,17 +203,18 @@ class Block(nn.Module):
         wqkv, bqkv = w(self.attn.qkv.weight), self.attn.qkv.bias
         ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[C:],
                     None if bqkv is None else bqkv[C:], ctx.qkv, ctx.ws, col0=C)
-        ops.ln_gemm(X, cls_map, B, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[:C],
-                    None if bqkv is None else bqkv[:C], ctx.qkv, ctx.ws, rowmap=cls_map)
-        o_cls = ctx.o[:B]                   # compact [B, C] rows (ctx.o is free again)
-        ops.attn_spatial_cls(ctx.qkv, o_cls, B, T, L, heads, self.attn.scale)
-        ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,
-                 M=B)
-        h_cls = ctx.hid[:B]
-        ops.ln_gemm(X, cls_map, B, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
-                    self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
-        ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,
-                 M=B)
+        with ops.skinny():                  # the CLS rows' GEMMs: K-split skinny kernel
+            ops.ln_gemm(X, cls_map, B, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[:C],
+                        None if bqkv is None else bqkv[:C], ctx.qkv, ctx.ws, rowmap=cls_map)
+            o_cls = ctx.o[:B]               # compact [B, C] rows (ctx.o is free again)
+            ops.attn_spatial_cls(ctx.qkv, o_cls, B, T, L, heads, self.attn.scale)
+            ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID,
+                     rowmap=cls_map, M=B)
+            h_cls = ctx.hid[:B]
+            ops.ln_gemm(X, cls_map, B, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
+                        self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
+            ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,
+                     M=B)
 
     def _run_split(self, X, ctx, probs):
         """Divided block with each residual sub-layer as GEMM (d = f(x), bias epilogue, storage

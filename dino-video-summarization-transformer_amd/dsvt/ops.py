@@ -4,6 +4,7 @@ current HIP stream; every computation is a libdsvt.so kernel.
 Storage dtype ("mode"): torch.bfloat16 (perf) or torch.float32 (parity).  The token
 tensor X, LayerNorm/softmax statistics and losses are always fp32.
 """
+import contextlib
 import os
 
 import torch
@@ -60,6 +61,18 @@ def _sk_workspace(dev):
         nbytes = int(_lib.lib().dsvt_workspace_bytes(_lib.WS_GEMM_SK, _lib.BF16, 1, 1, 1))
         ws = _SK_WS[key] = torch.zeros(nbytes // 4, device=dev, dtype=torch.int32)
     return ws
+
+
+@contextlib.contextmanager
+def skinny():
+    """The GEMM launches inside run the K-split skinny kernel where eligible (dsvt_set_gemm_skinny):
+    for the few-row GEMMs of the CLS-only last block and of the DINO head, chosen by call site so a
+    batch split over streams runs the same kernel as the whole batch."""
+    call("dsvt_set_gemm_skinny", 1)
+    try:
+        yield
+    finally:
+        call("dsvt_set_gemm_skinny", 0)
 
 
 def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=None):

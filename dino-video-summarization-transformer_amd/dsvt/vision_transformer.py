@@ -235,11 +235,12 @@ class DINOHead(nn.Module):
         h = torch.empty(R, x.shape[1], device=dev, dtype=mode)
         ops.cast(x, h)
         linears = [self.mlp] if isinstance(self.mlp, nn.Linear) else [m for m in self.mlp if isinstance(m, nn.Linear)]
-        for i, lin in enumerate(linears):
-            last = i == len(linears) - 1
-            out = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32 if last else mode)
-            ops.gemm(h, w(lin.weight), lin.bias, out, epilogue=EPI_BIAS if last else EPI_BIAS_GELU, out_f32=last)
-            h = out
+        with ops.skinny():                  # R = a few crops' CLS rows: K-split skinny kernel
+            for i, lin in enumerate(linears):
+                last = i == len(linears) - 1
+                out = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32 if last else mode)
+                ops.gemm(h, w(lin.weight), lin.bias, out, epilogue=EPI_BIAS if last else EPI_BIAS_GELU, out_f32=last)
+                h = out
         z = torch.empty(R, h.shape[1], device=dev, dtype=mode)
         ops.head_norm(h, z)                                                   # F.normalize (:280)
         ll = self.last_layer

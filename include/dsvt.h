@@ -490,13 +490,20 @@ int dsvt_gather_rows(const void *src, int64_t row_bytes, const int32_t *idx, int
 
 /* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
  * 1 = 128x128 / 4-wave kernel, 3-6 / 9-13 = 256x128 and 256x256 staged / persistent kernels,
- * 20 = 256x256 phase-interleaved persistent kernel (21-29: its diagnostic builds).
- * Process-global. */
+ * 20 = 256x256 phase-interleaved persistent kernel (21-29: its diagnostic builds), 33 / 40 / 41:
+ * X-streamed residual / stream-K / tail split, 50 = K-split skinny kernel.
+ * Per calling thread. */
 int dsvt_set_gemm_variant(int variant);
+/* Call-site scope (on = 1 / off = 0) for the following GEMM launches of the calling thread: the
+ * few-row GEMMs of the CLS-only last block (timesformer.py:181-184 on the CLS rows) and of the
+ * DINOHead MLP (vision_transformer.py DINOHead.forward) take the K-split skinny kernel where it is
+ * eligible, whatever their row count (so a batch split over streams stays bitwise equal to the
+ * whole batch).  Not a reference interface: a dsvt scheduling hint. */
+int dsvt_set_gemm_skinny(int on);
 /* Tuning knob (benchmarking / tests only): bf16 short-sequence attention kernel. 0 = automatic,
  * 1 = 16-key-tile x 4 waves, 2 = 13 x 8 waves, 3 = 13 x 4 waves, 4 = streaming flash kernel
- * (5, 6: diagnostic builds of 3).
- * Process-global. */
+ * (5, 6, 9, 10: diagnostic builds; 11: the pipelined persistent kernel).
+ * Per calling thread. */
 int dsvt_set_attn_variant(int variant);
 /* Tuning knob (tests only): attention backward, 0 = automatic (bf16 MFMA kernel for sequences
  * <= 256), 1 = the generic two-pass VALU kernels.  Process-global. */

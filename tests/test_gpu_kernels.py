@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20, 33, 40])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 20, 33, 40, 50])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -67,6 +67,52 @@ def test_gemm_bias_gelu(dtype, M, N, K, gemm_variant):
             ops.gemm(A, W, Bt, out, epilogue=epi, out_f32=out_f32)
             torch.cuda.synchronize()
             check(back(out), f(ref), dtype, "gemm epi=%d f32out=%d" % (epi, out_f32))
+
+
+@pytest.mark.parametrize("M", [1, 16, 17, 48, 64, 65, 130])
+@pytest.mark.parametrize("N,K", [(768, 768), (768, 3072), (3072, 768), (2304, 768), (256, 2048)])
+def test_gemm_skinny(M, N, K):
+    """The K-split skinny kernel (variant 50: 64-row blocks, 8 waves splitting K, partials added
+    in a fixed order through LDS) -- the CLS-only last block's and the DINO head's shapes: bias
+    (bf16 / fp32 out), GELU, and the fp32 residual through the CLS-row map (1, L, 0), against
+    float64; bitwise repeatable; each row's result independent of M (the first row block of M
+    rows equals the same rows computed alone)."""
+    from dsvt import _lib, ops
+    from dsvt._lib import EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID
+    a, w, b = rnd((M, K), 61), rnd((N, K), 62, 0.03), rnd((N,), 63)
+    A, W, Bt = to(a, torch.bfloat16), to(w, torch.bfloat16), to(b, torch.float32)
+    ref = back(A) @ back(W).T + b
+    _lib.call("dsvt_set_gemm_variant", 50)
+    try:
+        for epi, f in ((EPI_BIAS, lambda v: v), (EPI_BIAS_GELU, O.gelu)):
+            for out_f32 in (False, True):
+                outs = []
+                for _ in range(2):
+                    out = torch.full((M, N), 5.0, device=dev(), dtype=torch.float32 if out_f32 else torch.bfloat16)
+                    ops.gemm(A, W, Bt, out, epilogue=epi, out_f32=out_f32)
+                    outs.append(out)
+                torch.cuda.synchronize()
+                check(back(outs[0]), f(ref), torch.bfloat16, "skinny epi=%d f32out=%d" % (epi, out_f32))
+                assert torch.equal(outs[0], outs[1])
+                if M > 1:                          # rows do not depend on M (split-stream invariance)
+                    part = torch.full((1, N), 5.0, device=dev(), dtype=outs[0].dtype)
+                    ops.gemm(A[M - 1:], W, Bt, part, epilogue=epi, out_f32=out_f32)
+                    torch.cuda.synchronize()
+                    assert torch.equal(part[0], outs[0][M - 1])
+        if N == 768:                                   # residual into the CLS rows of M clips
+            L = 5
+            x0 = rnd((M * L, N), 64)
+            X = to(x0, torch.float32)
+            ops.gemm(A, W, Bt, X, epilogue=EPI_BIAS_RESID, rowmap=(1, L, 0), M=M)
+            torch.cuda.synchronize()
+            exp = x0.astype(np.float64).copy()
+            exp[np.arange(M) * L] += ref
+            err = np.abs(back(X) - exp).max() / np.abs(exp).max()
+            assert err < 1e-5, err
+            others = np.setdiff1d(np.arange(M * L), np.arange(M) * L)
+            np.testing.assert_array_equal(back(X)[others], x0[others])
+    finally:
+        _lib.call("dsvt_set_gemm_variant", 0)
 
 
 @pytest.mark.parametrize("variant", [10, 20, 33, 40])
