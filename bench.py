@@ -466,12 +466,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-train", action="store_true", help="skip the config-3 SSL training-step measurement")
-    ap.add_argument("--grouped", nargs="?", const="1", default=None, choices=["1", "2", "3", "4"],
-                    help="1: run the teacher / student backbone calls as one grouped lockstep forward (DSVT_GROUPED=1; "
-                         "A/B: measured 354 vs 370 clips/s for the concurrent streams); 2: group only the "
-                         "global-crop calls, the local-crop call on a concurrent stream; 3: three concurrent "
-                         "grouped forwards, each over a balanced share of every call's clips; 4: the two global "
-                         "calls minus r clips each plain, one grouped call over the rest, all concurrent")
+    ap.add_argument("--ln-fold", default="auto", choices=["auto", "on", "off"],
+                    help="LayerNorm folded into the GEMM that reads it (VisionTransformer.ln_fold; A/B)")
     ap.add_argument("--no-other", action="store_true", help="skip the config-4 / config-5 backbone measurements")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-grad-overlap", dest="grad_overlap", action="store_false",
@@ -482,8 +478,6 @@ def main():
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: allow N ranks on fewer GPUs (rank r uses GPU r %% count; needs --backend gloo)")
     args = ap.parse_args()
-    if args.grouped:
-        os.environ["DSVT_GROUPED"] = args.grouped
 
     from dsvt import dist as ddist
 
@@ -516,6 +510,8 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     student, teacher, dino_loss = build(dtype, device)
+    for net in (student, teacher):
+        net.backbone.ln_fold = {"auto": "auto", "on": True, "off": False}[args.ln_fold]
     crops = synthetic_crops(args.clips, device, seed=1234 + rank)
 
     from dsvt.utils import dino_forward
@@ -649,23 +645,6 @@ def main():
                                     "/ measured time",
                         "all_gemm_tflops": round(float(np.sum(work)) / (all_ms * 1e-3) / 1e12, 1)}
 
-    from dsvt.utils import _groupable
-    with torch.no_grad():
-        grouped = _groupable(student, teacher, crops)
-    grouped_desc = ("grouped: the teacher / student backbone calls advance in lockstep over one token buffer, every "
-                    "Linear of a layer ONE launch over all calls (dsvt_gemm_grouped_fwd), one stream")
-    if os.environ.get("DSVT_GROUPED") == "4":
-        grouped_desc = ("remainder grouped: the teacher's and the student's global-crop calls minus r clips each as "
-                        "plain forwards, one grouped forward over their last r clips and the local crops, three "
-                        "concurrent HIP streams")
-    if os.environ.get("DSVT_GROUPED") == "3":
-        grouped_desc = ("balanced grouped: three concurrent HIP streams, each a lockstep grouped forward over a "
-                        "balanced share of the teacher-global, student-global and student-local clips (every Linear "
-                        "one dsvt_gemm_grouped_fwd launch per stream)")
-    if os.environ.get("DSVT_GROUPED") == "2":
-        grouped_desc = ("grouped global crops: the teacher's and the student's global-crop calls in lockstep, every "
-                        "Linear of a layer ONE launch over both (dsvt_gemm_grouped_fwd); the local-crop call on a "
-                        "concurrent stream")
     value = world * args.clips * args.steps / elapsed
     step_ms = elapsed / args.steps * 1e3
     folded = student.backbone.fold_temporal_fc
@@ -685,8 +664,9 @@ def main():
                       "parallelism": "dp%d" % world,
                       "weights": "random init (torch seed 0)",
                       "launch": "eager" if graph is None else "hip_graph (forward+loss captured; center all-reduce eager)",
-                      "streams": grouped_desc if grouped else
-                      ("serial" if args.serial else "3 backbone calls on concurrent HIP streams")},
+                      "streams": "serial" if args.serial else "3 backbone calls on concurrent HIP streams",
+                      "layernorm": ("folded into the GEMM that reads it (dsvt_gemm_lnx_fwd)"
+                                    if student.backbone.ln_fold else "LayerNorm pass + GEMM")},
            "step_roofline": {"achieved": round(step_tflops / world, 1), "peak": PEAK_TFLOPS[args.dtype],
                              "unit": "TFLOP/s per GPU", "flops": "executed",
                              "frac": round(step_tflops / world / PEAK_TFLOPS[args.dtype], 4),

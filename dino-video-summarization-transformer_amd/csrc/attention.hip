@@ -263,8 +263,7 @@ __device__ __forceinline__ sv4 ds_read_tr16_asm(const bf16_t* lds_ptr) {
 }
 
 // One 16-query tile of a short sequence against its K / V staged in LDS (`lds` layout below):
-// scores, exact two-pass softmax, P.V and the output stores.  Shared by the one-item kernel
-// and the pipelined persistent one.
+// scores, exact two-pass softmax, P.V and the output stores.
 template <int NKT, int DBG, bool SWZ>
 __device__ __forceinline__ void short_tile(const AttnParams& p, const bf16_t* Ks, const bf16_t* Vs, const sv8 qf0,
                                            const sv8 qf1, const int qt, const int L, const int nkt, const int64_t seq,
@@ -518,77 +517,13 @@ __global__ __launch_bounds__(64 * NW, SWZ ? 3 : 2) void attn_short_bf16(AttnPara
   }
 }
 
-// Pipelined persistent form (1 + 196 keys, the swizzled layout; opt-in, DSVT_ATTN_PIPE=1 or
-// variant 11): one 512-thread workgroup per CU walks the (sequence, head) items with a stride of
-// the grid; Q, K and V of its NEXT item are staged by LDS-DMA into the other half of 156 KB of
-// LDS while the 8 waves run the current item's query tiles.  Bitwise the one-item kernel's
-// results, but SLOWER: 54-57 vs 44-48 us at the bench's global call, and 56.5 us with the overlap
-// defeated (intrinsic V^T reads, before which the compiler waits for every in-flight LDS-DMA) --
-// one 8-wave workgroup per CU computes an item about 3x slower than three co-resident 4-wave
-// ones, which the overlap does not buy back (bench 385 vs 388-389 clips/s).
-// Every staged row is a 128-byte head slice of one token row; a wave DMA instruction moves 8 of
-// them (lane = row (l >> 3), physical 16-B chunk l & 7, loading logical chunk (l & 7) ^ (row & 7)
-// -- the `lds` swizzle).  Rows past L are staged as row L - 1: finite, their keys are masked,
-// their probabilities are 0 and their queries are not stored.
-template <int NKT>
-__global__ __launch_bounds__(512, 1) void attn_short_pipe_bf16(AttnParams p, int64_t items) {
-  constexpr int NW = 8, LP = NKT * 16, BUFE = LP * 64, NI = LP / 8;   // NI: DMA instructions per buffer
-  constexpr int QT_W = (NKT + NW - 1) / NW;
-  __shared__ __attribute__((aligned(16))) bf16_t sm[2][3][BUFE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r16 = lane & 15, g = lane >> 4;
-  const bf16_t* qkv = (const bf16_t*)p.qkv;
-  const int64_t C = p.C, heads = p.heads, G = gridDim.x;
-  const int L = (int)p.seqlen, nkt = (L + 15) >> 4, nqt = nkt;
-  const float sl2 = p.scale * 1.4426950408889634f;
-  auto stage = [&](int buf, int64_t item) {
-    const int h = (int)(item % heads);
-    const int64_t seq = item / heads, b = seq / p.tin, t = seq % p.tin;
-    for (int i = wave; i < 3 * NI; i += NW) {   // wave-uniform
-      const int role = i / NI, ri = i - role * NI;
-      const int r = ri * 8 + (lane >> 3), c = (lane & 7) ^ (r & 7);
-      const bf16_t* src = qkv + tok_row(p, b, t, r < L ? r : L - 1) * p.ld_qkv + role * C + h * 64 + c * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(&sm[buf][role][ri * 512]), 16, 0, 0);
-    }
-  };
-  int64_t item = blockIdx.x;
-  if (item < items) stage(0, item);
-  for (int buf = 0; item < items; item += G, buf ^= 1) {
-    // this wave's DMAs of `item` have landed (vmcnt 0); the barrier: every wave's have, and
-    // every wave is done reading the other buffer (the previous item)
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), lgkmcnt / expcnt untouched
-    __syncthreads();
-    const int h = (int)(item % heads);
-    const int64_t seq = item / heads, b = seq / p.tin, t = seq % p.tin;
-    // the DropPath scale is read BEFORE the next item's staging: a global load issued behind the
-    // staging DMAs would make the compiler wait for all of them (vmcnt counts in order)
-    const float oscale = p.seq_scale ? p.seq_scale[seq] : 1.0f;
-    asm volatile("" ::"v"(oscale));
-    if (item + G < items) stage(buf ^ 1, item + G);
-    const bf16_t* Qs = sm[buf][0];
-    const bf16_t* Ks = sm[buf][1];
-    const bf16_t* Vs = sm[buf][2];
-#pragma unroll
-    for (int w = 0; w < QT_W; ++w) {
-      const int qt = wave + NW * w;
-      if (qt >= nqt) break;
-      const int qr = qt * 16 + r16;
-      const sv8 qf0 = *reinterpret_cast<const sv8*>(Qs + qr * 64 + ((g ^ (qr & 7)) << 3));
-      const sv8 qf1 = *reinterpret_cast<const sv8*>(Qs + qr * 64 + (((g + 4) ^ (qr & 7)) << 3));
-      short_tile<NKT, 5, true>(p, Ks, Vs, qf0, qf1, qt, L, nkt, seq, b, t, h, sl2, r16, g, oscale);
-    }
-  }
-}
-
 // 0 = auto; otherwise forced (tools/attn_check.py, tests).  Per calling thread: a diagnostic
 // override on one thread never changes the kernels another thread's launches pick.
 static thread_local int g_attn_variant = 0;
 void set_attn_variant(int v) { g_attn_variant = v; }
 
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
-  // DSVT_ATTN_PIPE=1: the pipelined persistent kernel for 1 + 196 keys (variant 11) by default
-  static const int pipe = getenv("DSVT_ATTN_PIPE") ? atoi(getenv("DSVT_ATTN_PIPE")) : 0;
-  const int v = g_attn_variant ? g_attn_variant : (pipe && p.seqlen > 192 && p.seqlen <= 208) ? 11 : 0;
+  const int v = g_attn_variant;
   if (dtype == 0 && p.seqlen <= 256 && v != 4) {
     dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
     // measured at 1 + 196 keys x 8 frames x 16 clips (tools/attn_bench.py): <13, 4> 60 us,
@@ -603,10 +538,6 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
     else if (v == 9 && p.seqlen <= 208) attn_short_bf16<13, 4, 3, true><<<grid, 256, 0, s>>>(p);   // diagnostic
     else if (v == 10 && p.seqlen <= 208)                                      // (sequence, head) grid
       attn_short_bf16<13, 4, 4, true><<<dim3(grid.y, grid.x), 256, 0, s>>>(p);
-    else if (v == 11 && p.seqlen <= 208 && p.seqlen > 192) {                  // pipelined persistent
-      const int64_t items = (int64_t)grid.x * grid.y;
-      attn_short_pipe_bf16<13><<<dim3((unsigned)(items < 256 ? items : 256)), 512, 0, s>>>(p, items);
-    }
     // 1 + 196 patches: swizzled exact-tile LDS, 3 workgroups per CU -- 53.4 vs 62.2 us at the
     // bench's global call (16 clips x 8 frames x 12 heads); 25.3 vs 24.5 us at 1 + 36 (kept <4, 4>)
     else if (p.seqlen <= 208) attn_short_bf16<13, 4, 0, true><<<grid, 256, 0, s>>>(p);

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/dsvt.h"
+#include "../../include/dsvt_debug.h"
 #include "internal.h"
 
 using namespace dsvt;
@@ -74,9 +75,8 @@ int probed(int family, double work, hipStream_t s, const char* where, F&& launch
 // GEMM instantiation id: gemm_kernel<T = dtype ? float : bf16, EPI = epi, OUT_F32 = f32>
 // probe tag of a GEMM launch: variant * 32 + dtype * 16 + epilogue * 2 + fp32-output, so the
 // host can name the exact kernel instantiation rocprofv3 reports (dsvt/ops.py gemm_kernel_name)
-constexpr int ROWLN_PROBE_TAG = 30 * 32 + 2 * 2 + 1;   // "variant 30": gemm_rowln_kernel (dsvt/ops.py)
 constexpr int WGRAD_PROBE_TAG = 31 * 32 + 1;            // "variant 31": wgrad_kernel
-constexpr int GROUPED_PROBE_TAG = 50 * 32;               // "variant 50": gemm_8ph_kernel<..., SEG = true>
+static_assert(LN_PARTS == DSVT_LN_PARTS && LN_PARTS * 64 == DSVT_LN_FOLD_C, "LayerNorm partials");
 
 // algorithmic HBM bytes of one GEMM launch: A and W once, the output once (+ the fp32 residual
 // X read for EPI_RESID, + the aux tensor for the training epilogues), the bias
@@ -140,7 +140,6 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_SELECT: return up(select_frames_ws_bytes(M, N));                    // M = scores, N = unsampled
     case DSVT_WS_AUGMENT: return up(augment_ws_bytes(M, N));                          // M = frames, N = size
     case DSVT_WS_WGRAD: return up(wgrad_workspace_floats(M, N, K) * 4);              // M = rows, N, K: G [N, K]
-    case DSVT_WS_GEMM_SK: return SK_WS_BYTES;                                        // any shape
     case DSVT_WS_ATTN_CLS: return up(attn_cls_ws_bytes(M, N, K));                    // M = B*T, N = heads, K = keys
     default: return -1;
   }
@@ -149,73 +148,15 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
 int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, const void* W, int64_t ldw,
                   const float* bias, void* out, int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg,
                   int64_t gstride, int64_t goff, void* stream) {
+  const bool few = (epilogue & DSVT_GEMM_FEW_ROWS) != 0;
+  epilogue &= ~DSVT_GEMM_FEW_ROWS;
   if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
   REQUIRE(epilogue <= 2, "gemm: epilogue %d is reachable only through dsvt_patch_embed_fwd / dsvt_gemm_aux_fwd",
           epilogue);
   norm_map(rpg, gstride, goff);
   GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.few_rows = few;
   return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_fwd",
-                [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
-                gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
-}
-
-int dsvt_gemm_grouped_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, int64_t ldw, void* out,
-                          int64_t ldo, int64_t N, int64_t K, int nseg, const dsvt_gemm_seg* segs, void* stream) {
-  REQUIRE(nseg >= 1 && nseg <= GemmParams::MAX_SEG && segs, "gemm_grouped: nseg must be 1..%d",
-          GemmParams::MAX_SEG);
-  REQUIRE(epilogue <= 2, "gemm_grouped: epilogue %d not supported", epilogue);
-  int64_t vrows = 0;
-  double flops = 0, bytes = 0;
-  for (int i = 0; i < nseg; ++i) {
-    const dsvt_gemm_seg& q = segs[i];
-    REQUIRE(q.M >= 1 && q.a_row0 >= 0, "gemm_grouped: segment %d: bad rows", i);
-    if (int e = check_gemm(dtype, epilogue, (const char*)A + q.a_row0 * lda * (dtype == DSVT_BF16 ? 2 : 4), lda,
-                           q.W, ldw, q.bias, out, ldo, q.M, N, K))
-      return e;
-    vrows += (q.M + 255) / 256 * 256;
-    flops += 2.0 * q.M * N * K;
-    bytes += gemm_bytes(dtype, epilogue, out_f32, q.M, N, K);
-  }
-  GemmParams p{A, lda, segs[0].W, ldw, segs[0].bias, out, ldo, vrows, N, K, 0, 0, 0,
-               nullptr, nullptr, nullptr, nullptr, 1};
-  p.nseg = nseg;
-  int64_t mt = 0;
-  for (int i = 0; i < nseg; ++i) {
-    const dsvt_gemm_seg& q = segs[i];
-    int64_t rpg = q.rpg, gs = q.gstride, go = q.goff;
-    if (rpg <= 0) { rpg = INT64_MAX; gs = 0; }
-    p.seg[i] = GemmParams::Seg{q.W, q.bias, q.a_row0, q.M, rpg, gs, go, mt};
-    mt += (q.M + 255) / 256;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  const bool grouped = dtype == DSVT_BF16 && gemm_8ph_grouped_ok(p, epilogue, out_f32);
-  return probed(DSVT_PROBE_GEMM, flops, s, "dsvt_gemm_grouped_fwd", [&]() -> hipError_t {
-    if (grouped) return launch_gemm_8ph_grouped(p, epilogue, out_f32, s);
-    for (int i = 0; i < nseg; ++i) {          // one plain launch per segment
-      const dsvt_gemm_seg& q = segs[i];
-      GemmParams g{(const char*)A + q.a_row0 * lda * (dtype == DSVT_BF16 ? 2 : 4), lda, q.W, ldw, q.bias, out, ldo,
-                   q.M, N, K, q.rpg, q.gstride, q.goff, nullptr, nullptr, nullptr, nullptr, 1};
-      if (g.rpg <= 0) { g.rpg = INT64_MAX; g.gstride = 0; }   // identity map, keeping the segment's out row offset
-      if (hipError_t e = launch_gemm(g, dtype, epilogue, out_f32, s)) return e;
-    }
-    return hipSuccess;
-  }, grouped ? GROUPED_PROBE_TAG + dtype * 16 + epilogue * 2 + (out_f32 || epilogue == EPI_RESID) : 0, bytes);
-}
-
-int dsvt_gemm_sk_fwd(int dtype, int epilogue, int out_f32, const void* A, int64_t lda, const void* W, int64_t ldw,
-                     const float* bias, void* out, int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg,
-                     int64_t gstride, int64_t goff, void* workspace, int64_t workspace_bytes, void* stream) {
-  if (int e = check_gemm(dtype, epilogue, A, lda, W, ldw, bias, out, ldo, M, N, K)) return e;
-  REQUIRE(epilogue <= 2, "gemm_sk: epilogue %d is reachable only through dsvt_patch_embed_fwd / dsvt_gemm_aux_fwd",
-          epilogue);
-  REQUIRE(workspace && workspace_bytes >= SK_WS_BYTES && ((uintptr_t)workspace & 255) == 0,
-          "gemm_sk: workspace must be >= %lld bytes (dsvt_workspace_bytes(DSVT_WS_GEMM_SK)), 256-byte aligned",
-          (long long)SK_WS_BYTES);
-  norm_map(rpg, gstride, goff);
-  GemmParams p{A, lda, W, ldw, bias, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
-  p.sk_cnt = (int*)workspace;
-  p.sk_part = (float*)((char*)workspace + SK_CNT_BYTES);
-  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_sk_fwd",
                 [&] { return launch_gemm(p, dtype, epilogue, out_f32, (hipStream_t)stream); },
                 gemm_tag(p, dtype, epilogue, out_f32), gemm_bytes(dtype, epilogue, out_f32, M, N, K));
 }
@@ -264,53 +205,65 @@ int dsvt_layernorm_fwd(int dtype, int out_f32, const float* x, void* y, const fl
   });
 }
 
-int dsvt_add_layernorm_fwd(int d_dtype, int y_dtype, float* x, const void* d, void* y, const float* gamma,
-                           const float* beta, int64_t rows, int64_t C, int64_t L, int dmode, int ymode, float eps,
-                           void* stream) {
-  REQUIRE(d_dtype == DSVT_BF16 || d_dtype == DSVT_F32, "add_layernorm: bad d dtype");
-  REQUIRE(y_dtype == DSVT_BF16 || y_dtype == DSVT_F32, "add_layernorm: bad y dtype");
-  REQUIRE(dmode >= 0 && dmode <= 2 && ymode >= 0 && ymode <= 2, "add_layernorm: dmode / ymode must be in [0, 2]");
-  REQUIRE(dmode != 0 || ymode != 0, "add_layernorm: nothing to do (dmode = ymode = 0)");
-  REQUIRE(C == 768, "add_layernorm: C must be 768 (got %lld)", (long long)C);
-  REQUIRE(rows > 0 && L >= 1 && rows % L == 0, "add_layernorm: rows must be a positive multiple of L");
-  REQUIRE(dmode != 2 || L >= 2, "add_layernorm: the patch layout needs L >= 2");
-  REQUIRE(ymode != 2 || L >= 2, "add_layernorm: the patch layout needs L >= 2");
-  REQUIRE(x && (dmode == 0 || d) && (ymode == 0 || (y && gamma && beta)), "add_layernorm: null pointer");
-  REQUIRE(aligned16(x) && (dmode == 0 || aligned16(d)) && (ymode == 0 || (aligned16(y) && aligned16(gamma) && aligned16(beta))),
-          "add_layernorm: pointers must be 16-byte aligned");
-  const double drows = dmode == 2 ? (double)rows / L * (L - 1) : dmode == 1 ? (double)rows : 0.0;
-  const double yrows = ymode == 2 ? (double)rows / L * (L - 1) : ymode == 1 ? (double)rows : 0.0;
-  const double bytes = (double)C * (4.0 * rows + 4.0 * drows + drows * esize(d_dtype) + yrows * esize(y_dtype));
-  return probed(DSVT_PROBE_NORM, bytes, (hipStream_t)stream, "dsvt_add_layernorm_fwd", [&] {
-    return launch_add_layernorm(d_dtype == DSVT_F32, y_dtype == DSVT_F32, x, d, y, gamma, beta, rows, L, dmode, ymode,
-                                eps, (hipStream_t)stream);
-  });
+int dsvt_ln_fold_weights(const float* W, const float* gamma, const float* beta, const float* bias, void* Wf,
+                         float* wsum, float* bias_f, int64_t N, int64_t K, void* stream) {
+  REQUIRE(W && gamma && beta && Wf && wsum && bias_f, "ln_fold_weights: null pointer");
+  REQUIRE(N > 0 && K > 0 && K % 256 == 0, "ln_fold_weights: need N > 0, K %% 256 == 0 (N=%lld K=%lld)", (long long)N,
+          (long long)K);
+  REQUIRE(aligned16(W) && aligned16(gamma) && aligned16(beta) && aligned16(Wf), "ln_fold_weights: pointers must be 16-byte aligned");
+  hipError_t e = launch_ln_fold(W, gamma, beta, bias, Wf, wsum, bias_f, N, K, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "ln_fold_weights");
 }
 
-int dsvt_gemm_resid_ln_fwd(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, float* X,
-                           int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
-                           const float* gamma, const float* beta, float eps, void* Y, int ymode, int64_t L,
-                           void* stream) {
-  REQUIRE(A && W && X, "gemm_resid_ln: null pointer");
-  REQUIRE(N == 768, "gemm_resid_ln: N must be 768 (got %lld)", (long long)N);
-  REQUIRE(M > 0 && K > 0 && K % 128 == 0, "gemm_resid_ln: need M > 0, K > 0, K %% 128 == 0 (M=%lld K=%lld)",
-          (long long)M, (long long)K);
-  REQUIRE(lda >= K && ldw >= K && lda % 8 == 0 && ldw % 8 == 0, "gemm_resid_ln: lda/ldw must be >= K, multiples of 8");
-  REQUIRE(M * lda * 2 <= (int64_t)UINT32_MAX && N * ldw * 2 <= (int64_t)UINT32_MAX,
-          "gemm_resid_ln: A and W must span < 4 GiB (32-bit DMA offsets)");
-  REQUIRE(aligned16(A) && aligned16(W) && aligned16(X) && (!bias || aligned16(bias)),
-          "gemm_resid_ln: pointers must be 16-byte aligned");
-  REQUIRE(ymode == DSVT_ROWLN_NONE || ymode == DSVT_ROWLN_X || ymode == DSVT_ROWLN_COMPACT, "gemm_resid_ln: bad ymode");
-  REQUIRE(ymode == DSVT_ROWLN_NONE || (gamma && beta && Y && aligned16(gamma) && aligned16(beta) && aligned16(Y)),
-          "gemm_resid_ln: LayerNorm output needs gamma, beta, Y (16-byte aligned)");
-  REQUIRE(ymode != DSVT_ROWLN_COMPACT || L > 1, "gemm_resid_ln: compact output needs L > 1");
+int dsvt_ln_stats_fwd(const float* x, void* xb, float* stats, int64_t rows, int64_t C, void* stream) {
+  REQUIRE(x && xb && stats, "ln_stats: null pointer");
+  REQUIRE(rows > 0 && C == DSVT_LN_FOLD_C, "ln_stats: need rows > 0 and C == %d (got %lld)", DSVT_LN_FOLD_C, (long long)C);
+  REQUIRE(aligned16(x) && aligned16(xb) && ((uintptr_t)stats & 7) == 0, "ln_stats: x / xb 16-byte, stats 8-byte aligned");
+  return probed(DSVT_PROBE_NORM, (double)rows * C * 6 + (double)rows * LN_PARTS * 8, (hipStream_t)stream,
+                "dsvt_ln_stats_fwd", [&] { return launch_ln_stats(x, xb, stats, rows, (hipStream_t)stream); });
+}
+
+int dsvt_gemm_resid_stats_fwd(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, float* X,
+                              void* xb, float* stats, int64_t ldx, int64_t M, int64_t N, int64_t K, int64_t rpg,
+                              int64_t gstride, int64_t goff, void* stream) {
+  if (int e = check_gemm(DSVT_BF16, EPI_RESID, A, lda, W, ldw, bias, X, ldx, M, N, K)) return e;
+  REQUIRE(xb && stats && aligned16(xb) && ((uintptr_t)stats & 7) == 0,
+          "gemm_resid_stats: xb (16-byte aligned) and stats (8-byte aligned) are required");
+  REQUIRE(N == DSVT_LN_FOLD_C && ldx == N, "gemm_resid_stats: N and ldx must be %d (got %lld, %lld)", DSVT_LN_FOLD_C,
+          (long long)N, (long long)ldx);
   norm_map(rpg, gstride, goff);
-  RowLnParams p{};
-  p.A = A; p.lda = lda; p.W = W; p.ldw = ldw; p.bias = bias; p.X = X; p.M = M; p.K = K;
-  p.rpg = rpg; p.gstride = gstride; p.goff = goff;
-  p.gamma = gamma; p.beta = beta; p.eps = eps; p.Y = (unsigned short*)Y; p.ymode = ymode; p.L = L;
-  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_resid_ln_fwd",
-                [&] { return launch_gemm_rowln(p, (hipStream_t)stream); }, ROWLN_PROBE_TAG);
+  GemmParams p{A, lda, W, ldw, bias, X, ldx, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.xb_out = xb;
+  p.stats_out = stats;
+  REQUIRE(gemm_8ph_ok(p, EPI_RESID), "gemm_resid_stats: A / W exceed the 32-bit DMA offsets or K %% 64 != 0");
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_resid_stats_fwd",
+                [&] { return launch_gemm(p, DSVT_BF16, EPI_RESID, 1, (hipStream_t)stream); },
+                gemm_tag(p, DSVT_BF16, EPI_RESID, 1),
+                gemm_bytes(DSVT_BF16, EPI_RESID, 1, M, N, K) + 2.0 * M * N + 8.0 * M * LN_PARTS);
+}
+
+int dsvt_gemm_lnx_fwd(int epilogue, const void* xb, int64_t ldxb, int64_t a_rpg, int64_t a_gstride, int64_t a_goff,
+                      const float* stats, float eps, const void* Wf, const float* wsum, const float* bias_f, void* out,
+                      int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
+                      void* stream) {
+  REQUIRE(epilogue == DSVT_EPI_BIAS || epilogue == DSVT_EPI_BIAS_GELU, "gemm_lnx: epilogue must be BIAS or BIAS_GELU");
+  if (int e = check_gemm(DSVT_BF16, epilogue, xb, ldxb, Wf, K, bias_f, out, ldo, M, N, K)) return e;
+  REQUIRE(K == DSVT_LN_FOLD_C, "gemm_lnx: K must be %d (got %lld)", DSVT_LN_FOLD_C, (long long)K);
+  REQUIRE(N % 256 == 0, "gemm_lnx: N must be a multiple of 256 (got %lld)", (long long)N);
+  REQUIRE(stats && wsum && bias_f && ((uintptr_t)stats & 7) == 0 && aligned16(wsum),
+          "gemm_lnx: stats (8-byte aligned), wsum and bias_f (16-byte aligned) are required");
+  norm_map(rpg, gstride, goff);
+  norm_map(a_rpg, a_gstride, a_goff);
+  GemmParams p{xb, ldxb, Wf, K, bias_f, out, ldo, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.a_rpg = a_rpg; p.a_gstride = a_gstride; p.a_goff = a_goff;
+  p.ln_stats = stats; p.ln_wsum = wsum; p.ln_eps = eps; p.ln_invk = 1.0f / (float)K;
+  // the last A row the DMA offsets reach (32-bit, like gemm_8ph_ok's check)
+  const int64_t last = (M - 1) / a_rpg * a_gstride + a_goff + (M - 1) % a_rpg;
+  REQUIRE(last * ldxb * 2 + K * 2 <= (int64_t)UINT32_MAX && last < INT32_MAX && gemm_8ph_ok(p, epilogue),
+          "gemm_lnx: A / W exceed the 32-bit DMA offsets");
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_lnx_fwd",
+                [&] { return launch_gemm(p, DSVT_BF16, epilogue, 0, (hipStream_t)stream); },
+                gemm_tag(p, DSVT_BF16, epilogue, 0), gemm_bytes(DSVT_BF16, epilogue, 0, M, N, K) + 8.0 * M * LN_PARTS);
 }
 
 int dsvt_ln_gemm_fwd(int dtype, int epilogue, int out_f32, const float* x, int64_t in_rpg, int64_t in_gstride,
@@ -320,7 +273,7 @@ int dsvt_ln_gemm_fwd(int dtype, int epilogue, int out_f32, const float* x, int64
   REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_GEMM, dtype, M, N, K),
           "ln_gemm: workspace too small (%lld < %lld)", (long long)workspace_bytes,
           (long long)dsvt_workspace_bytes(DSVT_WS_LN_GEMM, dtype, M, N, K));
-  if (int e = check_gemm(dtype, epilogue, workspace, K, W, K, bias, out, ldo, M, N, K)) return e;
+  if (int e = check_gemm(dtype, epilogue & ~DSVT_GEMM_FEW_ROWS, workspace, K, W, K, bias, out, ldo, M, N, K)) return e;
   if (int e = dsvt_layernorm_fwd(dtype, 0, x, workspace, gamma, beta, M, K, in_rpg, in_gstride, in_goff, eps, stream))
     return e;
   return dsvt_gemm_fwd(dtype, epilogue, out_f32, workspace, K, W, K, bias, out, ldo, M, N, K, rpg, gstride, goff, stream);
@@ -557,22 +510,15 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 }
 
 int dsvt_set_gemm_variant(int variant) {
-  REQUIRE(variant == 0 || variant == 1 || variant == 2 || (variant >= 3 && variant <= 6) || (variant >= 9 && variant <= 13) ||
-              (variant >= 20 && variant <= 29 && variant != 24) || variant == 14 || variant == 24 || variant == 34 ||
-              variant == 33 || variant == 40 || variant == 41 || variant == 50,
-          "gemm variant must be 0-6, 9-13, 20, 33 (X-streamed residual), 40 (stream-K), 41 (auto + tail split), 50 (K-split skinny; "
-          "14/24/34: ablation builds)");
+  REQUIRE(variant == 0 || variant == 1 || variant == 10 || (variant >= 20 && variant <= 29 && variant != 24) ||
+              variant == 50,
+          "gemm variant must be 0 (auto), 1, 10, 20 (21-29 but 24: ablation builds) or 50");
   set_gemm_variant(variant);
   return 0;
 }
 
-int dsvt_set_gemm_skinny(int on) {
-  set_gemm_skinny(on ? 1 : 0);
-  return 0;
-}
-
 int dsvt_set_attn_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 11, "attention variant must be 0-11");
+  REQUIRE(variant >= 0 && variant <= 10, "attention variant must be 0-10");
   set_attn_variant(variant);
   return 0;
 }

@@ -294,134 +294,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   else epilogue_128<T, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
 }
 
-// ---- variant 2: the same 128x128 bf16 tile on a 4-deep LDS-DMA ring with counted waits.
-// One MFMA k-step (64 B of K) per stage, 16 KB per stage, 64 KB per workgroup (2 per CU).
-// Stage kt+3 is issued right after the barrier that retires stage kt-1, so three stages are
-// in flight and each wave waits only for its own oldest stage (vmcnt 8 / 4 / 0) -- no
-// vmcnt(0) drain per K step.  The k-steps run in the same order as variant 1's, so the two
-// produce bitwise-identical results.  Row r of a stage holds its four 16-B K chunks at
-// slot = chunk ^ pswz(r), pswz(r) = -(r >> 2) mod 4: the 16 lanes of every ds_read_b128
-// lane group then cover all 64 banks.
-// Measured on MI355X (tools/gemm_bench.py, same box, interleaved): 10-17 % SLOWER than
-// variant 1 on every hot-path shape (proj 62.7 vs 58.3 us, fc2 160 vs 138 us): twice the
-// barriers per K and 64-B row segments per load cost more than the drain they remove, since
-// variant 1's second resident workgroup already covers it.  Kept opt-in (DSVT_GEMM_VARIANT=2).
-constexpr int PB = 64;                        // K bytes per stage
-constexpr int P_TILE = BM * PB;               // 8 KB per operand per stage
-constexpr int P_STAGE = 2 * P_TILE;
-constexpr int P_NST = 4;
-
-__device__ __forceinline__ int pswz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
-
-__device__ __forceinline__ void stage_tile64(const char* __restrict__ g, int64_t ld_bytes, int64_t row0, int64_t rows,
-                                             int64_t kbyte0, char* lds_tile, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int piece = wave * 2 + i;           // 8 pieces of 16 rows x 64 B, lane-linear in LDS
-    const int r = piece * 16 + (lane >> 2), cl = lane & 3;
-    int64_t gr = row0 + r;
-    gr = gr < rows ? gr : rows - 1;
-    const char* src = g + gr * ld_bytes + kbyte0 + ((cl ^ pswz(r)) << 4);
-    __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void p_vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt immediate");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
-}
-
-template <int EPI, bool OUT_F32>
-__global__ __launch_bounds__(256, 2) void gemm_pipe_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[P_NST * P_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1, r16 = lane & 15, g = lane >> 4;
-  const int tilesN = (int)((p.N + BN - 1) / BN);
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int64_t m0 = (int64_t)(wg / tilesN) * BM;
-  const int64_t n0 = (int64_t)(wg % tilesN) * BN;
-  const char* A = (const char*)p.A;
-  const char* W = (const char*)p.W;
-  const int64_t lda_b = p.lda * 2, ldw_b = p.ldw * 2;
-  const int nk = (int)(p.K * 2 / PB);
-
-  fv4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int st = 0; st < P_NST - 1; ++st) {
-    if (st < nk) {
-      stage_tile64(A, lda_b, m0, p.M, (int64_t)st * PB, smem + st * P_STAGE, wave, lane);
-      stage_tile64(W, ldw_b, n0, p.N, (int64_t)st * PB, smem + st * P_STAGE + P_TILE, wave, lane);
-    }
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int later = nk - 1 - kt;            // stages issued beyond kt (at most 2 here)
-    if (later >= 2) p_vm_wait<8>();
-    else if (later == 1) p_vm_wait<4>();
-    else p_vm_wait<0>();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();             // stage kt landed for all waves; stage kt-1 read by all
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + P_NST - 1 < nk) {
-      char* nxt = smem + ((kt + P_NST - 1) & (P_NST - 1)) * P_STAGE;
-      stage_tile64(A, lda_b, m0, p.M, (int64_t)(kt + P_NST - 1) * PB, nxt, wave, lane);
-      stage_tile64(W, ldw_b, n0, p.N, (int64_t)(kt + P_NST - 1) * PB, nxt + P_TILE, wave, lane);
-    }
-    const char* At = smem + (kt & (P_NST - 1)) * P_STAGE;
-    const char* Wt = At + P_TILE;
-    sv8 a[4], b[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wm * 64 + i * 16 + r16;
-      a[i] = *reinterpret_cast<const sv8*>(At + row * PB + ((g ^ pswz(row)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = wn * 64 + j * 16 + r16;
-      b[j] = *reinterpret_cast<const sv8*>(Wt + row * PB + ((g ^ pswz(row)) << 4));
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-  }
-  mfma_result_fence();
-  if (m0 + BM <= p.M && n0 + BN <= p.N) epilogue_128<bf16_t, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
-  else epilogue_128<bf16_t, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
-}
-
-static bool gemm_pipe_ok(const GemmParams& p) { return p.K % 32 == 0 && p.K >= 32; }
-
-static hipError_t launch_pipe(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
-  const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid((unsigned)tiles), block(256);
-  switch (epi) {
-    case EPI_BIAS:
-      if (out_f32) gemm_pipe_kernel<EPI_BIAS, true><<<grid, block, 0, s>>>(p);
-      else gemm_pipe_kernel<EPI_BIAS, false><<<grid, block, 0, s>>>(p);
-      break;
-    case EPI_GELU:
-      if (out_f32) gemm_pipe_kernel<EPI_GELU, true><<<grid, block, 0, s>>>(p);
-      else gemm_pipe_kernel<EPI_GELU, false><<<grid, block, 0, s>>>(p);
-      break;
-    case EPI_RESID: gemm_pipe_kernel<EPI_RESID, true><<<grid, block, 0, s>>>(p); break;
-    case EPI_GELU_SAVE: gemm_pipe_kernel<EPI_GELU_SAVE, false><<<grid, block, 0, s>>>(p); break;
-    case EPI_DGELU:
-      if (out_f32) gemm_pipe_kernel<EPI_DGELU, true><<<grid, block, 0, s>>>(p);
-      else gemm_pipe_kernel<EPI_DGELU, false><<<grid, block, 0, s>>>(p);
-      break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
 template <typename T>
 static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
   const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -435,12 +307,10 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
       if (out_f32) gemm_kernel<T, EPI_GELU, true><<<grid, block, 0, s>>>(p);
       else gemm_kernel<T, EPI_GELU, false><<<grid, block, 0, s>>>(p);
       break;
-    case EPI_RESID: {
-      static const int pref = getenv("DSVT_RESID_PREF") ? atoi(getenv("DSVT_RESID_PREF")) : 1;   // tuning only
-      if (pref && sizeof(T) == 2) gemm_kernel<T, EPI_RESID, true, true><<<grid, block, 0, s>>>(p);
+    case EPI_RESID:   // bf16: the instantiation with the residual-tile prefetch (PREF)
+      if (sizeof(T) == 2) gemm_kernel<T, EPI_RESID, true, true><<<grid, block, 0, s>>>(p);
       else gemm_kernel<T, EPI_RESID, true><<<grid, block, 0, s>>>(p);
       break;
-    }
     case EPI_PATCH: gemm_kernel<T, EPI_PATCH, true><<<grid, block, 0, s>>>(p); break;
     case EPI_GELU_SAVE: gemm_kernel<T, EPI_GELU_SAVE, false><<<grid, block, 0, s>>>(p); break;
     case EPI_DGELU:
@@ -452,55 +322,25 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
   return hipGetLastError();
 }
 
-static thread_local int g_gemm_variant = 0; // 0 = auto; otherwise forced (tools/gemm_bench.py, tests)
+static thread_local int g_gemm_variant = 0; // 0 = auto; otherwise forced (dsvt_debug.h: tools, tests)
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
-// call-site scope (dsvt_set_gemm_skinny): the few-row GEMMs of the CLS-only tail and the DINO head
-static thread_local int g_skinny_scope = 0;
-void set_gemm_skinny(int on) { g_skinny_scope = on; }
 
-// Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, >= 2: gemm_big.hip variants, 20:
-// gemm_8ph.hip).
-// Measured on MI355X (tools/gemm_bench.py): every big bf16 projection with K <= 1024 (qkv
-// N=2304, fc1 N=3072, proj / folded temporal fc N=768) -> persistent staggered 256x128 (v10:
-// 2 WGs/CU, the epilogue of one overlaps the MFMA loop of the other, the next tile's loads fly
-// under the store tail); K = 3072 (fc2), small M (DINO head) and the patch GEMM -> 128x128.
-// Stream-K (variant 40) for the calls that pass a workspace (dsvt_gemm_sk_fwd): DSVT_SK = 0
-// (default) never, 1 bias / GELU projections, 2 also the fp32 residual ones.  Opt-in: measured
-// slower than the data-parallel kernels on every hot-path shape (qkv 118 vs 104 us, fc2 172 vs
-// 137 us): writing and re-reading 256 KB fp32 partial tiles costs more than the tail round.
-static bool sk_auto(int epi) {
-  static const int mode = [] {
-    const char* e = getenv("DSVT_SK");
-    return e ? atoi(e) : 0;
-  }();
-  return mode >= 2 || (mode == 1 && epi != EPI_RESID);
-}
-
-// the residual GEMMs' X stream (variant 33) in the auto choice: DSVT_RESID_XS = 1 on, 0 off
-static bool xs_auto() {
-  static const int mode = [] {
-    const char* e = getenv("DSVT_RESID_XS");
-    return e ? atoi(e) : 0;
-  }();
-  return mode != 0;
-}
-
+// Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, 10 = persistent staggered 256x128
+// (gemm_big.hip), 20 = 256x256 phase-interleaved (gemm_8ph.hip), 50 = K-split skinny).
+// Measured on MI355X (tools/gemm_bench.py and same-box A/Bs of the whole step).
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
-  if (p.sk_part && !p.row_scale && gemm_sk_ok(p, epi, out_f32) &&
-      (g_gemm_variant == 40 || (g_gemm_variant == 0 && sk_auto(epi))))
-    return 40;
-  // forced stream-K on an ineligible shape, or 41 (auto + tail split): the automatic choice
-  const int gv = (g_gemm_variant == 40 || g_gemm_variant == 41 || g_gemm_variant == 50) ? 0 : g_gemm_variant;
-  // inside a dsvt_set_gemm_skinny scope (the CLS-only tail's and the DINO head's few-row GEMMs,
-  // chosen by call site so that a batch split over streams picks the same kernel as the whole
-  // batch): the K-split skinny kernel (variant 50 forces it where eligible) -- bench 397.7-398.7
-  // vs 395.1-396.0 clips/s with the 128x128 kernel (same box, three interleaved rounds;
-  // DSVT_SKINNY=0 turns the scopes off for A/B)
-  static const int skinny = getenv("DSVT_SKINNY") ? atoi(getenv("DSVT_SKINNY")) : 1;
-  if ((g_gemm_variant == 50 || (g_gemm_variant == 0 && skinny && g_skinny_scope)) && gemm_skinny_ok(p, epi)) return 50;
+  const int gv = g_gemm_variant;
+  // DSVT_GEMM_FEW_ROWS call sites (the CLS-only tail's and the DINO head's few-row GEMMs, chosen
+  // by call site so that a batch split over streams picks the same kernel as the whole batch):
+  // the K-split skinny kernel (variant 50 forces it where eligible) -- bench 397.7-398.7 vs
+  // 395.1-396.0 clips/s with the 128x128 kernel (same box, three interleaved rounds)
+  if ((gv == 50 || (gv == 0 && p.few_rows)) && gemm_skinny_ok(p, epi)) return 50;
+  // the LayerNorm-folded A operand (dsvt_gemm_lnx_fwd) and the residual epilogue that writes
+  // the next LayerNorm's row statistics (dsvt_gemm_resid_stats_fwd): the 256x256 kernel only
+  if (p.ln_stats || p.stats_out) return 20;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
   // 195 vs 254 us (persistent 256x128) and 215 vs 231 us at 25104 x 3072 x 768 (tools/aux_bench.py)
@@ -508,23 +348,13 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
       gemm_8ph_ok(p, epi))
     return 20;
   // 256x256 kernel for the big N = 768 GEMMs: see the residual / N = 768 rules below
-  static const int64_t min_t = getenv("DSVT_8PH_MIN_TILES") ? atoll(getenv("DSVT_8PH_MIN_TILES")) : 128;
-  const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= min_t;
-  static const int r8 = getenv("DSVT_RESID_8PH") ? atoi(getenv("DSVT_RESID_8PH")) : 2;
-  // training DropPath residual GEMMs (s[m] * bias in the epilogue) likewise
-  // (the row-scaled ones are opt-in, DSVT_RESID_RS_8PH=1: 117.1 / 117.2 vs 117.4 / 117.6 train
-  // clips/s on the same box -- no gain, the 128x128 kernel stays their default)
-  static const int rs8 = getenv("DSVT_RESID_RS_8PH") ? atoi(getenv("DSVT_RESID_RS_8PH")) : 0;
-  if (epi == EPI_RESID && p.row_scale && gemm_8ph_ok(p, epi) &&
-      (gv == 20 || (gv == 0 && rs8 && r8 && big8 && (r8 >= 2 || p.K >= 2048))))
-    return 20;
-  if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels only
+  const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= 128;
+  if (epi == EPI_RESID && p.row_scale && gv == 20 && gemm_8ph_ok(p, epi)) return 20;
+  if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   if (gv >= 20 && gv <= 29) return gemm_8ph_ok(p, epi) ? gv : 1;
-  if (gv == 33) return gemm_8ph_xs_ok(p, epi) ? 33 : gemm_8ph_ok(p, epi) ? 20 : 1;
-  if (gv == 2) return (gemm_pipe_ok(p) && epi != EPI_PATCH) ? 2 : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
-    if (gv == 1 || gv == 9 || gv == 10) return gv;
+    if (gv == 1 || gv == 10) return gv;
     return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   }
   if (gv) return gv;
@@ -537,73 +367,19 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // the slower one (proj 73.6 vs 57.6 us, fc2 165 vs 138 us against the 128x128 kernel: 297
   // tiles on 256 CUs leave a 1.16-round tail), but the forward runs three backbone calls on
   // concurrent streams whose kernels fill that tail, and there its higher per-tile rate wins:
-  // 379.7 / 380.0 vs 360.6 / 359.7 clips/s on the bench line (same box, two interleaved rounds;
-  // DSVT_RESID_8PH = 0 -> 128x128, 1 -> only K >= 2048, 2 -> all, the default).
+  // 379.7 / 380.0 vs 360.6 / 359.7 clips/s on the bench line (same box, two interleaved rounds).
   // Below ~half a round of 256x256 tiles (config 4's single 2-clip call: 75 tiles) the 128x128
-  // kernel's 4x more tiles win even with other streams beside it (DSVT_8PH_MIN_TILES).
-  if (epi == EPI_RESID) {
-    if (r8 && big8 && gemm_8ph_ok(p, epi) && (r8 >= 2 || p.K >= 2048)) return xs_auto() && gemm_8ph_xs_ok(p, epi) ? 33 : 20;
-    return 1;
-  }
-  // N = 768 bias-only (the split residual path's proj / temporal fc, the backward's dX GEMMs):
-  // the 128x128 kernel -- 43.4 vs 53.8 us (persistent 256x128) at 25104 x 768 x 768 alone;
-  // DSVT_N768_8PH = 1 (A/B knob) puts them on the 256x256 kernel like the residual GEMMs.
-  if (epi == EPI_BIAS && p.N < 1024) {
-    static const int n8 = getenv("DSVT_N768_8PH") ? atoi(getenv("DSVT_N768_8PH")) : 1;
-    if (n8 && big8 && gemm_8ph_ok(p, epi)) return 20;
-    return 1;
-  }
+  // kernel's 4x more tiles win even with other streams beside it.
+  if (epi == EPI_RESID) return (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
+  // N = 768 bias-only (the backward's dX GEMMs): the 256x256 kernel on big calls
+  if (epi == EPI_BIAS && p.N < 1024) return (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
-}
-
-// Tail split (DSVT_TAIL_SPLIT=1, opt-in): a 256x256 launch whose last round of tiles is at most
-// half full -- the global-crop residual GEMMs: 297 tiles = one round + 41; qkv: 891 = three
-// rounds + 123 -- runs its full rounds on the 256x256 kernel and the rows of the last round on the
-// 128x128 kernel (4x the tiles for the same rows: the tail round's work spread over more CUs).
-// Alone it is faster (proj 72.4 -> 61.1 us, fc2 163 -> 134 us, qkv unchanged), inside the DINO
-// step slower (374 vs 385 clips/s, three interleaved rounds): the three concurrent backbone
-// calls already fill the tail round, and the second launch waits for the whole first one.
-// Bias / plain residual epilogues only (no row scales, no aux operand); with a row map the split
-// falls on a row-group boundary so the second launch's map is the first's shifted by whole groups.
-// Returns the first launch's row count, 0 = no split.
-static int64_t tail_split_rows(const GemmParams& p, int epi) {
-  static const int on = getenv("DSVT_TAIL_SPLIT") ? atoi(getenv("DSVT_TAIL_SPLIT")) : 0;
-  // variant 41 = the automatic choice with the tail split (tests, A/B on one thread)
-  if (!(g_gemm_variant == 41 || (on && g_gemm_variant == 0)) || p.row_scale || p.nseg || p.sk_part ||
-      !(epi == EPI_BIAS || epi == EPI_RESID))
-    return 0;
-  const int64_t tn = (p.N + 255) / 256, tiles = ((p.M + 255) / 256) * tn, full = tiles / 256;
-  const int64_t rem = tiles - full * 256;
-  if (full < 1 || rem == 0 || rem * 2 > 256) return 0;
-  int64_t rows_a = (full * 256 / tn) * 256;
-  const bool ident = p.rpg >= p.M && p.goff == 0;
-  if (!ident) rows_a = p.rpg > 0 ? rows_a / p.rpg * p.rpg : 0;
-  return (rows_a > 0 && rows_a < p.M) ? rows_a : 0;
 }
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
-  if (v == 20) {
-    if (const int64_t ra = tail_split_rows(p, epi)) {
-      GemmParams a = p, b = p;
-      a.M = ra;
-      if (hipError_t e = launch_gemm_8ph(a, epi, out_f32, s)) return e;
-      b.M = p.M - ra;
-      b.A = (const char*)p.A + ra * p.lda * 2;
-      if (p.rpg >= p.M && p.goff == 0) {            // identity map: shift the output rows
-        const int64_t osz = (epi == EPI_RESID || out_f32) ? 4 : 2;
-        b.out = (char*)p.out + ra * p.ldo * osz;
-        if (p.resid) b.resid = p.resid + ra * p.ldo;
-        b.rpg = b.M;
-      } else {                                      // row groups: shift the map by ra / rpg groups
-        b.goff = p.goff + (ra / p.rpg) * p.gstride;
-      }
-      return launch_t<bf16_t>(b, epi, out_f32, s);
-    }
-  }
-  if (v == 40) return launch_gemm_sk(p, epi, out_f32, s);
+  if ((p.ln_stats || p.stats_out) && v != 20) return hipErrorInvalidValue;
   if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);
-  if (v == 2) return launch_pipe(p, epi, out_f32, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);
   return launch_t<float>(p, epi, out_f32, s);

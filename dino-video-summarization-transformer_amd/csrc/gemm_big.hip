@@ -1,14 +1,13 @@
-// Large-tile bf16 MFMA GEMM for the big hot-path projections (M = tokens of a whole
-// backbone call: 13.9k-25.1k rows; N = 768 / 2304 / 3072; K = 768 / 3072).
+// Persistent 256x128 bf16 MFMA GEMM (variant 10: the training epilogues and the backward's dX
+// GEMMs) and the K-split skinny GEMM (variant 50: the few-row GEMMs).
 //
-// Geometry: BM x BN output tile per 512-thread workgroup (8 waves as WM x WN), wave tile
-// 128x64 (256x256) or 64x64 (256x128) = MI x NJ MFMA 16x16x32 tiles.  K advances 32 bf16
-// (64-byte rows) per stage; a 4-stage LDS ring keeps THREE stages in flight behind the one
-// being computed (global_load_lds_dwordx4 straight into LDS, counted `s_waitcnt vmcnt(N)`
-// and one raw s_barrier per stage -- no vmcnt(0) drain in the loop).  The LDS image is
-// linear per 1 KB LDS-DMA piece (16 rows x 64 B); the swizzle chunk' = chunk ^ H[(row>>2)&3],
-// H = {0,2,3,1}, is applied to the SOURCE address and to the ds_read_b128 address, which makes
-// all four 16-lane groups of a fragment read bank-conflict free.
+// Persistent kernel geometry: BM x BN output tile per workgroup (WM x WN waves), wave tile 128x64
+// = MI x NJ MFMA 16x16x32 tiles, two workgroups per CU.  K advances 32 bf16 (64-byte rows) per
+// stage; an NST-stage LDS ring keeps NST - 2 stages in flight behind the one being computed
+// (global_load_lds_dwordx4 straight into LDS, counted `s_waitcnt vmcnt(N)` and one raw s_barrier
+// per stage).  The LDS image is linear per 1 KB LDS-DMA piece (16 rows x 64 B); the swizzle
+// chunk' = chunk ^ H[(row>>2)&3], H = {0,2,3,1}, is applied to the SOURCE address and to the
+// ds_read_b128 address, which makes all four 16-lane groups of a fragment read bank-conflict free.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -35,246 +34,6 @@ __device__ __forceinline__ void wait_stages(int k) {
   if constexpr (2 * PS < 16) { if (k >= 2) { wait_vm<2 * PS>(); return; } }
   if (k >= 1) { wait_vm<PS>(); return; }
   wait_vm<0>();
-}
-
-// ABL (diagnostic ablation builds, benchmarking only): 0 = normal, 1 = no MFMA (LDS reads
-// kept live), 2 = no global loads after the prologue (MFMA + LDS reads on stale tiles).
-template <int BM, int BN, int WM, int WN, int NST, bool STAGED, int EPI, bool OUT_F32, int ABL = 0, bool DB = true>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_big_kernel(GemmParams p) {
-  constexpr int NW = WM * WN;
-  constexpr int A_BYTES = BM * BIG_ROWB, B_BYTES = BN * BIG_ROWB, ST_BYTES = A_BYTES + B_BYTES;
-  constexpr int WTM = BM / WM, WTN = BN / WN, MI = WTM / 16, NJ = WTN / 16;
-  constexpr int A_PIECES = A_BYTES / 1024 / NW, B_PIECES = B_BYTES / 1024 / NW;  // per wave per stage
-  constexpr int PER_STAGE = A_PIECES + B_PIECES;
-  static_assert(A_PIECES * NW * 1024 == A_BYTES && B_PIECES * NW * 1024 == B_BYTES, "piece split");
-  static_assert((NST - 2) * PER_STAGE < 16, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[NST * ST_BYTES];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int r16 = lane & 15, g = lane >> 4;
-
-  const int tilesN = (int)((p.N + BN - 1) / BN);
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-  const int64_t m0 = (int64_t)(wg / tilesN) * BM;
-  const int64_t n0 = (int64_t)(wg % tilesN) * BN;
-
-  const char* A = (const char*)p.A;
-  const char* W = (const char*)p.W;
-  const int64_t lda_b = p.lda * 2, ldw_b = p.ldw * 2;
-  const int nk = (int)(p.K / 32);
-
-  // per-lane source rows / chunks of this wave's LDS-DMA pieces (fixed over the K loop)
-  const int prow = lane >> 2, pch = lane & 3;
-  int64_t a_off[A_PIECES], b_off[B_PIECES];
-#pragma unroll
-  for (int i = 0; i < A_PIECES; ++i) {
-    const int r = (wave * A_PIECES + i) * 16 + prow;
-    int64_t gr = m0 + r;
-    gr = gr < p.M ? gr : p.M - 1;
-    a_off[i] = gr * lda_b + ((pch ^ swz64(r)) << 4);
-  }
-#pragma unroll
-  for (int i = 0; i < B_PIECES; ++i) {
-    const int r = (wave * B_PIECES + i) * 16 + prow;
-    int64_t gr = n0 + r;
-    gr = gr < p.N ? gr : p.N - 1;
-    b_off[i] = gr * ldw_b + ((pch ^ swz64(r)) << 4);
-  }
-
-#define DSVT_ISSUE(kt)                                                                            \
-  {                                                                                               \
-    char* st_ = smem + ((kt) % NST) * ST_BYTES;                                                   \
-    const int64_t kb_ = (int64_t)(kt) * BIG_ROWB;                                                 \
-    _Pragma("unroll") for (int i = 0; i < A_PIECES; ++i)                                          \
-        __builtin_amdgcn_global_load_lds((const void*)(A + a_off[i] + kb_),                       \
-                                         LDS_PTR(st_ + (wave * A_PIECES + i) * 1024), 16, 0, 0);  \
-    _Pragma("unroll") for (int i = 0; i < B_PIECES; ++i)                                          \
-        __builtin_amdgcn_global_load_lds((const void*)(W + b_off[i] + kb_),                       \
-                                         LDS_PTR(st_ + A_BYTES + (wave * B_PIECES + i) * 1024),   \
-                                         16, 0, 0);                                               \
-  }
-
-  fv4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment read offsets: row = base + r16, physical chunk = g ^ swz64(r16)
-  // (declared before use by the pipeline macros below)
-  const int frag_off = r16 * BIG_ROWB + ((g ^ swz64(r16)) << 4);
-  const int a_base = wm * WTM * BIG_ROWB + frag_off;
-  const int b_base = A_BYTES + wn * WTN * BIG_ROWB + frag_off;
-
-  // Fragment double buffering: the ds_reads of stage kt+1 are in flight under the 32 MFMAs
-  // of stage kt (whose fragments were read one iteration earlier).
-#define DSVT_READ(FA, FB, kt)                                                                         \
-  {                                                                                                   \
-    const char* st_ = smem + ((kt) % NST) * ST_BYTES;                                                 \
-    _Pragma("unroll") for (int i = 0; i < MI; ++i)                                                    \
-        FA[i] = *reinterpret_cast<const sv8*>(st_ + a_base + i * 16 * BIG_ROWB);                      \
-    _Pragma("unroll") for (int j = 0; j < NJ; ++j)                                                    \
-        FB[j] = *reinterpret_cast<const sv8*>(st_ + b_base + j * 16 * BIG_ROWB);                      \
-  }
-#define DSVT_MMA(FA, FB)                                                                              \
-  {                                                                                                   \
-    if constexpr (ABL == 1) {                                                                         \
-      _Pragma("unroll") for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(FA[i]));                   \
-      _Pragma("unroll") for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(FB[j]));                   \
-    } else {                                                                                          \
-      _Pragma("unroll") for (int i = 0; i < MI; ++i)                                                  \
-          _Pragma("unroll") for (int j = 0; j < NJ; ++j)                                              \
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[i][j], 0, 0, 0); \
-    }                                                                                                 \
-  }
-  // one pipeline step: stage kt computed from (CA, CB), stage kt+1 read into (NA, NB)
-#define DSVT_STEP(kt, CA, CB, NA, NB)                                                                 \
-  {                                                                                                   \
-    if ((kt) + 1 < nk) {                                                                              \
-      const int ahead_ = nk - 2 - (kt) < NST - 2 ? nk - 2 - (kt) : NST - 2;                           \
-      wait_stages<PER_STAGE>(ahead_);                                                                 \
-    }                                                                                                 \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                               \
-    __builtin_amdgcn_s_barrier();                                                                     \
-    asm volatile("" ::: "memory");                                                                    \
-    if (ABL != 2 && (kt) + NST < nk) DSVT_ISSUE((kt) + NST);                                          \
-    if ((kt) + 1 < nk) DSVT_READ(NA, NB, (kt) + 1);                                                   \
-    DSVT_MMA(CA, CB);                                                                                 \
-  }
-
-  if constexpr (DB) {
-    sv8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
-    static_assert(NST == 3 || NST == 4, "ring depth");
-    DSVT_ISSUE(0);
-    if (nk > 1) DSVT_ISSUE(1);
-    if (nk > 2) DSVT_ISSUE(2);
-    if (NST == 4 && nk > 3) DSVT_ISSUE(3);
-    wait_stages<PER_STAGE>((nk < NST ? nk : NST) - 1);   // stage 0 landed; the rest may fly
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    DSVT_READ(fa0, fb0, 0);
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-      DSVT_STEP(kt, fa0, fb0, fa1, fb1);
-      DSVT_STEP(kt + 1, fa1, fb1, fa0, fb0);
-    }
-    if (kt < nk) DSVT_STEP(kt, fa0, fb0, fa1, fb1);
-
-  } else {
-    // single fragment set: wait(stage kt) -> barrier -> issue kt+NST-1 -> read kt -> MMA kt
-    sv8 fa[MI], fb[NJ];
-    DSVT_ISSUE(0);
-    if (nk > 1) DSVT_ISSUE(1);
-    if (NST == 4 && nk > 2) DSVT_ISSUE(2);
-    for (int kt = 0; kt < nk; ++kt) {
-      // issued so far: stages <= kt + NST - 2; stage kt must land, the later ones may fly
-      const int ahead = nk - 1 - kt < NST - 2 ? nk - 1 - kt : NST - 2;
-      wait_stages<PER_STAGE>(ahead);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (ABL != 2 && kt + NST - 1 < nk) DSVT_ISSUE(kt + NST - 1);
-      DSVT_READ(fa, fb, kt);
-      DSVT_MMA(fa, fb);
-    }
-  }
-#undef DSVT_STEP
-#undef DSVT_MMA
-#undef DSVT_READ
-#undef DSVT_ISSUE
-
-  mfma_result_fence();   // acc is read under the branches below
-  // ---- epilogue.  Lane holds C[m = .. + r16][n = .. + 4g + 0..3] per (i, j) subtile.
-  // Bias / GELU are applied on the way to LDS; the tile is staged through LDS in row chunks
-  // (padded rows: conflict-free 8-/16-B writes), then written back as WHOLE rows with 16 B
-  // per lane (full 128-B lines; the row map / residual / patch-embed adds are per row).
-  if constexpr (ABL == 3) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-  using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
-  if constexpr (!STAGED) {
-    epilogue_direct<MI, NJ, EPI, OUT_F32>(p, acc, m0 + wm * WTM, n0 + wn * WTN, r16, g);
-    return;
-  }
-  // Wave-local staging: each wave transposes its own WTM x WTN sub-tile through a private LDS
-  // slice (chunk' = chunk ^ ((row>>1)&7): conflict-free 8-/16-B writes), then stores whole
-  // 128-B lines, 16 B per lane -- 8 full lines per store instruction instead of 16 partial ones.
-  constexpr int ES = (int)sizeof(OutT);
-  constexpr int RB = WTN * ES;                           // bytes per sub-tile row (128 or 256)
-  constexpr int CPR = RB / 16;                           // 16-B chunks per row
-  constexpr int SLICE0 = (NST * ST_BYTES / NW) < 16384 ? (NST * ST_BYTES / NW) : 16384;
-  constexpr int SROWS0 = (SLICE0 / RB) / 16 * 16 < WTM ? (SLICE0 / RB) / 16 * 16 : WTM;
-  constexpr int SROWS = (WTM % SROWS0 == 0) ? SROWS0 : 16;  // rows staged per pass
-  constexpr int SLICE = SROWS * RB;
-  static_assert(SROWS >= 16 && NW * SLICE <= NST * ST_BYTES, "wave slices fit the ring");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();                          // the ring is no longer read by anyone
-  asm volatile("" ::: "memory");
-  char* wslice = smem + wave * SLICE;
-#pragma unroll
-  for (int ps = 0; ps < WTM / SROWS; ++ps) {
-    // (1) this wave's rows [ps*SROWS, (ps+1)*SROWS) -> LDS (bias / GELU applied)
-#pragma unroll
-    for (int i = ps * (SROWS / 16); i < (ps + 1) * (SROWS / 16); ++i) {
-      const int R = (i - ps * (SROWS / 16)) * 16 + r16;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int col = j * 16 + 4 * g;                  // column inside the sub-tile
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        const int64_t n = n0 + wn * WTN + col;
-        if (p.bias && n < p.N) {
-          const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-          v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
-        }
-        if constexpr (EPI == EPI_GELU) {
-          constexpr bool BO = std::is_same<OutT, bf16_t>::value;
-          v0 = gelu_out<BO>(v0); v1 = gelu_out<BO>(v1); v2 = gelu_out<BO>(v2); v3 = gelu_out<BO>(v3);
-        }
-        const int byte = col * ES;
-        const int chunk = (byte >> 4) ^ ((R >> 1) & 7 & (CPR - 1));
-        store4(reinterpret_cast<OutT*>(wslice + R * RB + (chunk << 4) + (byte & 15)), v0, v1, v2, v3);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // (2) read back whole rows and store 16 B per lane
-    constexpr int RPI = 64 / CPR;                        // rows per wave instruction
-#pragma unroll
-    for (int rr = 0; rr < SROWS; rr += RPI) {
-      const int R = rr + lane / CPR, c = lane % CPR;
-      const uint4 v = *reinterpret_cast<const uint4*>(wslice + R * RB + ((c ^ ((R >> 1) & 7 & (CPR - 1))) << 4));
-      const int64_t m = m0 + wm * WTM + ps * SROWS + R;
-      const int64_t n = n0 + wn * WTN + c * (16 / ES);
-      if (m >= p.M || n >= p.N) continue;
-      const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
-      if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
-        *reinterpret_cast<uint4*>(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n) = v;
-      } else if constexpr (EPI == EPI_RESID) {
-        float4* xo = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + orow * p.ldo + n);
-        float4 x = *reinterpret_cast<const float4*>(resid_src(p) + orow * p.ldo + n);
-        x.x += __uint_as_float(v.x); x.y += __uint_as_float(v.y);
-        x.z += __uint_as_float(v.z); x.w += __uint_as_float(v.w);
-        *xo = x;
-      } else {  // EPI_PATCH
-        const int64_t rrw = m % p.rpg;
-        const int64_t np = rrw / p.T, t = rrw % p.T;
-        const float4 pe = *reinterpret_cast<const float4*>(p.pos + (1 + (int64_t)p.pidx[np]) * p.N + n);
-        float4 o = make_float4(__uint_as_float(v.x) + pe.x, __uint_as_float(v.y) + pe.y,
-                               __uint_as_float(v.z) + pe.z, __uint_as_float(v.w) + pe.w);
-        if (p.temb) {
-          const float4 te = *reinterpret_cast<const float4*>(p.temb + (int64_t)p.tidx[t] * p.N + n);
-          o.x += te.x; o.y += te.y; o.z += te.z; o.w += te.w;
-        }
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + orow * p.ldo + n) = o;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next pass
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -435,36 +194,11 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int NST, bool STAGED, bool DB>
-static hipError_t launch_big_t(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
-  const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid((unsigned)tiles), block(64 * WM * WN);
-#define DSVT_K(E, F) gemm_big_kernel<BM, BN, WM, WN, NST, STAGED, E, F, 0, DB><<<grid, block, 0, s>>>(p)
-  switch (epi) {
-    case EPI_BIAS: if (out_f32) DSVT_K(EPI_BIAS, true); else DSVT_K(EPI_BIAS, false); break;
-    case EPI_GELU: if (out_f32) DSVT_K(EPI_GELU, true); else DSVT_K(EPI_GELU, false); break;
-    case EPI_RESID: DSVT_K(EPI_RESID, true); break;
-    case EPI_PATCH: DSVT_K(EPI_PATCH, true); break;
-    default: return hipErrorInvalidValue;
-  }
-#undef DSVT_K
-  return hipGetLastError();
-}
-
-// variant: 3 = 256x128 / 8 waves / 4 stages (fragment double-buffered);
-// 4 = 256x128 / 4 waves (wave tile 128x64) / 3 stages = 72 KB LDS -> 2 WGs per CU, the
-// epilogue of one overlaps the MFMA loop of the other; 5 = 128x256 / 4 waves / 3 stages.
+// variant 10 = the persistent staggered 256x128 kernel (2 WGs per CU); 20 = gemm_8ph.hip (21-29:
+// its diagnostic ablation builds, tools/gemm_bench.py)
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s) {
   switch (variant) {
-    case 3: return launch_big_t<256, 128, 4, 2, 4, true, true>(p, epi, out_f32, s);
-    case 4: return launch_big_t<256, 128, 2, 2, 3, false, false>(p, epi, out_f32, s);
-    case 5: return launch_big_t<128, 256, 1, 4, 3, false, false>(p, epi, out_f32, s);
-    case 6: return launch_big_t<256, 128, 2, 2, 3, true, false>(p, epi, out_f32, s);
-    case 9: return launch_persist_t<256, 128, 2, 2, false>(p, epi, out_f32, s);
     case 10: return launch_persist_t<256, 128, 2, 2, true>(p, epi, out_f32, s);
-    case 11: return launch_persist_t<128, 256, 1, 4, true>(p, epi, out_f32, s);
-    case 12: return launch_persist_t<256, 256, 2, 4, false, 5>(p, epi, out_f32, s);
-    case 13: return launch_persist_t<256, 256, 2, 4, false, 4>(p, epi, out_f32, s);
     case 20: return launch_gemm_8ph(p, epi, out_f32, s);
     case 21: return launch_gemm_8ph(p, epi, out_f32, s, 1);
     case 22: return launch_gemm_8ph(p, epi, out_f32, s, 2);
@@ -474,19 +208,10 @@ hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f3
     case 27: return launch_gemm_8ph(p, epi, out_f32, s, 18);
     case 28: return launch_gemm_8ph(p, epi, out_f32, s, 32);
     case 29: return launch_gemm_8ph(p, epi, out_f32, s, 64);
-    case 33: return launch_gemm_8ph_xs(p, epi, s);
-    default: break;
-  }
-  // ablation builds (EPI_BIAS, bf16 out only) of variant 4: 14 no-MFMA, 24 no-load, 34 no-epilogue
-  dim3 grid((unsigned)(((p.M + 255) / 256) * ((p.N + 127) / 128))), block(256);
-  switch (variant) {
-    case 14: gemm_big_kernel<256, 128, 2, 2, 3, false, EPI_BIAS, false, 1, false><<<grid, block, 0, s>>>(p); break;
-    case 24: gemm_big_kernel<256, 128, 2, 2, 3, false, EPI_BIAS, false, 2, false><<<grid, block, 0, s>>>(p); break;
-    case 34: gemm_big_kernel<256, 128, 2, 2, 3, false, EPI_BIAS, false, 3, false><<<grid, block, 0, s>>>(p); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
+
 
 // ---- skinny GEMM (variant 50): a few rows -- the CLS-only last block's Q / proj / fc1 / fc2 over
 // the B clips' CLS rows and the DINO head's layers.  The 128x128 kernel runs these as N / 128
@@ -567,7 +292,7 @@ __global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
 
 bool gemm_skinny_ok(const GemmParams& p, int epi) {
   return p.M >= 1 && p.K >= 512 && p.K % (SKN_NW * 32) == 0 && p.N % 32 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
-         (epi == EPI_BIAS || epi == EPI_GELU || epi == EPI_RESID) && !p.row_scale && !p.nseg && !p.sk_part &&
+         (epi == EPI_BIAS || epi == EPI_GELU || epi == EPI_RESID) && !p.row_scale &&
          ((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0;
 }
 

@@ -410,4 +410,125 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
   }
 }
 
+// ---- LayerNorm folded into the GEMM (dsvt_gemm_lnx_fwd; GemmParams::ln_stats).  The A operand
+// was the bf16 copy of the fp32 token rows and W the bf16 W * gamma, so acc = W'.x; with the
+// row's mean / rstd from its LN_PARTS partials (written by whoever produced the row):
+//   acc <- rstd * (acc - mu * wsum[n]) + bias[n]          (bias = b + W . beta, fp32)
+// = LayerNorm(x) . W^T + b up to the bf16 roundings of x and W * gamma.  Lane (r16, g) sums the
+// partials 3g .. 3g + 2 of its rows and the four lane groups combine by two butterflies (every
+// lane gets the same bits: IEEE addition commutes).  Rows past M are clamped (never stored).
+template <int MI, int NJ>
+__device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
+                                          int r16, int g) {
+  static_assert(NJ == 4 && MI % 4 == 0, "64-column wave slab");
+  const float invk = p.ln_invk;
+  float mu[MI], rs[MI];
+  const uint32_t a_rpg = (uint32_t)(p.a_rpg < p.M ? p.a_rpg : p.M), a_gs = (uint32_t)p.a_gstride;
+  const uint32_t a_go = (uint32_t)p.a_goff, mlast = (uint32_t)(p.M - 1);
+#pragma unroll
+  for (int i0 = 0; i0 < MI; i0 += 4) {        // four rows' partials in flight at a time
+    float2 st[4][3];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      uint32_t m = (uint32_t)(rbase + (i0 + ii) * 16 + r16);
+      m = m < mlast ? m : mlast;
+      const uint32_t xr = (m / a_rpg) * a_gs + a_go + m % a_rpg;   // rows < 2^31 (host-checked)
+      const float2* sp = reinterpret_cast<const float2*>(p.ln_stats) + (uint64_t)(xr * LN_PARTS + 3 * g);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) st[ii][k] = sp[k];
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      float s = (st[ii][0].x + st[ii][1].x) + st[ii][2].x;
+      float q = (st[ii][0].y + st[ii][1].y) + st[ii][2].y;
+      s += __shfl_xor(s, 16, 64);
+      q += __shfl_xor(q, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float m_ = s * invk;
+      const float var = fmaxf(q * invk - m_ * m_, 0.f);
+      rs[i0 + ii] = 1.0f / sqrtf(var + p.ln_eps);
+      mu[i0 + ii] = -m_ * rs[i0 + ii];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int64_t n = cbase + j * 16 + 4 * g;
+    const float4 w4 = *reinterpret_cast<const float4*>(p.ln_wsum + n);
+    const float4 b4 = *reinterpret_cast<const float4*>(p.bias + n);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      acc[i][j][0] = fmaf(rs[i], acc[i][j][0], fmaf(mu[i], w4.x, b4.x));
+      acc[i][j][1] = fmaf(rs[i], acc[i][j][1], fmaf(mu[i], w4.y, b4.y));
+      acc[i][j][2] = fmaf(rs[i], acc[i][j][2], fmaf(mu[i], w4.z, b4.z));
+      acc[i][j][3] = fmaf(rs[i], acc[i][j][3], fmaf(mu[i], w4.w, b4.w));
+    }
+  }
+}
+
+// ---- residual epilogue that also writes the next LayerNorm's inputs (dsvt_gemm_resid_stats_fwd;
+// GemmParams::stats_out): X[row(m)] += acc (the bias is in acc), and for every updated row its
+// bf16 copy (xb_out, row stride ldo) and the (sum, sum of squares) of the new values over this
+// wave's 64-column slab (stats_out[row][cbase / 64]).  The X loads run a rolling window of W rows
+// ahead of the stores like the plain residual epilogue; FULL (wave-uniform): no row past M, no
+// per-lane bounds branch around the stores (which would make the compiler drain vmcnt).
+template <int MI, int NJ, bool FULL>
+__device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
+                                                 int r16, int g) {
+  static_assert(NJ == 4, "64-column wave slab");
+  constexpr int W = 2;
+  const bool ident = p.rpg >= p.M && p.goff == 0;
+  const int part = (int)(cbase >> 6);
+  auto orow_of = [&](int i) -> int64_t {
+    int64_t m = rbase + i * 16 + r16;
+    if constexpr (!FULL) m = m < p.M ? m : p.M - 1;
+    return ident ? m : map_row(m, p.rpg, p.gstride, p.goff);
+  };
+  float4 x[W][NJ];
+  auto load_row = [&](int i) {
+    const float* src = resid_src(p) + orow_of(i) * p.ldo + cbase + 4 * g;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) x[i % W][j] = *reinterpret_cast<const float4*>(src + j * 16);
+  };
+#pragma unroll
+  for (int i = 0; i < W; ++i) load_row(i);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int64_t orow = orow_of(i);
+    fv4 v[NJ];
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float4 xv = x[i % W][j];
+      v[j] = fv4{xv.x + acc[i][j][0], xv.y + acc[i][j][1], xv.z + acc[i][j][2], xv.w + acc[i][j][3]};
+      s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+      q += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
+    }
+    if (i + W < MI) load_row(i + W);
+    s += __shfl_xor(s, 16, 64);
+    q += __shfl_xor(q, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    q += __shfl_xor(q, 32, 64);
+    const bool ok = FULL || rbase + i * 16 + r16 < p.M;
+    if (ok) {
+      float* dst = (float*)p.out + orow * p.ldo + cbase + 4 * g;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) *reinterpret_cast<fv4*>(dst + j * 16) = v[j];
+      bf16_t* xb = (bf16_t*)p.xb_out + orow * p.ldo + cbase;
+      store_pair_bf16(xb, v[0], v[1], g);
+      store_pair_bf16(xb + 32, v[2], v[3], g);
+      // the four lanes of the row store the same 8 bytes (no per-lane branch)
+      *reinterpret_cast<float2*>(p.stats_out + (orow * LN_PARTS + part) * 2) = make_float2(s, q);
+    }
+  }
+}
+
+template <int MI, int NJ>
+__device__ __forceinline__ void epilogue_resid_stats(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
+                                                     int64_t cbase, int r16, int g) {
+  if (rbase + MI * 16 <= p.M) resid_stats_rows<MI, NJ, true>(p, acc, rbase, cbase, r16, g);
+  else resid_stats_rows<MI, NJ, false>(p, acc, rbase, cbase, r16, g);
+}
+
 }  // namespace dsvt

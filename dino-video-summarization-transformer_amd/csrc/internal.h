@@ -28,23 +28,28 @@ struct GemmParams {
   // is not scaled.  Only the 128x128 and persistent kernels take it (gemm_variant_for).
   const float* row_scale = nullptr;
   int64_t rs_group = 1;
-  // stream-K 256x256 kernel: partial-sum slots ([2 * grid][256 x 256] fp32) and one arrival
-  // counter per output tile (zero on entry, left zero on exit)
-  float* sk_part = nullptr;
-  int* sk_cnt = nullptr;
-  // grouped launch (dsvt_gemm_grouped_fwd, 256x256 kernel): nseg > 0 segments of rows, each with
-  // its own W / bias / output row map; M is then the sum of the segments' 256-row-padded extents
-  // (segment s owns the virtual m-tiles [seg[s].mtile0, seg[s + 1].mtile0))
-  struct Seg {
-    const void* W; const float* bias;
-    int64_t a_row0, M;           // A rows [a_row0, a_row0 + M)
-    int64_t rpg, gstride, goff;  // out row of segment row m (map_row)
-    int64_t mtile0;
-  };
-  static constexpr int MAX_SEG = 4;
-  int nseg = 0;
-  Seg seg[MAX_SEG] = {};
+  // K-split skinny kernel for this call (DSVT_GEMM_FEW_ROWS: the few-row GEMMs of the CLS-only
+  // tail and the DINO head, chosen by call site)
+  bool few_rows = false;
+  // LayerNorm folded into the GEMM (dsvt_gemm_lnx_fwd, 256x256 kernel): A = the bf16 copy of the
+  // fp32 token rows, read through the A row map a_row(m) = (m / a_rpg) * a_gstride + a_goff +
+  // m % a_rpg; W = W * gamma (bf16); the epilogue forms
+  //   out = rstd(r) * (acc - mu(r) * ln_wsum[n]) + bias[n]      (bias = b + W . beta)
+  // with mu / rstd of A row r from ln_stats[r][LN_PARTS] (float2 partial sums of x and x^2 over
+  // 64-column slabs, written by the residual epilogue that produced the row) and ln_eps.
+  const float* ln_stats = nullptr;
+  const float* ln_wsum = nullptr;
+  float ln_eps = 0.f, ln_invk = 0.f;   // ln_invk = 1 / K
+  int64_t a_rpg = INT64_MAX, a_gstride = 0, a_goff = 0;
+  // residual epilogue that also writes the next LayerNorm's inputs (dsvt_gemm_resid_stats_fwd):
+  // the bf16 copy of every updated X row (xb_out, row stride ldo) and its LN_PARTS partials
+  // (stats_out, rows of the output row map)
+  void* xb_out = nullptr;
+  float* stats_out = nullptr;
 };
+
+// float2 (sum, sum of squares) partials per token row: one per 64-column slab of C = 768
+constexpr int LN_PARTS = 12;
 
 // the DropPath scale of GEMM row m (1 when none)
 __device__ __forceinline__ float row_scale_of(const GemmParams& p, int64_t m) {
@@ -70,38 +75,7 @@ bool gemm_8ph_ok(const GemmParams& p, int epi);
 // K split over the 8 waves of a workgroup, 64-row blocks (variant 50, gemm_big.hip)
 bool gemm_skinny_ok(const GemmParams& p, int epi);
 hipError_t launch_gemm_skinny(const GemmParams& p, int epi, int out_f32, hipStream_t s);
-void set_gemm_skinny(int on);   // this thread's launches: the skinny kernel where eligible (gemm.hip)
-// the 256x256 kernel with the residual tile streamed into the accumulators (variant 33)
-bool gemm_8ph_xs_ok(const GemmParams& p, int epi);
-hipError_t launch_gemm_8ph_xs(const GemmParams& p, int epi, hipStream_t s);
-// grouped (segmented) launch of the 256x256 kernel: bias / GELU / residual epilogues
-bool gemm_8ph_grouped_ok(const GemmParams& p, int epi, int out_f32);
-hipError_t launch_gemm_8ph_grouped(const GemmParams& p, int epi, int out_f32, hipStream_t s);
-// stream-K 256x256 GEMM (variant 40): workspace = [SK_MAX_TILES int32 counters][2 x 256 slots of
-// 256 x 256 fp32 partial sums]
-constexpr int64_t SK_MAX_TILES = 65536;
-constexpr int64_t SK_CNT_BYTES = SK_MAX_TILES * 4;
-constexpr int64_t SK_WS_BYTES = SK_CNT_BYTES + 2 * 256 * 256 * 256 * 4;
-bool gemm_sk_ok(const GemmParams& p, int epi, int out_f32);
-hipError_t launch_gemm_sk(const GemmParams& p, int epi, int out_f32, hipStream_t s);
 void set_gemm_variant(int v);
-
-// Full-row residual GEMM + fused LayerNorm (gemm_rowln.hip), bf16, N = 768:
-//   X[map(m)] += A[m] . W^T + bias;  Y[yrow] = LN(X[map(m)]) (ymode: see ROWLN_Y_*)
-enum { ROWLN_Y_NONE = 0, ROWLN_Y_X = 1, ROWLN_Y_COMPACT = 2 };
-struct RowLnParams {
-  const void* A; int64_t lda;
-  const void* W; int64_t ldw;
-  const float* bias;
-  float* X;                         // fp32 token rows, ld 768
-  int64_t M, K;
-  int64_t rpg, gstride, goff;       // X row of GEMM row m (map_row)
-  const float* gamma; const float* beta; float eps;
-  unsigned short* Y;                // LayerNorm output rows, ld 768
-  int ymode;
-  int64_t L;                        // tokens per clip (ROWLN_Y_COMPACT: row t == 0 of a clip is CLS)
-};
-hipError_t launch_gemm_rowln(const RowLnParams& p, hipStream_t s);
 
 // multi-tensor bf16 weight copies (backward.hip)
 hipError_t launch_cast_multi(const float* const* src, void* const* dst, const int64_t* sizes, const int32_t* ctensor,
@@ -117,9 +91,11 @@ int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
 hipError_t launch_wgrad(const unsigned short* dy, int64_t ldy, const unsigned short* x, int64_t ldx, float* G,
                         float* db, int64_t M, int64_t N, int64_t K, int accumulate, float* partial, hipStream_t s);
 
-hipError_t launch_add_layernorm(int d_f32, int y_f32, float* x, const void* d, void* y, const float* g,
-                                const float* b, int64_t rows, int64_t L, int dmode, int ymode, float eps,
-                                hipStream_t s);
+// bf16 copy + LN_PARTS row-statistics partials of fp32 rows [rows, 768] (dsvt_ln_stats_fwd)
+hipError_t launch_ln_stats(const float* x, void* xb, float* stats, int64_t rows, hipStream_t s);
+// LayerNorm-folded GEMM weights: Wf = bf16(W * gamma), wsum = row sums of Wf, bf = b + W . beta
+hipError_t launch_ln_fold(const float* W, const float* gamma, const float* beta, const float* b, void* Wf, float* wsum,
+                          float* bf, int64_t N, int64_t K, hipStream_t s);
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
                             int64_t goff, float eps, hipStream_t s);

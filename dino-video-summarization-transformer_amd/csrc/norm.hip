@@ -126,141 +126,85 @@ __global__ __launch_bounds__(256) void layernorm768_kernel(const float* __restri
   }
 }
 
-// ---------------------------------------------------------------- residual add + LayerNorm
-// x = x + d ; y = LayerNorm(x)   (timesformer.py:133-135 / :181 / :184 `x + f(x)` followed by the
-// next sub-layer's norm), C = 768.  The sub-layer GEMM writes d = f(x) (storage dtype) with a
-// plain bias epilogue -- the MFMA kernel then never touches the fp32 token rows -- and this
-// streaming pass does the fp32 residual read-modify-write together with the LayerNorm that
-// re-reads the same rows anyway.  Per X row r of a clip (L rows, row 0 = CLS):
-//   DMODE 0: no d (y = LN(x) only), 1: d row r, 2: d row of the compact patch layout
-//            (b * (L - 1) + j - 1; the CLS row j = 0 has none: the temporal branch);
-//   YMODE 0: no LN output, 1: y row r, 2: y row of the compact patch layout (CLS rows skipped).
-// Same summation order as layernorm768_kernel (a row's result does not depend on the grid).
-template <typename DT, typename OutT, int DMODE, int YMODE>
-__global__ __launch_bounds__(256) void add_layernorm768_kernel(float* __restrict__ x, const DT* __restrict__ d,
-                                                               OutT* __restrict__ y, const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta, int64_t rows,
-                                                               int64_t L, float eps) {
+// ---------------------------------------------------------------- LayerNorm inputs of a folded GEMM
+// For dsvt_gemm_lnx_fwd (the LayerNorm folded into the GEMM that reads its output): the bf16 copy
+// of every fp32 token row and its row-statistics partials, float2 (sum x, sum x^2) over each
+// 64-column slab (LN_PARTS = 12 for C = 768) -- what the residual epilogue of
+// dsvt_gemm_resid_stats_fwd writes for the rows it updates; this pass covers the rows a forward
+// starts with (after the patch embedding).  One wave per row, grid-strided, C = 768.
+__global__ __launch_bounds__(256) void ln_stats768_kernel(const float* __restrict__ x, bf16_t* __restrict__ xb,
+                                                          float* __restrict__ stats, int64_t rows) {
   constexpr int C = 768;
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  float4 gg[3], bb[3];
-  if constexpr (YMODE != 0) {
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    float4 v[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v[i] = *reinterpret_cast<const float4*>(x + r * C + i * 256 + lane * 4);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      gg[i] = *reinterpret_cast<const float4*>(gamma + i * 256 + lane * 4);
-      bb[i] = *reinterpret_cast<const float4*>(beta + i * 256 + lane * 4);
-    }
-  }
-  // compact patch row of X row rr (-1 for a CLS row)
-  auto patch_row = [&](int64_t rr) -> int64_t {
-    const int64_t b = rr / L, j = rr - b * L;
-    return j == 0 ? -1 : b * (L - 1) + j - 1;
-  };
-  auto d_row = [&](int64_t rr) -> int64_t { return DMODE == 1 ? rr : DMODE == 2 ? patch_row(rr) : -1; };
-  float4 cur[3], curd[3];
-  auto load_row = [&](int64_t rr, float4 (&xv)[3], float4 (&dv)[3]) {
-    const float* xr = x + rr * C;
+      store4(xb + r * C + i * 256 + lane * 4, v[i].x, v[i].y, v[i].z, v[i].w);
+      // lanes 16q .. 16q + 15 of chunk i hold slab 4i + q
+      float s = (v[i].x + v[i].y) + (v[i].z + v[i].w);
+      float q = (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) xv[i] = *reinterpret_cast<const float4*>(xr + i * 256 + lane * 4);
-    const int64_t dr = d_row(rr);                    // wave-uniform
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      float t[4] = {0.f, 0.f, 0.f, 0.f};
-      if (DMODE != 0 && dr >= 0) load4(d + dr * C + i * 256 + lane * 4, t);
-      dv[i] = make_float4(t[0], t[1], t[2], t[3]);
-    }
-  };
-  load_row(r, cur, curd);
-  while (true) {
-    const int64_t rn = r + nw;
-    float4 nxt[3], nxtd[3];
-    load_row(rn < rows ? rn : r, nxt, nxtd);        // clamped: branch-free prefetch
-    float v[12];
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float4 f = cur[i], e = curd[i];
-      v[4 * i] = f.x + e.x; v[4 * i + 1] = f.y + e.y; v[4 * i + 2] = f.z + e.z; v[4 * i + 3] = f.w + e.w;
-      s += (v[4 * i] + v[4 * i + 1]) + (v[4 * i + 2] + v[4 * i + 3]);
-    }
-    if (DMODE != 0 && d_row(r) >= 0) {
-      float* xr = x + r * C;
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        *reinterpret_cast<float4*>(xr + i * 256 + lane * 4) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-    }
-    if constexpr (YMODE != 0) {
-      const int64_t yrow = YMODE == 1 ? r : patch_row(r);
-      if (yrow >= 0) {
-        const float mean = wave_sum(s) / C;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) { v[i] -= mean; q += v[i] * v[i]; }
-        const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
-        OutT* yr = y + yrow * C;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const float4 g4 = gg[i], b4 = bb[i];
-          store4(yr + i * 256 + lane * 4, v[4 * i] * rstd * g4.x + b4.x, v[4 * i + 1] * rstd * g4.y + b4.y,
-                 v[4 * i + 2] * rstd * g4.z + b4.z, v[4 * i + 3] * rstd * g4.w + b4.w);
-        }
+      for (int o = 1; o < 16; o <<= 1) {
+        s += __shfl_xor(s, o);
+        q += __shfl_xor(q, o);
       }
+      if ((lane & 15) == 0)
+        *reinterpret_cast<float2*>(stats + (r * LN_PARTS + i * 4 + (lane >> 4)) * 2) = make_float2(s, q);
     }
-    if (rn >= rows) break;
-    r = rn;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) { cur[i] = nxt[i]; curd[i] = nxtd[i]; }
   }
 }
 
-// d_f32: d is fp32 (else bf16); y_f32: y is fp32 (else bf16)
-hipError_t launch_add_layernorm(int d_f32, int y_f32, float* x, const void* d, void* y, const float* g,
-                                const float* b, int64_t rows, int64_t L, int dmode, int ymode, float eps,
-                                hipStream_t s) {
-  if (dmode < 0 || dmode > 2 || ymode < 0 || ymode > 2) return hipErrorInvalidValue;
-  const int64_t nblk = (rows + 3) / 4;
-  dim3 grid((unsigned)(nblk < 1024 ? nblk : 1024)), block(256);
-#define DSVT_ALN(DT, YT, DM, YM) \
-  add_layernorm768_kernel<DT, YT, DM, YM><<<grid, block, 0, s>>>(x, (const DT*)d, (YT*)y, g, b, rows, L, eps)
-#define DSVT_ALN_Y(DT, YT, DM)                         \
-  switch (ymode) {                                     \
-    case 0: DSVT_ALN(DT, YT, DM, 0); break;            \
-    case 1: DSVT_ALN(DT, YT, DM, 1); break;            \
-    default: DSVT_ALN(DT, YT, DM, 2); break;           \
-  }
-#define DSVT_ALN_D(DT, YT)                             \
-  switch (dmode) {                                     \
-    case 0: DSVT_ALN_Y(DT, YT, 0); break;              \
-    case 1: DSVT_ALN_Y(DT, YT, 1); break;              \
-    default: DSVT_ALN_Y(DT, YT, 2); break;             \
-  }
-  if (d_f32 && y_f32) { DSVT_ALN_D(float, float); }
-  else if (d_f32) { DSVT_ALN_D(float, bf16_t); }
-  else if (y_f32) { DSVT_ALN_D(bf16_t, float); }
-  else { DSVT_ALN_D(bf16_t, bf16_t); }
-#undef DSVT_ALN_D
-#undef DSVT_ALN_Y
-#undef DSVT_ALN
+hipError_t launch_ln_stats(const float* x, void* xb, float* stats, int64_t rows, hipStream_t s) {
+  const int64_t wg = (rows + 3) / 4;
+  ln_stats768_kernel<<<dim3((unsigned)(wg < 1024 ? wg : 1024)), dim3(256), 0, s>>>(x, (bf16_t*)xb, stats, rows);
   return hipGetLastError();
 }
 
-static int ln_grid_cap() {   // workgroups of the C = 768 kernel (0: the one-row-per-wave kernel)
-  static const int cap = [] {
-    const char* e = getenv("DSVT_LN_GRID");
-    return e ? atoi(e) : 1024;
-  }();
-  return cap;
+// The weights of a LayerNorm-folded GEMM (dsvt_ln_fold_weights): for W [N, K] fp32 following
+// LayerNorm(gamma, beta):  Wf = bf16(W * gamma) [N, K],  wsum[n] = sum_k Wf[n, k] (of the bf16
+// values the MFMA multiplies),  bf[n] = b[n] + sum_k W[n, k] * beta[k].  One wave per row.
+__global__ __launch_bounds__(256) void ln_fold_kernel(const float* __restrict__ W, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, const float* __restrict__ b,
+                                                      bf16_t* __restrict__ Wf, float* __restrict__ wsum,
+                                                      float* __restrict__ bf, int64_t N, int64_t K) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  float s = 0.f, t = 0.f;
+  for (int64_t k = lane * 4; k < K; k += 256) {
+    const float4 w = *reinterpret_cast<const float4*>(W + n * K + k);
+    const float4 gg = *reinterpret_cast<const float4*>(gamma + k);
+    const float4 bb = *reinterpret_cast<const float4*>(beta + k);
+    const unsigned lo = cvt_pk_bf16(w.x * gg.x, w.y * gg.y), hi = cvt_pk_bf16(w.z * gg.z, w.w * gg.w);
+    *reinterpret_cast<uint2*>(Wf + n * K + k) = make_uint2(lo, hi);
+    s += (__uint_as_float(lo << 16) + __uint_as_float(lo & 0xffff0000u)) +
+         (__uint_as_float(hi << 16) + __uint_as_float(hi & 0xffff0000u));
+    t += (w.x * bb.x + w.y * bb.y) + (w.z * bb.z + w.w * bb.w);
+  }
+  s = wave_sum(s);
+  t = wave_sum(t);
+  if (lane == 0) {
+    wsum[n] = s;
+    bf[n] = (b ? b[n] : 0.f) + t;
+  }
+}
+
+hipError_t launch_ln_fold(const float* W, const float* gamma, const float* beta, const float* b, void* Wf, float* wsum,
+                          float* bf, int64_t N, int64_t K, hipStream_t s) {
+  ln_fold_kernel<<<dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s>>>(W, gamma, beta, b, (bf16_t*)Wf, wsum, bf, N, K);
+  return hipGetLastError();
 }
 
 template <typename OutT, bool MAPOUT>
 static hipError_t ln_t(const float* x, OutT* y, const float* g, const float* b, int64_t rows, int64_t C,
                        int64_t rpg, int64_t gstride, int64_t goff, float eps, hipStream_t s) {
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
-  const int cap = ln_grid_cap();
-  if (C == 768 && cap > 0) {
+  const int cap = 1024;                 // workgroups of the C = 768 kernel
+  if (C == 768) {
     if (grid.x > (unsigned)cap) grid.x = (unsigned)cap;
     layernorm768_kernel<OutT, MAPOUT><<<grid, block, 0, s>>>(x, y, g, b, rows, rpg, gstride, goff, eps);
   } else if (C % 256 == 0)

@@ -11,20 +11,15 @@ LIB_PATH = os.environ.get("DSVT_LIB", os.path.join(_HERE, "libdsvt.so"))
 BF16, F32 = 0, 1
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID = 0, 1, 2
 EPI_GELU_SAVE, EPI_DGELU = 4, 5
+GEMM_FEW_ROWS = 0x100           # OR-ed into the epilogue: a few-row GEMM (the K-split skinny kernel)
+LN_FOLD_C, LN_PARTS = 768, 12   # dsvt_gemm_lnx_fwd: C of the folded LayerNorm, float2 partials per row
 TOKENS_NT, TOKENS_FRAME = 0, 1
-ROWLN_NONE, ROWLN_X, ROWLN_COMPACT = 0, 1, 2
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
 WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
 WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
-WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_GEMM_SK, WS_ATTN_CLS = 10, 11, 12, 13, 14
+WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_ATTN_CLS = 10, 11, 12, 14
 
 _i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
-
-
-class GemmSeg(ctypes.Structure):
-    """dsvt_gemm_seg (include/dsvt.h): one row segment of dsvt_gemm_grouped_fwd."""
-    _fields_ = [("W", _p), ("bias", _p), ("a_row0", _i64), ("M", _i64), ("rpg", _i64), ("gstride", _i64),
-                ("goff", _i64)]
 
 # name -> (restype, argtypes); must mirror include/dsvt.h exactly (tests/test_capi_symbols.py)
 SIGNATURES = {
@@ -33,15 +28,14 @@ SIGNATURES = {
     "dsvt_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
     "dsvt_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
                              _i64, _i64, _i64, _p]),
-    "dsvt_gemm_sk_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
-                                _i64, _i64, _i64, _p, _i64, _p]),
-    "dsvt_gemm_grouped_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _i64, _p, _i64, _i64, _i64, _i32,
-                                     ctypes.POINTER(GemmSeg), _p]),
     "dsvt_gemm_resid_fwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
-    "dsvt_gemm_resid_ln_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _f32,
-                                      _p, _i32, _i64, _p]),
     "dsvt_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
-    "dsvt_add_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _i32, _f32, _p]),
+    "dsvt_ln_fold_weights": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "dsvt_ln_stats_fwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "dsvt_gemm_resid_stats_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
+                                         _i64, _p]),
+    "dsvt_gemm_lnx_fwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _p, _f32, _p, _p, _p, _p, _i64, _i64, _i64,
+                                 _i64, _i64, _i64, _i64, _p]),
     "dsvt_ln_gemm_fwd": (_i32, [_i32, _i32, _i32, _p, _i64, _i64, _i64, _p, _p, _f32, _p, _p, _p, _i64,
                                 _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvt_patch_embed_fwd": (_i32, [_i32, _i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p,
@@ -100,13 +94,15 @@ SIGNATURES = {
     # the params struct pointer is bound with its ctypes.Structure type in dsvt/augment.py
     "dsvt_video_augment": (_i32, [_p, _i32, _i64, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _i32, _p,
                                   ctypes.c_size_t, _p]),
-    "dsvt_set_gemm_variant": (_i32, [_i32]),
-    "dsvt_set_gemm_skinny": (_i32, [_i32]),
-    "dsvt_set_attn_variant": (_i32, [_i32]),
-    "dsvt_set_attn_bwd_variant": (_i32, [_i32]),
     "dsvt_probe_enable": (_i32, [_i32, _i32]),
     "dsvt_probe_disable": (_i32, []),
     "dsvt_probe_read": (_i32, [_p, _p, _p, _p, _p, _i32]),
+}
+# include/dsvt_debug.h: kernel-choice overrides for tools and tests (not the drop-in interface)
+DEBUG_SIGNATURES = {
+    "dsvt_set_gemm_variant": (_i32, [_i32]),
+    "dsvt_set_attn_variant": (_i32, [_i32]),
+    "dsvt_set_attn_bwd_variant": (_i32, [_i32]),
 }
 
 
@@ -125,7 +121,7 @@ def lib():
             raise DsvtError("libdsvt.so not found at %s -- run `python -c 'import __graft_entry__ as g; "
                             "g.build()'` (or make -C dino-video-summarization-transformer_amd/csrc)" % LIB_PATH)
         handle = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in list(SIGNATURES.items()) + list(DEBUG_SIGNATURES.items()):
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

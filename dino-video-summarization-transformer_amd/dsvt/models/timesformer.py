@@ -19,13 +19,14 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .._lib import EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, ROWLN_COMPACT, ROWLN_NONE, ROWLN_X, TOKENS_FRAME, \
-    TOKENS_NT, WS_ATTN_SPATIAL, WS_LN_GEMM, WS_PATCH_EMBED, DsvtError
+from .._lib import EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, LN_FOLD_C, LN_PARTS, TOKENS_FRAME, TOKENS_NT, \
+    WS_ATTN_SPATIAL, WS_LN_GEMM, WS_PATCH_EMBED, DsvtError
 from ..weights import WeightCache
 from .vit_utils import DropPath, to_2tuple, trunc_normal_
 
 _DEFAULT_DTYPE = [torch.bfloat16]
 SPLIT_ROWS = 8192           # token rows per concurrent chunk of an auto-split inference batch
+LN_FOLD_MIN_ROWS = 8192     # "auto" LayerNorm folding: calls of at least this many token rows
 
 
 def set_default_dtype(dtype):
@@ -100,57 +101,77 @@ class Block(nn.Module):
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
 
     # -------------------------------------------------------------- HIP forward
-    def run(self, X, ctx, probs=None, cls_tail=False):
+    def run(self, X, ctx, probs=None, cls_tail=False, last=False):
         """One block on the fp32 token tensor X (in place).  ctx: per-forward buffers.
         probs (divided only): stop after the spatial softmax and write it there -- the
         return_attn path of timesformer.py:155-157 (X is then left mid-block).
         cls_tail (the LAST block of a CLS-only forward): after the temporal branch and the
         spatial qkv (the keys / values of every row), only the CLS rows are carried on -- see
-        _run_cls_tail."""
+        _run_cls_tail.  last: no LayerNorm reads this block's output rows (ctx.lnx: the final
+        residual GEMM writes no LayerNorm inputs).
+        ctx.lnx (bf16, C = 768): every LayerNorm is folded into the GEMM that reads it
+        (dsvt_gemm_lnx_fwd on the bf16 rows ctx.xb and their statistics ctx.st, which every
+        residual GEMM keeps current: dsvt_gemm_resid_stats_fwd) -- no LayerNorm pass."""
         w = ctx.w
         if cls_tail:
             return self._run_cls_tail(X, ctx)
-        C, heads = ctx.C, self.attn.num_heads
-        eps1, eps2 = self.norm1.eps, self.norm2.eps
-        if getattr(ctx, "fuse_ln", False) and self.attention_type == "divided_space_time":
-            return self._run_fused(X, ctx, probs)
-        if getattr(ctx, "split_resid", False) and self.attention_type == "divided_space_time":
-            return self._run_split(X, ctx, probs)
+        heads = self.attn.num_heads
         if self.attention_type == 'divided_space_time':
             B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
             R = B * Np * T
             patch_map = (Np * T, L, 1)          # compact patch row m -> X row b*L + 1 + m % (Np*T)
             ta = self.temporal_attn
-            # temporal: LN -> qkv (timesformer.py:127-131)
-            ops.ln_gemm(X, patch_map, R, self.temporal_norm1.weight, self.temporal_norm1.bias,
-                        self.temporal_norm1.eps, w(ta.qkv.weight), ta.qkv.bias, ctx.qkv, ctx.ws)
+            # temporal: LN -> qkv (timesformer.py:127-131) -> attention -> proj . temporal_fc + residual
+            self._qkv(X, ctx, R, patch_map, self.temporal_norm1, ta.qkv)
             ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
-            if ctx.fold_temporal:   # temporal_fc(proj(o)) as one GEMM (WeightCache.folded) + residual
-                wf, bf = ctx.fold(self.temporal_fc, ta.proj)
-                ops.gemm(ctx.o, wf, bf, X, epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)
-            else:
-                ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)             # proj (:83)
-                ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X,    # fc + residual
-                         epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)                   # (:133-135)
+            self._temporal_out(X, ctx, R, patch_map)
             # spatial with CLS replicate/mean (:139-181)
-            ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, eps1, w(self.attn.qkv.weight),
-                        self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            self._qkv(X, ctx, B * L, None, self.norm1, self.attn.qkv)
             if probs is not None:
                 ops.attn_spatial_probs(ctx.qkv, ctx.o, probs, B, T, L, heads, self.attn.scale, ctx.cls_ws)
                 return
             ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
         else:
             nb, L = ctx.nb, ctx.L
-            ops.ln_gemm(X, None, nb * L, self.norm1.weight, self.norm1.bias, eps1, w(self.attn.qkv.weight),
-                        self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            self._qkv(X, ctx, nb * L, None, self.norm1, self.attn.qkv)
             ops.attn_joint(ctx.qkv, ctx.o, nb, L, heads, self.attn.scale)
         rows = ctx.rows
-        ops.gemm(ctx.o, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
+        self._resid(X, ctx, ctx.o, self.attn.proj, rows)
         # MLP (:184)
-        ops.ln_gemm(X, None, rows, self.norm2.weight, self.norm2.bias, eps2, w(self.mlp.fc1.weight),
-                    self.mlp.fc1.bias, ctx.hid, ctx.ws, epilogue=EPI_BIAS_GELU)
-        ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, M=rows)
+        if ctx.lnx:
+            ops.gemm_lnx(ctx.xb, ctx.st, self.norm2.eps, ctx.fold_ln(self.mlp.fc1, self.norm2), ctx.hid, rows,
+                         epilogue=EPI_BIAS_GELU)
+        else:
+            ops.ln_gemm(X, None, rows, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
+                        self.mlp.fc1.bias, ctx.hid, ctx.ws, epilogue=EPI_BIAS_GELU)
+        self._resid(X, ctx, ctx.hid, self.mlp.fc2, rows, stats=not last)
 
+    def _qkv(self, X, ctx, M, rowmap, ln, lin):
+        """qkv = Linear(LayerNorm(rows of X through rowmap)) into ctx.qkv (compact rows)."""
+        if ctx.lnx:
+            ops.gemm_lnx(ctx.xb, ctx.st, ln.eps, ctx.fold_ln(lin, ln), ctx.qkv, M, in_rowmap=rowmap)
+        else:
+            ops.ln_gemm(X, rowmap, M, ln.weight, ln.bias, ln.eps, ctx.w(lin.weight), lin.bias, ctx.qkv, ctx.ws)
+
+    def _resid(self, X, ctx, a, lin, M, rowmap=None, stats=True, w=None, b=None):
+        """X[row(m)] += a[m] . W^T + b (lin's W / b unless given); under ctx.lnx the rows' bf16 copy
+        and LayerNorm statistics are updated too (stats=False: nothing reads them)."""
+        w = ctx.w(lin.weight) if w is None else w
+        b = lin.bias if b is None else b
+        if ctx.lnx and stats:
+            ops.gemm_resid_stats(a, w, b, X, ctx.xb, ctx.st, rowmap=rowmap, M=M)
+        else:
+            ops.gemm(a, w, b, X, epilogue=EPI_BIAS_RESID, rowmap=rowmap, M=M)
+
+    def _temporal_out(self, X, ctx, R, patch_map):
+        """x[patch rows] += temporal_fc(proj(o)) (timesformer.py:83, 133-135)."""
+        ta = self.temporal_attn
+        if ctx.fold_temporal:   # temporal_fc(proj(o)) as one GEMM (WeightCache.folded) + residual
+            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
+            self._resid(X, ctx, ctx.o, None, R, rowmap=patch_map, w=wf, b=bf)
+        else:
+            ops.gemm(ctx.o, ctx.w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)             # proj (:83)
+            self._resid(X, ctx, ctx.r1, self.temporal_fc, R, rowmap=patch_map)            # fc + residual
 
     def _run_cls_tail(self, X, ctx):
         """The last divided block when forward_features returns the CLS token only
@@ -170,125 +191,46 @@ class Block(nn.Module):
             # query over all L rows
             nb, L = ctx.nb, ctx.L
             cmap = (1, L, 0)
-            ops.ln_gemm(X, None, nb * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, w(self.attn.qkv.weight),
-                        self.attn.qkv.bias, ctx.qkv, ctx.ws)
+            self._qkv(X, ctx, nb * L, None, self.norm1, self.attn.qkv)
             o_cls, h_cls = ctx.o[:nb], ctx.hid[:nb]
             ops.attn_spatial_cls(ctx.qkv, o_cls, nb, 1, L, heads, self.attn.scale)
-            with ops.skinny():              # the CLS rows' GEMMs: K-split skinny kernel
-                ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID,
-                         rowmap=cmap, M=nb)
-                ops.ln_gemm(X, cmap, nb, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
-                            self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
-                ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap,
-                         M=nb)
+            self._cls_rows_out(X, ctx, o_cls, h_cls, nb, cmap)
             return
         B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
         R = B * Np * T
         patch_map = (Np * T, L, 1)
         cls_map = (1, L, 0)                 # CLS row b -> X row b*L
         ta = self.temporal_attn
-        ops.ln_gemm(X, patch_map, R, self.temporal_norm1.weight, self.temporal_norm1.bias,
-                    self.temporal_norm1.eps, w(ta.qkv.weight), ta.qkv.bias, ctx.qkv, ctx.ws)
+        self._qkv(X, ctx, R, patch_map, self.temporal_norm1, ta.qkv)
         ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
-        if ctx.fold_temporal:
-            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
-            ops.gemm(ctx.o, wf, bf, X, epilogue=EPI_BIAS_RESID, rowmap=patch_map, M=R)
-        else:
-            ops.gemm(ctx.o, w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
-            ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, X, epilogue=EPI_BIAS_RESID,
-                     rowmap=patch_map, M=R)
+        self._temporal_out(X, ctx, R, patch_map)
         # spatial qkv: keys / values of every row, queries of the CLS rows only (the patch rows'
         # queries have no consumer here)
         C = ctx.C
         wqkv, bqkv = w(self.attn.qkv.weight), self.attn.qkv.bias
-        ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[C:],
-                    None if bqkv is None else bqkv[C:], ctx.qkv, ctx.ws, col0=C)
-        with ops.skinny():                  # the CLS rows' GEMMs: K-split skinny kernel
-            ops.ln_gemm(X, cls_map, B, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[:C],
-                        None if bqkv is None else bqkv[:C], ctx.qkv, ctx.ws, rowmap=cls_map)
-            o_cls = ctx.o[:B]               # compact [B, C] rows (ctx.o is free again)
-            ops.attn_spatial_cls(ctx.qkv, o_cls, B, T, L, heads, self.attn.scale)
-            ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID,
-                     rowmap=cls_map, M=B)
-            h_cls = ctx.hid[:B]
-            ops.ln_gemm(X, cls_map, B, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
-                        self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU)
-            ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cls_map,
-                     M=B)
-
-    def _run_split(self, X, ctx, probs):
-        """Divided block with each residual sub-layer as GEMM (d = f(x), bias epilogue, storage
-        dtype) + one add-LayerNorm pass (x += d; the next norm of the updated rows): ctx.a enters
-        holding temporal_norm1 of the patch rows (compact) and leaves holding the NEXT block's
-        (ctx.next_ln; after the last block X is only updated).  timesformer.py:127-184."""
-        w = ctx.w
-        B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
-        heads = self.attn.num_heads
-        R, rows = B * Np * T, ctx.rows
-        ta = self.temporal_attn
-        a, d = ctx.a, ctx.d
-        # temporal (:127-135): qkv (LN already applied) -> attention -> proj . temporal_fc
-        ops.gemm(a[:R], w(ta.qkv.weight), ta.qkv.bias, ctx.qkv[:R])
-        ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
-        if ctx.fold_temporal:
-            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
-            ops.gemm(ctx.o[:R], wf, bf, d[:R])
+        if ctx.lnx:
+            ops.gemm_lnx(ctx.xb, ctx.st, self.norm1.eps, ctx.fold_ln(self.attn.qkv, self.norm1), ctx.qkv, B * L,
+                         rows=(C, 3 * C), col0=C)
         else:
-            ops.gemm(ctx.o[:R], w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
-            ops.gemm(ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias, d[:R])
-        # x[patch rows] += d ; a = norm1(x) on every row (CLS rows unchanged by the temporal branch)
-        ops.add_layernorm(X, d, L, ROWLN_COMPACT, ln=self.norm1, y=a, ymode=ROWLN_X)
-        # spatial with CLS replicate / mean (:139-181)
-        ops.gemm(a, w(self.attn.qkv.weight), self.attn.qkv.bias, ctx.qkv)
-        if probs is not None:
-            ops.attn_spatial_probs(ctx.qkv, ctx.o, probs, B, T, L, heads, self.attn.scale, ctx.cls_ws)
-            return
-        ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
-        ops.gemm(ctx.o, w(self.attn.proj.weight), self.attn.proj.bias, d, M=rows)
-        ops.add_layernorm(X, d, L, ROWLN_X, ln=self.norm2, y=a, ymode=ROWLN_X)
-        # MLP (:184): fc1 + GELU, fc2, x += d and the next block's temporal_norm1 (patch rows)
-        ops.gemm(a, w(self.mlp.fc1.weight), self.mlp.fc1.bias, ctx.hid, epilogue=EPI_BIAS_GELU)
-        ops.gemm(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, d, M=rows)
-        nxt = ctx.next_ln
-        ops.add_layernorm(X, d, L, ROWLN_X, ln=nxt, y=a if nxt is not None else None,
-                          ymode=ROWLN_COMPACT if nxt is not None else ROWLN_NONE)
+            ops.ln_gemm(X, None, B * L, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[C:],
+                        None if bqkv is None else bqkv[C:], ctx.qkv, ctx.ws, col0=C)
+        # the CLS rows' GEMMs: K-split skinny kernel (few_rows)
+        ops.ln_gemm(X, cls_map, B, self.norm1.weight, self.norm1.bias, self.norm1.eps, wqkv[:C],
+                    None if bqkv is None else bqkv[:C], ctx.qkv, ctx.ws, rowmap=cls_map, few_rows=True)
+        o_cls = ctx.o[:B]                   # compact [B, C] rows (ctx.o is free again)
+        ops.attn_spatial_cls(ctx.qkv, o_cls, B, T, L, heads, self.attn.scale)
+        self._cls_rows_out(X, ctx, o_cls, ctx.hid[:B], B, cls_map)
 
-    def _run_fused(self, X, ctx, probs):
-        """Divided block with every residual projection fused with the LayerNorm that follows
-        it (csrc/gemm_rowln.hip): ctx.a enters holding temporal_norm1 of the patch rows
-        (compact) and leaves holding the NEXT block's (ctx.next_ln; none after the last)."""
+    def _cls_rows_out(self, X, ctx, o_cls, h_cls, n, cmap):
+        """attn.proj + residual, norm2 -> fc1 + GELU, fc2 + residual on the n CLS rows (:181-184),
+        on the K-split skinny kernel (few_rows)."""
         w = ctx.w
-        B, T, Np, L, C = ctx.B, ctx.T, ctx.Np, ctx.L, ctx.C
-        heads = self.attn.num_heads
-        R, rows = B * Np * T, ctx.rows
-        patch_map = (Np * T, L, 1)
-        ta = self.temporal_attn
-        a = ctx.a
-        # temporal: qkv (LN already applied) -> attention -> proj . temporal_fc + residual, norm1
-        ops.gemm(a[:R], w(ta.qkv.weight), ta.qkv.bias, ctx.qkv[:R])
-        ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
-        if ctx.fold_temporal:
-            wf, bf = ctx.fold(self.temporal_fc, ta.proj)
-            src, wt, bt = ctx.o[:R], wf, bf
-        else:
-            ops.gemm(ctx.o[:R], w(ta.proj.weight), ta.proj.bias, ctx.r1, M=R)
-            src, wt, bt = ctx.r1, w(self.temporal_fc.weight), self.temporal_fc.bias
-        ops.gemm_resid_ln(src, wt, bt, X, M=R, rowmap=patch_map, ln=self.norm1, Y=a, ymode=ROWLN_X)
-        # norm1 of the CLS rows (untouched by the temporal branch), written to their own rows of a
-        ops.layernorm(X, B, C, self.norm1.weight, self.norm1.bias, self.norm1.eps, a, rowmap=(1, L, 0), out_f32=2)
-        # spatial with CLS replicate / mean, proj + residual, norm2
-        ops.gemm(a, w(self.attn.qkv.weight), self.attn.qkv.bias, ctx.qkv)
-        if probs is not None:
-            ops.attn_spatial_probs(ctx.qkv, ctx.o, probs, B, T, L, heads, self.attn.scale, ctx.cls_ws)
-            return
-        ops.attn_spatial(ctx.qkv, ctx.o, B, T, L, heads, self.attn.scale, ctx.cls_ws)
-        ops.gemm_resid_ln(ctx.o, w(self.attn.proj.weight), self.attn.proj.bias, X, M=rows, ln=self.norm2, Y=a,
-                          ymode=ROWLN_X)
-        # MLP: fc1 + GELU, fc2 + residual, the next block's temporal_norm1 (patch rows, compact)
-        ops.gemm(a, w(self.mlp.fc1.weight), self.mlp.fc1.bias, ctx.hid, epilogue=EPI_BIAS_GELU)
-        nxt = ctx.next_ln
-        ops.gemm_resid_ln(ctx.hid, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, M=rows, ln=nxt, Y=a,
-                          ymode=ROWLN_COMPACT if nxt is not None else ROWLN_NONE, L=L)
+        ops.gemm(o_cls, w(self.attn.proj.weight), self.attn.proj.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap, M=n,
+                 few_rows=True)
+        ops.ln_gemm(X, cmap, n, self.norm2.weight, self.norm2.bias, self.norm2.eps, w(self.mlp.fc1.weight),
+                    self.mlp.fc1.bias, h_cls, ctx.ws, epilogue=EPI_BIAS_GELU, few_rows=True)
+        ops.gemm(h_cls, w(self.mlp.fc2.weight), self.mlp.fc2.bias, X, epilogue=EPI_BIAS_RESID, rowmap=cmap, M=n,
+                 few_rows=True)
 
 
 class PatchEmbed(nn.Module):
@@ -360,19 +302,10 @@ class VisionTransformer(nn.Module):
         # fold temporal_attn.proj and temporal_fc into one Linear (exact algebra, one GEMM less
         # per block); False runs the two GEMMs of the reference literally
         self.fold_temporal_fc = True
-        # opt-in (bf16, divided, C = 768): every residual projection (temporal_fc, attn.proj,
-        # mlp.fc2) as one full-row kernel that also writes the LayerNorm the next GEMM reads
-        # (csrc/gemm_rowln.hip).  Off by default: measured slower than GEMM + LayerNorm (95 vs 87 us
-        # at K = 768, 210 vs 185 us at K = 3072, 25k rows) -- a full-row workgroup must pull all of
-        # W through LDS-DMA for only ~100 rows, which caps it at ~20-25 GB/s per CU
-        self.fuse_ln = os.environ.get("DSVT_FUSE_LN", "0") == "1"
-        # opt-in (divided, C = 768, inference): every residual projection (temporal_fc, attn.proj,
-        # mlp.fc2) writes d = f(x) with a plain bias epilogue and one streaming pass does x += d
-        # together with the LayerNorm the next GEMM reads (dsvt_add_layernorm_fwd).  Off by
-        # default: measured slower (serial step 26.6 vs 26.0 ms, graph bench 347 vs 356 clips/s):
-        # the bias-only GEMM saves ~9 us per launch over the fp32 residual epilogue, the add-LN
-        # pass (231 MB at 6.3 TB/s, 35 us) costs ~19 us more than the LayerNorm it replaces
-        self.split_resid = os.environ.get("DSVT_SPLIT_RESID", "0") == "1"
+        # bf16 inference, C = 768: every LayerNorm folded into the GEMM that reads it
+        # (dsvt_gemm_lnx_fwd + dsvt_gemm_resid_stats_fwd, Block.run) -- True / False / "auto" (calls
+        # of at least LN_FOLD_MIN_ROWS token rows, where every GEMM runs on the 256x256 kernel)
+        self.ln_fold = "auto"
         # inference: split a batch into this many clip chunks on concurrent HIP streams (each
         # kernel's last partly-filled wave of tiles then runs beside the other chunk's kernels);
         # "auto" = one chunk per SPLIT_ROWS token rows, at most 3 (2 from SPLIT_ROWS / 2 rows and
@@ -423,7 +356,20 @@ class VisionTransformer(nn.Module):
                 else:
                     lins += [blk.temporal_attn.proj, blk.temporal_fc]
             ws += [lin.weight for lin in lins]
+            if self._ln_fold_on(mode, LN_FOLD_MIN_ROWS if self.ln_fold == "auto" else 0):
+                for lin, ln in ((blk.attn.qkv, blk.norm1), (blk.mlp.fc1, blk.norm2)) + \
+                        (((blk.temporal_attn.qkv, blk.temporal_norm1),) if blk.attention_type == 'divided_space_time'
+                         else ()):
+                    self._wcache.ln_folded(lin, ln)
         self._wcache.refresh(ws, mode, flat={id(self.patch_embed.proj.weight)})   # one launch
+
+    def _ln_fold_on(self, mode, rows):
+        """Fold every LayerNorm into the GEMM that reads it for a call of `rows` token rows?"""
+        if mode != torch.bfloat16 or self.embed_dim != LN_FOLD_C:
+            return False
+        if self.ln_fold == "auto":
+            return rows >= LN_FOLD_MIN_ROWS
+        return bool(self.ln_fold)
 
     def _indices(self, Hp, Wp, T, device):
         key = (Hp, Wp, T, device)
@@ -593,26 +539,20 @@ class VisionTransformer(nn.Module):
         ctx.hid = torch.empty(ctx.rows, self.blocks[0].mlp.fc1.out_features, device=dev, dtype=mode)
         ctx.fold_temporal = self.fold_temporal_fc
         ctx.fold = lambda outer, inner: self._wcache.folded(mode, outer, inner)
-        ctx.fuse_ln = (self.fuse_ln and mode == torch.bfloat16 and C == 768
-                       and self.attention_type == 'divided_space_time')
         if self.attention_type == 'divided_space_time':
             if not ctx.fold_temporal:
                 ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
             nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
             ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
-        ctx.split_resid = (not ctx.fuse_ln and self.split_resid and C == 768
-                           and self.attention_type == 'divided_space_time')
-        if ctx.split_resid:
-            ctx.d = torch.empty(ctx.rows, C, device=dev, dtype=mode)
-        if ctx.fuse_ln or ctx.split_resid:   # block 0's temporal_norm1 on the patch rows (compact) into ctx.a
-            ctx.a = torch.empty(ctx.rows, C, device=dev, dtype=mode)
-            tn = self.blocks[0].temporal_norm1
-            ops.layernorm(X, B * Np * T, C, tn.weight, tn.bias, tn.eps, ctx.a, rowmap=(Np * T, ctx.L, 1),
-                          out_f32=False)
+        ctx.lnx = self._ln_fold_on(mode, ctx.rows)
+        if ctx.lnx:             # the bf16 rows + LayerNorm statistics the folded GEMMs read
+            ctx.xb = torch.empty(ctx.rows, C, device=dev, dtype=torch.bfloat16)
+            ctx.st = torch.empty(ctx.rows, LN_PARTS, 2, device=dev, dtype=torch.float32)
+            ctx.fold_ln = self._wcache.ln_folded
+            ops.ln_stats(X, ctx.xb, ctx.st, ctx.rows)
         nblk = len(self.blocks)
         if get_attn:            # timesformer.py:325-331: the last block's attention instead of features
-            for i, blk in enumerate(self.blocks[:-1]):
-                ctx.next_ln = self.blocks[i + 1].temporal_norm1 if (ctx.fuse_ln or ctx.split_resid) else None
+            for blk in self.blocks[:-1]:
                 blk.run(X, ctx)
             if self.attention_type == 'divided_space_time':
                 heads = self.blocks[-1].attn.num_heads
@@ -621,15 +561,12 @@ class VisionTransformer(nn.Module):
                 return probs
             # space-only / joint: the reference Block has no return_attn branch and returns its
             # output tokens (un-normed)
-            self.blocks[-1].run(X, ctx)
+            self.blocks[-1].run(X, ctx, last=True)
             return X.view(ctx.nb, ctx.L, C)
         divided = self.attention_type == 'divided_space_time'
-        cls_tail = (self.cls_tail and not get_all and not (ctx.fuse_ln or ctx.split_resid)
-                    and ops.attn_cls_ok(T if divided else 1, ctx.L))
+        cls_tail = self.cls_tail and not get_all and ops.attn_cls_ok(T if divided else 1, ctx.L)
         for i, blk in enumerate(self.blocks):
-            ctx.next_ln = (self.blocks[i + 1].temporal_norm1
-                           if ((ctx.fuse_ln or ctx.split_resid) and i + 1 < nblk) else None)
-            blk.run(X, ctx, cls_tail=cls_tail and i + 1 == nblk)
+            blk.run(X, ctx, cls_tail=cls_tail and i + 1 == nblk, last=i + 1 == nblk)
         L = ctx.L
         if self.attention_type == 'space_only':      # mean over frames (:338-340)
             Xm = torch.empty(B * L, C, device=dev, dtype=torch.float32)

@@ -4,9 +4,6 @@ current HIP stream; every computation is a libdsvt.so kernel.
 Storage dtype ("mode"): torch.bfloat16 (perf) or torch.float32 (parity).  The token
 tensor X, LayerNorm/softmax statistics and losses are always fp32.
 """
-import contextlib
-import os
-
 import torch
 
 from . import _lib
@@ -44,39 +41,9 @@ def workspace_bytes(op, mode, M, N, K):
     return int(_lib.lib().dsvt_workspace_bytes(op, _dt(mode), M, N, K))
 
 
-_SK_WS = {}          # (device index, stream handle) -> zero-filled stream-K scratch (dsvt_gemm_sk_fwd)
-
-
-def _sk_workspace(dev):
-    """The stream-K GEMM scratch of the current stream: allocated (zero-filled) on first use
-    outside graph capture and kept; the kernels leave it zero.  One per stream, so GEMMs on
-    concurrent streams never share counters.  None while capturing a stream that has none (the
-    plain kernels run then) and unless DSVT_SK=1 / 2 (opt-in: measured slower than the
-    data-parallel kernels on every hot-path shape)."""
-    if os.environ.get("DSVT_SK", "0") == "0":
-        return None
-    key = (dev.index, _stream())
-    ws = _SK_WS.get(key)
-    if ws is None and not torch.cuda.is_current_stream_capturing():
-        nbytes = int(_lib.lib().dsvt_workspace_bytes(_lib.WS_GEMM_SK, _lib.BF16, 1, 1, 1))
-        ws = _SK_WS[key] = torch.zeros(nbytes // 4, device=dev, dtype=torch.int32)
-    return ws
-
-
-@contextlib.contextmanager
-def skinny():
-    """The GEMM launches inside run the K-split skinny kernel where eligible (dsvt_set_gemm_skinny):
-    for the few-row GEMMs of the CLS-only last block and of the DINO head, chosen by call site so a
-    batch split over streams runs the same kernel as the whole batch."""
-    call("dsvt_set_gemm_skinny", 1)
-    try:
-        yield
-    finally:
-        call("dsvt_set_gemm_skinny", 0)
-
-
-def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=None):
-    """out[row(m)] (op)= a[m] . w^T (+bias ...); a [M,K] mode, w [N,K] mode."""
+def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=None, few_rows=False):
+    """out[row(m)] (op)= a[m] . w^T (+bias ...); a [M,K] mode, w [N,K] mode.  few_rows: a few-row
+    call site (the CLS-only tail, the DINO head) -- the K-split skinny kernel (DSVT_GEMM_FEW_ROWS)."""
     mode = w.dtype
     _check(a, mode, "A")
     _check(w, mode, "W")
@@ -84,32 +51,9 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     K = a.shape[-1]
     N = w.shape[0]
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
-    ws = _sk_workspace(a.device) if mode == torch.bfloat16 else None
-    if ws is not None:
-        call("dsvt_gemm_sk_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
-             _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _ptr(ws), ws.numel() * 4, _stream())
-    else:
-        call("dsvt_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
-             _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _stream())
-    return out
-
-
-def gemm_grouped(a, segs, out, epilogue=_lib.EPI_BIAS, out_f32=False):
-    """One launch over row segments of `a` with their own weights: segs = [(w, bias, a_row0, M,
-    rowmap or None, out_row0)], out row of segment row m = out_row0 + map(m) (dsvt_gemm_grouped_fwd)."""
-    mode = a.dtype
-    _check(a, mode, "A")
-    arr = (_lib.GemmSeg * len(segs))()
-    K = a.shape[-1]
-    N = segs[0][0].shape[0]
-    for i, (w, bias, a_row0, M, rowmap, out_row0) in enumerate(segs):
-        _check(w, mode, "W")
-        if w.shape[0] != N or w.shape[1] != K:
-            raise _lib.DsvtError("gemm_grouped: every segment's W must be [%d, %d]" % (N, K))
-        rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
-        arr[i] = _lib.GemmSeg(w.data_ptr(), _ptr(bias), int(a_row0), int(M), int(rpg), int(gs), int(go + out_row0))
-    call("dsvt_gemm_grouped_fwd", _dt(mode), epilogue, int(out_f32), _ptr(a), K, K, _ptr(out), out.shape[-1], N, K,
-         len(segs), arr, _stream())
+    epi = epilogue | (_lib.GEMM_FEW_ROWS if few_rows else 0)
+    call("dsvt_gemm_fwd", _dt(mode), epi, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
+         _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _stream())
     return out
 
 
@@ -141,59 +85,54 @@ def gemm_resid(a, w, bias, x_in, x_out, rowmap=None, M=None, bias_row_scale=None
     return x_out
 
 
-def add_layernorm(X, d, L, dmode, ln=None, y=None, ymode=_lib.ROWLN_NONE):
-    """X[r] += d[drow(r)] (fp32 X [rows, 768], clips of L rows), then y[yrow(r)] = ln(X[r]).
-    dmode / ymode: 0 none, ROWLN_X the row itself, ROWLN_COMPACT the patch-row layout of the
-    temporal branch (CLS rows have no d / y row).  One streaming pass: the sub-layer GEMM before
-    it writes d with a plain bias epilogue."""
+# ---------------------------------------------------------------- LayerNorm folded into the GEMM
+def ln_fold_weights(W, ln, bias, Wf, wsum, bias_f):
+    """Wf = bf16(W * ln.weight), wsum = row sums of Wf, bias_f = bias + W . ln.bias (dsvt_ln_fold_weights)."""
+    _check(W, torch.float32, "W")
+    _check(Wf, torch.bfloat16, "Wf")
+    N, K = W.shape
+    call("dsvt_ln_fold_weights", _ptr(W), _ptr(ln.weight), _ptr(ln.bias), _ptr(bias), _ptr(Wf), _ptr(wsum),
+         _ptr(bias_f), N, K, _stream())
+
+
+def ln_stats(X, xb, stats, rows):
+    """xb[r] = bf16(X[r]), stats[r] = the LN_PARTS (sum, sum of squares) partials, r < rows."""
     _check(X, torch.float32, "X")
-    rows, C = X.shape
-    if dmode != _lib.ROWLN_NONE and d.dtype not in (torch.bfloat16, torch.float32):
-        raise _lib.DsvtError("add_layernorm: d must be bf16 or fp32 (got %s)" % d.dtype)
-    if dmode != _lib.ROWLN_NONE:
-        _check(d, d.dtype, "d")
-        need = rows if dmode == _lib.ROWLN_X else rows // L * (L - 1)
-        if d.numel() < need * C:
-            raise _lib.DsvtError("add_layernorm: d holds %d rows, %d needed" % (d.numel() // C, need))
-    if ymode != _lib.ROWLN_NONE:
-        if y.dtype not in (torch.bfloat16, torch.float32):
-            raise _lib.DsvtError("add_layernorm: y must be bf16 or fp32 (got %s)" % y.dtype)
-        _check(y, y.dtype, "y")
-        need = rows if ymode == _lib.ROWLN_X else rows // L * (L - 1)
-        if y.numel() < need * C:
-            raise _lib.DsvtError("add_layernorm: y holds %d rows, %d needed" % (y.numel() // C, need))
-    g = ln.weight if ln is not None else None
-    b = ln.bias if ln is not None else None
-    eps = ln.eps if ln is not None else 0.0
-    call("dsvt_add_layernorm_fwd", _dt(d.dtype) if d is not None else _lib.BF16,
-         _dt(y.dtype) if y is not None else _lib.BF16, _ptr(X), _ptr(d), _ptr(y), _ptr(g), _ptr(b), rows, C, L,
-         int(dmode), int(ymode), float(eps), _stream())
-    return X
+    call("dsvt_ln_stats_fwd", _ptr(X), _ptr(xb), _ptr(stats), rows, X.shape[-1], _stream())
 
 
-def gemm_resid_ln(a, w, bias, X, M=None, rowmap=None, ln=None, Y=None, ymode=_lib.ROWLN_NONE, L=0):
-    """X[row(m)] += a[m] . w^T + bias (fp32 X, N = 768), then (ymode != NONE) Y[yrow] =
-    LayerNorm(X[row(m)]) in bf16 -- one full-row kernel (csrc/gemm_rowln.hip).  ln = the
-    nn.LayerNorm whose weight / bias / eps apply."""
+def gemm_resid_stats(a, w, bias, X, xb, stats, rowmap=None, M=None):
+    """X[row(m)] += a[m] . w^T + bias, and xb / stats of the updated rows (dsvt_gemm_resid_stats_fwd)."""
     _check(a, torch.bfloat16, "A")
     _check(w, torch.bfloat16, "W")
     _check(X, torch.float32, "X")
     M = a.shape[0] if M is None else M
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
-    if ymode != _lib.ROWLN_NONE:
-        _check(Y, torch.bfloat16, "Y")
-    g = ln.weight if ln is not None else None
-    b = ln.bias if ln is not None else None
-    eps = ln.eps if ln is not None else 0.0
-    call("dsvt_gemm_resid_ln_fwd", _ptr(a), a.shape[-1], _ptr(w), w.shape[1], _ptr(bias), _ptr(X), M, w.shape[0],
-         a.shape[-1], rpg, gs, go, _ptr(g), _ptr(b), float(eps), _ptr(Y), int(ymode), int(L), _stream())
+    call("dsvt_gemm_resid_stats_fwd", _ptr(a), a.shape[-1], _ptr(w), w.shape[1], _ptr(bias), _ptr(X), _ptr(xb),
+         _ptr(stats), X.shape[-1], M, w.shape[0], a.shape[-1], rpg, gs, go, _stream())
     return X
 
 
+def gemm_lnx(xb, stats, eps, folded, out, M, in_rowmap=None, epilogue=_lib.EPI_BIAS, col0=0, rows=None):
+    """out[m] = epilogue(LayerNorm(x[a_row(m)]) . W^T + b) from the bf16 rows xb and their stats
+    (dsvt_gemm_lnx_fwd); folded = (Wf, wsum, bias_f) of ln_fold_weights, optionally the row slice
+    `rows` = (n0, n1) of it; the N columns land in out's columns [col0, col0 + N)."""
+    Wf, wsum, bf = folded
+    if rows is not None:
+        Wf, wsum, bf = Wf[rows[0]:rows[1]], wsum[rows[0]:rows[1]], bf[rows[0]:rows[1]]
+    N, K = Wf.shape
+    if col0 < 0 or col0 + N > out.shape[-1]:
+        raise _lib.DsvtError("gemm_lnx: columns [%d, %d) outside out's %d" % (col0, col0 + N, out.shape[-1]))
+    irpg, igs, igo = in_rowmap if in_rowmap is not None else (0, 0, 0)
+    call("dsvt_gemm_lnx_fwd", epilogue, _ptr(xb), xb.shape[-1], irpg, igs, igo, _ptr(stats), float(eps), _ptr(Wf),
+         _ptr(wsum), _ptr(bf), out.data_ptr() + col0 * out.element_size(), out.shape[-1], M, N, K, 0, 0, 0, _stream())
+    return out
+
+
 def ln_gemm(x, in_rowmap, M, ln_w, ln_b, eps, w, bias, out, ws, epilogue=_lib.EPI_BIAS, out_f32=False,
-            rowmap=None, col0=0):
+            rowmap=None, col0=0, few_rows=False):
     """LayerNorm(rows of fp32 x through in_rowmap) -> GEMM with epilogue.  col0: the GEMM's N
-    columns land in out's columns [col0, col0 + N) (out's row stride kept)."""
+    columns land in out's columns [col0, col0 + N) (out's row stride kept).  few_rows as gemm()."""
     mode = w.dtype
     _check(x, torch.float32, "x")
     K = x.shape[-1]
@@ -201,7 +140,8 @@ def ln_gemm(x, in_rowmap, M, ln_w, ln_b, eps, w, bias, out, ws, epilogue=_lib.EP
         raise _lib.DsvtError("ln_gemm: columns [%d, %d) outside out's %d" % (col0, col0 + w.shape[0], out.shape[-1]))
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
     irpg, igs, igo = in_rowmap if in_rowmap is not None else (0, 0, 0)
-    call("dsvt_ln_gemm_fwd", _dt(mode), epilogue, int(out_f32), _ptr(x), irpg, igs, igo, _ptr(ln_w), _ptr(ln_b),
+    epi = epilogue | (_lib.GEMM_FEW_ROWS if few_rows else 0)
+    call("dsvt_ln_gemm_fwd", _dt(mode), epi, int(out_f32), _ptr(x), irpg, igs, igo, _ptr(ln_w), _ptr(ln_b),
          float(eps), _ptr(w), _ptr(bias), out.data_ptr() + col0 * out.element_size(), out.shape[-1], M, w.shape[0],
          K, rpg, gs, go, _ptr(ws), ws.numel() * ws.element_size(), _stream())
     return out
@@ -539,18 +479,16 @@ def gemm_kernel_name(tag):
         return "void dsvt::gemm_kernel<float, %d, %s>" % (epi, f32)
     if variant == 1:
         # the fp32-residual launches use the instantiation with the residual-tile prefetch
-        # (csrc/gemm.hip PREF) unless DSVT_RESID_PREF=0
-        pref = epi == _lib.EPI_BIAS_RESID and os.environ.get("DSVT_RESID_PREF", "1") != "0"
+        # (csrc/gemm.hip PREF)
+        pref = epi == _lib.EPI_BIAS_RESID
         return "void dsvt::gemm_kernel<unsigned short, %d, %s%s>" % (epi, f32, ", true" if pref else "")
-    persist = {9: "256, 128, 2, 2, 3, %d, %s, false", 10: "256, 128, 2, 2, 3, %d, %s, true"}
+    persist = {10: "256, 128, 2, 2, 3, %d, %s, true"}
     if variant in persist:
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
-    if variant in (20, 50):       # 50: the grouped (segmented) instantiations, same prefix
+    if variant == 20:
         return "void dsvt::gemm_8ph_kernel<%d, %s, 0, " % (epi, f32)
-    if variant == 33:
-        return "void dsvt::gemm_8ph_kernel<2, true, 0, false, false, true"
-    if variant == 30:
-        return "void dsvt::gemm_rowln_kernel<"
+    if variant == 50:
+        return "void dsvt::gemm_skinny_kernel<%d, %s>" % (epi, f32)
     if variant == 31:
         return "void dsvt::wgrad_kernel<0>"
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)

@@ -99,30 +99,9 @@ def prepare_weights(module):
             fn()
 
 
-def _groupable(student, teacher, images):
-    if os.environ.get("DSVT_GROUPED", "0") not in ("1", "2", "3", "4") or not images[0].is_cuda:
-        return False
-    if not all(isinstance(m, MultiCropWrapper) and not m.vary_fr for m in (student, teacher)):
-        return False
-    if torch.is_grad_enabled() and any(p.requires_grad for m in (student, teacher) for p in m.parameters()):
-        return False
-    from .grouped import eligible
-    return eligible([teacher.backbone, student.backbone])
-
-
 def dino_forward(student, teacher, images, n_global=2, concurrent=True):
     """train_ssl.py:523-527: teacher on the `n_global` global views, student on all views.
-    The two networks are independent and their backbone calls run on concurrent streams.
-    DSVT_GROUPED=1 (opt-in) runs dsvt divided-attention backbones in inference GROUPED instead,
-    every layer's Linear of all calls as one launch (dsvt.grouped): bitwise the same features,
-    measured slower (354 vs 370 clips/s on the bench line, same box: one stream loses the overlap
-    of the attention / LayerNorm kernels with the other calls' GEMMs).  DSVT_GROUPED=2 groups only
-    the same-shape calls (teacher and student global crops) and runs the rest beside them."""
-    if _groupable(student, teacher, images):
-        from .grouped import dino_forward_grouped
-        mode = os.environ.get("DSVT_GROUPED")
-        return dino_forward_grouped(student, teacher, images, n_global, same_shape_only=mode == "2",
-                                    balanced=3 if mode == "3" else 0, remainder=mode == "4")
+    The two networks are independent and their backbone calls run on concurrent streams."""
     if not concurrent:
         return student(images), teacher(images[:n_global])
     for net in (student, teacher):

@@ -119,6 +119,7 @@ class VisionTransformer(nn.Module):
         ctx = _Ctx()
         ctx.w, ctx.C, ctx.B, ctx.T, ctx.Np, ctx.nb, ctx.L = wget, C, B, 1, Np, B, 1 + Np
         ctx.rows = B * ctx.L
+        ctx.lnx = False
         X = torch.empty(ctx.rows, C, device=dev, dtype=torch.float32)
         nbytes = max(ops.workspace_bytes(WS_LN_GEMM, mode, ctx.rows, 0, C),
                      ops.workspace_bytes(WS_PATCH_EMBED, mode, B * Np, C, Cin * 256))
@@ -179,6 +180,8 @@ class WeightNormLinear(nn.Module):
         nn.init.uniform_(self.weight_v, -bound, bound)
 
 
+HEAD_FEW_ROWS = 512            # DINOHead MLP rows that still take the K-split skinny kernel
+
 class DINOHead(nn.Module):
     """vision_transformer.py:248-282."""
 
@@ -235,12 +238,15 @@ class DINOHead(nn.Module):
         h = torch.empty(R, x.shape[1], device=dev, dtype=mode)
         ops.cast(x, h)
         linears = [self.mlp] if isinstance(self.mlp, nn.Linear) else [m for m in self.mlp if isinstance(m, nn.Linear)]
-        with ops.skinny():                  # R = a few crops' CLS rows: K-split skinny kernel
-            for i, lin in enumerate(linears):
-                last = i == len(linears) - 1
-                out = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32 if last else mode)
-                ops.gemm(h, w(lin.weight), lin.bias, out, epilogue=EPI_BIAS if last else EPI_BIAS_GELU, out_f32=last)
-                h = out
+        # R = a few crops' CLS rows: the K-split skinny kernel (a fixed row cap: it streams all of K
+        # per 64-row block, so many rows -- head inference over whole videos -- take the tiled kernels)
+        few = R <= HEAD_FEW_ROWS
+        for i, lin in enumerate(linears):
+            last = i == len(linears) - 1
+            out = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32 if last else mode)
+            ops.gemm(h, w(lin.weight), lin.bias, out, epilogue=EPI_BIAS if last else EPI_BIAS_GELU, out_f32=last,
+                     few_rows=few)
+            h = out
         z = torch.empty(R, h.shape[1], device=dev, dtype=mode)
         ops.head_norm(h, z)                                                   # F.normalize (:280)
         ll = self.last_layer

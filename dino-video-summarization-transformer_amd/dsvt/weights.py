@@ -151,6 +151,29 @@ class WeightCache:
         self._c[key] = (stamp, (w, b32)) + self._event()
         return w, b32
 
+    def ln_folded(self, linear, ln):
+        """(Wf, wsum, bias_f) of nn.Linear `linear` after nn.LayerNorm `ln` for the LayerNorm-folded
+        GEMM (dsvt_gemm_lnx_fwd): Wf = bf16(W * gamma), wsum = its row sums, bias_f = b + W . beta,
+        one dsvt_ln_fold_weights launch, cached until any of the four parameters changes."""
+        params = (linear.weight, linear.bias, ln.weight, ln.bias)
+        stamp = tuple((None, 0) if p is None else (p._version, p.data_ptr()) for p in params)
+        key = ("lnfold", id(linear), id(ln))
+        ent = self._c.get(key)
+        if ent is not None and ent[0] == stamp:
+            self._sync(ent)
+            return ent[1]
+        W = linear.weight.detach()
+        if W.dtype != torch.float32 or not W.is_contiguous():
+            raise TypeError("dsvt expects contiguous fp32 master weights, got %s" % W.dtype)
+        N, K = W.shape
+        dev = W.device
+        Wf = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+        wsum = torch.empty(N, device=dev, dtype=torch.float32)
+        bf = torch.empty(N, device=dev, dtype=torch.float32)
+        ops.ln_fold_weights(W, ln, None if linear.bias is None else linear.bias.detach(), Wf, wsum, bf)
+        self._c[key] = (stamp, (Wf, wsum, bf)) + self._event()
+        return Wf, wsum, bf
+
     def refresh(self, params, mode, transposed=False, flat=()):
         """Bring the storage-dtype copies (transposed: the W^T copies) of many parameters up to
         date in ONE multi-tensor launch instead of one cast per weight -- after every optimizer

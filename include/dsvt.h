@@ -39,6 +39,11 @@ extern "C" {
 #define DSVT_EPI_BIAS_RESID 2 /* X[row(m)]  += acc + bias   (fp32 X)       (residual adds)   */
 #define DSVT_EPI_GELU_SAVE 4  /* out = GELU_erf(acc + bias), aux = acc + bias (training fc1)   */
 #define DSVT_EPI_DGELU 5      /* out = acc * GELU_erf'(aux)               (fc1 backward)    */
+/* OR-ed into the epilogue argument of dsvt_gemm_fwd / dsvt_ln_gemm_fwd: a few-row GEMM (the
+ * CLS-only last block's rows, timesformer.py:181-184 on the CLS tokens, and the DINOHead MLP,
+ * vision_transformer.py:271-281) -- the K-split skinny kernel where eligible, whatever M is, so a
+ * batch split over streams stays bitwise equal to the whole batch.  A per-call flag: no state. */
+#define DSVT_GEMM_FEW_ROWS 0x100
 
 /* token orders for patch embedding */
 #define DSVT_TOKENS_NT 0      /* divided / joint: X[b][1 + n*T + t]   (timesformer.py:312-323)  */
@@ -64,7 +69,6 @@ extern "C" {
 #define DSVT_WS_SELECT 10      /* M = number of scores, N = frames of the unsampled video */
 #define DSVT_WS_AUGMENT 11     /* M = output frames T, N = output size S */
 #define DSVT_WS_WGRAD 12       /* M = rows, N, K: the weight gradient is [N, K] */
-#define DSVT_WS_GEMM_SK 13     /* stream-K GEMM scratch (any shape) */
 #define DSVT_WS_ATTN_CLS 14    /* M = B*T sequences, N = heads, K = keys per sequence 1 + (L-1)/T */
 
 int dsvt_version(void);
@@ -85,39 +89,6 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
 int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
                   int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N,
                   int64_t K, int64_t rpg, int64_t gstride, int64_t goff, void *stream);
-/* One row segment of a grouped GEMM: rows [a_row0, a_row0 + M) of A times ITS W [N, K] (+ bias)
- * into out rows goff + (m / rpg) * gstride + m % rpg (m = 0 .. M-1 within the segment; rpg <= 0:
- * out row goff + m). */
-typedef struct {
-  const void *W;
-  const float *bias;
-  int64_t a_row0, M;
-  int64_t rpg, gstride, goff;
-} dsvt_gemm_seg;
-
-/* Grouped GEMM: up to 4 row segments of one A and one out buffer, each with its own weights and
- * output row map, in ONE launch of the 256 x 256 kernel (bf16; EPI_BIAS / EPI_BIAS_GELU with a
- * bf16 output, EPI_BIAS_RESID in place).  The same Linear of the teacher's and the student's
- * backbone calls of one DINO step (models/timesformer.py:63-64, 71, 83, 133, 41-52 under
- * train_ssl.py:523-527; identical shapes, different weights) then share one set of tile
- * rounds.  `segs` is a HOST array.  Other dtypes / shapes run one dsvt_gemm_fwd per segment
- * (same results). */
-int dsvt_gemm_grouped_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, int64_t ldw, void *out,
-                          int64_t ldo, int64_t N, int64_t K, int nseg, const dsvt_gemm_seg *segs, void *stream);
-
-/* dsvt_gemm_fwd with a caller-owned scratch: bf16 projections whose 256 x 256 tiles leave a
- * partly filled last round of workgroups run stream-K -- the tiles x K-steps are split evenly
- * over the grid, partial tiles meet in the workspace and the last workgroup to finish one runs
- * its epilogue (deterministic: partial sums added in a fixed order).  Other shapes / dtypes
- * take the dsvt_gemm_fwd kernels.  workspace >= dsvt_workspace_bytes(DSVT_WS_GEMM_SK, ...),
- * 256-byte aligned, ZERO-FILLED before its first use (the calls leave it that way); calls that
- * may run concurrently need separate workspaces.  Replaces the same nn.Linear calls as
- * dsvt_gemm_fwd (models/timesformer.py:63, 71, 41-52, 127-135). */
-int dsvt_gemm_sk_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
-                     int64_t ldw, const float *bias, void *out, int64_t ldo, int64_t M, int64_t N, int64_t K,
-                     int64_t rpg, int64_t gstride, int64_t goff, void *workspace, int64_t workspace_bytes,
-                     void *stream);
-
 /* Out-of-place residual GEMM (training forward): x_out[row(m)] = x_in[row(m)] + A[m] . W^T +
  * bias, fp32 x_in / x_out with the same row map and row stride ldx, rows of x_out outside the
  * map untouched.  The reference's `x = x + drop_path(sublayer(norm(x)))`
@@ -136,36 +107,41 @@ int dsvt_gemm_resid_scaled_fwd(int dtype, const void *A, int64_t lda, const void
                                const float *bias_row_scale, const float *x_in, float *x_out, int64_t ldx, int64_t M,
                                int64_t N, int64_t K, void *stream);
 
-/* The residual add of a sub-layer and the LayerNorm that reads the updated rows next, as one
- * streaming pass (models/timesformer.py:133-135, 181, 184 `x = x + f(x)`, then norm1 :105,
- * norm2 :112/184 or the next block's temporal_norm1 :99), C = 768.  The sub-layer GEMM writes
- * d = f(x) with a plain bias epilogue (dsvt_gemm_fwd, DSVT_EPI_BIAS); per X row r (clips of L
- * rows, row 0 of a clip = CLS):
- *   X[r] += d[drow(r)]                 dmode 0: none; DSVT_ROWLN_X: drow = r;
- *                                      DSVT_ROWLN_COMPACT: the patch-row index (r/L)*(L-1) + r%L - 1
- *                                      (CLS rows have none: the temporal branch)
- *   y[yrow(r)] = LayerNorm(X[r])*gamma + beta   ymode, same three layouts (0: no y)
- * x fp32 [rows, 768]; d / y in d_dtype / y_dtype (DSVT_BF16 / DSVT_F32); rows a multiple of L. */
-int dsvt_add_layernorm_fwd(int d_dtype, int y_dtype, float *x, const void *d, void *y, const float *gamma,
-                           const float *beta, int64_t rows, int64_t C, int64_t L, int dmode, int ymode,
-                           float eps, void *stream);
-
-/* K7 + K3 fused, bf16 only, N = 768 (ViT-B): the residual projections attn.proj / temporal_fc /
- * mlp.fc2 with their residual add (models/timesformer.py:133-135, 181, 184) and the LayerNorm
- * that reads the updated rows next (norm1 :105, norm2 :112/184, the next block's
- * temporal_norm1 :99), in one full-row kernel:
- *   X[row(m)] += A[m] . W^T + bias        m < M; row(m) = map (rpg, gstride, goff); X fp32, ld 768
- *   Y[yrow] = LayerNorm(X[row(m)])*gamma + beta   (bf16, ld 768)
- * ymode DSVT_ROWLN_NONE: no Y;  DSVT_ROWLN_X: yrow = row(m);  DSVT_ROWLN_COMPACT: yrow = the
- * patch-row index of X row r in clips of L tokens ((r/L)*(L-1) + r%L - 1; CLS rows, r%L == 0,
- * get none).  A [M, K] bf16 (lda), W [768, K] bf16 (ldw), K % 128 == 0, A and W < 4 GiB. */
-#define DSVT_ROWLN_NONE 0
-#define DSVT_ROWLN_X 1
-#define DSVT_ROWLN_COMPACT 2
-int dsvt_gemm_resid_ln_fwd(const void *A, int64_t lda, const void *W, int64_t ldw, const float *bias,
-                           float *X, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride,
-                           int64_t goff, const float *gamma, const float *beta, float eps, void *Y,
-                           int ymode, int64_t L, void *stream);
+/* ------------------------------------------------------------------------------------------
+ * LayerNorm folded into the GEMM that reads it (bf16, C = 768): norm1 -> attn.qkv, temporal_norm1
+ * -> temporal_attn.qkv, norm2 -> mlp.fc1 (models/timesformer.py:127/131, :159, :184).  With
+ * W' = W * gamma and mu / rstd the row's statistics,
+ *   LayerNorm(x) . W^T + b = rstd * (x . W'^T - mu * sum_k W'[n, k]) + (b + W . beta),
+ * so the GEMM reads the bf16 copy of the fp32 token row directly and applies the affine in its
+ * epilogue; the row statistics come as LN_PARTS = 12 float2 (sum x, sum x^2) partials per row
+ * (one per 64-column slab), written by the residual GEMM that produced the row
+ * (dsvt_gemm_resid_stats_fwd: attn.proj / temporal_fc / mlp.fc2 + residual, :133-135, 181, 184)
+ * or, for the rows a forward starts with, by dsvt_ln_stats_fwd.  No LayerNorm pass and no
+ * normalized copy of the rows in HBM.
+ * ------------------------------------------------------------------------------------------ */
+#define DSVT_LN_FOLD_C 768
+#define DSVT_LN_PARTS 12
+/* Wf [N, K] bf16 = W * gamma (per column k), wsum[N] = row sums of Wf, bias_f[N] = bias + W . beta
+ * (bias nullable).  W [N, K] fp32 (nn.Linear weight), gamma / beta [K] (the nn.LayerNorm before it). */
+int dsvt_ln_fold_weights(const float *W, const float *gamma, const float *beta, const float *bias, void *Wf,
+                         float *wsum, float *bias_f, int64_t N, int64_t K, void *stream);
+/* xb [rows, 768] bf16 = x, stats [rows, 12] float2 = the partials of x [rows, 768] fp32. */
+int dsvt_ln_stats_fwd(const float *x, void *xb, float *stats, int64_t rows, int64_t C, void *stream);
+/* The residual GEMM X[row(m)] += A[m] . W^T + bias (as dsvt_gemm_fwd, DSVT_EPI_BIAS_RESID, bf16,
+ * N = ldx = 768) that also writes, for every row it updates, xb[row] = bf16(X[row]) and
+ * stats[row][12] (the partials dsvt_gemm_lnx_fwd reads). */
+int dsvt_gemm_resid_stats_fwd(const void *A, int64_t lda, const void *W, int64_t ldw, const float *bias, float *X,
+                              void *xb, float *stats, int64_t ldx, int64_t M, int64_t N, int64_t K, int64_t rpg,
+                              int64_t gstride, int64_t goff, void *stream);
+/* out[row(m)] = epilogue(LayerNorm(x[a_row(m)]) . W^T + b) with xb = bf16(x) rows (ldxb) read
+ * through the A row map a_row(m) = (m / a_rpg) * a_gstride + a_goff + m % a_rpg (a_rpg <= 0:
+ * identity), stats[a_row(m)] their partials, Wf / wsum / bias_f from dsvt_ln_fold_weights;
+ * epilogue DSVT_EPI_BIAS or DSVT_EPI_BIAS_GELU, bf16 out, K = 768, N % 256 == 0.  Replaces
+ * dsvt_ln_gemm_fwd on the bf16 hot path (same results up to the bf16 rounding of x and W*gamma). */
+int dsvt_gemm_lnx_fwd(int epilogue, const void *xb, int64_t ldxb, int64_t a_rpg, int64_t a_gstride, int64_t a_goff,
+                      const float *stats, float eps, const void *Wf, const float *wsum, const float *bias_f, void *out,
+                      int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
+                      void *stream);
 
 /* K3: LayerNorm(eps) over rows of fp32 X read through a row map, written compact
  * (rows x C) in dtype (or fp32 when out_f32 bit 0); with out_f32 bit 1 the output rows follow
@@ -488,26 +464,7 @@ int dsvt_video_augment(const void *frames, int frames_u8, int64_t T_in, int64_t 
  * frame_selection_loader.py:166 / any frame gather); rows <= 65535. */
 int dsvt_gather_rows(const void *src, int64_t row_bytes, const int32_t *idx, int64_t rows, void *dst, void *stream);
 
-/* Tuning knob (benchmarking only): bf16 GEMM kernel choice. 0 = automatic (default),
- * 1 = 128x128 / 4-wave kernel, 3-6 / 9-13 = 256x128 and 256x256 staged / persistent kernels,
- * 20 = 256x256 phase-interleaved persistent kernel (21-29: its diagnostic builds), 33 / 40 / 41:
- * X-streamed residual / stream-K / tail split, 50 = K-split skinny kernel.
- * Per calling thread. */
-int dsvt_set_gemm_variant(int variant);
-/* Call-site scope (on = 1 / off = 0) for the following GEMM launches of the calling thread: the
- * few-row GEMMs of the CLS-only last block (timesformer.py:181-184 on the CLS rows) and of the
- * DINOHead MLP (vision_transformer.py DINOHead.forward) take the K-split skinny kernel where it is
- * eligible, whatever their row count (so a batch split over streams stays bitwise equal to the
- * whole batch).  Not a reference interface: a dsvt scheduling hint. */
-int dsvt_set_gemm_skinny(int on);
-/* Tuning knob (benchmarking / tests only): bf16 short-sequence attention kernel. 0 = automatic,
- * 1 = 16-key-tile x 4 waves, 2 = 13 x 8 waves, 3 = 13 x 4 waves, 4 = streaming flash kernel
- * (5, 6, 9, 10: diagnostic builds; 11: the pipelined persistent kernel).
- * Per calling thread. */
-int dsvt_set_attn_variant(int variant);
-/* Tuning knob (tests only): attention backward, 0 = automatic (bf16 MFMA kernel for sequences
- * <= 256), 1 = the generic two-pass VALU kernels.  Process-global. */
-int dsvt_set_attn_bwd_variant(int variant);
+/* Kernel-choice overrides for tools and tests: include/dsvt_debug.h (not part of this interface). */
 
 /* Measurement probe: when enabled, every launch of a family in `mask` is bracketed by a
  * pair of hipEvents on its own stream (diagnostic; not thread-safe). */

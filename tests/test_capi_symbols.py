@@ -10,10 +10,11 @@ import pytest
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "dsvt.h")
+DEBUG_HEADER = os.path.join(ROOT, "include", "dsvt_debug.h")
 
 
-def header_functions():
-    src = open(HEADER).read()
+def header_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(dsvt_\w+)\s*\(", src)))
 
@@ -25,24 +26,32 @@ def L():
 
 
 def test_header_symbols_exported(L):
-    names = header_functions()
+    names = header_functions() + header_functions(DEBUG_HEADER)
     assert len(names) >= 20
     for n in names:
         assert hasattr(L, n), n
 
 
 def test_python_binding_covers_header():
-    from dsvt._lib import SIGNATURES
+    from dsvt._lib import DEBUG_SIGNATURES, SIGNATURES
     assert sorted(SIGNATURES) == header_functions()
+    assert sorted(DEBUG_SIGNATURES) == header_functions(DEBUG_HEADER)
+
+
+def test_hot_path_header_has_no_mutable_knobs():
+    """The drop-in header holds no setter whose effect a later hot-path call depends on (the
+    kernel-choice overrides live in dsvt_debug.h; the few-row choice is a per-call flag)."""
+    assert not [n for n in header_functions() if n.startswith("dsvt_set_")]
 
 
 def test_binding_arity_matches_header():
-    from dsvt._lib import SIGNATURES
-    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
-    for name, (_, args) in SIGNATURES.items():
-        m = re.search(r"\b%s\s*\(([^)]*)\)" % name, src)
-        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
-        assert len(params) == len(args), (name, len(params), len(args))
+    from dsvt._lib import DEBUG_SIGNATURES, SIGNATURES
+    for path, sigs in ((HEADER, SIGNATURES), (DEBUG_HEADER, DEBUG_SIGNATURES)):
+        src = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+        for name, (_, args) in sigs.items():
+            m = re.search(r"\b%s\s*\(([^)]*)\)" % name, src)
+            params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+            assert len(params) == len(args), (name, len(params), len(args))
 
 
 def test_version_and_workspace(L):
@@ -59,16 +68,23 @@ def test_validation_rejects_before_launch(L):
     # K not a multiple of 64 (bf16)
     rc = L.dsvt_gemm_fwd(_lib.BF16, 0, 0, fake, 100, fake, 100, None, fake, 64, 16, 64, 100, 0, 0, 0, None)
     assert rc == 1 and b"multiple of 64" in L.dsvt_last_error()
-    # grouped GEMM: segment count, per-segment shape checks
-    segs = (_lib.GemmSeg * 2)(_lib.GemmSeg(256, None, 0, 100, 0, 0, 0), _lib.GemmSeg(256, None, 100, 0, 0, 0, 0))
-    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 768, 768, fake, 768, 768, 768, 0, segs, None)
-    assert rc == 1 and b"nseg" in L.dsvt_last_error()
-    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 768, 768, fake, 768, 768, 768, 5, segs, None)
-    assert rc == 1 and b"nseg" in L.dsvt_last_error()
-    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 768, 768, fake, 768, 768, 768, 2, segs, None)
-    assert rc == 1 and b"segment 1" in L.dsvt_last_error()
-    rc = L.dsvt_gemm_grouped_fwd(_lib.BF16, 0, 0, fake, 100, 100, fake, 768, 768, 100, 1, segs, None)
-    assert rc == 1 and b"multiple of 64" in L.dsvt_last_error()
+    # LayerNorm-folded GEMM: K must be 768, N a multiple of 256, stats / wsum required
+    rc = L.dsvt_gemm_lnx_fwd(0, fake, 512, 0, 0, 0, fake, ctypes.c_float(1e-6), fake, fake, fake, fake, 768, 100, 768,
+                             512, 0, 0, 0, None)
+    assert rc == 1 and b"K must be 768" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_lnx_fwd(0, fake, 768, 0, 0, 0, fake, ctypes.c_float(1e-6), fake, fake, fake, fake, 768, 100, 640,
+                             768, 0, 0, 0, None)
+    assert rc == 1 and b"multiple of 256" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_lnx_fwd(0, fake, 768, 0, 0, 0, None, ctypes.c_float(1e-6), fake, fake, fake, fake, 768, 100, 512,
+                             768, 0, 0, 0, None)
+    assert rc == 1 and b"stats" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_lnx_fwd(2, fake, 768, 0, 0, 0, fake, ctypes.c_float(1e-6), fake, fake, fake, fake, 768, 100, 512,
+                             768, 0, 0, 0, None)
+    assert rc == 1 and b"BIAS or BIAS_GELU" in L.dsvt_last_error()
+    rc = L.dsvt_gemm_resid_stats_fwd(fake, 768, fake, 768, None, fake, fake, fake, 512, 100, 512, 768, 0, 0, 0, None)
+    assert rc == 1 and b"768" in L.dsvt_last_error()
+    rc = L.dsvt_ln_stats_fwd(fake, fake, fake, 10, 512, None)
+    assert rc == 1 and b"768" in L.dsvt_last_error()
     # head_dim must be 64
     rc = L.dsvt_attn_temporal_fwd(_lib.BF16, fake, fake, 4, 8, 3, 32, ctypes.c_float(0.1), None)
     assert rc == 1 and b"head_dim" in L.dsvt_last_error()

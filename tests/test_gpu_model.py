@@ -520,51 +520,40 @@ def test_capture_split_streams():
         assert torch.equal(o, r), (o - r).abs().max().item()
 
 
-@pytest.mark.parametrize("variant,mode,tail", [(20, "1", False), (0, "1", False), (20, "1", True), (20, "2", True),
-                                               (20, "2", False), (20, "3", True), (20, "4", True)])
-def test_grouped_forward_bitwise(variant, mode, tail, monkeypatch):
-    """dsvt.grouped: the three backbone calls of a DINO step (teacher on 2 global crops, student on
-    2 global + 2 local) as one lockstep forward with every Linear a grouped launch
-    (dsvt_gemm_grouped_fwd, a row segment per call with its own weights) against the same calls
-    run separately (DSVT_GROUPED=0).  With the separate calls' GEMMs on the same 256x256 kernel
-    (variant 20) the student / teacher logits are BITWISE equal; with the automatic kernel choice
-    (small separate calls take the 128x128 kernel) within BF16_TOL.  Also fp32 parity mode (the
-    grouped op's per-segment fallback) within 1e-5.  mode "2" (DSVT_GROUPED=2) groups only the
-    global-crop calls and runs the local one beside them, mode "3" runs three concurrent grouped
-    forwards over balanced shares of every call's clips; tail: the CLS-only last block on both
-    sides (the per-call CLS kernels are the separate calls' own, so still bitwise)."""
-    from dsvt import _lib
-    from dsvt.utils import MultiCropWrapper, dino_forward
-    from dsvt.vision_transformer import DINOHead
-    cfg = dict(embed_dim=768, num_heads=12, depth=2, img_size=64, num_frames=8)
-
-    def net(seed, dtype):
-        m = tsf(P.timesformer_state(seed, **cfg), dtype, **cfg)
-        hd = DINOHead(768, 4096)
-        hd.load_state_dict({k: torch.from_numpy(v) for k, v in P.dino_head_state(seed + 1, 768, 4096).items()})
-        hd = hd.cuda()
-        hd.dsvt_dtype = dtype
-        return MultiCropWrapper(m, hd)
-    crops = [cu(P.clip(1601 + i, (3, 3, 8, 64, 64))) for i in range(2)] + \
-            [cu(P.clip(1611 + i, (3, 3, 8, 32, 32))) for i in range(2)]
-    for dtype in (torch.bfloat16, torch.float32):
-        student, teacher = net(1701, dtype), net(1801, dtype)
-        for m in (student, teacher):
-            m.backbone.cls_tail = tail
-        outs = {}
-        _lib.call("dsvt_set_gemm_variant", variant)
-        try:
-            for grouped in (mode, "0"):
-                monkeypatch.setenv("DSVT_GROUPED", grouped)
-                with torch.no_grad():
-                    s, t = dino_forward(student, teacher, crops, concurrent=False)
-                torch.cuda.synchronize()
-                outs[grouped] = (s.clone(), t.clone())
-        finally:
-            _lib.call("dsvt_set_gemm_variant", 0)
-        for a, b in zip(outs[mode], outs["0"]):
-            assert torch.isfinite(a).all()
-            if dtype == torch.bfloat16 and variant == 20:
-                assert torch.equal(a, b), "grouped forward differs from the separate calls"
-            else:
-                assert rel(a.cpu(), b.cpu()) < (BF16_TOL if dtype == torch.bfloat16 else 1e-5)
+@pytest.mark.parametrize("tail", [True, False])
+def test_ln_fold_golden(base_sd, tail):
+    """VisionTransformer.ln_fold (bf16, C = 768): every LayerNorm folded into the GEMM that reads it
+    (dsvt_gemm_lnx_fwd on the bf16 token rows + their statistics kept by dsvt_gemm_resid_stats_fwd)
+    forced on at the reference goldens' small shapes -- divided 8x224^2, 96^2, 32^2 with get_all,
+    T = 3 and T = 30, get_attn, joint and space-only -- within BF16_TOL, with and without the
+    CLS-only last block; and against the LayerNorm-pass path (ln_fold False) at 3 bench clips and 6
+    local crops within 1e-2."""
+    f = g("base_div")
+    m = tsf(base_sd, torch.bfloat16)
+    m.cls_tail = tail
+    errs = {}
+    with torch.no_grad():
+        m.ln_fold = True
+        errs["small"] = rel(m(cu(P.clip(201, (2, 3, 8, 32, 32)))).cpu(), f["cls_small"])
+        errs["all_small"] = rel(m.forward_features(cu(P.clip(201, (2, 3, 8, 32, 32))), get_all=True).cpu(),
+                                f["all_small"])
+        errs["224"] = rel(m(cu(P.clip(202, (1, 3, 8, 224, 224)))).cpu(), f["cls_224"])
+        errs["96"] = rel(m(cu(P.clip(203, (1, 3, 8, 96, 96)))).cpu(), f["cls_96"])
+        errs["t3"] = rel(m(cu(P.clip(204, (1, 3, 3, 224, 224)))).cpu(), f["cls_t3"])
+        errs["t30"] = rel(m(cu(P.clip(205, (1, 3, 30, 224, 224)))).cpu(), f["cls_t30"])
+        errs["attn"] = rel(m.forward_features(cu(P.clip(206, (1, 3, 8, 64, 64))), get_attn=True).cpu(), f["attn_64"])
+        for attn, seed, name, clip in (("joint_space_time", 3, "base_joint", (1, 3, 4, 64, 64)),
+                                       ("space_only", 4, "base_sonly", (2, 3, 4, 64, 64))):
+            mo = tsf(P.timesformer_state(seed, attention_type=attn), torch.bfloat16, attention_type=attn)
+            mo.ln_fold, mo.cls_tail = True, tail
+            errs[attn] = rel(mo(cu(P.clip(301 if seed == 3 else 401, clip))).cpu(), g(name)["cls_small"])
+        for x in (P.clip(211, (3, 3, 8, 224, 224)), P.clip(212, (6, 3, 8, 96, 96))):
+            m.ln_fold = True
+            y1 = m(cu(x)).clone()
+            m.ln_fold = False
+            y0 = m(cu(x)).clone()
+            errs["vs_ln_pass_%d" % x.shape[-1]] = rel(y1.cpu(), y0.cpu())
+            assert torch.isfinite(y1).all()
+    print("ln_fold tail=%s" % tail, errs)
+    assert max(v for k, v in errs.items() if not k.startswith("vs_")) < BF16_TOL, errs
+    assert max(v for k, v in errs.items() if k.startswith("vs_")) < 1e-2, errs
