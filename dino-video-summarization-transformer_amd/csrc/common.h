@@ -49,6 +49,15 @@ __device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
 }
 __device__ __forceinline__ int pair_off(int g) { return ((g & 1) << 4) | ((g >> 1) << 3); }
 
+// sum over a lane's four 16-lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48) by two VALU permlane
+// swaps (no LDS traffic); every lane gets the same bits: (x0 + x2) + (x1 + x3) in one order
+__device__ __forceinline__ float sum_lane_groups(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Bias of a wave's 64 output columns cbase .. cbase+63 (cbase wave-uniform) as the lane's
 // 4 x float4 (fragment j, columns cbase + 16j + 4g .. +3).  Read through the constant address
 // space, i.e. SCALAR loads counted on lgkmcnt: a vector load here would sit on vmcnt behind

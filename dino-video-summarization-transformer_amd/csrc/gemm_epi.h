@@ -415,8 +415,11 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
 // row's mean / rstd from its LN_PARTS partials (written by whoever produced the row):
 //   acc <- rstd * (acc - mu * wsum[n]) + bias[n]          (bias = b + W . beta, fp32)
 // = LayerNorm(x) . W^T + b up to the bf16 roundings of x and W * gamma.  Lane (r16, g) sums the
-// partials 3g .. 3g + 2 of its rows and the four lane groups combine by two butterflies (every
-// lane gets the same bits: IEEE addition commutes).  Rows past M are clamped (never stored).
+// partials 3g .. 3g + 2 of its rows and the four lane groups combine by two permlane swaps
+// (sum_lane_groups: every lane gets the same bits).  Rows past M are clamped (never stored).
+#ifndef DSVT_LNX_ABL
+#define DSVT_LNX_ABL 0   // diagnostic builds (tools/build_ab.sh): 1 no stats loads, 2 no wsum / bias loads
+#endif
 template <int MI, int NJ>
 __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
                                           int r16, int g) {
@@ -435,16 +438,14 @@ __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ
       const uint32_t xr = (m / a_rpg) * a_gs + a_go + m % a_rpg;   // rows < 2^31 (host-checked)
       const float2* sp = reinterpret_cast<const float2*>(p.ln_stats) + (uint64_t)(xr * LN_PARTS + 3 * g);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) st[ii][k] = sp[k];
+      for (int k = 0; k < 3; ++k) st[ii][k] = DSVT_LNX_ABL == 1 ? make_float2(xr * 1e-3f, k * 1e-3f) : sp[k];
     }
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
       float s = (st[ii][0].x + st[ii][1].x) + st[ii][2].x;
       float q = (st[ii][0].y + st[ii][1].y) + st[ii][2].y;
-      s += __shfl_xor(s, 16, 64);
-      q += __shfl_xor(q, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 32, 64);
+      s = sum_lane_groups(s);
+      q = sum_lane_groups(q);
       const float m_ = s * invk;
       const float var = fmaxf(q * invk - m_ * m_, 0.f);
       rs[i0 + ii] = 1.0f / sqrtf(var + p.ln_eps);
@@ -455,8 +456,8 @@ __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int64_t n = cbase + j * 16 + 4 * g;
-    const float4 w4 = *reinterpret_cast<const float4*>(p.ln_wsum + n);
-    const float4 b4 = *reinterpret_cast<const float4*>(p.bias + n);
+    const float4 w4 = DSVT_LNX_ABL == 2 ? make_float4(n * 1e-3f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(p.ln_wsum + n);
+    const float4 b4 = DSVT_LNX_ABL == 2 ? make_float4(0.f, n * 1e-3f, 0.f, 0.f) : *reinterpret_cast<const float4*>(p.bias + n);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       acc[i][j][0] = fmaf(rs[i], acc[i][j][0], fmaf(mu[i], w4.x, b4.x));
@@ -477,7 +478,10 @@ template <int MI, int NJ, bool FULL>
 __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
                                                  int r16, int g) {
   static_assert(NJ == 4, "64-column wave slab");
-  constexpr int W = 2;
+#ifndef DSVT_STATS_W
+#define DSVT_STATS_W 3
+#endif
+  constexpr int W = DSVT_STATS_W;
   const bool ident = p.rpg >= p.M && p.goff == 0;
   const int part = (int)(cbase >> 6);
   auto orow_of = [&](int i) -> int64_t {
@@ -506,10 +510,8 @@ __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)
       q += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
     }
     if (i + W < MI) load_row(i + W);
-    s += __shfl_xor(s, 16, 64);
-    q += __shfl_xor(q, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    q += __shfl_xor(q, 32, 64);
+    s = sum_lane_groups(s);
+    q = sum_lane_groups(q);
     const bool ok = FULL || rbase + i * 16 + r16 < p.M;
     if (ok) {
       float* dst = (float*)p.out + orow * p.ldo + cbase + 4 * g;
