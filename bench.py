@@ -425,9 +425,11 @@ def other_configs(args, device):
     scorer = FrameScorer(fm, local_clip_size=3, global_clip_size=30)
     video = torch.randn(64, 3, 224, 224, device=device)
     with torch.no_grad():
-        t = timed(lambda: scorer.score(video), reps=2, warm=1)
+        te = timed(lambda: scorer.score(video), reps=2, warm=1)
+        t = graph_timed(lambda: scorer.score(video), reps=10)
     gf = (vit_fwd_flops(3, 224) + vit_fwd_flops(30, 224)) / 1e9
     res["frame_score"] = {"value": round(64 / t, 2), "unit": "frames/s", "frames": 64, "views": "local 3 / global 30",
+                          "launch": "hip_graph (10 replays)", "eager_value": round(64 / te, 2),
                           "gflop_per_frame": round(gf, 1), "tflops": round(64 * gf / t / 1e3, 1)}
     return res
 

@@ -546,7 +546,8 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
   }
   // contiguous sequences (joint space-time, space-only): the LDS-DMA flash kernel
   // (attn_flash.hip); variant 8 keeps the register-staged kernel below (A/B, tests)
-  if (v != 8 && attn_flash_ok(dtype, p)) return launch_attn_flash(p, s);
+  // variant 11 / 12: the flash kernel with 64 / 128 queries per workgroup forced
+  if (v != 8 && attn_flash_ok(dtype, p)) return launch_attn_flash(p, s, v == 11 ? 1 : v == 12 ? 2 : 0);
   dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)(p.nb * p.tin));
   if (dtype == 0) attn_seq_bf16<<<grid, 256, 0, s>>>(p);
   else attn_seq_f32<<<grid, 64, 0, s>>>(p);
@@ -863,9 +864,12 @@ __global__ __launch_bounds__(256) void attn_cls_part_kernel(const TI* __restrict
   }
 }
 
+// seq_scale (nullable): frame t's output of clip b scaled by seq_scale[b * T + t] before the mean --
+// training DropPath over the (b, t) sequences of the spatial branch (timesformer.py:159)
 template <typename TI>
 __global__ __launch_bounds__(256) void attn_cls_merge_kernel(const float* __restrict__ part, TI* __restrict__ out,
-                                                             int64_t ld_out, int64_t B, int T, int nchunk, int heads) {
+                                                             int64_t ld_out, int64_t B, int T, int nchunk, int heads,
+                                                             const float* __restrict__ seq_scale) {
   const int64_t C = (int64_t)heads * 64;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * C) return;
@@ -882,7 +886,7 @@ __global__ __launch_bounds__(256) void attn_cls_merge_kernel(const float* __rest
       l = fmaf(pp[k * 66 + 65], f, l);
       o = fmaf(pp[k * 66 + d], f, o);
     }
-    m += o / l;
+    m += seq_scale ? seq_scale[b * T + t] * (o / l) : o / l;
   }
   out[b * ld_out + hc] = Elem<TI>::from_f(m / (float)T);
 }
@@ -892,7 +896,7 @@ int64_t attn_cls_ws_bytes(int64_t nseq, int64_t heads, int64_t seqlen) {
 }
 
 hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
-                           int64_t heads, float scale, float* ws, hipStream_t s) {
+                           int64_t heads, float scale, float* ws, hipStream_t s, const float* seq_scale) {
   const int64_t seqlen = 1 + (L - 1) / T;
   const int nchunk = (int)((seqlen + ATTN_CLS_CHUNK - 1) / ATTN_CLS_CHUNK);
   const int64_t items = B * T * heads * nchunk;
@@ -900,12 +904,184 @@ hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out
   if (dtype == 0) {
     attn_cls_part_kernel<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)qkv, ws, items, L, (int)T, (int)seqlen, nchunk,
                                                     (int)heads, scale);
-    attn_cls_merge_kernel<bf16_t><<<g2, 256, 0, s>>>(ws, (bf16_t*)out, ld_out, B, (int)T, nchunk, (int)heads);
+    attn_cls_merge_kernel<bf16_t><<<g2, 256, 0, s>>>(ws, (bf16_t*)out, ld_out, B, (int)T, nchunk, (int)heads,
+                                                     seq_scale);
   } else {
     attn_cls_part_kernel<float><<<g1, 256, 0, s>>>((const float*)qkv, ws, items, L, (int)T, (int)seqlen, nchunk,
                                                    (int)heads, scale);
-    attn_cls_merge_kernel<float><<<g2, 256, 0, s>>>(ws, (float*)out, ld_out, B, (int)T, nchunk, (int)heads);
+    attn_cls_merge_kernel<float><<<g2, 256, 0, s>>>(ws, (float*)out, ld_out, B, (int)T, nchunk, (int)heads,
+                                                    seq_scale);
   }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- CLS-query attention backward
+// The training form of the CLS-only last block (dsvt.training, VisionTransformer.cls_tail): only
+// the CLS query of every frame sequence (b, t) is evaluated, o_cls[b] = (1/T) sum_t s_bt O_bt
+// (s = the DropPath scale of the sequence, 1 without), so the backward of that attention is one
+// query per (b, t, head):
+//   dO = s_bt / T * do_cls[b];  P = softmax(scale q.k_j);  dP_j = dO.v_j;  D = sum_j P_j dP_j;
+//   dS_j = P_j (dP_j - D);  dq = scale sum_j dS_j k_j;  dk_j = scale dS_j q;  dv_j = P_j dO.
+// One wave per (b, t, head) (lane layout of attn_cls_part_kernel: 8 groups of 8 lanes, a group one
+// key row per step, a lane 8 of its 64 dims).  The patch rows of frame t belong to that sequence
+// only: their dk / dv go straight to dqkv (bf16 / fp32 storage) and their dq is written ZERO (the
+// patch rows' queries do not exist in the CLS-only block).  The CLS row is in all T sequences: its
+// dq, dk, dv partials go to ws[(b*T + t)][3C] (fp32), summed over t in order by
+// attn_cls_bwd_reduce_kernel into the CLS row of dqkv (deterministic).  Keys <= ATTN_CLS_BWD_MAX.
+constexpr int ATTN_CLS_BWD_MAX = 512;
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void attn_cls_bwd_kernel(const TI* __restrict__ qkv, const TO* __restrict__ dout,
+                                                           TI* __restrict__ dqkv, float* __restrict__ ws,
+                                                           const float* __restrict__ seq_scale, int64_t items,
+                                                           int64_t L, int T, int seqlen, int heads, float scale) {
+  __shared__ float sp[4][ATTN_CLS_BWD_MAX], sdp[4][ATTN_CLS_BWD_MAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t item = (int64_t)blockIdx.x * 4 + w;        // (b * T + t) * heads + h
+  if (item >= items) return;                                // wave-uniform; no block barrier below
+  const int h = (int)(item % heads);
+  const int64_t bt = item / heads;
+  const int t = (int)(bt % T);
+  const int64_t b = bt / T;
+  const int grp = lane >> 3, c = lane & 7;
+  const int64_t C = (int64_t)heads * 64, ld = 3 * C;
+  const TI* base = qkv + b * L * ld;
+  auto key_row = [&](int j) -> int64_t { return j == 0 ? 0 : 1 + (int64_t)(j - 1) * T + t; };
+  float q[8], dO[8];
+  load8f(base + h * 64 + c * 8, q);
+  {
+    float d[8];
+    load8f(dout + b * C + h * 64 + c * 8, d);
+    const float f = (seq_scale ? seq_scale[bt] : 1.0f) / (float)T;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dO[i] = d[i] * f;
+  }
+  float* s = sp[w];
+  float* dp = sdp[w];
+  // pass 1: scores and dP for every key (a group per key row, 8 rows per step)
+  float mx = -INFINITY;
+  for (int j0 = 0; j0 < seqlen; j0 += 8) {
+    const int j = j0 + grp;
+    const int jl = j < seqlen ? j : seqlen - 1;
+    float k[8], v[8];
+    load8f(base + key_row(jl) * ld + C + h * 64 + c * 8, k);
+    load8f(base + key_row(jl) * ld + 2 * C + h * 64 + c * 8, v);
+    float a = 0.f, e = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a = fmaf(q[i], k[i], a);
+      e = fmaf(dO[i], v[i], e);
+    }
+    a += __shfl_xor(a, 1); a += __shfl_xor(a, 2); a += __shfl_xor(a, 4);
+    e += __shfl_xor(e, 1); e += __shfl_xor(e, 2); e += __shfl_xor(e, 4);
+    a *= scale;
+    if (j < seqlen) {
+      if (c == 0) { s[j] = a; dp[j] = e; }
+      mx = fmaxf(mx, a);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  float sum = 0.f;
+  for (int j = lane; j < seqlen; j += 64) {
+    const float e = __expf(s[j] - mx);
+    s[j] = e;
+    sum += e;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
+  const float inv = 1.0f / sum;
+  float D = 0.f;
+  for (int j = lane; j < seqlen; j += 64) {
+    const float pj = s[j] * inv;
+    s[j] = pj;
+    D = fmaf(pj, dp[j], D);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) D += __shfl_xor(D, o);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // pass 2: dk_j, dv_j of every key; dq accumulated per group
+  float dq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dq[i] = 0.f;
+  float* cw = ws + bt * ld;                                 // this sequence's CLS-row partials
+  for (int j0 = 0; j0 < seqlen; j0 += 8) {
+    const int j = j0 + grp;
+    if (j < seqlen) {                                       // group-uniform branch
+      const float pj = s[j], dsj = pj * (dp[j] - D);
+      float k[8];
+      load8f(base + key_row(j) * ld + C + h * 64 + c * 8, k);
+      float dk[8], dv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dq[i] = fmaf(dsj, k[i], dq[i]);
+        dk[i] = scale * dsj * q[i];
+        dv[i] = pj * dO[i];
+      }
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          cw[C + h * 64 + c * 8 + i] = dk[i];
+          cw[2 * C + h * 64 + c * 8 + i] = dv[i];
+        }
+      } else {
+        TI* dr = dqkv + (b * L + key_row(j)) * ld + h * 64 + c * 8;
+        store4(dr, 0.f, 0.f, 0.f, 0.f);
+        store4(dr + 4, 0.f, 0.f, 0.f, 0.f);
+        store4(dr + C, dk[0], dk[1], dk[2], dk[3]);
+        store4(dr + C + 4, dk[4], dk[5], dk[6], dk[7]);
+        store4(dr + 2 * C, dv[0], dv[1], dv[2], dv[3]);
+        store4(dr + 2 * C + 4, dv[4], dv[5], dv[6], dv[7]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dq[i] += __shfl_xor(dq[i], 8);
+    dq[i] += __shfl_xor(dq[i], 16);
+    dq[i] += __shfl_xor(dq[i], 32);
+  }
+  if (grp == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cw[h * 64 + c * 8 + i] = scale * dq[i];
+  }
+}
+
+// CLS row of clip b: dqkv[b * L][:] = sum over t (in order) of ws[b * T + t][:]
+template <typename TI>
+__global__ __launch_bounds__(256) void attn_cls_bwd_reduce_kernel(const float* __restrict__ ws, TI* __restrict__ dqkv,
+                                                                  int64_t B, int T, int64_t L, int64_t C3) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C3) return;
+  const int64_t b = i / C3, c = i % C3;
+  float v = 0.f;
+  for (int t = 0; t < T; ++t) v += ws[(b * T + t) * C3 + c];
+  dqkv[b * L * C3 + c] = Elem<TI>::from_f(v);
+}
+
+int64_t attn_cls_bwd_ws_bytes(int64_t nseq, int64_t heads) { return nseq * heads * 64 * 3 * 4; }
+
+hipError_t launch_attn_cls_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, float* ws,
+                               const float* seq_scale, int64_t B, int64_t T, int64_t L, int64_t heads, float scale,
+                               hipStream_t s) {
+  const int64_t seqlen = 1 + (L - 1) / T;
+  if (seqlen > ATTN_CLS_BWD_MAX) return hipErrorInvalidValue;
+  const int64_t items = B * T * heads, C3 = heads * 64 * 3;
+  const unsigned g1 = (unsigned)((items + 3) / 4), g2 = (unsigned)((B * C3 + 255) / 256);
+#define DSVT_CB(TI, TO) attn_cls_bwd_kernel<TI, TO><<<g1, 256, 0, s>>>((const TI*)qkv, (const TO*)dout, (TI*)dqkv, ws, \
+                                                                       seq_scale, items, L, (int)T, (int)seqlen,       \
+                                                                       (int)heads, scale)
+  if (dtype == 0) {
+    DSVT_CB(bf16_t, bf16_t);
+    attn_cls_bwd_reduce_kernel<bf16_t><<<g2, 256, 0, s>>>(ws, (bf16_t*)dqkv, B, (int)T, L, C3);
+  } else {
+    DSVT_CB(float, float);
+    attn_cls_bwd_reduce_kernel<float><<<g2, 256, 0, s>>>(ws, (float*)dqkv, B, (int)T, L, C3);
+  }
+#undef DSVT_CB
   return hipGetLastError();
 }
 

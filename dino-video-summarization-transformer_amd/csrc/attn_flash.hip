@@ -226,10 +226,20 @@ bool attn_flash_ok(int dtype, const AttnParams& p) {
          p.seqlen >= 1 && p.seqlen <= p.L && p.C >= 64 * p.heads && p.ld_qkv >= 3 * p.C;
 }
 
-hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s) {
-  constexpr int QT = 2;
-  dim3 grid((unsigned)((p.seqlen + 64 * QT - 1) / (64 * QT)), (unsigned)p.heads, (unsigned)p.nb);
-  attn_flash_bf16<QT><<<grid, 256, 0, s>>>(p);
+// qt: 0 = automatic -- 128 queries per workgroup (QT = 2) when that grid gives every CU two
+// workgroups, else 64 (QT = 1: twice the workgroups for the same keys).  Measured at L = 3137, 12
+// heads (tools/attn_joint_bench.py): one clip (300 workgroups at QT = 2) 77.0 vs 84.7 us, two
+// clips (600) 121.2 vs 113.2 us.
+hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s, int qt) {
+  const int64_t blocks2 = (p.seqlen + 127) / 128 * p.heads * p.nb;
+  if (qt == 0) qt = blocks2 >= 2 * 256 ? 2 : 1;
+  if (qt == 2) {
+    dim3 grid((unsigned)((p.seqlen + 127) / 128), (unsigned)p.heads, (unsigned)p.nb);
+    attn_flash_bf16<2><<<grid, 256, 0, s>>>(p);
+  } else {
+    dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)p.nb);
+    attn_flash_bf16<1><<<grid, 256, 0, s>>>(p);
+  }
   return hipGetLastError();
 }
 

@@ -141,6 +141,7 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     case DSVT_WS_AUGMENT: return up(augment_ws_bytes(M, N));                          // M = frames, N = size
     case DSVT_WS_WGRAD: return up(wgrad_workspace_floats(M, N, K) * 4);              // M = rows, N, K: G [N, K]
     case DSVT_WS_ATTN_CLS: return up(attn_cls_ws_bytes(M, N, K));                    // M = B*T, N = heads, K = keys
+    case DSVT_WS_ATTN_CLS_BWD: return up(attn_cls_bwd_ws_bytes(M, N));               // M = B*T, N = heads
     default: return -1;
   }
 }
@@ -375,6 +376,47 @@ int dsvt_attn_spatial_cls_fwd(int dtype, const void* qkv, void* out, int64_t ld_
   });
 }
 
+int dsvt_attn_spatial_cls_scaled_fwd(int dtype, const void* qkv, void* out, int64_t ld_out, const float* seq_scale,
+                                     int64_t B, int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                                     void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(seq_scale, "attn_spatial_cls_scaled: seq_scale is null");
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial_cls_scaled: bad dtype");
+  REQUIRE(qkv && out && aligned16(qkv), "attn_spatial_cls_scaled: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_spatial_cls_scaled: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_cls_scaled: need (L-1) %% T == 0");
+  const int64_t C = heads * 64;
+  REQUIRE(heads >= 1 && ld_out >= C, "attn_spatial_cls_scaled: need heads >= 1, ld_out >= C");
+  REQUIRE(workspace && aligned16(workspace) &&
+              workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_CLS, dtype, B * T, heads, 1 + (L - 1) / T),
+          "attn_spatial_cls_scaled: workspace too small");
+  const int64_t seqlen = 1 + (L - 1) / T;
+  const double flops = 4.0 * B * T * heads * (double)seqlen * 64;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, "dsvt_attn_spatial_cls_scaled_fwd", [&] {
+    return launch_attn_cls(dtype, qkv, out, ld_out, B, T, L, heads, scale, (float*)workspace, (hipStream_t)stream,
+                           seq_scale);
+  });
+}
+
+int dsvt_attn_spatial_cls_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, const float* seq_scale,
+                              int64_t B, int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                              void* workspace, int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_spatial_cls_bwd: bad dtype");
+  REQUIRE(qkv && dout && dqkv && aligned16(qkv) && aligned16(dout) && aligned16(dqkv),
+          "attn_spatial_cls_bwd: null/misaligned pointer");
+  REQUIRE(head_dim == 64, "attn_spatial_cls_bwd: head_dim must be 64");
+  REQUIRE(B > 0 && T > 0 && L > 1 && (L - 1) % T == 0, "attn_spatial_cls_bwd: need (L-1) %% T == 0");
+  REQUIRE(1 + (L - 1) / T <= 512, "attn_spatial_cls_bwd: at most 512 keys per sequence");
+  REQUIRE(workspace && aligned16(workspace) &&
+              workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_CLS_BWD, dtype, B * T, heads, 0),
+          "attn_spatial_cls_bwd: workspace too small");
+  const int64_t seqlen = 1 + (L - 1) / T;
+  const double flops = 8.0 * B * T * heads * (double)seqlen * 64;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, "dsvt_attn_spatial_cls_bwd", [&] {
+    return launch_attn_cls_bwd(dtype, qkv, dout, dqkv, (float*)workspace, seq_scale, B, T, L, heads, scale,
+                               (hipStream_t)stream);
+  });
+}
+
 int dsvt_attn_spatial_scaled_fwd(int dtype, const void* qkv, void* out, const float* seq_scale, int64_t B, int64_t T,
                                  int64_t L, int64_t heads, int64_t head_dim, float scale, void* workspace,
                                  int64_t workspace_bytes, void* stream) {
@@ -518,7 +560,7 @@ int dsvt_set_gemm_variant(int variant) {
 }
 
 int dsvt_set_attn_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 10, "attention variant must be 0-10");
+  REQUIRE(variant >= 0 && variant <= 12, "attention variant must be 0-12");
   set_attn_variant(variant);
   return 0;
 }

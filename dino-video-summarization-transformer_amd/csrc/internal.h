@@ -130,12 +130,17 @@ struct AttnParams {
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s);
 // flash attention over contiguous sequences (attn_flash.hip): joint space-time / space-only
 bool attn_flash_ok(int dtype, const AttnParams& p);
-hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s);
+hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s, int qt = 0);   // qt: queries / 64 per workgroup, 0 = auto
 void set_attn_variant(int v);
 // CLS query only of every spatial sequence, mean over frames -> out[b * ld_out + c] (attention.hip)
 int64_t attn_cls_ws_bytes(int64_t nseq, int64_t heads, int64_t seqlen);   // nseq = B*T
 hipError_t launch_attn_cls(int dtype, const void* qkv, void* out, int64_t ld_out, int64_t B, int64_t T, int64_t L,
-                           int64_t heads, float scale, float* ws, hipStream_t s);
+                           int64_t heads, float scale, float* ws, hipStream_t s, const float* seq_scale = nullptr);
+// its backward (training CLS-only last block): dqkv [B*L, 3C] from do_cls [B, C]; ws [B*T, 3C] fp32
+int64_t attn_cls_bwd_ws_bytes(int64_t nseq, int64_t heads);
+hipError_t launch_attn_cls_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, float* ws,
+                               const float* seq_scale, int64_t B, int64_t T, int64_t L, int64_t heads, float scale,
+                               hipStream_t s);
 hipError_t launch_attn_temporal(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T,
                                 int64_t heads, int64_t C, float scale, hipStream_t s);
 

@@ -17,7 +17,7 @@ TOKENS_NT, TOKENS_FRAME = 0, 1
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
 WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
 WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
-WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_ATTN_CLS = 10, 11, 12, 14
+WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_ATTN_CLS, WS_ATTN_CLS_BWD = 10, 11, 12, 14, 15
 
 _i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -46,6 +46,9 @@ SIGNATURES = {
     "dsvt_attn_spatial_probs_fwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
     "dsvt_attn_joint_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_attn_spatial_cls_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
+    "dsvt_attn_spatial_cls_scaled_fwd": (_i32, [_i32, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64,
+                                                _p]),
+    "dsvt_attn_spatial_cls_bwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
     "dsvt_frame_mean_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
     "dsvt_cast_fwd": (_i32, [_i32, _p, _p, _i64, _p]),
     "dsvt_dino_head_norm_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _f32, _p]),

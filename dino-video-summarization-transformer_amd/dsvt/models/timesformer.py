@@ -428,12 +428,20 @@ class VisionTransformer(nn.Module):
         # bitwise equal (the split changes the GEMMs' row counts, hence their kernels).
         from ..utils import fork_depth
         if k > 1 and not get_attn and clips[0].is_cuda and not self._grad_path() and fork_depth() == 0:
-            return self._forward_split(clips, B, k, shape, get_all, out)
+            return self._forward_split(clips, B, k, shape, get_all, out,
+                                       lnx=self._ln_fold_on(self.dsvt_dtype, B * self._rows_per_clip(shape)))
         srcs = [(c, None, c.shape[0]) for c in clips]
         return self._forward_sources(srcs, B, shape[1], shape[2], shape[3], shape[0], get_all, get_attn, out)
 
-    def _forward_split(self, clips, B, k, shape, get_all, out):
-        """forward_features on k clip chunks, one HIP stream each, writing into one output."""
+    def _rows_per_clip(self, shape):
+        _, T, H, W = shape
+        Np = (H // 16) * (W // 16)
+        return T * (1 + Np) if self.attention_type == 'space_only' else 1 + Np * T
+
+    def _forward_split(self, clips, B, k, shape, get_all, out, lnx=None):
+        """forward_features on k clip chunks, one HIP stream each, writing into one output.  lnx:
+        the whole batch's LayerNorm-folding choice, so every chunk runs the kernels the unsplit
+        batch would (bitwise-equal split)."""
         from ..utils import run_concurrent, stream_slot
         C, T, H, W = shape
         L = 1 + (H // 16) * (W // 16) * (1 if self.attention_type == 'space_only' else T)
@@ -455,7 +463,8 @@ class VisionTransformer(nn.Module):
             return srcs
 
         def job(b0, b1):
-            return lambda: self._forward_sources(chunk(b0, b1), b1 - b0, T, H, W, C, get_all, False, out[b0:b1])
+            return lambda: self._forward_sources(chunk(b0, b1), b1 - b0, T, H, W, C, get_all, False, out[b0:b1],
+                                                 lnx=lnx)
         self.prepare_weights()              # weight copies and index maps made before the fork
         self._indices(H // 16, W // 16, T, dev)
         run_concurrent([job(b0, b1) for b0, b1 in zip(bounds[:-1], bounds[1:])], dev,
@@ -485,7 +494,7 @@ class VisionTransformer(nn.Module):
         _, Cin, H, W = frames.shape
         return self._forward_sources([(frames, frame_index, B)], B, T, H, W, Cin, get_all, False, out)
 
-    def _forward_sources(self, srcs, B, T, H, W, Cin, get_all, get_attn, out):
+    def _forward_sources(self, srcs, B, T, H, W, Cin, get_all, get_attn, out, lnx=None):
         for src, _, _ in srcs:
             self._check_supported(src)
         if self._grad_path():
@@ -544,7 +553,8 @@ class VisionTransformer(nn.Module):
                 ctx.r1 = torch.empty(B * Np * T, C, device=dev, dtype=mode)
             nbytes = ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0)
             ctx.cls_ws = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
-        ctx.lnx = self._ln_fold_on(mode, ctx.rows)
+        ctx.lnx = self._ln_fold_on(mode, ctx.rows) if lnx is None else (lnx and mode == torch.bfloat16
+                                                                          and C == LN_FOLD_C)
         if ctx.lnx:             # the bf16 rows + LayerNorm statistics the folded GEMMs read
             ctx.xb = torch.empty(ctx.rows, C, device=dev, dtype=torch.bfloat16)
             ctx.st = torch.empty(ctx.rows, LN_PARTS, 2, device=dev, dtype=torch.float32)

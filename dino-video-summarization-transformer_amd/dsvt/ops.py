@@ -52,8 +52,9 @@ def gemm(a, w, bias, out, epilogue=_lib.EPI_BIAS, out_f32=False, rowmap=None, M=
     N = w.shape[0]
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
     epi = epilogue | (_lib.GEMM_FEW_ROWS if few_rows else 0)
+    ldo = out.stride(0) if out.dim() == 2 else out.shape[-1]      # a column slice of a wider tensor keeps its stride
     call("dsvt_gemm_fwd", _dt(mode), epi, int(out_f32), _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias),
-         _ptr(out), out.shape[-1], M, N, K, rpg, gs, go, _stream())
+         _ptr(out), ldo, M, N, K, rpg, gs, go, _stream())
     return out
 
 
@@ -206,13 +207,29 @@ def attn_cls_ok(T, L):
     return T >= 1 and L > 1 and (L - 1) % T == 0
 
 
-def attn_spatial_cls(qkv, out, B, T, L, heads, scale):
-    """CLS output only of attn_spatial (mean over the T frame sequences): out [B, C] rows."""
+def attn_spatial_cls(qkv, out, B, T, L, heads, scale, seq_scale=None):
+    """CLS output only of attn_spatial (mean over the T frame sequences): out [B, C] rows.
+    seq_scale [B*T] (training DropPath): frame t's output scaled before the mean."""
     _check(out, qkv.dtype, "out")
     ws = _ws(_lib.WS_ATTN_CLS, torch.float32, B * T, heads, 1 + (L - 1) // T, qkv.device)
-    call("dsvt_attn_spatial_cls_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.stride(0), B, T, L, heads, 64,
-         float(scale), _ptr(ws), ws.numel() * 4, _stream())
+    if seq_scale is None:
+        call("dsvt_attn_spatial_cls_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.stride(0), B, T, L, heads, 64,
+             float(scale), _ptr(ws), ws.numel() * 4, _stream())
+    else:
+        _check(seq_scale, torch.float32, "seq_scale")
+        call("dsvt_attn_spatial_cls_scaled_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.stride(0), _ptr(seq_scale),
+             B, T, L, heads, 64, float(scale), _ptr(ws), ws.numel() * 4, _stream())
     return out
+
+
+def attn_spatial_cls_bwd(qkv, dout, dqkv, B, T, L, heads, scale, seq_scale=None):
+    """Backward of attn_spatial_cls: dqkv [B*L, 3C] (every row written) from dout [B, C]."""
+    _check(dout, qkv.dtype, "dout")
+    _check(dqkv, qkv.dtype, "dqkv")
+    ws = _ws(_lib.WS_ATTN_CLS_BWD, torch.float32, B * T, heads, 0, qkv.device)
+    call("dsvt_attn_spatial_cls_bwd", _dt(qkv.dtype), _ptr(qkv), _ptr(dout), _ptr(dqkv), _ptr(seq_scale), B, T, L,
+         heads, 64, float(scale), _ptr(ws), ws.numel() * 4, _stream())
+    return dqkv
 
 
 def attn_joint(qkv, out, nb, L, heads, scale):

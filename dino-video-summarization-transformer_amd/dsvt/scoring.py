@@ -109,6 +109,7 @@ class FrameScorer:
         self.loss = PairwiseDINOLoss(model.embed_dim, teacher_temp, student_temp).to(model.pos_embed.device)
         self.frames_per_call = frames_per_call
         self.crop_size = crop_size if crop_size is not None else model.patch_embed.img_size[0]
+        self._views = {}
 
     @torch.no_grad()
     def dummy_scores(self, device):
@@ -129,18 +130,20 @@ class FrameScorer:
         F = frames.shape[0]
         if tuple(frames.shape[-2:]) != (self.crop_size, self.crop_size):
             return self.dummy_scores(frames.device)
-        li, gi = view_index(F, self.local_clip_size, self.global_clip_size)
         dev = frames.device
-        li_t = torch.from_numpy(li).to(dev)
-        gi_t = torch.from_numpy(gi).to(dev)
+        key = (F, dev)
+        if key not in self._views:       # device index maps made once per video length (a HIP
+            li, gi = view_index(F, self.local_clip_size, self.global_clip_size)    # graph replays them)
+            self._views[key] = (li.shape[1], gi.shape[1], torch.from_numpy(li).to(dev), torch.from_numpy(gi).to(dev))
+        ts, G, li_t, gi_t = self._views[key]
         frames = frames.float().contiguous()
         scores = torch.empty(F, device=dev, dtype=torch.float32)
         n = self.frames_per_call
         for s0 in range(0, F, n):
             s1 = min(F, s0 + n)
             b = s1 - s0
-            st = self.model.forward_frame_bank(frames, li_t[s0:s1].reshape(-1).contiguous(), b, li.shape[1])
-            te = self.model.forward_frame_bank(frames, gi_t[s0:s1].reshape(-1).contiguous(), b, gi.shape[1])
+            st = self.model.forward_frame_bank(frames, li_t[s0:s1].reshape(-1), b, ts)
+            te = self.model.forward_frame_bank(frames, gi_t[s0:s1].reshape(-1), b, G)
             scores[s0:s1] = self.loss.per_row(st, te)
         return scores
 

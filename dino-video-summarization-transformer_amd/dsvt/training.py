@@ -25,8 +25,8 @@ import numpy as np
 import torch
 
 from . import ops
-from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SPATIAL, WS_PATCH_EMBED, TOKENS_NT, \
-    DsvtError
+from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SPATIAL, WS_LN_GEMM, WS_PATCH_EMBED, \
+    TOKENS_NT, DsvtError
 
 
 def wgrad(dy, x, G, p, view=None, bias=None):
@@ -204,6 +204,7 @@ def _masks(model, nblk, B, Np, T, L, device):
         rows_s[:, 0] = st.mean(1)
         rows_s[:, 1:] = st.unsqueeze(1).expand(B, Np, T).reshape(B, Np * T)
         m.s_rows = rows_s.reshape(-1).contiguous()
+        m.s_cls = rows_s[:, 0].contiguous()                    # the CLS rows' (frame-mean) scale
         m.m_rows = m.m.view(B, 1).expand(B, L).reshape(-1).contiguous()
         out.append(m)
     return out
@@ -251,8 +252,13 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
     st.masks = masks
     cls_ws = torch.empty(ops.workspace_bytes(WS_ATTN_SPATIAL, mode, B * T, C, 0) // 4, device=dev)
     patch_map = (Np * T, L, 1)
+    # CLS-only last block (VisionTransformer.cls_tail): the features are the final norm of the CLS
+    # rows (timesformer.py:341-345), so past its spatial qkv the last block carries the CLS rows only
+    # -- in the forward and in the backward (_tail_backward)
+    depth = len(model.blocks)
+    st.tail = bool(getattr(model, "cls_tail", False)) and ops.attn_cls_ok(T, L) and 1 + Np <= 512
     st.blocks = []
-    for blk, mk in zip(model.blocks, masks):
+    for bi, (blk, mk) in enumerate(zip(model.blocks, masks)):
         S = _S()
         heads = blk.attn.num_heads
         ta = blk.temporal_attn
@@ -278,6 +284,11 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
         S.X1 = X
         S.a_s = torch.empty(rows, C, device=dev, dtype=mode)
         ops.layernorm(X, rows, C, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, S.a_s, out_f32=False)
+        if st.tail and bi == depth - 1:
+            X = _tail_forward(blk, S, mk, X, w, B, T, Np, L, C, rows, mode, dev)
+            if save:
+                st.blocks.append(S)
+            break
         S.qkv_s = torch.empty(rows, 3 * C, device=dev, dtype=mode)
         ops.gemm(S.a_s, w(blk.attn.qkv.weight), blk.attn.qkv.bias, S.qkv_s)
         S.o_s = torch.empty(rows, C, device=dev, dtype=mode)
@@ -310,8 +321,88 @@ def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
     if save:
         st.X = X
     feats = torch.empty(B, C, device=dev, dtype=torch.float32)
-    ops.layernorm(X, B, C, model.norm.weight, model.norm.bias, model.norm.eps, feats, rowmap=(1, L, 0))
+    # (CLS tail: X holds the B compact CLS rows)
+    ops.layernorm(X, B, C, model.norm.weight, model.norm.bias, model.norm.eps, feats,
+                  rowmap=None if st.tail else (1, L, 0))
     return feats, st
+
+
+def _tail_forward(blk, S, mk, X, w, B, T, Np, L, C, rows, mode, dev):
+    """The last divided block past its spatial LayerNorm (S.a_s) on the CLS rows alone: keys /
+    values of every row, the CLS rows' queries, the CLS query of every frame sequence with its
+    DropPath scale and the mean over frames (dsvt_attn_spatial_cls[_scaled]_fwd), then
+    attn.proj + residual, norm2 and the MLP on the B compact CLS rows (timesformer.py:139-184).
+    Returns the compact [B, C] rows."""
+    ws = torch.empty(ops.workspace_bytes(WS_LN_GEMM, mode, B, 0, C) // 2, device=dev, dtype=torch.bfloat16)
+    heads = blk.attn.num_heads
+    cls_map = (1, L, 0)
+    wq, bq = w(blk.attn.qkv.weight), blk.attn.qkv.bias
+    S.tail = True
+    S.qkv_s = torch.empty(rows, 3 * C, device=dev, dtype=mode)
+    ops.gemm(S.a_s, wq[C:], None if bq is None else bq[C:], S.qkv_s[:, C:])              # k, v: every row
+    ops.ln_gemm(X, cls_map, B, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, wq[:C],   # q: the CLS rows
+                None if bq is None else bq[:C], S.qkv_s, ws, rowmap=cls_map, few_rows=True)
+    S.o_cls = torch.empty(B, C, device=dev, dtype=mode)
+    ops.attn_spatial_cls(S.qkv_s, S.o_cls, B, T, L, heads, blk.attn.scale, seq_scale=None if mk is None else mk.s)
+    S.Xc1 = X.view(B, L, C)[:, 0].contiguous()                                             # the CLS rows (fp32)
+    Xc2 = torch.empty_like(S.Xc1)
+    ops.gemm_resid(S.o_cls, w(blk.attn.proj.weight), blk.attn.proj.bias, S.Xc1, Xc2,
+                   bias_row_scale=None if mk is None else mk.s_cls)
+    S.Xc2 = Xc2
+    S.a_m = torch.empty(B, C, device=dev, dtype=mode)
+    ops.layernorm(Xc2, B, C, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, S.a_m, out_f32=False)
+    hid = blk.mlp.fc1.out_features
+    S.pre = torch.empty(B, hid, device=dev, dtype=mode)
+    S.h = torch.empty(B, hid, device=dev, dtype=mode)
+    Xc3 = torch.empty_like(Xc2)
+    if mk is None:
+        ops.gemm_aux(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, S.pre, EPI_GELU_SAVE)
+        ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, Xc2, Xc3)
+    else:
+        ops.gemm_rowscale(S.a_m, w(blk.mlp.fc1.weight), blk.mlp.fc1.bias, S.h, mk.m, 1, aux=S.pre,
+                          epilogue=EPI_GELU_SAVE)
+        ops.gemm_resid(S.h, w(blk.mlp.fc2.weight), blk.mlp.fc2.bias, Xc2, Xc3, bias_row_scale=mk.m)
+    return Xc3
+
+
+def _tail_backward(blk, S, mk, dXc, wt, G, B, T, L, C, rows, mode, dev):
+    """Backward of _tail_forward: dXc [B, C] (the CLS rows' gradient after the final norm) through
+    the MLP, attn.proj and the CLS-query attention (dsvt_attn_spatial_cls_bwd: dk / dv of every
+    row, dq of the CLS rows) and the spatial qkv; returns dX [rows, C] fp32 holding the gradient
+    at the block's spatial input (the CLS rows' residual path + the norm1 path of every row)."""
+    heads = blk.attn.num_heads
+    fc1, fc2 = blk.mlp.fc1, blk.mlp.fc2
+    dXb = torch.empty(B, C, device=dev, dtype=mode)
+    ops.cast_rows(dXc, dXb, B)
+    if mk is None:
+        dXs = dXb
+        _colsum(dXc, G, fc2.bias)
+    else:
+        dXs = torch.empty(B, C, device=dev, dtype=mode)
+        ops.cast_rows(dXc, dXs, B, row_scale=mk.m, group=1)
+        _colsum(dXc, G, fc2.bias, row_scale=mk.m)
+    wgrad(dXb, S.h, G, fc2.weight)
+    dpre = torch.empty(B, fc1.out_features, device=dev, dtype=mode)
+    ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
+    wgrad(dpre, S.a_m, G, fc1.weight, bias=fc1.bias)
+    da = torch.empty(B, C, device=dev, dtype=mode)
+    ops.gemm(dpre, wt(fc1.weight), None, da)
+    _ln_bwd(S.Xc2, da, blk.norm2, dXc, B, G)
+    dXb = torch.empty(B, C, device=dev, dtype=mode)            # fresh: the fc2 wgrad may still read the last
+    ops.cast_rows(dXc, dXb, B)
+    wgrad(dXb, S.o_cls, G, blk.attn.proj.weight)
+    _colsum(dXc, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_cls)
+    do = torch.empty(B, C, device=dev, dtype=mode)
+    ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)
+    dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
+    ops.attn_spatial_cls_bwd(S.qkv_s, do, dqkv, B, T, L, heads, blk.attn.scale, seq_scale=None if mk is None else mk.s)
+    wgrad(dqkv, S.a_s, G, blk.attn.qkv.weight, bias=blk.attn.qkv.bias)
+    da = torch.empty(rows, C, device=dev, dtype=mode)
+    ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da)
+    dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
+    dX.view(B, L, C)[:, 0].copy_(dXc)                            # the CLS rows' residual path
+    _ln_bwd(S.X1, da, blk.norm1, dX, rows, G)
+    return dX
 
 
 def _backbone_backward(model, st, dfeat, G, ready=None):
@@ -333,13 +424,25 @@ def _divided_backward(model, st, dfeat, G, ready=None):
     wt = model._wcache.transposed(mode)
     patch_map = (Np * T, L, 1)
     # final norm on the CLS rows (timesformer.py:342-345)
-    dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
-    _ln_bwd(st.X, dfeat, model.norm, dX, B, G, rowmap=(1, L, 0))
+    if st.tail:                       # st.X: the compact CLS rows of the CLS-only last block
+        dXc = torch.zeros(B, C, device=dev, dtype=torch.float32)
+        _ln_bwd(st.X, dfeat, model.norm, dXc, B, G)
+    else:
+        dX = torch.zeros(rows, C, device=dev, dtype=torch.float32)
+        _ln_bwd(st.X, dfeat, model.norm, dX, B, G, rowmap=(1, L, 0))
     depth = len(model.blocks)
     for bi, blk, S, mk in zip(range(depth - 1, -1, -1), reversed(model.blocks), reversed(st.blocks),
                               reversed(st.masks)):
         heads = blk.attn.num_heads
         ta = blk.temporal_attn
+        if getattr(S, "tail", False):
+            dX = _tail_backward(blk, S, mk, dXc, wt, G, B, T, L, C, rows, mode, dev)
+            _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map)
+            for k in list(vars(S)):
+                setattr(S, k, None)
+            if ready is not None:
+                ready(bi)
+            continue
         # ---- MLP
         fc1, fc2 = blk.mlp.fc1, blk.mlp.fc2
         dXb = torch.empty(rows, C, device=dev, dtype=mode)
@@ -374,29 +477,43 @@ def _divided_backward(model, st, dfeat, G, ready=None):
         ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da)
         del dqkv, do
         _ln_bwd(S.X1, da, blk.norm1, dX, rows, G)
-        # ---- temporal (patch rows of X only)
-        dY = torch.empty(R, C, device=dev, dtype=mode)
-        ops.cast_rows(dX, dY, R, rowmap=patch_map)
-        wgrad(dY, S.u, G, blk.temporal_fc.weight, bias=blk.temporal_fc.bias)
-        du = torch.empty(R, C, device=dev, dtype=mode)
-        if mk is None:
-            ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
-        else:
-            ops.gemm_rowscale(dY, wt(blk.temporal_fc.weight), None, du, mk.t, T)
-        wgrad(du, S.o_t, G, ta.proj.weight, bias=ta.proj.bias)
-        do_t = torch.empty(R, C, device=dev, dtype=mode)
-        ops.gemm(du, wt(ta.proj.weight), None, do_t)
-        dqkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
-        ops.attn_temporal_bwd(S.qkv_t, do_t, dqkv_t, B * Np, T, heads, ta.scale)
-        wgrad(dqkv_t, S.a_t, G, ta.qkv.weight, bias=ta.qkv.bias)
-        da_t = torch.empty(R, C, device=dev, dtype=mode)
-        ops.gemm(dqkv_t, wt(ta.qkv.weight), None, da_t)
-        _ln_bwd(S.X0, da_t, blk.temporal_norm1, dX, R, G, rowmap=patch_map)
+        _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map)
         for k in list(vars(S)):
             setattr(S, k, None)        # free this block's activations as soon as it is done
         if ready is not None:
             ready(bi)
     # ---- patch embedding + token embeddings (timesformer.py:201-209, 288-323)
+    _embed_backward(model, st, dX, G, B, T, Np, L, C, R, mode, dev, patch_map)
+    if ready is not None:
+        ready(depth)
+    return G
+
+
+def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map):
+    """Backward of the temporal branch (patch rows of X only, timesformer.py:127-137): adds into dX."""
+    heads = blk.attn.num_heads
+    ta = blk.temporal_attn
+    dY = torch.empty(R, C, device=dev, dtype=mode)
+    ops.cast_rows(dX, dY, R, rowmap=patch_map)
+    wgrad(dY, S.u, G, blk.temporal_fc.weight, bias=blk.temporal_fc.bias)
+    du = torch.empty(R, C, device=dev, dtype=mode)
+    if mk is None:
+        ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
+    else:
+        ops.gemm_rowscale(dY, wt(blk.temporal_fc.weight), None, du, mk.t, T)
+    wgrad(du, S.o_t, G, ta.proj.weight, bias=ta.proj.bias)
+    do_t = torch.empty(R, C, device=dev, dtype=mode)
+    ops.gemm(du, wt(ta.proj.weight), None, do_t)
+    dqkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
+    ops.attn_temporal_bwd(S.qkv_t, do_t, dqkv_t, B * Np, T, heads, ta.scale)
+    wgrad(dqkv_t, S.a_t, G, ta.qkv.weight, bias=ta.qkv.bias)
+    da_t = torch.empty(R, C, device=dev, dtype=mode)
+    ops.gemm(dqkv_t, wt(ta.qkv.weight), None, da_t)
+    _ln_bwd(S.X0, da_t, blk.temporal_norm1, dX, R, G, rowmap=patch_map)
+
+
+def _embed_backward(model, st, dX, G, B, T, Np, L, C, R, mode, dev, patch_map):
+    """Patch embedding + token embeddings backward (timesformer.py:201-209, 288-323)."""
     dP = torch.empty(R, C, device=dev, dtype=mode)
     ops.cast_rows(dX, dP, R, rowmap=patch_map)
     conv = model.patch_embed.proj
@@ -405,9 +522,6 @@ def _divided_backward(model, st, dfeat, G, ready=None):
         wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
     ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
                   G.zeros(model.cls_token))
-    if ready is not None:
-        ready(depth)
-    return G
 
 
 # ======================================================================= joint / space-only

@@ -70,6 +70,7 @@ extern "C" {
 #define DSVT_WS_AUGMENT 11     /* M = output frames T, N = output size S */
 #define DSVT_WS_WGRAD 12       /* M = rows, N, K: the weight gradient is [N, K] */
 #define DSVT_WS_ATTN_CLS 14    /* M = B*T sequences, N = heads, K = keys per sequence 1 + (L-1)/T */
+#define DSVT_WS_ATTN_CLS_BWD 15 /* M = B*T sequences, N = heads */
 
 int dsvt_version(void);
 const char *dsvt_last_error(void);
@@ -209,6 +210,21 @@ int dsvt_attn_spatial_fwd(int dtype, const void *qkv, void *out, int64_t B, int6
 int dsvt_attn_spatial_cls_fwd(int dtype, const void *qkv, void *out, int64_t ld_out, int64_t B, int64_t T,
                               int64_t L, int64_t heads, int64_t head_dim, float scale, void *workspace,
                               int64_t workspace_bytes, void *stream);
+/* dsvt_attn_spatial_cls_fwd with frame t's output scaled by seq_scale[b*T + t] before the mean over
+ * frames: the training CLS-only last block under DropPath (timesformer.py:159 drop_path over the
+ * [(B*T), 1+N, C] batch, then the CLS mean :160-163). */
+int dsvt_attn_spatial_cls_scaled_fwd(int dtype, const void *qkv, void *out, int64_t ld_out, const float *seq_scale,
+                                     int64_t B, int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                                     void *workspace, int64_t workspace_bytes, void *stream);
+/* Backward of dsvt_attn_spatial_cls_fwd / _scaled_fwd (the training CLS-only last block: the
+ * patch rows' queries do not exist there): dqkv [B*L, 3C] (storage dtype, every row written) from
+ * qkv and dout [B, C] (the gradient of the frame-mean CLS output, storage dtype, compact rows).
+ * Patch rows get the dk / dv of their frame's CLS query and dq = 0; the CLS row the sums over t
+ * of its dq, dk, dv (fixed order).  seq_scale nullable.  Keys per sequence <= 512.
+ * workspace >= dsvt_workspace_bytes(DSVT_WS_ATTN_CLS_BWD, ., B*T, heads, 0). */
+int dsvt_attn_spatial_cls_bwd(int dtype, const void *qkv, const void *dout, void *dqkv, const float *seq_scale,
+                              int64_t B, int64_t T, int64_t L, int64_t heads, int64_t head_dim, float scale,
+                              void *workspace, int64_t workspace_bytes, void *stream);
 /* dsvt_attn_spatial_fwd with the output of sequence (b,t) scaled by seq_scale[b*T + t] before the
  * CLS mean: training-mode DropPath of the spatial branch, whose mask is per (b,t) sequence
  * (timesformer.py:159 drop_path over the [(B*T), 1+N, C] batch). */

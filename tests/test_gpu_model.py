@@ -396,11 +396,24 @@ def test_frame_scores_vitb_local3_global30(base_sd, dtype, tol):
     m = tsf(base_sd, dtype)
     F_ = 31
     frames = P.clip(44, (F_, 3, 224, 224))
-    scores = FrameScorer(m, 3, 30, frames_per_call=8).score(cu(frames)).cpu().numpy()
+    scores_dev = FrameScorer(m, 3, 30, frames_per_call=8).score(cu(frames))
+    scores = scores_dev.cpu().numpy()
     ref_model = TC.TimeSformerCPU(base_sd, 12)
     ref = _ref_scores(lambda x: ref_model.forward_features(x).numpy(), frames, F_, 3, 30)
     assert scores.shape == (F_,)
     assert rel(scores, ref) < tol, (np.max(np.abs(scores - ref)), scores, ref)
+    # the product output: the frames the "adaptive" selector picks from these scores
+    # (frame_selection_loader.py:115-170), against the indices the oracle's scores give
+    from dsvt.selection import adaptive_frame_indices
+    picked = mismatched = 0
+    for rate in (1, 4):
+        for N in (4, 8, 12, 16, 24):
+            want = O.adaptive_frame_selection(ref, F_, F_ * rate, rate, N)[0]
+            got, _ = adaptive_frame_indices(scores_dev, F_, F_ * rate, rate, N)
+            picked += N
+            mismatched += int(np.sum(np.asarray(got) != want))
+    print("frame selection %s: %d of %d indices differ from the oracle's" % (dtype, mismatched, picked))
+    assert mismatched == 0
 
 
 def test_bf16_vs_fp32_full_size(base_sd):
@@ -432,12 +445,13 @@ def test_bench_shape_repeatable_and_finite(base_sd):
     assert rel(one.cpu(), outs[0][5:6].cpu()) < BF16_TOL
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_split_streams_bitwise_equal(base_sd, dtype):
+@pytest.mark.parametrize("dtype,ln_fold", [(torch.float32, False), (torch.bfloat16, False), (torch.bfloat16, True)])
+def test_split_streams_bitwise_equal(base_sd, dtype, ln_fold):
     """Inference batches split over concurrent HIP streams (VisionTransformer.dsvt_streams):
     features, all-token outputs and list inputs (MultiCropWrapper groups, ragged 3 + 4 clips)
-    are bit-identical to the unsplit batch."""
+    are bit-identical to the unsplit batch, with and without the LayerNorm folding."""
     m = tsf(base_sd, dtype)
+    m.ln_fold = ln_fold
     xs = [cu(P.clip(51, (3, 3, 4, 64, 64))), cu(P.clip(52, (4, 3, 4, 64, 64)))]
     outs = {}
     with torch.no_grad():

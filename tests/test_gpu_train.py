@@ -113,11 +113,14 @@ def test_student_grads_plain_attention(gold_plain, attn, dtype, tag, monkeypatch
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("tag", ["eval", "drop"])
-def test_student_grads_match_reference(gold, dtype, tag, monkeypatch):
+@pytest.mark.parametrize("tail", [True, False])
+def test_student_grads_match_reference(gold, dtype, tag, tail, monkeypatch):
     """loss.backward() through MultiCropWrapper(TimeSformer divided, DINOHead) + DINOLoss: loss,
     student logits and EVERY student parameter gradient vs the reference.  'drop': training-mode
     DropPath (rate 0.5) replaying the reference's masks in its call order (per (b, patch)
-    temporal, per (b, frame) spatial, per clip MLP)."""
+    temporal, per (b, frame) spatial, per clip MLP).  tail: the CLS-only last block
+    (VisionTransformer.cls_tail, the default: forward and backward of that block past its spatial
+    qkv on the CLS rows alone) and the full last block."""
     from dsvt import training
     from dsvt.loss import DINOLoss
     if tag == "drop":
@@ -132,6 +135,7 @@ def test_student_grads_match_reference(gold, dtype, tag, monkeypatch):
             return torch.from_numpy(m.copy()).to(device)
         monkeypatch.setattr(training, "_keep_scale", replay)
     net = _student(dtype, tag == "drop")
+    net.backbone.cls_tail = tail
     crops = [torch.from_numpy(P.clip(1210 + i, (2, 3, 4, 64, 64))).cuda() for i in range(2)] + \
             [torch.from_numpy(P.clip(1220 + i, (2, 3, 4, 32, 32))).cuda() for i in range(2)]
     s_out = net(crops)
@@ -175,6 +179,39 @@ def _ref_spatial(qkv, B, T, Np, H, scale, seq_scale=None):
         o = o * seq_scale.view(B, T, 1, 1, 1)
     out = torch.cat([o[:, :, :1].mean(1), o[:, :, 1:].permute(0, 2, 1, 3, 4).reshape(B, Np * T, H, 64)], dim=1)
     return out.reshape(B * L, C)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("B,T,Np,H,scaled", [(2, 3, 5, 2, False), (1, 4, 49, 3, True), (2, 8, 16, 1, True),
+                                             (3, 8, 196, 12, True), (2, 1, 36, 2, False)])
+def test_attn_spatial_cls_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled):
+    """The CLS-only spatial attention of the training CLS tail: forward (dsvt_attn_spatial_cls
+    [_scaled]_fwd, the DropPath scale per (b, t) before the frame mean) and backward
+    (dsvt_attn_spatial_cls_bwd: dk / dv of every row, dq of the CLS rows, dq = 0 elsewhere) against
+    torch fp32 autograd of the full spatial attention's CLS rows (_ref_spatial)."""
+    from dsvt import ops
+    C, L = H * 64, 1 + Np * T
+    g = torch.Generator().manual_seed(B * 1000 + T * 100 + Np)
+    qkv32 = (torch.randn(B * L, 3 * C, generator=g) * 1.5)
+    dout32 = torch.randn(B, C, generator=g)
+    sc = (torch.rand(B * T, generator=g) * 2.0) if scaled else None
+    qkv = qkv32.to(dtype).cuda()
+    dout = dout32.to(dtype).cuda()
+    x = qkv.float().cpu().requires_grad_(True)
+    o = _ref_spatial(x, B, T, Np, H, 0.125, None if sc is None else sc)
+    o_cls = o.view(B, L, C)[:, 0]
+    (o_cls * dout.float().cpu()).sum().backward()
+    out = torch.empty(B, C, device="cuda", dtype=dtype)
+    ops.attn_spatial_cls(qkv, out, B, T, L, H, 0.125, seq_scale=None if sc is None else sc.cuda())
+    dq = torch.full((B * L, 3 * C), 7.0, device="cuda", dtype=dtype)
+    ops.attn_spatial_cls_bwd(qkv, dout, dq, B, T, L, H, 0.125, seq_scale=None if sc is None else sc.cuda())
+    torch.cuda.synchronize()
+    assert rel(out.float().cpu().numpy(), o_cls.detach().numpy()) < tol
+    assert rel(dq.float().cpu().numpy(), x.grad.numpy()) < tol
+    dq2 = torch.empty_like(dq)
+    ops.attn_spatial_cls_bwd(qkv, dout, dq2, B, T, L, H, 0.125, seq_scale=None if sc is None else sc.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(dq, dq2)
 
 
 @pytest.fixture(params=[0, 1], ids=["auto", "generic"])
