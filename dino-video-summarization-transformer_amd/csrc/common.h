@@ -38,14 +38,15 @@ __device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
   const b2_t h = __builtin_convertvector((f2_t){a, b}, b2_t);
   return __builtin_bit_cast(unsigned, h);
 }
-__device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
-  const unsigned a0 = cvt_pk_bf16(a[0], a[1]);
-  const unsigned a1 = cvt_pk_bf16(a[2], a[3]);
-  const unsigned b0 = cvt_pk_bf16(b[0], b[1]);
-  const unsigned b1 = cvt_pk_bf16(b[2], b[3]);
+// same, from the four already-packed bf16 pairs (a0 = a[0..1], a1 = a[2..3], b0, b1)
+__device__ __forceinline__ uint4 pack_pair_words(unsigned a0, unsigned a1, unsigned b0, unsigned b1) {
   const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
   return make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+__device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
+  return pack_pair_words(cvt_pk_bf16(a[0], a[1]), cvt_pk_bf16(a[2], a[3]), cvt_pk_bf16(b[0], b[1]),
+                         cvt_pk_bf16(b[2], b[3]));
 }
 __device__ __forceinline__ int pair_off(int g) { return ((g & 1) << 4) | ((g >> 1) << 3); }
 
@@ -198,6 +199,21 @@ __device__ __forceinline__ float gelu_out(float x) {
   else return gelu_erf(x);
 }
 
+// (GELU(x), GELU'(x)) in one evaluation: the erf tail and exp(-x^2/2) shared (the training fc1
+// epilogue saves GELU'(pre) for the backward); .x is bitwise gelu_erf(x), .y gelu_erf_grad(x)
+__device__ __forceinline__ float2 gelu_erf_and_grad(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);   // exp(-x^2/2)
+  const float tail = p * t * e;                                            // 1 - erf(z)
+  const float one_plus_erf = x >= 0.f ? 2.0f - tail : tail;
+  const float cdf = 0.5f * one_plus_erf;
+  return make_float2(0.5f * x * one_plus_erf, cdf + x * e * 0.3989422804014327f);
+}
 // d GELU / dx = Phi(x) + x phi(x) (same A&S 7.1.26 erf as gelu_erf): the Mlp.fc1 backward.
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float z = fabsf(x) * 0.70710678118654752f;

@@ -118,10 +118,18 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
             const float4 ba = bias4[j], bb = bias4[j + 1];
             a[0] += ba.x; a[1] += ba.y; a[2] += ba.z; a[3] += ba.w;
             b[0] += bb.x; b[1] += bb.y; b[2] += bb.z; b[3] += bb.w;
-            *reinterpret_cast<uint4*>((bf16_t*)p.aux + orow[i] * p.ld_aux + cbase + jp * 32 + po) = pack_pair_bf16(a, b);
+            // (GELU * rs, GELU'(pre)) packed a pair at a time (GELU' is what DGELU multiplies by)
+            unsigned ho[4], go[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) { a[e] = gelu_erf(a[e]) * rs; b[e] = gelu_erf(b[e]) * rs; }
-            *reinterpret_cast<uint4*>(span) = pack_pair_bf16(a, b);
+            for (int q = 0; q < 4; ++q) {
+              const fv4& s = q < 2 ? a : b;
+              const float2 r0 = gelu_erf_and_grad(s[2 * (q & 1)]), r1 = gelu_erf_and_grad(s[2 * (q & 1) + 1]);
+              ho[q] = cvt_pk_bf16(r0.x * rs, r1.x * rs);
+              go[q] = cvt_pk_bf16(r0.y, r1.y);
+            }
+            *reinterpret_cast<uint4*>((bf16_t*)p.aux + orow[i] * p.ld_aux + cbase + jp * 32 + po) =
+                pack_pair_words(go[0], go[1], go[2], go[3]);
+            *reinterpret_cast<uint4*>(span) = pack_pair_words(ho[0], ho[1], ho[2], ho[3]);
           } else {
             // the accumulators in the pair layout: v[k] = column k, v[4 + k] = column 4 + k
             float v[8];
@@ -136,8 +144,8 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
             const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              v[2 * q] *= gelu_erf_grad(__uint_as_float(w[q] << 16));
-              v[2 * q + 1] *= gelu_erf_grad(__uint_as_float(w[q] & 0xffff0000u));
+              v[2 * q] *= __uint_as_float(w[q] << 16);
+              v[2 * q + 1] *= __uint_as_float(w[q] & 0xffff0000u);
             }
             *reinterpret_cast<uint4*>(span) = make_uint4(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]),
                                                          cvt_pk_bf16(v[4], v[5]), cvt_pk_bf16(v[6], v[7]));
@@ -177,12 +185,17 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           if constexpr (EPI == EPI_GELU_SAVE) {
             const float4 bb = bias4[j];
             v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-            store4((bf16_t*)p.aux + orow * p.ld_aux + n, v[0], v[1], v[2], v[3]);
+            float gp[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]) * rs;
+            for (int e = 0; e < 4; ++e) {
+              const float2 r = gelu_erf_and_grad(v[e]);
+              v[e] = r.x * rs;
+              gp[e] = r.y;
+            }
+            store4((bf16_t*)p.aux + orow * p.ld_aux + n, gp[0], gp[1], gp[2], gp[3]);
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] *= gelu_erf_grad(pre[j][e]);
+            for (int e = 0; e < 4; ++e) v[e] *= pre[j][e];
           }
           store4(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n, v[0], v[1], v[2], v[3]);
         }
@@ -202,9 +215,14 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
         if constexpr (EPI == EPI_GELU_SAVE) {
           const float4 bb = bias4[j];
           v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-          store4((bf16_t*)p.aux + orow * p.ld_aux + n, v[0], v[1], v[2], v[3]);
+          float gp[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+          for (int e = 0; e < 4; ++e) {
+            const float2 r = gelu_erf_and_grad(v[e]);
+            v[e] = r.x;
+            gp[e] = r.y;
+          }
+          store4((bf16_t*)p.aux + orow * p.ld_aux + n, gp[0], gp[1], gp[2], gp[3]);
           if constexpr (RS) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] *= rsc[i];
@@ -213,7 +231,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           float pre[4];
           load4((const bf16_t*)p.aux + orow * p.ld_aux + n, pre);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] *= gelu_erf_grad(pre[e]);
+          for (int e = 0; e < 4; ++e) v[e] *= pre[e];
         }
         store4(reinterpret_cast<OutT*>(p.out) + orow * p.ldo + n, v[0], v[1], v[2], v[3]);
       }

@@ -63,8 +63,8 @@ __host__ __device__ inline const float* resid_src(const GemmParams& p) {
   return p.resid ? p.resid : (const float*)p.out;
 }
 
-// EPI_GELU_SAVE: out = GELU(acc + bias), aux = acc + bias (the pre-activation, for the backward)
-// EPI_DGELU:     out = acc * GELU'(aux)   (Mlp.fc1 backward through nn.GELU, bias ignored)
+// EPI_GELU_SAVE: out = GELU(acc + bias), aux = GELU'(acc + bias) (what the backward multiplies by)
+// EPI_DGELU:     out = acc * aux          (Mlp.fc1 backward through nn.GELU, bias ignored)
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_PATCH = 3, EPI_GELU_SAVE = 4, EPI_DGELU = 5 };
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s);

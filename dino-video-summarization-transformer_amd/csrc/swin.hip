@@ -173,7 +173,8 @@ hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, co
                                                                   (int)ldo, eps);                             \
     return hipGetLastError();                                                                                   \
   }
-  if (((uintptr_t)x & 7) == 0 && ((uintptr_t)out & 3) == 0 && ldo % 2 == 0) {
+  // the small kernel stores column pairs: 4-byte bf16 / 8-byte fp32 aligned out
+  if (((uintptr_t)x & 7) == 0 && ((uintptr_t)out & (dtype == 0 ? 3 : 7)) == 0 && ldo % 2 == 0) {
     if (C == 96) DSVT_SLN(96, 16)
     if (C == 192) DSVT_SLN(192, 16)
     if (C == 384) DSVT_SLN(384, 32)

@@ -98,6 +98,7 @@ class BlockGradReducer:
         self.world = dist.get_world_size(group)
         self.avg = dist.get_backend(group) == "nccl"
         self._works, self._arena, self._seeded = [], None, []
+        self._local = False     # a no_sync backward left local sums in p.grad since the last sync
         backbone.dsvt_grad_reducer = self
 
     def params(self):
@@ -111,6 +112,10 @@ class BlockGradReducer:
         """False inside DDP's no_sync() (gradient accumulation without communication)."""
         return self.ddp is None or getattr(self.ddp, "require_backward_grad_sync", True)
 
+    def note_local(self):
+        """Called for a backward inside no_sync(): the next synchronised arena seeds from p.grad."""
+        self._local = True
+
     def arena(self, device):
         """A fresh flat fp32 arena for this backward (the returned views become p.grad), the
         id(p) -> view map the gradient buffers come from, and the ids of the views SEEDED with
@@ -120,7 +125,10 @@ class BlockGradReducer:
         no_sync backwards leave LOCAL sums in p.grad.  DDP all-reduces the whole accumulated
         gradient on the sync step, so the arena starts from those sums (the backward then
         accumulates onto them) and the caller must REPLACE p.grad with the reduced view instead
-        of letting autograd add it (`take_seeded`)."""
+        of letting autograd add it (`take_seeded`).  Only after such a no_sync backward
+        (`note_local`): otherwise an existing p.grad (zeros left by zero_grad(set_to_none=False), a
+        previous synchronised step's reduced sum) is already global, and autograd adds the reduced
+        view onto it without an fp32 copy of every gradient through the arena."""
         buckets = self.params()
         sizes = [[(p.numel() + 63) // 64 * 64 for p in b] for b in buckets]
         flat = torch.empty(sum(sum(s) for s in sizes), device=device, dtype=torch.float32)
@@ -131,12 +139,12 @@ class BlockGradReducer:
             for p, n in zip(b, s):
                 v = flat[off:off + p.numel()].view(p.shape)
                 views[id(p)] = v
-                if p.grad is not None:
+                if self._local and p.grad is not None:
                     v.copy_(p.grad)
                     self._seeded.append(p)
                 off += n
             self._slices.append(flat[start:off])
-        self._arena, self._works = flat, []
+        self._arena, self._works, self._local = flat, [], False
         return views, {id(p) for p in self._seeded}
 
     def take_seeded(self):

@@ -310,7 +310,7 @@ def _ws(op, mode, M, N, K, device):
 
 
 def gemm_aux(a, w, bias, out, aux, epilogue, out_f32=False, rowmap=None, M=None):
-    """GELU_SAVE: out = GELU(a.w^T + b), aux = a.w^T + b; DGELU: out = (a.w^T) * GELU'(aux)."""
+    """GELU_SAVE: out = GELU(a.w^T + b), aux = GELU'(a.w^T + b); DGELU: out = (a.w^T) * aux."""
     mode = w.dtype
     _check(a, mode, "A")
     _check(w, mode, "W")
@@ -325,7 +325,7 @@ def gemm_aux(a, w, bias, out, aux, epilogue, out_f32=False, rowmap=None, M=None)
 
 def gemm_rowscale(a, w, bias, out, row_scale, group, aux=None, epilogue=_lib.EPI_BIAS):
     """out[m] = (a[m] . w^T + bias) * row_scale[m // group] (EPI_BIAS), or with aux:
-    aux = a.w^T + b, out = GELU(aux) * row_scale[m // group] (EPI_GELU_SAVE)."""
+    aux = GELU'(a.w^T + b), out = GELU(a.w^T + b) * row_scale[m // group] (EPI_GELU_SAVE)."""
     mode = w.dtype
     _check(a, mode, "A")
     _check(w, mode, "W")

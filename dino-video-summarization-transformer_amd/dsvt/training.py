@@ -154,6 +154,7 @@ class BackboneFn(torch.autograd.Function):
         model, dfeat = ctx.model, dfeat.float().contiguous()
         red = getattr(model, "dsvt_grad_reducer", None)         # data-parallel: dist.BlockGradReducer
         if red is not None and not red.active():
+            red.note_local()
             red = None
         arena, seeded = red.arena(dfeat.device) if red is not None else (None, ())
         G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None,

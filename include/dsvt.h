@@ -37,8 +37,8 @@ extern "C" {
 #define DSVT_EPI_BIAS 0       /* out[row(m)] = acc + bias                  (Linear)          */
 #define DSVT_EPI_BIAS_GELU 1  /* out[row(m)] = GELU_erf(acc + bias)        (Mlp.fc1 + act)   */
 #define DSVT_EPI_BIAS_RESID 2 /* X[row(m)]  += acc + bias   (fp32 X)       (residual adds)   */
-#define DSVT_EPI_GELU_SAVE 4  /* out = GELU_erf(acc + bias), aux = acc + bias (training fc1)   */
-#define DSVT_EPI_DGELU 5      /* out = acc * GELU_erf'(aux)               (fc1 backward)    */
+#define DSVT_EPI_GELU_SAVE 4  /* out = GELU_erf(acc + bias), aux = GELU_erf'(acc + bias) (fc1) */
+#define DSVT_EPI_DGELU 5      /* out = acc * aux                          (fc1 backward)    */
 /* OR-ed into the epilogue argument of dsvt_gemm_fwd / dsvt_ln_gemm_fwd: a few-row GEMM (the
  * CLS-only last block's rows, timesformer.py:181-184 on the CLS tokens, and the DINOHead MLP,
  * vision_transformer.py:271-281) -- the K-split skinny kernel where eligible, whatever M is, so a
@@ -285,8 +285,8 @@ int dsvt_center_ema(float *center, const float *colsum, int64_t D, float momentu
  * ------------------------------------------------------------------------------------------ */
 
 /* dsvt_gemm_fwd with a second storage-dtype operand aux [M, ld_aux] (rows through the output
- * row map): DSVT_EPI_GELU_SAVE (Mlp.fc1 + nn.GELU saving the pre-activation, timesformer.py:
- * 46-47) or DSVT_EPI_DGELU (dX of fc1 through GELU: out = (dY . W2) * GELU'(pre)). */
+ * row map): DSVT_EPI_GELU_SAVE (Mlp.fc1 + nn.GELU saving GELU'(pre-activation), timesformer.py:
+ * 46-47) or DSVT_EPI_DGELU (dX of fc1 through GELU: out = (dY . W2) * aux, aux = GELU'(pre)). */
 int dsvt_gemm_aux_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,
                       int64_t ldw, const float *bias, void *out, int64_t ldo, void *aux, int64_t ld_aux,
                       int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,

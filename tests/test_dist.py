@@ -137,6 +137,11 @@ def _worker(rank, world, port, errq):
             for p in b:
                 p.grad = torch.full(p.shape, 10.0 * (rank + 1) + i)
         ddp.require_backward_grad_sync = True
+        # an existing p.grad WITHOUT a no_sync backward before (zero_grad(set_to_none=False), a
+        # previous synchronised step) is already global: not seeded, autograd adds onto it
+        views, seeded = red.arena(torch.device("cpu"))
+        assert not seeded
+        red.note_local()                                   # what the no_sync backward records
         views, seeded = red.arena(torch.device("cpu"))
         assert seeded == {id(p) for b in buckets for p in b}
         for i, b in enumerate(buckets):

@@ -463,7 +463,7 @@ def test_gemm_resid_scaled_bias(dtype, M, K):
 @pytest.mark.parametrize("epi", ["bias", "gelu_save"])
 def test_gemm_rowscale(M, group, epi):
     """dsvt_gemm_rowscale_fwd (training DropPath fused into the GEMM epilogue) is bit-identical
-    to the unscaled GEMM followed by the row-scale kernel; the saved pre-activation is unscaled.
+    to the unscaled GEMM followed by the row-scale kernel; the saved GELU'(pre-activation) is unscaled.
     M = 300 runs the 128x128 kernel, the others the persistent one."""
     from dsvt import ops
     from dsvt._lib import EPI_BIAS, EPI_GELU_SAVE

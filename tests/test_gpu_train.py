@@ -367,7 +367,7 @@ def test_layernorm_bwd_rowmap_vs_autograd(C, dy_dtype):
 @pytest.mark.parametrize("M", [300, 4037, 4613])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
 def test_gelu_save_and_dgelu_epilogues(dtype, tol, M):
-    """fc1 forward saving the pre-activation, and (dY.W2) * GELU'(pre) -- vs torch autograd.
+    """fc1 forward saving GELU'(pre-activation), and (dY.W2) * GELU'(pre) -- vs torch autograd.
     M = 4037: the persistent kernel with a ragged last tile (its branch-free epilogue clamps the
     rows past M to identical rewrites of row M - 1); M = 4613: the 256x256 kernel's 16-byte pair
     epilogue (ragged last tile too)."""
@@ -379,17 +379,18 @@ def test_gelu_save_and_dgelu_epilogues(dtype, tol, M):
     w = (torch.randn(N, K, device="cuda", generator=g) * 0.1).to(dtype)
     b = torch.randn(N, device="cuda", generator=g)
     h = torch.empty(M, N, device="cuda", dtype=dtype)
-    pre = torch.empty(M, N, device="cuda", dtype=dtype)
-    ops.gemm_aux(a, w, b, h, pre, EPI_GELU_SAVE)
-    pre_ref = a.float() @ w.float().t() + b
-    assert rel(pre.float().cpu(), pre_ref.cpu()) < tol
-    assert rel(h.float().cpu(), F.gelu(pre_ref).cpu()) < tol
+    gp = torch.empty(M, N, device="cuda", dtype=dtype)
+    ops.gemm_aux(a, w, b, h, gp, EPI_GELU_SAVE)
+    pre_ref = (a.float() @ w.float().t() + b).requires_grad_(True)
+    F.gelu(pre_ref).sum().backward()
+    assert rel(h.float().cpu(), F.gelu(pre_ref.detach()).cpu()) < tol
+    assert rel(gp.float().cpu(), pre_ref.grad.cpu()) < tol
     w2 = (torch.randn(K, N, device="cuda", generator=g) * 0.1).to(dtype)      # fc2 weight [out=K, in=N]
     dy = torch.randn(M, K, device="cuda", generator=g).to(dtype)
     w2t = w2.float().t().contiguous().to(dtype)                                # W2^T [N, K]
     dpre = torch.empty(M, N, device="cuda", dtype=dtype)
-    ops.gemm_aux(dy, w2t, None, dpre, pre, EPI_DGELU)
-    x = pre.float().requires_grad_(True)
+    ops.gemm_aux(dy, w2t, None, dpre, gp, EPI_DGELU)
+    x = pre_ref.detach().clone().requires_grad_(True)
     F.gelu(x).backward(dy.float() @ w2.float())
     torch.cuda.synchronize()
     assert rel(dpre.float().cpu(), x.grad.cpu()) < tol
