@@ -243,6 +243,40 @@ int dsvt_gemm_resid_stats_fwd(const void* A, int64_t lda, const void* W, int64_t
                 gemm_bytes(DSVT_BF16, EPI_RESID, 1, M, N, K) + 2.0 * M * N + 8.0 * M * LN_PARTS);
 }
 
+int dsvt_ln_fold_qkv_heads(const float* W, const float* gamma, const float* beta, const float* bias, void* Wf,
+                           float* wsum, float* bias_f, int64_t heads, int64_t K, void* stream) {
+  REQUIRE(W && gamma && beta && Wf && wsum && bias_f, "ln_fold_qkv_heads: null pointer");
+  REQUIRE(heads > 0 && heads <= 64 && K > 0 && K % 256 == 0, "ln_fold_qkv_heads: need 0 < heads <= 64, K %% 256 == 0");
+  REQUIRE(aligned16(W) && aligned16(gamma) && aligned16(beta) && aligned16(Wf),
+          "ln_fold_qkv_heads: pointers must be 16-byte aligned");
+  hipError_t e = launch_ln_fold(W, gamma, beta, bias, Wf, wsum, bias_f, 3 * heads * 64, K, (hipStream_t)stream, (int)heads);
+  return e == hipSuccess ? 0 : hip_fail(e, "ln_fold_qkv_heads");
+}
+
+int dsvt_qkv_temporal_attn_fwd(const void* xb, int64_t ldxb, int64_t a_rpg, int64_t a_gstride, int64_t a_goff,
+                               const float* stats, float eps, const void* Wf, const float* wsum, const float* bias_f,
+                               void* out, int64_t ldo, int64_t M, int64_t heads, int64_t T, float scale, void* stream) {
+  REQUIRE(xb && stats && Wf && wsum && bias_f && out, "qkv_temporal_attn: null pointer");
+  REQUIRE(T == 8, "qkv_temporal_attn: T must be 8 (got %lld)", (long long)T);
+  REQUIRE(heads * 64 == DSVT_LN_FOLD_C, "qkv_temporal_attn: heads * 64 must be %d", DSVT_LN_FOLD_C);
+  REQUIRE(M >= 8 && M % 8 == 0, "qkv_temporal_attn: M must be a positive multiple of T (got %lld)", (long long)M);
+  REQUIRE(ldxb >= DSVT_LN_FOLD_C && ldxb % 8 == 0 && ldo >= heads * 64 && ldo % 4 == 0,
+          "qkv_temporal_attn: ldxb >= 768 (multiple of 8), ldo >= heads * 64 (multiple of 4)");
+  REQUIRE(aligned16(xb) && aligned16(Wf) && aligned16(wsum) && aligned16(bias_f) && ((uintptr_t)stats & 7) == 0 &&
+              ((uintptr_t)out & 7) == 0,
+          "qkv_temporal_attn: misaligned pointer");
+  norm_map(a_rpg, a_gstride, a_goff);
+  const int64_t N = 3 * heads * 64, K = DSVT_LN_FOLD_C;
+  GemmParams p{xb, ldxb, Wf, K, bias_f, out, ldo, M, N, K, M, 0, 0, nullptr, nullptr, nullptr, nullptr, T};
+  p.a_rpg = a_rpg; p.a_gstride = a_gstride; p.a_goff = a_goff;
+  p.ln_stats = stats; p.ln_wsum = wsum; p.ln_eps = eps; p.ln_invk = 1.0f / (float)K;
+  p.attn_scale = scale;
+  REQUIRE(gemm_tattn_ok(p), "qkv_temporal_attn: A / W exceed the 32-bit DMA offsets");
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K + 4.0 * M * T * heads * 64, (hipStream_t)stream,
+                "dsvt_qkv_temporal_attn_fwd", [&] { return launch_gemm_tattn(p, (hipStream_t)stream); },
+                32 * 32 /* tag: pseudo-variant 32 = the temporal-attention GEMM */, 2.0 * (M * K + N * K + M * heads * 64) + 8.0 * M * LN_PARTS);
+}
+
 int dsvt_gemm_lnx_fwd(int epilogue, const void* xb, int64_t ldxb, int64_t a_rpg, int64_t a_gstride, int64_t a_goff,
                       const float* stats, float eps, const void* Wf, const float* wsum, const float* bias_f, void* out,
                       int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
@@ -553,8 +587,8 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 
 int dsvt_set_gemm_variant(int variant) {
   REQUIRE(variant == 0 || variant == 1 || variant == 10 || (variant >= 20 && variant <= 29 && variant != 24) ||
-              variant == 50,
-          "gemm variant must be 0 (auto), 1, 10, 20 (21-29 but 24: ablation builds) or 50");
+              variant == 30 || variant == 50,
+          "gemm variant must be 0 (auto), 1, 10, 20 (21-29 but 24: ablation builds), 30 or 50");
   set_gemm_variant(variant);
   return 0;
 }

@@ -333,12 +333,20 @@ void set_gemm_variant(int v) { g_gemm_variant = v; }
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
-  const int gv = g_gemm_variant;
+  int gv = g_gemm_variant;
+  if (gv == 30 && !(out_f32 && !p.ln_stats && gemm_192_ok(p, epi))) gv = 0;   // forced, ineligible: auto
   // DSVT_GEMM_FEW_ROWS call sites (the CLS-only tail's and the DINO head's few-row GEMMs, chosen
   // by call site so that a batch split over streams picks the same kernel as the whole batch):
   // the K-split skinny kernel (variant 50 forces it where eligible) -- bench 397.7-398.7 vs
   // 395.1-396.0 clips/s with the 128x128 kernel (same box, three interleaved rounds)
   if ((gv == 50 || (gv == 0 && p.few_rows)) && gemm_skinny_ok(p, epi)) return 50;
+  if (gv == 30) return 30;
+  // fp32 residual GEMMs with N % 192 == 0 (the N = 768 proj / temporal fc / fc2): the 256x192 kernel
+#ifndef DSVT_RESID192
+#define DSVT_RESID192 0
+#endif
+  if (DSVT_RESID192 && gv == 0 && epi == EPI_RESID && out_f32 && !p.ln_stats && p.M >= 4096 && gemm_192_ok(p, epi))
+    return 30;
   // the LayerNorm-folded A operand (dsvt_gemm_lnx_fwd) and the residual epilogue that writes
   // the next LayerNorm's row statistics (dsvt_gemm_resid_stats_fwd): the 256x256 kernel only
   if (p.ln_stats || p.stats_out) return 20;
@@ -379,7 +387,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
-  if ((p.ln_stats || p.stats_out) && v != 20) return hipErrorInvalidValue;
+  if ((p.ln_stats && v != 20) || (p.stats_out && v != 20 && v != 30)) return hipErrorInvalidValue;
   if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);

@@ -195,7 +195,7 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
 }
 
 // variant 10 = the persistent staggered 256x128 kernel (2 WGs per CU); 20 = gemm_8ph.hip (21-29:
-// its diagnostic ablation builds, tools/gemm_bench.py)
+// its diagnostic ablation builds, tools/gemm_bench.py); 30 = gemm_192.hip
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s) {
   switch (variant) {
     case 10: return launch_persist_t<256, 128, 2, 2, true>(p, epi, out_f32, s);
@@ -208,6 +208,7 @@ hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f3
     case 27: return launch_gemm_8ph(p, epi, out_f32, s, 18);
     case 28: return launch_gemm_8ph(p, epi, out_f32, s, 32);
     case 29: return launch_gemm_8ph(p, epi, out_f32, s, 64);
+    case 30: return launch_gemm_192(p, epi, out_f32, s);
     default: return hipErrorInvalidValue;
   }
 }

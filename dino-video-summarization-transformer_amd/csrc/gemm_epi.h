@@ -441,7 +441,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
 template <int MI, int NJ>
 __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
                                           int r16, int g) {
-  static_assert(NJ == 4 && MI % 4 == 0, "64-column wave slab");
+  static_assert(MI % 4 == 0, "rows in batches of four");
   const float invk = p.ln_invk;
   float mu[MI], rs[MI];
   const uint32_t a_rpg = (uint32_t)(p.a_rpg < p.M ? p.a_rpg : p.M), a_gs = (uint32_t)p.a_gstride;

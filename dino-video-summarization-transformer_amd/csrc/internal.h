@@ -46,6 +46,8 @@ struct GemmParams {
   // (stats_out, rows of the output row map)
   void* xb_out = nullptr;
   float* stats_out = nullptr;
+  // temporal attention epilogue (launch_gemm_tattn): softmax scale
+  float attn_scale = 0.f;
 };
 
 // float2 (sum, sum of squares) partials per token row: one per 64-column slab of C = 768
@@ -72,6 +74,11 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // 
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
 bool gemm_8ph_ok(const GemmParams& p, int epi);
+hipError_t launch_gemm_192(const GemmParams& p, int epi, int out_f32, hipStream_t s);    // variant 30
+bool gemm_192_ok(const GemmParams& p, int epi);
+// the LayerNorm-folded temporal qkv GEMM with the T = 8 attention in its epilogue (gemm_192.hip)
+bool gemm_tattn_ok(const GemmParams& p);
+hipError_t launch_gemm_tattn(const GemmParams& p, hipStream_t s);
 // K split over the 8 waves of a workgroup, 64-row blocks (variant 50, gemm_big.hip)
 bool gemm_skinny_ok(const GemmParams& p, int epi);
 hipError_t launch_gemm_skinny(const GemmParams& p, int epi, int out_f32, hipStream_t s);
@@ -95,7 +102,7 @@ hipError_t launch_wgrad(const unsigned short* dy, int64_t ldy, const unsigned sh
 hipError_t launch_ln_stats(const float* x, void* xb, float* stats, int64_t rows, hipStream_t s);
 // LayerNorm-folded GEMM weights: Wf = bf16(W * gamma), wsum = row sums of Wf, bf = b + W . beta
 hipError_t launch_ln_fold(const float* W, const float* gamma, const float* beta, const float* b, void* Wf, float* wsum,
-                          float* bf, int64_t N, int64_t K, hipStream_t s);
+                          float* bf, int64_t N, int64_t K, hipStream_t s, int heads = 0);
 hipError_t launch_layernorm(int dtype, int out_f32, const float* x, void* y, const float* g,
                             const float* b, int64_t rows, int64_t C, int64_t rpg, int64_t gstride,
                             int64_t goff, float eps, hipStream_t s);

@@ -167,20 +167,28 @@ hipError_t launch_ln_stats(const float* x, void* xb, float* stats, int64_t rows,
 // The weights of a LayerNorm-folded GEMM (dsvt_ln_fold_weights): for W [N, K] fp32 following
 // LayerNorm(gamma, beta):  Wf = bf16(W * gamma) [N, K],  wsum[n] = sum_k Wf[n, k] (of the bf16
 // values the MFMA multiplies),  bf[n] = b[n] + sum_k W[n, k] * beta[k].  One wave per row.
+// heads > 0 (an attention qkv weight, N = 3 * heads * 64): output row o(n) head-interleaved for the
+// temporal-attention GEMM (gemm_192.hip) -- row n = part*C + h*64 + d (part q / k / v) goes to
+// o = h*192 + (d / 32)*96 + part*32 + d % 32.
 __global__ __launch_bounds__(256) void ln_fold_kernel(const float* __restrict__ W, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ b,
                                                       bf16_t* __restrict__ Wf, float* __restrict__ wsum,
-                                                      float* __restrict__ bf, int64_t N, int64_t K) {
+                                                      float* __restrict__ bf, int64_t N, int64_t K, int heads) {
   const int lane = threadIdx.x & 63;
   const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
+  int64_t o = n;
+  if (heads > 0) {
+    const int64_t C = N / 3, part = n / C, h = (n % C) / 64, d = n % 64;
+    o = h * 192 + (d / 32) * 96 + part * 32 + d % 32;
+  }
   float s = 0.f, t = 0.f;
   for (int64_t k = lane * 4; k < K; k += 256) {
     const float4 w = *reinterpret_cast<const float4*>(W + n * K + k);
     const float4 gg = *reinterpret_cast<const float4*>(gamma + k);
     const float4 bb = *reinterpret_cast<const float4*>(beta + k);
     const unsigned lo = cvt_pk_bf16(w.x * gg.x, w.y * gg.y), hi = cvt_pk_bf16(w.z * gg.z, w.w * gg.w);
-    *reinterpret_cast<uint2*>(Wf + n * K + k) = make_uint2(lo, hi);
+    *reinterpret_cast<uint2*>(Wf + o * K + k) = make_uint2(lo, hi);
     s += (__uint_as_float(lo << 16) + __uint_as_float(lo & 0xffff0000u)) +
          (__uint_as_float(hi << 16) + __uint_as_float(hi & 0xffff0000u));
     t += (w.x * bb.x + w.y * bb.y) + (w.z * bb.z + w.w * bb.w);
@@ -188,14 +196,15 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(const float* __restrict__ 
   s = wave_sum(s);
   t = wave_sum(t);
   if (lane == 0) {
-    wsum[n] = s;
-    bf[n] = (b ? b[n] : 0.f) + t;
+    wsum[o] = s;
+    bf[o] = (b ? b[n] : 0.f) + t;
   }
 }
 
 hipError_t launch_ln_fold(const float* W, const float* gamma, const float* beta, const float* b, void* Wf, float* wsum,
-                          float* bf, int64_t N, int64_t K, hipStream_t s) {
-  ln_fold_kernel<<<dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s>>>(W, gamma, beta, b, (bf16_t*)Wf, wsum, bf, N, K);
+                          float* bf, int64_t N, int64_t K, hipStream_t s, int heads) {
+  ln_fold_kernel<<<dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s>>>(W, gamma, beta, b, (bf16_t*)Wf, wsum, bf, N, K,
+                                                                    heads);
   return hipGetLastError();
 }
 

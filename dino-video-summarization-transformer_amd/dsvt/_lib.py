@@ -31,6 +31,9 @@ SIGNATURES = {
     "dsvt_gemm_resid_fwd": (_i32, [_i32, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "dsvt_layernorm_fwd": (_i32, [_i32, _i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_ln_fold_weights": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "dsvt_ln_fold_qkv_heads": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "dsvt_qkv_temporal_attn_fwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _f32, _p, _p, _p, _p, _i64, _i64, _i64,
+                                          _i64, _f32, _p]),
     "dsvt_ln_stats_fwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
     "dsvt_gemm_resid_stats_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _p]),

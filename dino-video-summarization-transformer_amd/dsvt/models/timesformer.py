@@ -120,10 +120,8 @@ class Block(nn.Module):
             B, T, Np, L = ctx.B, ctx.T, ctx.Np, ctx.L
             R = B * Np * T
             patch_map = (Np * T, L, 1)          # compact patch row m -> X row b*L + 1 + m % (Np*T)
-            ta = self.temporal_attn
             # temporal: LN -> qkv (timesformer.py:127-131) -> attention -> proj . temporal_fc + residual
-            self._qkv(X, ctx, R, patch_map, self.temporal_norm1, ta.qkv)
-            ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
+            self._temporal_attn(X, ctx, R, patch_map)
             self._temporal_out(X, ctx, R, patch_map)
             # spatial with CLS replicate/mean (:139-181)
             self._qkv(X, ctx, B * L, None, self.norm1, self.attn.qkv)
@@ -152,6 +150,20 @@ class Block(nn.Module):
             ops.gemm_lnx(ctx.xb, ctx.st, ln.eps, ctx.fold_ln(lin, ln), ctx.qkv, M, in_rowmap=rowmap)
         else:
             ops.ln_gemm(X, rowmap, M, ln.weight, ln.bias, ln.eps, ctx.w(lin.weight), lin.bias, ctx.qkv, ctx.ws)
+
+    def _temporal_attn(self, X, ctx, R, patch_map):
+        """ctx.o[:R] = temporal_attn(temporal_norm1(patch rows)) (timesformer.py:127-131): under
+        ctx.tattn one kernel (LayerNorm-folded qkv GEMM with the T = 8 attention in its epilogue,
+        dsvt_qkv_temporal_attn_fwd), else the qkv GEMM into ctx.qkv and the attention kernel."""
+        ta = self.temporal_attn
+        heads = ta.num_heads
+        if ctx.lnx and ctx.tattn:
+            ops.qkv_temporal_attn(ctx.xb, ctx.st, self.temporal_norm1.eps,
+                                  ctx.fold_ln(ta.qkv, self.temporal_norm1, heads), ctx.o, R, heads, ctx.T,
+                                  ta.scale, in_rowmap=patch_map)
+            return
+        self._qkv(X, ctx, R, patch_map, self.temporal_norm1, ta.qkv)
+        ops.attn_temporal(ctx.qkv, ctx.o, ctx.B * ctx.Np, ctx.T, heads, ta.scale)
 
     def _resid(self, X, ctx, a, lin, M, rowmap=None, stats=True, w=None, b=None):
         """X[row(m)] += a[m] . W^T + b (lin's W / b unless given); under ctx.lnx the rows' bf16 copy
@@ -200,9 +212,7 @@ class Block(nn.Module):
         R = B * Np * T
         patch_map = (Np * T, L, 1)
         cls_map = (1, L, 0)                 # CLS row b -> X row b*L
-        ta = self.temporal_attn
-        self._qkv(X, ctx, R, patch_map, self.temporal_norm1, ta.qkv)
-        ops.attn_temporal(ctx.qkv, ctx.o, B * Np, T, heads, ta.scale)
+        self._temporal_attn(X, ctx, R, patch_map)
         self._temporal_out(X, ctx, R, patch_map)
         # spatial qkv: keys / values of every row, queries of the CLS rows only (the patch rows'
         # queries have no consumer here)
@@ -316,6 +326,9 @@ class VisionTransformer(nn.Module):
         # its (spatial) qkv (Block._run_cls_tail) -- its patch-row outputs are discarded by
         # the reference (x[:, 0] after the final norm).  DSVT_CLS_TAIL=0 runs the full last block.
         self.cls_tail = os.environ.get("DSVT_CLS_TAIL", "1") != "0"
+        # under the LayerNorm fold with T = 8: the temporal branch's qkv GEMM and attention as one
+        # kernel (dsvt_qkv_temporal_attn_fwd, Block._temporal_attn); DSVT_TATTN=0 runs them apart
+        self.fuse_temporal_attn = os.environ.get("DSVT_TATTN", "1") != "0"
         self._wcache = WeightCache()
         self._index_cache = {}
 
@@ -361,6 +374,8 @@ class VisionTransformer(nn.Module):
                         (((blk.temporal_attn.qkv, blk.temporal_norm1),) if blk.attention_type == 'divided_space_time'
                          else ()):
                     self._wcache.ln_folded(lin, ln)
+                if blk.attention_type == 'divided_space_time' and self.fuse_temporal_attn:
+                    self._wcache.ln_folded(blk.temporal_attn.qkv, blk.temporal_norm1, blk.temporal_attn.num_heads)
         self._wcache.refresh(ws, mode, flat={id(self.patch_embed.proj.weight)})   # one launch
 
     def _ln_fold_on(self, mode, rows):
@@ -560,6 +575,8 @@ class VisionTransformer(nn.Module):
             ctx.st = torch.empty(ctx.rows, LN_PARTS, 2, device=dev, dtype=torch.float32)
             ctx.fold_ln = self._wcache.ln_folded
             ops.ln_stats(X, ctx.xb, ctx.st, ctx.rows)
+        ctx.tattn = ctx.lnx and self.fuse_temporal_attn and T == 8 and \
+            self.attention_type == 'divided_space_time' and self.blocks[0].temporal_attn.num_heads * 64 == C
         nblk = len(self.blocks)
         if get_attn:            # timesformer.py:325-331: the last block's attention instead of features
             for blk in self.blocks[:-1]:

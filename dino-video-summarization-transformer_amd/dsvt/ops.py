@@ -96,6 +96,27 @@ def ln_fold_weights(W, ln, bias, Wf, wsum, bias_f):
          _ptr(bias_f), N, K, _stream())
 
 
+def ln_fold_qkv_heads(W, ln, bias, Wf, wsum, bias_f, heads):
+    """ln_fold_weights of an attention qkv weight [3 * heads * 64, K] with its rows head-interleaved
+    for qkv_temporal_attn (dsvt_ln_fold_qkv_heads)."""
+    _check(W, torch.float32, "W")
+    _check(Wf, torch.bfloat16, "Wf")
+    if W.shape[0] != 3 * heads * 64:
+        raise _lib.DsvtError("ln_fold_qkv_heads: W has %d rows, not 3 * %d * 64" % (W.shape[0], heads))
+    call("dsvt_ln_fold_qkv_heads", _ptr(W), _ptr(ln.weight), _ptr(ln.bias), _ptr(bias), _ptr(Wf), _ptr(wsum),
+         _ptr(bias_f), heads, W.shape[1], _stream())
+
+
+def qkv_temporal_attn(xb, stats, eps, folded_heads, out, M, heads, T, scale, in_rowmap=None):
+    """out[m] = the T-frame temporal attention output of compact patch row m: LayerNorm -> qkv ->
+    attention in one kernel (dsvt_qkv_temporal_attn_fwd); folded_heads from ln_fold_qkv_heads."""
+    Wf, wsum, bf = folded_heads
+    irpg, igs, igo = in_rowmap if in_rowmap is not None else (0, 0, 0)
+    call("dsvt_qkv_temporal_attn_fwd", _ptr(xb), xb.shape[-1], irpg, igs, igo, _ptr(stats), float(eps), _ptr(Wf),
+         _ptr(wsum), _ptr(bf), _ptr(out), out.shape[-1], M, heads, T, float(scale), _stream())
+    return out
+
+
 def ln_stats(X, xb, stats, rows):
     """xb[r] = bf16(X[r]), stats[r] = the LN_PARTS (sum, sum of squares) partials, r < rows."""
     _check(X, torch.float32, "X")
@@ -504,6 +525,10 @@ def gemm_kernel_name(tag):
         return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
     if variant == 20:
         return "void dsvt::gemm_8ph_kernel<%d, %s, 0, " % (epi, f32)
+    if variant == 30:
+        return "void dsvt::gemm_192_kernel<"
+    if variant == 32:
+        return "void dsvt::gemm_192_kernel<2>"
     if variant == 50:
         return "void dsvt::gemm_skinny_kernel<%d, %s>" % (epi, f32)
     if variant == 31:

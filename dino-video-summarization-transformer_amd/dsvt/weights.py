@@ -151,13 +151,15 @@ class WeightCache:
         self._c[key] = (stamp, (w, b32)) + self._event()
         return w, b32
 
-    def ln_folded(self, linear, ln):
+    def ln_folded(self, linear, ln, heads=0):
         """(Wf, wsum, bias_f) of nn.Linear `linear` after nn.LayerNorm `ln` for the LayerNorm-folded
         GEMM (dsvt_gemm_lnx_fwd): Wf = bf16(W * gamma), wsum = its row sums, bias_f = b + W . beta,
-        one dsvt_ln_fold_weights launch, cached until any of the four parameters changes."""
+        one dsvt_ln_fold_weights launch, cached until any of the four parameters changes.
+        heads > 0: an attention qkv weight with its rows head-interleaved (dsvt_ln_fold_qkv_heads,
+        the temporal-attention GEMM's order)."""
         params = (linear.weight, linear.bias, ln.weight, ln.bias)
         stamp = tuple((None, 0) if p is None else (p._version, p.data_ptr()) for p in params)
-        key = ("lnfold", id(linear), id(ln))
+        key = ("lnfold", id(linear), id(ln), heads)
         ent = self._c.get(key)
         if ent is not None and ent[0] == stamp:
             self._sync(ent)
@@ -170,7 +172,11 @@ class WeightCache:
         Wf = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
         wsum = torch.empty(N, device=dev, dtype=torch.float32)
         bf = torch.empty(N, device=dev, dtype=torch.float32)
-        ops.ln_fold_weights(W, ln, None if linear.bias is None else linear.bias.detach(), Wf, wsum, bf)
+        b = None if linear.bias is None else linear.bias.detach()
+        if heads:
+            ops.ln_fold_qkv_heads(W, ln, b, Wf, wsum, bf, heads)
+        else:
+            ops.ln_fold_weights(W, ln, b, Wf, wsum, bf)
         self._c[key] = (stamp, (Wf, wsum, bf)) + self._event()
         return Wf, wsum, bf
 

@@ -143,6 +143,23 @@ int dsvt_gemm_lnx_fwd(int epilogue, const void *xb, int64_t ldxb, int64_t a_rpg,
                       const float *stats, float eps, const void *Wf, const float *wsum, const float *bias_f, void *out,
                       int64_t ldo, int64_t M, int64_t N, int64_t K, int64_t rpg, int64_t gstride, int64_t goff,
                       void *stream);
+/* The temporal branch's LayerNorm -> qkv -> T = 8 attention in ONE kernel (temporal_norm1 ->
+ * temporal_attn, models/timesformer.py:127-131 with Attention.forward :55-87 over the
+ * 'b (h w t) m -> (b h w) t m' sequences): out[m][h*64 + d] (bf16, compact patch rows m, ldo) =
+ * the attention output of head h for token m -- what dsvt_gemm_lnx_fwd into a [M, 3C] qkv
+ * followed by dsvt_attn_temporal_fwd gives, without the qkv tensor in HBM.  The patch rows m are
+ * read through the A row map like dsvt_gemm_lnx_fwd; consecutive groups of T rows are the
+ * sequences (M a multiple of T); T == 8, heads * 64 == 768; scale = head_dim ** -0.5.
+ * Wf / wsum / bias_f: the qkv weight folded with the LayerNorm in the head-interleaved row order of
+ * dsvt_ln_fold_qkv_heads. */
+int dsvt_qkv_temporal_attn_fwd(const void *xb, int64_t ldxb, int64_t a_rpg, int64_t a_gstride, int64_t a_goff,
+                               const float *stats, float eps, const void *Wf, const float *wsum, const float *bias_f,
+                               void *out, int64_t ldo, int64_t M, int64_t heads, int64_t T, float scale, void *stream);
+/* dsvt_ln_fold_weights for an attention qkv weight W [3 * heads * 64, K] with its rows written in
+ * the head-interleaved order dsvt_qkv_temporal_attn_fwd reads: row part*C + h*64 + d (part = q, k,
+ * v; C = heads * 64) goes to row h*192 + (d / 32)*96 + part*32 + d % 32 of Wf / wsum / bias_f. */
+int dsvt_ln_fold_qkv_heads(const float *W, const float *gamma, const float *beta, const float *bias, void *Wf,
+                           float *wsum, float *bias_f, int64_t heads, int64_t K, void *stream);
 
 /* K3: LayerNorm(eps) over rows of fp32 X read through a row map, written compact
  * (rows x C) in dtype (or fp32 when out_f32 bit 0); with out_f32 bit 1 the output rows follow

@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 10, 20, 50])
+@pytest.fixture(params=[0, 1, 10, 20, 30, 50])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -217,11 +217,11 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 10, 20])
+@pytest.mark.parametrize("variant", [0, 1, 10, 20, 30])
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8), (16, 196, 8)])
 def test_gemm_residual_k768(variant, B, Np, T):
     """The K = 768, N = 768 residual GEMM (attn.proj / folded temporal fc shape) at the bench's
-    row counts on the 128x128 kernel and the 256x256 one: through the temporal row map (CLS rows
+    row counts on the 128x128 kernel, the 256x256 and the 256x192 one: through the temporal row map (CLS rows
     untouched) and on all rows, in place and out of place, against float64."""
     from dsvt import ops
     from dsvt._lib import EPI_BIAS_RESID
@@ -354,12 +354,70 @@ def test_gemm_lnx(B, Np, T, epi):
         check(got[:, C:], (lnx @ w64.T + b64)[:, C:], torch.bfloat16, "lnx kv slice")
 
 
+@pytest.mark.parametrize("B,Np", [(2, 5), (4, 49), (16, 196)])
+def test_qkv_temporal_attn(B, Np):
+    """dsvt_qkv_temporal_attn_fwd (temporal_norm1 -> temporal qkv -> T = 8 attention in one
+    kernel) against LayerNorm -> Linear -> softmax attention over each patch's 8 frames in float64
+    on the same fp32 rows, through the temporal row map (compact patch rows m <- X row
+    b*L + 1 + m % (Np*T)); close to the unfused dsvt path (dsvt_gemm_lnx_fwd + attn_temporal);
+    bitwise repeatable.  B*Np*8 = 80 rows: one partial 256-row tile."""
+    import torch.nn as nn
+    from dsvt import ops
+    from dsvt.weights import WeightCache
+    C, T, H = 768, 8, 12
+    L = 1 + Np * T
+    rows, R = B * L, B * Np * T
+    x = rnd((rows, C), 80, 1.0) + rnd((rows, 1), 81, 1.0)
+    X = to(x, torch.float32)
+    xb = torch.empty(rows, C, device=dev(), dtype=torch.bfloat16)
+    st = torch.empty(rows, 12, 2, device=dev(), dtype=torch.float32)
+    ops.ln_stats(X, xb, st, rows)
+    lin = nn.Linear(C, 3 * C).to(dev())
+    ln = nn.LayerNorm(C, eps=1e-6).to(dev())
+    with torch.no_grad():
+        lin.weight.copy_(to(rnd((3 * C, C), 82, 0.05), torch.float32))
+        lin.bias.copy_(to(rnd((3 * C,), 83, 0.3), torch.float32))
+        ln.weight.copy_(to(1.0 + rnd((C,), 84, 0.3), torch.float32))
+        ln.bias.copy_(to(rnd((C,), 85, 0.2), torch.float32))
+    wc = WeightCache()
+    fh = wc.ln_folded(lin, ln, H)
+    scale = 64 ** -0.5
+    pmap = (Np * T, L, 1)
+    outs = []
+    for _ in range(2):
+        o = torch.full((R, C), float("nan"), device=dev(), dtype=torch.bfloat16)
+        ops.qkv_temporal_attn(xb, st, ln.eps, fh, o, R, H, T, scale, in_rowmap=pmap)
+        outs.append(o)
+    # the unfused dsvt path on the same inputs
+    qkv = torch.empty(R, 3 * C, device=dev(), dtype=torch.bfloat16)
+    ops.gemm_lnx(xb, st, ln.eps, wc.ln_folded(lin, ln), qkv, R, in_rowmap=pmap)
+    o_ref = torch.empty(R, C, device=dev(), dtype=torch.bfloat16)
+    ops.attn_temporal(qkv, o_ref, B * Np, T, H, scale)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    patch = (np.arange(R) // (Np * T)) * L + 1 + np.arange(R) % (Np * T)
+    lnx = _ln_ref(x.astype(np.float64)[patch], back(ln.weight.detach()), back(ln.bias.detach()))
+    q, k, v = np.split(lnx @ back(lin.weight.detach()).astype(np.float64).T + back(lin.bias.detach()), 3, axis=1)
+    q, k, v = (a.reshape(R // T, T, H, 64).transpose(0, 2, 1, 3) for a in (q, k, v))
+    s = q @ k.transpose(0, 1, 3, 2) * scale
+    p = np.exp(s - s.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    ref = (p @ v).transpose(0, 2, 1, 3).reshape(R, C)
+    check(back(outs[0]), ref, torch.bfloat16, "qkv_temporal_attn")
+    check(back(o_ref), ref, torch.bfloat16, "unfused")
+    d = np.abs(back(outs[0]).astype(np.float64) - back(o_ref)).max() / np.abs(ref).max()
+    assert d < 1e-2, d
+
+
 @pytest.mark.parametrize("B,Np,T", [(2, 5, 3), (16, 196, 8), (48, 36, 8)])
-def test_gemm_resid_stats(B, Np, T):
+@pytest.mark.parametrize("variant", [0, 30])
+def test_gemm_resid_stats(B, Np, T, variant):
     """dsvt_gemm_resid_stats_fwd: the residual update exactly as the plain residual GEMM on the
-    256x256 kernel (bitwise), and for every updated row its bf16 copy and the 12 partials of the
-    NEW values (what dsvt_ln_stats_fwd gives for those rows); rows outside the row map untouched
-    (CLS rows of the temporal branch) in X, xb and the statistics."""
+    same kernel (bitwise; the 256x256 one, or the 256x192 one forced), and for every updated row
+    its bf16 copy and the 12 partials of the NEW values (what dsvt_ln_stats_fwd gives for those
+    rows, up to the order of the sum: only the total over the 12 is the contract -- the 256x192
+    kernel writes a zero slot); rows outside the row map untouched (CLS rows of the temporal
+    branch) in X, xb and the statistics."""
     from dsvt import _lib, ops
     from dsvt._lib import EPI_BIAS_RESID
     C = 768
@@ -373,10 +431,11 @@ def test_gemm_resid_stats(B, Np, T):
         X = x0.clone()
         xb = torch.full((rows, C), 5.0, device=dev(), dtype=torch.bfloat16)
         st = torch.full((rows, 12, 2), 9.0, device=dev(), dtype=torch.float32)
-        ops.gemm_resid_stats(a, w, b, X, xb, st, rowmap=rowmap, M=M)
-        Xr = x0.clone()
-        _lib.call("dsvt_set_gemm_variant", 20)
+        _lib.call("dsvt_set_gemm_variant", variant)
         try:
+            ops.gemm_resid_stats(a, w, b, X, xb, st, rowmap=rowmap, M=M)
+            Xr = x0.clone()
+            _lib.call("dsvt_set_gemm_variant", variant or 20)
             ops.gemm(a, w, b, Xr, epilogue=EPI_BIAS_RESID, rowmap=rowmap, M=M)
         finally:
             _lib.call("dsvt_set_gemm_variant", 0)
@@ -388,7 +447,9 @@ def test_gemm_resid_stats(B, Np, T):
         upd = np.arange(rows) if rowmap is None else (np.arange(M) // (Np * T)) * L + 1 + np.arange(M) % (Np * T)
         keep = np.setdiff1d(np.arange(rows), upd)
         assert torch.equal(xb[upd], xb_r[upd])
-        np.testing.assert_allclose(back(st)[upd], back(st_r)[upd], rtol=1e-5, atol=1e-3)
+        if variant == 0:
+            np.testing.assert_allclose(back(st)[upd], back(st_r)[upd], rtol=1e-5, atol=1e-3)
+        np.testing.assert_allclose(back(st)[upd].sum(1), back(st_r)[upd].sum(1), rtol=1e-5, atol=1e-3)
         if len(keep):
             assert torch.equal(X[keep], x0[keep])
             assert bool((xb[keep] == 5.0).all()) and bool((st[keep] == 9.0).all())
