@@ -702,6 +702,48 @@ int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float
                 });
 }
 
+// ---- DINOHead(use_bn=True): BatchNorm1d + GELU (head_bn.hip)
+int dsvt_bn_stats_fwd(const float* x, int64_t R, int64_t D, double* sums, void* stream) {
+  REQUIRE(x && sums && R > 0 && D > 0, "bn_stats: bad args");
+  hipError_t e = launch_bn_colsum2(x, R, D, sums, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "bn_stats");
+}
+
+int dsvt_bn_finalize(const double* sums, double count, int64_t D, float eps, float momentum, int training,
+                     float* running_mean, float* running_var, float* mean, float* rstd, void* stream) {
+  REQUIRE(mean && rstd && D > 0, "bn_finalize: bad args");
+  REQUIRE(!training || (sums && count >= 1.0), "bn_finalize: training needs the sums and count >= 1");
+  REQUIRE(training || (running_mean && running_var), "bn_finalize: eval needs the running statistics");
+  hipError_t e = launch_bn_finalize(sums, count, D, eps, momentum, training, running_mean, running_var, mean, rstd,
+                                    (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "bn_finalize");
+}
+
+int dsvt_bn_gelu_fwd(int dtype, const float* x, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, void* y, void* gelu_grad, float* xhat, int64_t R, int64_t D, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "bn_gelu: bad dtype");
+  REQUIRE(x && mean && rstd && y && R > 0 && D > 0, "bn_gelu: bad args");
+  hipError_t e = launch_bn_gelu(dtype, x, mean, rstd, gamma, beta, y, gelu_grad, xhat, R, D, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "bn_gelu");
+}
+
+int dsvt_bn_bwd_sums(int dtype, const void* dz, const float* xhat, int64_t R, int64_t D, double* sums, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "bn_bwd_sums: bad dtype");
+  REQUIRE(dz && xhat && sums && R > 0 && D > 0, "bn_bwd_sums: bad args");
+  hipError_t e = launch_bn_bwd_sums(dtype, dz, xhat, R, D, sums, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "bn_bwd_sums");
+}
+
+int dsvt_bn_bwd(int dtype, const void* dz, const float* xhat, const double* sums, double count, const float* gamma,
+                const float* rstd, float* dx, float* dgamma, float* dbeta, int accumulate, int64_t R, int64_t D,
+                void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "bn_bwd: bad dtype");
+  REQUIRE(dz && xhat && sums && rstd && dx && R > 0 && D > 0 && count >= 1.0, "bn_bwd: bad args");
+  hipError_t e = launch_bn_bwd_dx(dtype, dz, xhat, sums, count, gamma, rstd, dx, dgamma, dbeta, accumulate, R, D,
+                                  (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "bn_bwd");
+}
+
 int dsvt_colsum_bwd(int dtype, const void* y, int64_t rows, int64_t C, int64_t ld, int64_t rpg, int64_t gstride,
                     int64_t goff, const float* row_scale, float* out, int accumulate, void* workspace,
                     int64_t workspace_bytes, void* stream) {

@@ -239,6 +239,18 @@ hipError_t launch_video_augment(const void* frames, int u8, int64_t T_in, int64_
                                 int64_t W, int64_t sT, int64_t sC, int64_t sH, int64_t sW, const ::dsvt_aug_params& p,
                                 float* out, int layout, void* ws, hipStream_t s);
 
+// BatchNorm1d + GELU of DINOHead(use_bn=True) (head_bn.hip); sums are fp64 [2D]
+hipError_t launch_bn_colsum2(const float* x, int64_t R, int64_t D, double* sums, hipStream_t s);
+hipError_t launch_bn_finalize(const double* sums, double count, int64_t D, float eps, float momentum, int training,
+                              float* run_mean, float* run_var, float* mean, float* rstd, hipStream_t s);
+hipError_t launch_bn_gelu(int dtype, const float* x, const float* mean, const float* rstd, const float* gamma,
+                          const float* beta, void* y, void* gelu_grad, float* xhat, int64_t R, int64_t D, hipStream_t s);
+hipError_t launch_bn_bwd_sums(int dtype, const void* dz, const float* xhat, int64_t R, int64_t D, double* sums,
+                              hipStream_t s);
+hipError_t launch_bn_bwd_dx(int dtype, const void* dz, const float* xhat, const double* sums, double count,
+                            const float* gamma, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                            int accumulate, int64_t R, int64_t D, hipStream_t s);
+
 hipError_t launch_softmax_stats(const float* x, const float* center, float inv_temp, int64_t rows,
                                 int64_t D, float* m_out, float* z_out, hipStream_t s);
 hipError_t launch_pair_ce(const float* student, const float* teacher, const float* center,

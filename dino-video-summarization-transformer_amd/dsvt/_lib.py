@@ -19,7 +19,7 @@ WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 
 WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
 WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_ATTN_CLS, WS_ATTN_CLS_BWD = 10, 11, 12, 14, 15
 
-_i32, _i64, _f32, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+_i32, _i64, _f32, _f64, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 
 # name -> (restype, argtypes); must mirror include/dsvt.h exactly (tests/test_capi_symbols.py)
 SIGNATURES = {
@@ -35,6 +35,11 @@ SIGNATURES = {
     "dsvt_qkv_temporal_attn_fwd": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _f32, _p, _p, _p, _p, _i64, _i64, _i64,
                                           _i64, _f32, _p]),
     "dsvt_ln_stats_fwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "dsvt_bn_stats_fwd": (_i32, [_p, _i64, _i64, _p, _p]),
+    "dsvt_bn_finalize": (_i32, [_p, _f64, _i64, _f32, _f32, _i32, _p, _p, _p, _p, _p]),
+    "dsvt_bn_gelu_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "dsvt_bn_bwd_sums": (_i32, [_i32, _p, _p, _i64, _i64, _p, _p]),
+    "dsvt_bn_bwd": (_i32, [_i32, _p, _p, _p, _f64, _p, _p, _p, _p, _p, _i32, _i64, _i64, _p]),
     "dsvt_gemm_resid_stats_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _p]),
     "dsvt_gemm_lnx_fwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _p, _f32, _p, _p, _p, _p, _i64, _i64, _i64,

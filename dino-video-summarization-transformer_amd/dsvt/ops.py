@@ -117,6 +117,61 @@ def qkv_temporal_attn(xb, stats, eps, folded_heads, out, M, heads, T, scale, in_
     return out
 
 
+# ---------------------------------------------------------------- DINOHead(use_bn=True)
+def _bn_allreduce(sums, count, group):
+    """SyncBatchNorm: the column sums and the row count over the process group (fp64)."""
+    import torch.distributed as dist
+    if group is False or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return count
+    cnt = torch.tensor([float(count)], device=sums.device, dtype=torch.float64)
+    dist.all_reduce(sums, group=group)
+    dist.all_reduce(cnt, group=group)
+    return float(cnt.item())
+
+
+def bn_gelu(x, bn, out, gelu_grad=None, xhat=None, sync_group=False):
+    """out = GELU(BatchNorm1d(x)) for x [R, D] fp32 (train mode: batch statistics, running
+    estimates updated; eval: running statistics); returns (mean, rstd, count) for the backward.
+    sync_group: the SyncBatchNorm process group (None = WORLD; False = this process only)."""
+    _check(x, torch.float32, "x")
+    R, D = x.shape
+    dev = x.device
+    mean = torch.empty(D, device=dev, dtype=torch.float32)
+    rstd = torch.empty(D, device=dev, dtype=torch.float32)
+    count = float(R)
+    training = bn.training or bn.running_mean is None
+    sums = None
+    if training:
+        sums = torch.empty(2 * D, device=dev, dtype=torch.float64)
+        call("dsvt_bn_stats_fwd", _ptr(x), R, D, _ptr(sums), _stream())
+        count = _bn_allreduce(sums, count, sync_group)
+        if bn.momentum is None:
+            raise NotImplementedError("BatchNorm1d(momentum=None) (cumulative average) is not supported")
+    upd = training and bn.track_running_stats and bn.running_mean is not None
+    call("dsvt_bn_finalize", _ptr(sums), count, D, float(bn.eps), float(bn.momentum or 0.0), int(training),
+         _ptr(bn.running_mean) if (upd or not training) else None,
+         _ptr(bn.running_var) if (upd or not training) else None, _ptr(mean), _ptr(rstd), _stream())
+    if upd:
+        bn.num_batches_tracked.add_(1)
+    w = bn.weight.detach() if bn.affine else None
+    b = bn.bias.detach() if bn.affine else None
+    call("dsvt_bn_gelu_fwd", _dt(out.dtype), _ptr(x), _ptr(mean), _ptr(rstd), _ptr(w), _ptr(b), _ptr(out),
+         _ptr(gelu_grad), _ptr(xhat), R, D, _stream())
+    return mean, rstd, count
+
+
+def bn_bwd(dz, xhat, rstd, count, bn, dx, dgamma=None, dbeta=None, accumulate=False, sync_group=False):
+    """dx (fp32) of BatchNorm1d in training mode from dz = dL/d(its output); dgamma / dbeta too."""
+    R, D = xhat.shape
+    sums = torch.empty(2 * D, device=dz.device, dtype=torch.float64)
+    call("dsvt_bn_bwd_sums", _dt(dz.dtype), _ptr(dz), _ptr(xhat), R, D, _ptr(sums), _stream())
+    _bn_allreduce(sums, count, sync_group)
+    w = bn.weight.detach() if bn.affine else None
+    call("dsvt_bn_bwd", _dt(dz.dtype), _ptr(dz), _ptr(xhat), _ptr(sums), float(count), _ptr(w), _ptr(rstd),
+         _ptr(dx), _ptr(dgamma), _ptr(dbeta), int(accumulate), R, D, _stream())
+    return dx
+
+
 def ln_stats(X, xb, stats, rows):
     """xb[r] = bf16(X[r]), stats[r] = the LN_PARTS (sum, sum of squares) partials, r < rows."""
     _check(X, torch.float32, "X")

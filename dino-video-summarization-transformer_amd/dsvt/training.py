@@ -738,8 +738,8 @@ class HeadFn(torch.autograd.Function):
 
 
 def _head_linears(head):
-    import torch.nn as nn
-    return [head.mlp] if isinstance(head.mlp, nn.Linear) else [m for m in head.mlp if isinstance(m, nn.Linear)]
+    from .vision_transformer import head_layers
+    return head_layers(head)
 
 
 def _head_forward(head, x):
@@ -751,18 +751,28 @@ def _head_forward(head, x):
     st.mode = mode
     h = torch.empty(R, x.shape[1], device=dev, dtype=mode)
     ops.cast(x, h)
+    from .vision_transformer import bn_sync_group
     lins = _head_linears(head)
-    st.a, st.pre = [], []
-    for i, lin in enumerate(lins):
+    st.a, st.pre, st.bn = [], [], []
+    for i, (lin, bn) in enumerate(lins):
         st.a.append(h)
         if i == len(lins) - 1:
             y = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32)
             ops.gemm(h, w(lin.weight), lin.bias, y, out_f32=True)
             st.pre.append(None)
+            st.bn.append(None)
         else:
             nxt = torch.empty(R, lin.out_features, device=dev, dtype=mode)
-            pre = torch.empty(R, lin.out_features, device=dev, dtype=mode)
-            ops.gemm_aux(h, w(lin.weight), lin.bias, nxt, pre, EPI_GELU_SAVE)
+            pre = torch.empty(R, lin.out_features, device=dev, dtype=mode)     # GELU'(GELU input)
+            if bn is None:
+                ops.gemm_aux(h, w(lin.weight), lin.bias, nxt, pre, EPI_GELU_SAVE)
+                st.bn.append(None)
+            else:                       # Linear -> BatchNorm1d -> GELU (use_bn), xhat kept fp32
+                y = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32)
+                ops.gemm(h, w(lin.weight), lin.bias, y, out_f32=True)
+                xhat = torch.empty_like(y)
+                _, rstd, count = ops.bn_gelu(y, bn, nxt, gelu_grad=pre, xhat=xhat, sync_group=bn_sync_group(bn))
+                st.bn.append((bn, xhat, rstd, count))
             st.pre.append(pre)
             h = nxt
     st.y = y
@@ -804,11 +814,12 @@ def _head_backward(head, st, dlogits):
     else:
         dz = torch.mm(dl, st.wn)                              # [R, bottleneck]
     dy = ops.head_norm_bwd(st.y, dz.contiguous())
+    from .vision_transformer import bn_sync_group
     lins = _head_linears(head)
     g = dy                                                    # gradient w.r.t. the current linear's output
     dx = None
     for i in range(len(lins) - 1, -1, -1):
-        lin = lins[i]
+        lin = lins[i][0]
         gb = g if g.dtype == mode else torch.empty(R, g.shape[1], device=dev, dtype=mode)
         if gb is not g:
             ops.cast(g.contiguous(), gb)
@@ -821,6 +832,16 @@ def _head_backward(head, st, dlogits):
             nxt = torch.empty(R, lin.in_features, device=dev, dtype=mode)
             ops.gemm_aux(gb, wt(lin.weight), None, nxt, st.pre[i - 1], EPI_DGELU)
             g = nxt
+            if st.bn[i - 1] is not None:    # through BatchNorm1d (batch statistics): fp32 dx
+                bn, xhat, rstd, count = st.bn[i - 1]
+                gx = torch.empty(R, nxt.shape[1], device=dev, dtype=torch.float32)
+                dg = G.acc(bn.weight) if bn.affine and bn.weight.requires_grad else (None, False)
+                db = G.acc(bn.bias) if bn.affine and bn.bias.requires_grad else (None, False)
+                if dg[0] is not None and db[0] is not None and dg[1] != db[1]:
+                    raise RuntimeError("BatchNorm weight / bias gradients out of step")
+                ops.bn_bwd(nxt, xhat, rstd, count, bn, gx, dg[0], db[0], accumulate=dg[1] or db[1],
+                           sync_group=bn_sync_group(bn))
+                g = gx
         else:
             dx = torch.empty(R, lin.in_features, device=dev, dtype=torch.float32)
             ops.gemm(gb, wt(lin.weight), None, dx, out_f32=True)

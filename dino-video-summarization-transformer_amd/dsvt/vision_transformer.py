@@ -182,21 +182,41 @@ class WeightNormLinear(nn.Module):
 
 HEAD_FEW_ROWS = 512            # DINOHead MLP rows that still take the K-split skinny kernel
 
+
+def head_layers(head):
+    """The DINOHead MLP as [(nn.Linear, BatchNorm or None)]: every Linear but the last is followed
+    by (BatchNorm1d / SyncBatchNorm when use_bn, then) GELU."""
+    from torch.nn.modules.batchnorm import _BatchNorm
+    if isinstance(head.mlp, nn.Linear):
+        return [(head.mlp, None)]
+    mods = list(head.mlp)
+    out = []
+    for i, m in enumerate(mods):
+        if isinstance(m, nn.Linear):
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            out.append((m, nxt if isinstance(nxt, _BatchNorm) else None))
+    return out
+
+
+def bn_sync_group(bn):
+    """The SyncBatchNorm process group of a head BatchNorm (None = WORLD); False: no sync."""
+    return bn.process_group if isinstance(bn, nn.SyncBatchNorm) else False
+
 class DINOHead(nn.Module):
     """vision_transformer.py:248-282."""
 
     def __init__(self, in_dim, out_dim, use_bn=False, norm_last_layer=True, nlayers=3, hidden_dim=2048,
                  bottleneck_dim=256):
         super().__init__()
-        if use_bn:
-            raise NotImplementedError("DINOHead(use_bn=True) is not on the DINO-SVT path (default False)")
         nlayers = max(nlayers, 1)
         if nlayers == 1:
             self.mlp = nn.Linear(in_dim, bottleneck_dim)
         else:
-            layers = [nn.Linear(in_dim, hidden_dim), nn.GELU()]
+            # same module order (state-dict keys mlp.0, mlp.1, ...) as the reference
+            layers = [nn.Linear(in_dim, hidden_dim)] + ([nn.BatchNorm1d(hidden_dim)] if use_bn else []) + [nn.GELU()]
             for _ in range(nlayers - 2):
-                layers += [nn.Linear(hidden_dim, hidden_dim), nn.GELU()]
+                layers += [nn.Linear(hidden_dim, hidden_dim)] + ([nn.BatchNorm1d(hidden_dim)] if use_bn else []) + \
+                    [nn.GELU()]
             layers.append(nn.Linear(hidden_dim, bottleneck_dim))
             self.mlp = nn.Sequential(*layers)
         self.apply(self._init_weights)
@@ -218,9 +238,8 @@ class DINOHead(nn.Module):
         if not self.last_layer.weight_v.is_cuda:
             return
         w = self._wcache.getter(self.dsvt_dtype)
-        for m in ([self.mlp] if isinstance(self.mlp, nn.Linear) else self.mlp):
-            if isinstance(m, nn.Linear):
-                w(m.weight)
+        for lin, _ in head_layers(self):
+            w(lin.weight)
 
     def forward(self, x):
         """x [R, in_dim] fp32 -> logits [R, out_dim] fp32 (GELU MLP, L2 normalize, weight-normed
@@ -237,15 +256,21 @@ class DINOHead(nn.Module):
         dev = x.device
         h = torch.empty(R, x.shape[1], device=dev, dtype=mode)
         ops.cast(x, h)
-        linears = [self.mlp] if isinstance(self.mlp, nn.Linear) else [m for m in self.mlp if isinstance(m, nn.Linear)]
+        layers = head_layers(self)
         # R = a few crops' CLS rows: the K-split skinny kernel (a fixed row cap: it streams all of K
         # per 64-row block, so many rows -- head inference over whole videos -- take the tiled kernels)
         few = R <= HEAD_FEW_ROWS
-        for i, lin in enumerate(linears):
-            last = i == len(linears) - 1
-            out = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32 if last else mode)
-            ops.gemm(h, w(lin.weight), lin.bias, out, epilogue=EPI_BIAS if last else EPI_BIAS_GELU, out_f32=last,
-                     few_rows=few)
+        for i, (lin, bn) in enumerate(layers):
+            last = i == len(layers) - 1
+            if bn is not None:          # Linear -> BatchNorm1d -> GELU (use_bn)
+                y = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32)
+                ops.gemm(h, w(lin.weight), lin.bias, y, out_f32=True, few_rows=few)
+                out = torch.empty(R, lin.out_features, device=dev, dtype=mode)
+                ops.bn_gelu(y, bn, out, sync_group=bn_sync_group(bn))
+            else:
+                out = torch.empty(R, lin.out_features, device=dev, dtype=torch.float32 if last else mode)
+                ops.gemm(h, w(lin.weight), lin.bias, out, epilogue=EPI_BIAS if last else EPI_BIAS_GELU,
+                         out_f32=last, few_rows=few)
             h = out
         z = torch.empty(R, h.shape[1], device=dev, dtype=mode)
         ops.head_norm(h, z)                                                   # F.normalize (:280)

@@ -161,6 +161,29 @@ int dsvt_qkv_temporal_attn_fwd(const void *xb, int64_t ldxb, int64_t a_rpg, int6
 int dsvt_ln_fold_qkv_heads(const float *W, const float *gamma, const float *beta, const float *bias, void *Wf,
                            float *wsum, float *bias_f, int64_t heads, int64_t K, void *stream);
 
+/* ------------------------------------------------------------------------------------------
+ * DINOHead(use_bn=True) (vision_transformer.py:255-262, --use_bn_in_head; train_ssl.py:319-321
+ * makes them SyncBatchNorm): Linear -> BatchNorm1d -> GELU per hidden layer.  x [R, D] fp32 is the
+ * Linear's output; sums [2D] fp64 = (column sums, column sums of squares) -- for SyncBatchNorm the
+ * caller all-reduces sums and the row count over the group between dsvt_bn_stats_fwd and
+ * dsvt_bn_finalize.  training = 1: batch statistics (biased variance normalises) and the running
+ * estimates updated in place (unbiased variance, momentum); 0: the running statistics.
+ * dsvt_bn_gelu_fwd: y = GELU_erf((x - mean) * rstd * gamma + beta) in dtype, optionally GELU'(.)
+ * (dtype) and xhat (fp32) for the backward.  Backward from dz = dL/d(BatchNorm output):
+ * dsvt_bn_bwd_sums (sum dz, sum dz * xhat; all-reduced for SyncBatchNorm), then dsvt_bn_bwd:
+ * dx = gamma * rstd * (dz - sum dz / count - xhat * sum(dz xhat) / count) (fp32), dgamma = sum
+ * dz xhat, dbeta = sum dz (nullable, accumulate into them when accumulate != 0).
+ * ------------------------------------------------------------------------------------------ */
+int dsvt_bn_stats_fwd(const float *x, int64_t R, int64_t D, double *sums, void *stream);
+int dsvt_bn_finalize(const double *sums, double count, int64_t D, float eps, float momentum, int training,
+                     float *running_mean, float *running_var, float *mean, float *rstd, void *stream);
+int dsvt_bn_gelu_fwd(int dtype, const float *x, const float *mean, const float *rstd, const float *gamma,
+                     const float *beta, void *y, void *gelu_grad, float *xhat, int64_t R, int64_t D, void *stream);
+int dsvt_bn_bwd_sums(int dtype, const void *dz, const float *xhat, int64_t R, int64_t D, double *sums, void *stream);
+int dsvt_bn_bwd(int dtype, const void *dz, const float *xhat, const double *sums, double count, const float *gamma,
+                const float *rstd, float *dx, float *dgamma, float *dbeta, int accumulate, int64_t R, int64_t D,
+                void *stream);
+
 /* K3: LayerNorm(eps) over rows of fp32 X read through a row map, written compact
  * (rows x C) in dtype (or fp32 when out_f32 bit 0); with out_f32 bit 1 the output rows follow
  * the same row map as the input.  nn.LayerNorm(eps=1e-6) at

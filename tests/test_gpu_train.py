@@ -396,6 +396,66 @@ def test_gelu_save_and_dgelu_epilogues(dtype, tol, M):
     assert rel(dpre.float().cpu(), x.grad.cpu()) < tol
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 4e-2)])
+@pytest.mark.parametrize("nlayers", [2, 3])
+def test_dino_head_use_bn(dtype, tol, nlayers):
+    """DINOHead(use_bn=True) (vision_transformer.py:255-262, --use_bn_in_head): Linear ->
+    BatchNorm1d -> GELU per hidden layer.  Train mode: the dsvt forward (GEMM, batch statistics,
+    GELU) and backward (HeadFn: the BatchNorm backward from the saved xhat) against torch
+    autograd on the same modules in fp32 -- logits, dx, every parameter gradient (BatchNorm
+    gamma / beta included), the updated running statistics and num_batches_tracked; then eval
+    mode (running statistics) against torch.  State-dict keys as the reference's (mlp.1 = the
+    first BatchNorm)."""
+    import copy
+    from dsvt.vision_transformer import DINOHead
+    torch.manual_seed(5)
+    head = DINOHead(192, 512, use_bn=True, nlayers=nlayers, hidden_dim=256, bottleneck_dim=64).cuda()
+    head.dsvt_dtype = dtype
+    assert "mlp.1.running_mean" in head.state_dict() and "mlp.1.weight" in head.state_dict()
+    with torch.no_grad():                                   # non-trivial affine / running stats
+        for m in head.mlp:
+            if isinstance(m, nn.BatchNorm1d):
+                m.weight.copy_(1.0 + 0.2 * torch.randn_like(m.weight))
+                m.bias.copy_(0.1 * torch.randn_like(m.bias))
+                m.running_mean.copy_(0.05 * torch.randn_like(m.running_mean))
+                m.running_var.copy_(1.0 + 0.3 * torch.rand_like(m.running_var))
+    ref_mlp = copy.deepcopy(head.mlp)
+    ll = head.last_layer
+    ref_v = ll.weight_v.detach().clone().requires_grad_(True)
+    ref_g = ll.weight_g.detach().clone()
+
+    def ref_forward(x):
+        z = F.normalize(ref_mlp(x), dim=-1, p=2)
+        return F.linear(z, ref_g * ref_v / ref_v.norm(dim=1, keepdim=True))
+
+    x = torch.randn(48, 192, device="cuda")
+    dl = torch.randn(48, 512, device="cuda")
+    xg = x.clone().requires_grad_(True)
+    out = head(xg)
+    out.backward(dl)
+    xr = x.clone().requires_grad_(True)
+    ref = ref_forward(xr)
+    ref.backward(dl)
+    torch.cuda.synchronize()
+    assert rel(out.detach().cpu(), ref.detach().cpu()) < tol
+    assert rel(xg.grad.cpu(), xr.grad.cpu()) < tol
+    assert rel(ll.weight_v.grad.cpu(), ref_v.grad.cpu()) < tol
+    for m, r in zip(head.mlp, ref_mlp):
+        for name, p in m.named_parameters():
+            assert rel(p.grad.cpu(), getattr(r, name).grad.cpu()) < tol, (m, name)
+        if isinstance(m, nn.BatchNorm1d):
+            assert rel(m.running_mean.cpu(), r.running_mean.cpu()) < 1e-4
+            assert rel(m.running_var.cpu(), r.running_var.cpu()) < 1e-4
+            assert int(m.num_batches_tracked) == int(r.num_batches_tracked) == 1
+    head.eval()
+    ref_mlp.eval()
+    with torch.no_grad():
+        got = head(x)
+        want = ref_forward(x)
+    torch.cuda.synchronize()
+    assert rel(got.cpu(), want.cpu()) < tol
+
+
 def test_head_norm_and_weight_norm_bwd():
     from dsvt import ops
     g = torch.Generator(device="cuda").manual_seed(12)
