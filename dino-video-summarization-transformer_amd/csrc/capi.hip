@@ -359,6 +359,14 @@ int dsvt_pos_bicubic_fwd(const float* pos_embed, float* out, int64_t s, int64_t 
   return e == hipSuccess ? 0 : hip_fail(e, "pos_bicubic");
 }
 
+int dsvt_pos_bicubic_bwd(const float* dout, float* dpos, int64_t s, int64_t OH, int64_t OW, int64_t C, double scale_h,
+                         double scale_w, int accumulate, void* stream) {
+  REQUIRE(dout && dpos && s > 0 && OH > 0 && OW > 0 && C > 0 && scale_h > 0 && scale_w > 0, "pos_bicubic_bwd: bad args");
+  hipError_t e = launch_pos_bicubic_bwd(dout, dpos, s, OH, OW, C, (float)(1.0 / scale_h), (float)(1.0 / scale_w),
+                                        accumulate, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "pos_bicubic_bwd");
+}
+
 int dsvt_attn_temporal_fwd(int dtype, const void* qkv, void* out, int64_t nseq, int64_t T, int64_t heads,
                            int64_t head_dim, float scale, void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_temporal: bad dtype");

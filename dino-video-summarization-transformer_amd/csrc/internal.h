@@ -111,6 +111,8 @@ hipError_t launch_im2col(int dtype, int order_nt, const float* x, void* a, int64
                          hipStream_t s);
 hipError_t launch_pos_bicubic(const float* pos, float* out, int64_t sgrid, int64_t OH, int64_t OW, int64_t C,
                               float inv_scale_h, float inv_scale_w, hipStream_t s);
+hipError_t launch_pos_bicubic_bwd(const float* dout, float* dpos, int64_t sgrid, int64_t OH, int64_t OW, int64_t C,
+                                  float inv_h, float inv_w, int accumulate, hipStream_t s);
 hipError_t launch_cls_init(float* X, const float* cls, const float* pos0, int64_t rows,
                            int64_t row_stride_elems, int64_t C, hipStream_t s);
 hipError_t launch_cls_mean(int dtype, const float* aux, void* out, int64_t B, int64_t T, int64_t L,

@@ -410,6 +410,50 @@ hipError_t launch_pos_bicubic(const float* pos, float* out, int64_t sgrid, int64
   return hipGetLastError();
 }
 
+// Backward of pos_bicubic (the 2-D ViT's interpolate_pos_encoding in training): dpos[1 + n][c]
+// (+)= sum over output cells o of w(o, n) * dout[o][c], w(o, n) = the sum of the forward's
+// stencil weights cy[i] * cx[j] whose (clamped) tap is source cell n; dpos[0] (+)= dout[0].
+// One workgroup per source row, a gather over every output cell: no atomics, one summation order.
+__global__ void pos_bicubic_bwd_kernel(const float* __restrict__ dout, float* __restrict__ dpos, int sg, int OH,
+                                       int OW, int C, float inv_h, float inv_w, int accumulate) {
+  const int n = blockIdx.x;  // 0 = CLS row
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    if (n == 0) {
+      acc = dout[c];
+    } else {
+      const int sy = (n - 1) / sg, sx = (n - 1) % sg;
+      for (int o = 1; o <= OH * OW; ++o) {
+        const int oy = (o - 1) / OW, ox = (o - 1) % OW;
+        const float ry = inv_h * ((float)oy + 0.5f) - 0.5f, rx = inv_w * ((float)ox + 0.5f) - 0.5f;
+        int iy = (int)floorf(ry); iy = iy < sg - 1 ? iy : sg - 1;
+        int ix = (int)floorf(rx); ix = ix < sg - 1 ? ix : sg - 1;
+        const float ty = fminf(fmaxf(ry - iy, 0.f), 1.f), tx = fminf(fmaxf(rx - ix, 0.f), 1.f);
+        float cy[4], cx[4];
+        cubic_coeffs(ty, cy);
+        cubic_coeffs(tx, cx);
+        float wy = 0.f, wx = 0.f;
+        for (int i = 0; i < 4; ++i) {
+          int yy = iy - 1 + i; yy = yy < 0 ? 0 : (yy > sg - 1 ? sg - 1 : yy);
+          if (yy == sy) wy += cy[i];
+          int xx = ix - 1 + i; xx = xx < 0 ? 0 : (xx > sg - 1 ? sg - 1 : xx);
+          if (xx == sx) wx += cx[i];
+        }
+        if (wy != 0.f && wx != 0.f) acc += (wy * wx) * dout[(int64_t)o * C + c];
+      }
+    }
+    float* d = dpos + (int64_t)n * C + c;
+    *d = accumulate ? *d + acc : acc;
+  }
+}
+
+hipError_t launch_pos_bicubic_bwd(const float* dout, float* dpos, int64_t sgrid, int64_t OH, int64_t OW, int64_t C,
+                                  float inv_h, float inv_w, int accumulate, hipStream_t s) {
+  pos_bicubic_bwd_kernel<<<(unsigned)(1 + sgrid * sgrid), 256, 0, s>>>(dout, dpos, (int)sgrid, (int)OH, (int)OW,
+                                                                      (int)C, inv_h, inv_w, accumulate);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- CLS rows
 // X[r*stride + c] = cls[c] + pos0[c]   (timesformer.py:288-305: cat(cls) then + pos_embed[0])
 __global__ void cls_init_kernel(float* __restrict__ X, const float* __restrict__ cls, const float* __restrict__ pos0,

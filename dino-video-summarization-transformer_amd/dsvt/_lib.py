@@ -49,6 +49,7 @@ SIGNATURES = {
     "dsvt_patch_embed_fwd": (_i32, [_i32, _i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p,
                                     _p, _p, _p, _i64, _p, _p, _p, _i64, _p]),
     "dsvt_pos_bicubic_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _p]),
+    "dsvt_pos_bicubic_bwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _f64, _f64, _i32, _p]),
     "dsvt_attn_temporal_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_attn_spatial_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),
     "dsvt_attn_spatial_probs_fwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),

@@ -259,6 +259,12 @@ def pos_bicubic(pos_embed, out, s, OH, OW, scale_h, scale_w):
     return out
 
 
+def pos_bicubic_bwd(dout, dpos, s, OH, OW, scale_h, scale_w, accumulate=False):
+    call("dsvt_pos_bicubic_bwd", _ptr(dout), _ptr(dpos), s, OH, OW, dout.shape[-1], float(scale_h), float(scale_w),
+         int(accumulate), _stream())
+    return dpos
+
+
 def attn_temporal(qkv, out, nseq, T, heads, scale):
     call("dsvt_attn_temporal_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), nseq, T, heads, 64, float(scale), _stream())
     return out

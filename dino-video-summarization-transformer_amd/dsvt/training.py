@@ -21,6 +21,8 @@ masks come from torch.rand on the device in that order, block by block.
 The gradients of every parameter are returned from Function.backward, so autograd's
 accumulation -- and DDP's bucketed all-reduce hooks -- see them like the reference's.
 """
+import math
+
 import numpy as np
 import torch
 
@@ -572,8 +574,17 @@ def _plain_forward(model, srcs, B, T, H, W, Cin, save=True):
         nb, L, order, per_clip = B, 1 + Np * T, TOKENS_NT, 1 + Np * T
     rows = nb * L
     dev = srcs[0][0].device
-    pidx, tidx = model._indices(Hp, Wp, T, dev)
     st = _S()
+    st.pos_interp = None
+    if hasattr(model, "_pos_table"):     # 2-D ViT: bicubic position table (vision_transformer.py:174-194)
+        pos, pidx = model._pos_table(H, W)
+        tidx = None
+        if pos is not model.pos_embed:
+            s = int(math.isqrt(model.pos_embed.shape[1] - 1))
+            st.pos_interp = (s, Hp, Wp, (Hp + 0.1) / s, (Wp + 0.1) / s)
+    else:
+        pos = model.pos_embed
+        pidx, tidx = model._indices(Hp, Wp, T, dev)
     st.mode, st.B, st.T, st.Np, st.L, st.C, st.nb, st.space = mode, B, T, Np, L, C, nb, space
     st.pidx, st.tidx = pidx, tidx
     X = torch.empty(rows, C, device=dev, dtype=torch.float32)
@@ -584,7 +595,7 @@ def _plain_forward(model, srcs, B, T, H, W, Cin, save=True):
         ws = torch.empty(ops.workspace_bytes(WS_PATCH_EMBED, mode, nbs * T * Np, C, K) // 2, device=dev,
                          dtype=torch.bfloat16)
         ops.patch_embed(src.float().contiguous(), w(model.patch_embed.proj.weight, flat=True),
-                        model.patch_embed.proj.bias, model.cls_token, model.pos_embed, pidx,
+                        model.patch_embed.proj.bias, model.cls_token, pos, pidx,
                         None if space else model.time_embed, tidx, X[row0 * per_clip:(row0 + nbs) * per_clip], ws,
                         order, frame_index=fidx, clip_shape=(nbs, T))
         st.im2col.append((row0, nbs, ws.view(mode)[:nbs * T * Np * K].view(nbs * T * Np, K)))
@@ -703,7 +714,14 @@ def _plain_backward(model, st, dfeat, G, ready=None):
     for row0, nbs, a in st.im2col:
         r0 = row0 * Np * T
         wgrad(dP[r0:r0 + nbs * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
-    if space:                            # frame-major rows: the NT map with T = 1 over B*T sequences
+    if space and st.pos_interp is not None:
+        # 2-D ViT at another resolution: the resized table's gradient, then the bicubic map's transpose
+        s, OH, OW, sh, sw = st.pos_interp
+        dtab = torch.zeros(1 + Np, C, device=dev, dtype=torch.float32)
+        ops.embed_bwd(dX, nb, Np, 1, st.pidx, None, dtab, None, G.zeros(model.cls_token))
+        buf, acc = G.acc(model.pos_embed)
+        ops.pos_bicubic_bwd(dtab, buf, s, OH, OW, sh, sw, accumulate=acc)
+    elif space:                          # frame-major rows: the NT map with T = 1 over B*T sequences
         ops.embed_bwd(dX, nb, Np, 1, st.pidx, None, G.zeros(model.pos_embed), None, G.zeros(model.cls_token))
     else:
         ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),

@@ -28,7 +28,12 @@ class PatchEmbed(nn.Module):
 
 
 class VisionTransformer(nn.Module):
-    """vision_transformer.py:134-224 (image ViT; blocks = plain pre-LN ViT blocks)."""
+    """vision_transformer.py:134-224 (image ViT; blocks = plain pre-LN ViT blocks).  Training (the
+    reference's default `--arch vit_small`, train_ssl.py:248-254) runs the space-only TimeSformer
+    training path with one frame (dsvt/training.py _plain_forward / _plain_backward: the same
+    blocks, DropPath per image), the bicubic position table and its backward included."""
+
+    attention_type = 'space_only'       # the training path's block structure (T = 1)
 
     def __init__(self, img_size=[224], patch_size=16, in_chans=3, num_classes=0, embed_dim=768, depth=12,
                  num_heads=12, mlp_ratio=4., qkv_bias=False, qk_scale=None, drop_rate=0., attn_drop_rate=0.,
@@ -101,13 +106,32 @@ class VisionTransformer(nn.Module):
             for lin in (blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2):
                 w(lin.weight)
 
+    def _grad_path(self):
+        """Training-mode forward (DropPath active) or a differentiated one: the training path."""
+        return (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())) or \
+            (self.training and self._drop[2] > 0)
+
+    def _train_forward(self, x):
+        """forward() through dsvt/training.py (space-only path, T = 1): autograd node when anything
+        requires grad, else the masked training forward without saved activations (a teacher in
+        train mode under no_grad)."""
+        if self.training and (self._drop[0] > 0 or self._drop[1] > 0):
+            raise NotImplementedError("training-mode dropout (drop_rate / attn_drop_rate > 0) is not in dsvt; "
+                                      "stochastic depth (drop_path_rate) is")
+        x = x.float().contiguous()
+        B, Cin, H, W = x.shape
+        srcs = [(x.unsqueeze(2), None, B)]
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from .training import BackboneFn
+            return BackboneFn.apply(self, [(srcs, B, 1, H, W, Cin)], *self.parameters())
+        from .training import backbone_forward_nosave
+        return backbone_forward_nosave(self, srcs, B, 1, H, W, Cin)
+
     def _run(self, x, keep_last=0):
         if not x.is_cuda or not self.pos_embed.is_cuda:
             raise DsvtError("dsvt runs only on the GPU (no CPU fallback)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("dsvt backward is not implemented yet: use torch.no_grad()")
-        if self.training and any(r > 0 for r in self._drop):
-            raise NotImplementedError("training-mode dropout / stochastic depth not implemented in dsvt")
+        if self._grad_path():
+            raise NotImplementedError("get_intermediate_layers is an inference export (no training path)")
         x = x.float().contiguous()
         B, Cin, w, h = x.shape
         mode = self.dsvt_dtype
@@ -140,6 +164,10 @@ class VisionTransformer(nn.Module):
 
     def forward(self, x):
         """vision_transformer.py:209-214 -> normed CLS [B, C]."""
+        if not x.is_cuda or not self.pos_embed.is_cuda:
+            raise DsvtError("dsvt runs only on the GPU (no CPU fallback)")
+        if self._grad_path():
+            return self._train_forward(x)
         X, ctx, _ = self._run(x)
         out = torch.empty(ctx.B, self.embed_dim, device=X.device, dtype=torch.float32)
         ops.layernorm(X, ctx.B, self.embed_dim, self.norm.weight, self.norm.bias, self.norm.eps, out,

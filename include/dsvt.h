@@ -224,6 +224,10 @@ int dsvt_patch_embed_fwd(int dtype, int tokens_order, const float *x, int64_t B,
  * s x s patch grid of pos_embed [1+s*s, C] to out [1+OH*OW, C] (row 0 = CLS pos copied). */
 int dsvt_pos_bicubic_fwd(const float *pos_embed, float *out, int64_t s, int64_t OH, int64_t OW,
                          int64_t C, double scale_h, double scale_w, void *stream);
+/* Its backward (2-D ViT training): dpos [1+s*s, C] (+)= the transpose of that linear map applied
+ * to dout [1+OH*OW, C] (fp32; a gather per source cell, no atomics). */
+int dsvt_pos_bicubic_bwd(const float *dout, float *dpos, int64_t s, int64_t OH, int64_t OW, int64_t C,
+                         double scale_h, double scale_w, int accumulate, void *stream);
 
 /* K5: temporal attention of the divided block (models/timesformer.py:127-131 via
  * Attention.forward :68-87).  qkv compact [(nseq*T), 3C] (sequence = (b,n), T rows each),

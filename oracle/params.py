@@ -116,6 +116,28 @@ def dino_head_state(seed, in_dim, out_dim, nlayers=3, hidden_dim=2048, bottlenec
     return sd
 
 
+def dino_head_bn_state(seed, in_dim, out_dim, nlayers=3, hidden_dim=2048, bottleneck_dim=256):
+    """Weights for vision_transformer.py:DINOHead(use_bn=True): Linear / BatchNorm1d / GELU per hidden
+    layer (keys mlp.0, mlp.1 = BatchNorm, mlp.3, ...), non-trivial BatchNorm affine and running stats."""
+    g = rng(seed)
+    sd = {}
+    idx = 0
+    dims = [in_dim] + [hidden_dim] * (nlayers - 1)
+    for i in range(nlayers - 1):
+        _linear(sd, g, "mlp.%d" % idx, hidden_dim, dims[i])
+        p = "mlp.%d." % (idx + 1)
+        sd[p + "weight"] = (1.0 + _normal(g, (hidden_dim,), 0.2)).astype(np.float32)
+        sd[p + "bias"] = _normal(g, (hidden_dim,), 0.1)
+        sd[p + "running_mean"] = _normal(g, (hidden_dim,), 0.05)
+        sd[p + "running_var"] = (1.0 + np.abs(_normal(g, (hidden_dim,), 0.3))).astype(np.float32)
+        sd[p + "num_batches_tracked"] = np.array(0, np.int64)
+        idx += 3
+    _linear(sd, g, "mlp.%d" % idx, bottleneck_dim, hidden_dim)
+    sd["last_layer.weight_g"] = np.ones((out_dim, 1), np.float32)
+    sd["last_layer.weight_v"] = _normal(g, (out_dim, bottleneck_dim), 0.02)
+    return sd
+
+
 def clip(seed, shape, std=1.0):
     """Synthetic decoded+normalized video clip, NCTHW fp32."""
     return _normal(rng(seed), shape, std)

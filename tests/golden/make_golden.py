@@ -151,6 +151,72 @@ def train_grads_plain_cases():
     return out
 
 
+def train_grads_vit2d_cases():
+    """The reference's DEFAULT architecture family (--arch vit_small, train_ssl.py:248-254): the 2-D
+    ViT (vision_transformer.py:134-214; tiny widths: C 64, 1 head, depth 2, 64^2 global crops and
+    32^2 local crops through interpolate_pos_encoding) with DINOHead(use_bn=True) (--use_bn_in_head,
+    BatchNorm in train mode), multi-crop as MultiCropWrapper calls it (one backbone call per
+    resolution), DINOLoss, backward: loss, student logits, every parameter gradient and the
+    BatchNorm running statistics after the step; eval (no DropPath) and DropPath 0.5 (masks recorded
+    in call order through the module-level drop_path of vision_transformer.py)."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29535")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    TL = _extract(os.path.join(REF, "train_ssl.py"), ["DINOLoss"])["DINOLoss"]
+    res = {}
+    for tag, dpr in (("eval", 0.0), ("drop", 0.5)):
+        bb = ref_vit.VisionTransformer(img_size=[64], patch_size=16, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
+                                       qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_path_rate=dpr)
+        _load(bb, P.vit2d_state(1241, embed_dim=64, depth=2, num_heads=1, img_size=64))
+        hd = ref_vit.DINOHead(64, 512, use_bn=True, hidden_dim=128, bottleneck_dim=64)
+        missing, unexpected = hd.load_state_dict(
+            {k: torch.from_numpy(np.asarray(v)) for k, v in
+             P.dino_head_bn_state(1242, 64, 512, hidden_dim=128, bottleneck_dim=64).items()}, strict=True)
+        masks = []
+        gen = torch.Generator().manual_seed(1243)
+        orig = ref_vit.drop_path
+
+        def dp(x, drop_prob=0., training=False):
+            if drop_prob == 0. or not training:
+                return x
+            keep = 1 - drop_prob
+            r = torch.floor(keep + torch.rand((x.shape[0],), generator=gen, dtype=x.dtype))
+            masks.append((r / keep).numpy().astype(np.float32))
+            return x.div(keep) * r.view((x.shape[0],) + (1,) * (x.ndim - 1))
+        ref_vit.drop_path = dp
+        try:
+            if tag == "eval":
+                bb.eval()
+            else:
+                bb.train()
+            hd.train()
+            g_in = [torch.from_numpy(P.clip(1250 + i, (2, 3, 64, 64))) for i in range(2)]
+            l_in = [torch.from_numpy(P.clip(1260 + i, (2, 3, 32, 32))) for i in range(2)]
+            s_out = hd(torch.cat([bb(torch.cat(g_in)), bb(torch.cat(l_in))]))
+            t_out = torch.from_numpy(P.uniform(1270, (4, 512)))
+            lf = TL(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2)
+            loss = lf(s_out, t_out, 0)
+            loss.backward()
+        finally:
+            ref_vit.drop_path = orig
+        res[tag + "_loss"] = np.float32(loss.item())
+        res[tag + "_student"] = s_out.detach().numpy()
+        res[tag + "_teacher"] = t_out.numpy()
+        for k, p in bb.named_parameters():
+            res[tag + "_bb." + k] = p.grad.numpy().copy()
+        for k, p in hd.named_parameters():
+            if p.grad is not None:
+                res[tag + "_hd." + k] = p.grad.numpy().copy()
+        for k, b in hd.named_buffers():
+            res[tag + "_hdbuf." + k] = b.numpy().copy()
+        if masks:
+            res[tag + "_masks"] = np.concatenate(masks)
+            res[tag + "_mask_sizes"] = np.array([len(m) for m in masks], np.int32)
+    return res
+
+
 SWIN_SMALL = dict(embed_dim=64, depths=[2, 2, 2, 2], num_heads=[2, 4, 8, 16])
 
 
@@ -574,7 +640,7 @@ def views_edge_cases():
 
 GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases,
           "train_step_fp16": train_step_fp16_cases, "train_grads_plain": train_grads_plain_cases,
-          "views_edge": views_edge_cases}
+          "views_edge": views_edge_cases, "train_grads_vit2d": train_grads_vit2d_cases}
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:             # regenerate only the named fixture groups

@@ -113,6 +113,79 @@ def test_student_grads_plain_attention(gold_plain, attn, dtype, tag, monkeypatch
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("tag", ["eval", "drop"])
+def test_student_grads_vit2d_bn_head(dtype, tag, monkeypatch):
+    """The reference's default architecture family trains (--arch vit_small, train_ssl.py:248-254):
+    the 2-D ViT (vision_transformer.py:134-214) through the space-only training path with one
+    frame, 64^2 global and 32^2 local crops (the local calls go through interpolate_pos_encoding:
+    the bicubic table and its backward, dsvt_pos_bicubic_bwd), with DINOHead(use_bn=True) (BatchNorm1d
+    in train mode), MultiCropWrapper + DINOLoss -- loss, logits, every parameter gradient and the
+    head's BatchNorm running statistics vs the reference's autograd (tests/golden/
+    train_grads_vit2d.npz), eval and DropPath 0.5 replaying the reference's per-image masks."""
+    from dsvt import training
+    from dsvt.loss import DINOLoss
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead, VisionTransformer
+    gold = dict(np.load("tests/golden/train_grads_vit2d.npz"))
+    if tag == "drop":
+        masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
+        state = {"off": 0, "i": 0}
+
+        def replay(n, p, device):
+            assert n == sizes[state["i"]], (n, sizes[state["i"]])
+            m = masks[state["off"]:state["off"] + n]
+            state["off"] += n
+            state["i"] += 1
+            return torch.from_numpy(m.copy()).to(device)
+        monkeypatch.setattr(training, "_keep_scale", replay)
+    bb = VisionTransformer(img_size=[64], patch_size=16, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
+                           qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                           drop_path_rate=0.5 if tag == "drop" else 0.0)
+    bb.load_state_dict({k: torch.from_numpy(v) for k, v in
+                        P.vit2d_state(1241, embed_dim=64, depth=2, num_heads=1, img_size=64).items()})
+    hd = DINOHead(64, 512, use_bn=True, hidden_dim=128, bottleneck_dim=64)
+    hd.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                        P.dino_head_bn_state(1242, 64, 512, hidden_dim=128, bottleneck_dim=64).items()})
+    bb.dsvt_dtype = hd.dsvt_dtype = dtype
+    net = MultiCropWrapper(bb, hd).cuda()
+    net.train()
+    if tag == "eval":
+        bb.eval()
+    crops = [torch.from_numpy(P.clip(1250 + i, (2, 3, 64, 64))).cuda() for i in range(2)] + \
+            [torch.from_numpy(P.clip(1260 + i, (2, 3, 32, 32))).cuda() for i in range(2)]
+    s_out = net(crops)
+    t_out = torch.from_numpy(gold[tag + "_teacher"]).cuda()
+    loss_fn = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    loss = loss_fn(s_out, t_out, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert abs(loss.item() - float(gold[tag + "_loss"])) < tol * abs(float(gold[tag + "_loss"]))
+    assert rel(s_out.detach().cpu().numpy(), gold[tag + "_student"]) < tol
+    named = [("bb." + k, p) for k, p in net.backbone.named_parameters()] + \
+            [("hd." + k, p) for k, p in net.head.named_parameters()]
+    checked = 0
+    for k, p in named:
+        key = tag + "_" + k
+        if key not in gold:
+            assert p.grad is None or not p.requires_grad, k
+            continue
+        assert p.grad is not None, k
+        err = rel(p.grad.cpu().numpy(), gold[key])
+        assert err < tol, "%s grad rel err %.3g" % (k, err)
+        checked += 1
+    for k, b in net.head.named_buffers():
+        want = gold[tag + "_hdbuf." + k]
+        if b.dtype == torch.int64:
+            assert int(b) == int(want), k
+        else:
+            assert rel(b.cpu().numpy(), want) < 1e-4, k
+    if tag == "drop":
+        assert state["i"] == len(sizes), "mask draws %d of %d" % (state["i"], len(sizes))
+    assert checked >= 24
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tag", ["eval", "drop"])
 @pytest.mark.parametrize("tail", [True, False])
 def test_student_grads_match_reference(gold, dtype, tag, tail, monkeypatch):
     """loss.backward() through MultiCropWrapper(TimeSformer divided, DINOHead) + DINOLoss: loss,

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 tests/test_gpu_kernels
 tail -1 gpurun_out/t6.log
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 tests/test_gpu_model.py > gpurun_out/t8.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t8.log | tail -30; exit 1; }
 tail -1 gpurun_out/t8.log
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 tests/test_gpu_train.py -k "gelu or grads_match or train_steps or cls_bwd or use_bn" > gpurun_out/t7.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t7.log | tail -30; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 tests/test_gpu_train.py -k "gelu or grads_match or train_steps or cls_bwd or use_bn or vit2d" > gpurun_out/t7.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t7.log | tail -30; exit 1; }
 tail -1 gpurun_out/t7.log
 DSVT_SHAPES=proj_g,fc2_g,proj_l,fc2_l DSVT_CUSTOM="proj_l:13872:768:768:2,fc2_l:13872:768:3072:2" timeout -k 10 300 python tools/gemm_bench.py 20 30 1 > gpurun_out/gb5.log 2>&1 || { tail -20 gpurun_out/gb5.log; exit 1; }
 tail -5 gpurun_out/gb5.log
