@@ -248,6 +248,29 @@ def swin_outputs():
     return res
 
 
+SWIN_BASE = dict(embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32])
+
+
+def swin_base_cases():
+    """The Swin config train_ssl.py builds for --arch swin (:237-239: SwinTransformer3D(depths=[2, 2,
+    18, 2], embed_dim=128, num_heads=[4, 8, 16, 32]), i.e. Swin-B): reference forward (eval) on an
+    8 x 224^2 clip, seeded weights (oracle/params.swin_state)."""
+    import models.vit_utils as ref_vu
+    for name in ("timm", "timm.models", "timm.models.layers"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["timm.models.layers"].DropPath = ref_vu.DropPath
+    sys.modules["timm.models.layers"].trunc_normal_ = ref_vu.trunc_normal_
+    import models.swin_transformer as ref_swin
+    m = ref_swin.SwinTransformer3D(**SWIN_BASE)
+    sd = P.swin_state(1304, {k: v.shape for k, v in m.state_dict().items()})
+    missing, unexpected = m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and all("relative_position_index" in k for k in missing)
+    m.eval()
+    with torch.no_grad():
+        out = m(torch.from_numpy(P.clip(1314, (1, 3, 8, 224, 224)))).numpy()
+    return {"base": out, "keys_base": np.array(sorted(m.state_dict().keys()))}
+
+
 def run(m, x, **kw):
     with torch.no_grad():
         return m.forward_features(torch.from_numpy(x), **kw).numpy()
@@ -640,7 +663,8 @@ def views_edge_cases():
 
 GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases,
           "train_step_fp16": train_step_fp16_cases, "train_grads_plain": train_grads_plain_cases,
-          "views_edge": views_edge_cases, "train_grads_vit2d": train_grads_vit2d_cases}
+          "views_edge": views_edge_cases, "train_grads_vit2d": train_grads_vit2d_cases,
+          "swin_base": swin_base_cases}
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:             # regenerate only the named fixture groups

@@ -44,6 +44,34 @@ def test_train_returns_none_like_reference():
     assert m.train() is None and m.eval() is None      # SURVEY §5 defect 6, kept for drop-in parity
 
 
+SWIN_BASE = dict(embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32])
+
+
+def test_swin_base_keys_match_reference():
+    """The Swin-B that train_ssl.py:237-239 builds for --arch swin: same state-dict keys as the
+    reference's (tests/golden/swin_base.npz)."""
+    from dsvt.models import SwinTransformer3D
+    gold = dict(np.load("tests/golden/swin_base.npz"))
+    assert sorted(SwinTransformer3D(**SWIN_BASE).state_dict()) == [str(k) for k in gold["keys_base"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_swin_base_forward_vs_reference(dtype):
+    """Swin-B (train_ssl.py:237-239, 24 blocks, C = 128..1024) on an 8 x 224^2 clip vs the
+    reference's forward (tests/golden/swin_base.npz)."""
+    gold = dict(np.load("tests/golden/swin_base.npz"))
+    m = _model(SWIN_BASE, 1304, dtype)
+    x = torch.from_numpy(P.clip(1314, (1, 3, 8, 224, 224))).cuda()
+    with torch.no_grad():
+        out = m(x)
+    torch.cuda.synchronize()
+    got, ref = out.cpu().numpy(), gold["base"]
+    assert got.shape == ref.shape
+    err = np.max(np.abs(got - ref)) / np.max(np.abs(ref))
+    assert err < TOL[dtype], err
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("tag,kw,shape,seed", [("small", SMALL, (2, 3, 8, 64, 64), 1301),

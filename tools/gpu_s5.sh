@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 tests/test_gpu_kernels.py -k "resid or stats or temporal_attn or bias_gelu or rowscale" > gpurun_out/t6.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t6.log | tail -30; exit 1; }
 tail -1 gpurun_out/t6.log
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 tests/test_gpu_model.py > gpurun_out/t8.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t8.log | tail -30; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 tests/test_gpu_model.py tests/test_gpu_swin.py > gpurun_out/t8.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t8.log | tail -30; exit 1; }
 tail -1 gpurun_out/t8.log
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 tests/test_gpu_train.py -k "gelu or grads_match or train_steps or cls_bwd or use_bn or vit2d" > gpurun_out/t7.log 2>&1 || { grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/t7.log | tail -30; exit 1; }
 tail -1 gpurun_out/t7.log
