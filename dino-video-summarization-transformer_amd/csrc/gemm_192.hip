@@ -83,14 +83,17 @@ __device__ __forceinline__ void resid192_rows(const GemmParams& p, fv4 (&acc)[4]
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int64_t orow = orow_of(i);
+    // training DropPath (dsvt_gemm_resid_scaled_fwd): A carries the row's scale, the bias takes it here
+    const float rs = p.row_scale ? row_scale_of(p, FULL ? rbase + i * 16 + r16 : min(rbase + i * 16 + r16, p.M - 1))
+                                 : 1.0f;
     fv4 v[NJ];
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const float4 xv = x[i % W][j];
       const float4 bb = bias4[j];
-      v[j] = fv4{xv.x + (acc[i][j][0] + bb.x), xv.y + (acc[i][j][1] + bb.y), xv.z + (acc[i][j][2] + bb.z),
-                 xv.w + (acc[i][j][3] + bb.w)};
+      v[j] = fv4{xv.x + (acc[i][j][0] + bb.x * rs), xv.y + (acc[i][j][1] + bb.y * rs),
+                 xv.z + (acc[i][j][2] + bb.z * rs), xv.w + (acc[i][j][3] + bb.w * rs)};
       if constexpr (STATS) {
         s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
         q += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
@@ -476,10 +479,11 @@ __global__ __launch_bounds__(512, 1) void gemm_192_kernel(GemmParams p) {
 #undef Q_COMPUTE
 }
 
-// the fp32 residual epilogue only (bias added in the epilogue, no DropPath row scales), N a
-// multiple of 192 with 16-byte aligned rows, K a multiple of 64, 32-bit LDS-DMA source offsets
+// the fp32 residual epilogue only (bias added in the epilogue, times the DropPath row scale when
+// p.row_scale), N a multiple of 192 with 16-byte aligned rows, K a multiple of 64, 32-bit LDS-DMA
+// source offsets
 bool gemm_192_ok(const GemmParams& p, int epi) {
-  return epi == EPI_RESID && !p.row_scale && p.K >= 64 && p.K % 64 == 0 && p.M >= 1 && p.N >= 192 &&
+  return epi == EPI_RESID && !(p.stats_out && p.row_scale) && p.K >= 64 && p.K % 64 == 0 && p.M >= 1 && p.N >= 192 &&
          p.N % 192 == 0 && p.ldo % 4 == 0 && ((uintptr_t)p.out & 15) == 0 && ((uintptr_t)resid_src(p) & 15) == 0 &&
          (!p.bias || ((uintptr_t)p.bias & 15) == 0) && (p.M - 1) * p.lda * 2 + p.K * 2 <= (int64_t)UINT32_MAX &&
          (p.N - 1) * p.ldw * 2 + p.K * 2 <= (int64_t)UINT32_MAX;
@@ -495,7 +499,7 @@ static dim3 grid_192(const GemmParams& p) {
 
 hipError_t launch_gemm_192(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
   if (!out_f32 || !gemm_192_ok(p, epi)) return hipErrorInvalidValue;
-  if (p.stats_out && (!p.xb_out || p.N != LN_PARTS * 64)) return hipErrorInvalidValue;
+  if (p.stats_out && (!p.xb_out || p.N != LN_PARTS * 64 || p.row_scale)) return hipErrorInvalidValue;
   if (p.stats_out) gemm_192_kernel<MODE_RESID_STATS><<<grid_192(p), dim3(512), 0, s>>>(p);
   else gemm_192_kernel<MODE_RESID><<<grid_192(p), dim3(512), 0, s>>>(p);
   return hipGetLastError();

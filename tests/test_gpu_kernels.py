@@ -494,7 +494,8 @@ def test_gemm_resid_scaled_bias(dtype, M, K):
     """dsvt_gemm_resid_scaled_fwd (training DropPath): x_out = x_in + A.W^T + s[m] * bias with
     A already scaled, against float64; s includes dropped rows (0) and 1/keep rows; x_in intact.
     The last two shapes (>= 128 tiles of 256x256, the last one ragged) also run the 256x256
-    kernel's row-scaled residual epilogue in bf16 (variant 20, opt-in in the product)."""
+    kernel's row-scaled residual epilogue in bf16 (variant 20, opt-in in the product); bf16 runs
+    the 256x192 kernel's (variant 30) at every shape."""
     from dsvt import _lib, ops
     N = 768 if K != 192 else 192
     a, w, b = rnd((M, K), 31), rnd((N, K), 32, 0.03), rnd((N,), 33)
@@ -505,7 +506,7 @@ def test_gemm_resid_scaled_bias(dtype, M, K):
     X_in = to(x0, torch.float32)
     X_out = torch.full_like(X_in, 7.0)
     ref = x0.astype(np.float64) + back(A).astype(np.float64) @ back(W).astype(np.float64).T + s[:, None] * b
-    for v in ([0, 20] if M > 10000 and dtype == torch.bfloat16 else [0]):
+    for v in ([0, 20, 30] if M > 10000 and dtype == torch.bfloat16 else [0, 30] if dtype == torch.bfloat16 else [0]):
         X_out.fill_(7.0)
         _lib.call("dsvt_set_gemm_variant", v)
         try:
