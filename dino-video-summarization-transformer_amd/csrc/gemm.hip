@@ -334,7 +334,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
   int gv = g_gemm_variant;
-  if (gv == 30 && !(out_f32 && !p.ln_stats && gemm_192_ok(p, epi))) gv = 0;   // forced, ineligible: auto
+  if (gv == 30 && !(!p.ln_stats && gemm_192_ok(p, epi))) gv = 0;   // forced, ineligible: auto
   // DSVT_GEMM_FEW_ROWS call sites (the CLS-only tail's and the DINO head's few-row GEMMs, chosen
   // by call site so that a batch split over streams picks the same kernel as the whole batch):
   // the K-split skinny kernel (variant 50 forces it where eligible) -- bench 397.7-398.7 vs
@@ -345,7 +345,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 #ifndef DSVT_RESID192
 #define DSVT_RESID192 0
 #endif
-  if (DSVT_RESID192 && gv == 0 && epi == EPI_RESID && out_f32 && !p.ln_stats && p.M >= 4096 && gemm_192_ok(p, epi))
+  if (DSVT_RESID192 && gv == 0 && !p.ln_stats && p.M >= 4096 && gemm_192_ok(p, epi))
     return 30;
   // the LayerNorm-folded A operand (dsvt_gemm_lnx_fwd) and the residual epilogue that writes
   // the next LayerNorm's row statistics (dsvt_gemm_resid_stats_fwd): the 256x256 kernel only

@@ -498,7 +498,8 @@ static dim3 grid_192(const GemmParams& p) {
 }
 
 hipError_t launch_gemm_192(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
-  if (!out_f32 || !gemm_192_ok(p, epi)) return hipErrorInvalidValue;
+  (void)out_f32;                                      // EPI_RESID: fp32 X whatever the flag says
+  if (!gemm_192_ok(p, epi)) return hipErrorInvalidValue;
   if (p.stats_out && (!p.xb_out || p.N != LN_PARTS * 64 || p.row_scale)) return hipErrorInvalidValue;
   if (p.stats_out) gemm_192_kernel<MODE_RESID_STATS><<<grid_192(p), dim3(512), 0, s>>>(p);
   else gemm_192_kernel<MODE_RESID><<<grid_192(p), dim3(512), 0, s>>>(p);
