@@ -403,10 +403,13 @@ def test_qkv_temporal_attn(B, Np):
     p = np.exp(s - s.max(-1, keepdims=True))
     p /= p.sum(-1, keepdims=True)
     ref = (p @ v).transpose(0, 2, 1, 3).reshape(R, C)
-    check(back(outs[0]), ref, torch.bfloat16, "qkv_temporal_attn")
-    check(back(o_ref), ref, torch.bfloat16, "unfused")
+    # both paths round q / k / v to bf16 after the folded LayerNorm (whose error grows with the row's
+    # mean over its spread, see test_gemm_lnx) and the output to bf16: the bf16 golden bar (2e-2)
+    # against float64, and fused vs unfused within 1e-2
+    errs = [np.abs(back(o).astype(np.float64) - ref).max() / np.abs(ref).max() for o in (outs[0], o_ref)]
+    assert errs[0] < 2e-2 and errs[1] < 2e-2, errs
     d = np.abs(back(outs[0]).astype(np.float64) - back(o_ref)).max() / np.abs(ref).max()
-    assert d < 1e-2, d
+    assert d < 1e-2, (d, errs)
 
 
 @pytest.mark.parametrize("B,Np,T", [(2, 5, 3), (16, 196, 8), (48, 36, 8)])
