@@ -943,71 +943,6 @@ def test_attn_spatial_short_local_shape(variant):
     check(back(outs[0]), spatial_ref(back(Q), B, T, L, heads, 0.125), torch.bfloat16, "spatial v%d" % variant)
 
 
-# ------------------------------------------------------------------ fused residual GEMM + LayerNorm
-@pytest.mark.parametrize("case", ["ident_x", "patchmap_x", "compact", "none", "bench_g", "bench_l"])
-def test_gemm_resid_ln(case):
-    """csrc/gemm_rowln.hip: X[row(m)] += A[m].W^T + b over full 768-column rows, then the LayerNorm
-    of the updated rows in bf16 (Y), against a float64 reference from the same bf16 operands.
-    Cases: identity rows (attn.proj -> norm2), patch-row map (the folded temporal_fc -> norm1),
-    compact patch-row output skipping CLS rows (mlp.fc2 -> next temporal_norm1, K = 3072), no
-    LayerNorm, and the bench's 25 104 / 13 872-row calls (7 / 4 units per workgroup), which
-    must also be bitwise repeatable.  Rows outside the map and CLS rows of Y stay untouched."""
-    import torch.nn as tnn
-    from dsvt import ops
-    from dsvt._lib import ROWLN_COMPACT, ROWLN_NONE, ROWLN_X
-    C = 768
-    B, Np, T = {"ident_x": (3, 5, 4), "patchmap_x": (2, 7, 3), "compact": (3, 4, 5), "none": (1, 9, 2),
-                "bench_g": (16, 196, 8), "bench_l": (48, 36, 8)}[case]
-    L = 1 + Np * T
-    rows, R = B * L, B * Np * T
-    K = 3072 if case in ("compact", "bench_g") else 768
-    mapped = case == "patchmap_x"
-    M = R if mapped else rows
-    ymode = {"ident_x": ROWLN_X, "patchmap_x": ROWLN_X, "compact": ROWLN_COMPACT, "none": ROWLN_NONE,
-             "bench_g": ROWLN_X, "bench_l": ROWLN_COMPACT}[case]
-    gen = torch.Generator(device="cuda").manual_seed(23)
-    A = torch.randn(M, K, device="cuda", generator=gen).to(torch.bfloat16)
-    W = (torch.randn(C, K, device="cuda", generator=gen) * K ** -0.5).to(torch.bfloat16)
-    bias = torch.randn(C, device="cuda", generator=gen) * 0.1
-    X0 = torch.randn(rows, C, device="cuda", generator=gen) * 2 + 0.3
-    ln = tnn.LayerNorm(C, eps=1e-6).cuda()
-    with torch.no_grad():
-        ln.weight.copy_(1 + 0.1 * torch.randn(C, device="cuda", generator=gen))
-        ln.bias.copy_(0.1 * torch.randn(C, device="cuda", generator=gen))
-    ny = R if ymode == ROWLN_COMPACT else rows
-    outs = []
-    for _ in range(2 if case.startswith("bench") else 1):
-        X = X0.clone()
-        Y = torch.full((ny, C), 3.0, device="cuda", dtype=torch.bfloat16)
-        ops.gemm_resid_ln(A, W, bias, X, M=M, rowmap=(Np * T, L, 1) if mapped else None,
-                          ln=None if ymode == ROWLN_NONE else ln, Y=Y, ymode=ymode, L=L)
-        outs.append((X, Y))
-    torch.cuda.synchronize()
-    X, Y = outs[0]
-    if len(outs) > 1:
-        assert torch.equal(outs[1][0], X) and torch.equal(outs[1][1], Y), "repeat launches differ"
-    xrows = torch.arange(M, device="cuda")
-    if mapped:
-        xrows = (xrows // (Np * T)) * L + 1 + xrows % (Np * T)
-    ref = X0.double().clone()
-    ref[xrows] += A.double() @ W.double().t() + bias.double()
-    err_x = ((X.double() - ref).abs().max() / ref.abs().max()).item()
-    assert err_x < 1e-5, err_x
-    if ymode == ROWLN_NONE:
-        assert torch.all(Y == 3.0)
-        return
-    yref = torch.nn.functional.layer_norm(ref, (C,), ln.weight.double(), ln.bias.double(), 1e-6).detach()
-    if ymode == ROWLN_COMPACT:
-        keep = torch.arange(rows, device="cuda") % L != 0
-        yref = yref[keep]
-        check(back(Y), yref.cpu().numpy(), torch.bfloat16, "resid_ln compact")
-        return
-    upd = torch.zeros(rows, dtype=torch.bool, device="cuda")
-    upd[xrows] = True
-    check(back(Y[upd]), yref[upd].cpu().numpy(), torch.bfloat16, "resid_ln")
-    assert torch.all(Y[~upd] == 3.0)
-
-
 def test_layernorm_mapped_output():
     """dsvt_layernorm_fwd with out_f32 bit 1: the output rows follow the input row map (the CLS
     rows' norm1 written into their own rows of the full-layout LN buffer)."""
