@@ -50,6 +50,14 @@ __device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
 }
 __device__ __forceinline__ int pair_off(int g) { return ((g & 1) << 4) | ((g >> 1) << 3); }
 
+// x0^2 + x1^2 + x2^2 + x3^2 as (fma(x0, x0, x1 x1)) + (fma(x2, x2, x3 x3)): written out so that no
+// template instantiation can contract it differently (-ffp-contract=fast lets the compiler fuse a
+// product into a neighbouring add where it likes; LayerNorm statistics must be the same bits
+// whichever kernel instantiation -- full or ragged tile -- produced a row)
+__device__ __forceinline__ float sumsq4(float x0, float x1, float x2, float x3) {
+  return __builtin_fmaf(x0, x0, x1 * x1) + __builtin_fmaf(x2, x2, x3 * x3);
+}
+
 // sum over a lane's four 16-lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48) by two VALU permlane
 // swaps (no LDS traffic); every lane gets the same bits: (x0 + x2) + (x1 + x3) in one order
 __device__ __forceinline__ float sum_lane_groups(float v) {

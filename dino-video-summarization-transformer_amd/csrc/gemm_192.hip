@@ -96,7 +96,7 @@ __device__ __forceinline__ void resid192_rows(const GemmParams& p, fv4 (&acc)[4]
                  xv.z + (acc[i][j][2] + bb.z * rs), xv.w + (acc[i][j][3] + bb.w * rs)};
       if constexpr (STATS) {
         s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-        q += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
+        q += sumsq4(v[j][0], v[j][1], v[j][2], v[j][3]);
       }
     }
     if (i + W < MI) load_row(i + W);

@@ -465,7 +465,7 @@ __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ
       s = sum_lane_groups(s);
       q = sum_lane_groups(q);
       const float m_ = s * invk;
-      const float var = fmaxf(q * invk - m_ * m_, 0.f);
+      const float var = fmaxf(__builtin_fmaf(-m_, m_, q * invk), 0.f);   // explicit: no contraction freedom
       rs[i0 + ii] = 1.0f / sqrtf(var + p.ln_eps);
       mu[i0 + ii] = -m_ * rs[i0 + ii];
     }
@@ -525,7 +525,7 @@ __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)
       const float4 xv = x[i % W][j];
       v[j] = fv4{xv.x + acc[i][j][0], xv.y + acc[i][j][1], xv.z + acc[i][j][2], xv.w + acc[i][j][3]};
       s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-      q += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
+      q += sumsq4(v[j][0], v[j][1], v[j][2], v[j][3]);
     }
     if (i + W < MI) load_row(i + W);
     s = sum_lane_groups(s);

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void ln_stats768_kernel(const float* __restric
       store4(xb + r * C + i * 256 + lane * 4, v[i].x, v[i].y, v[i].z, v[i].w);
       // lanes 16q .. 16q + 15 of chunk i hold slab 4i + q
       float s = (v[i].x + v[i].y) + (v[i].z + v[i].w);
-      float q = (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+      float q = sumsq4(v[i].x, v[i].y, v[i].z, v[i].w);
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
         s += __shfl_xor(s, o);
