@@ -92,8 +92,9 @@ __device__ __forceinline__ void resid192_rows(const GemmParams& p, fv4 (&acc)[4]
     for (int j = 0; j < NJ; ++j) {
       const float4 xv = x[i % W][j];
       const float4 bb = bias4[j];
-      v[j] = fv4{xv.x + (acc[i][j][0] + bb.x * rs), xv.y + (acc[i][j][1] + bb.y * rs),
-                 xv.z + (acc[i][j][2] + bb.z * rs), xv.w + (acc[i][j][3] + bb.w * rs)};
+      // explicit fma: the same bits in the full- and ragged-tile instantiations
+      v[j] = fv4{xv.x + __builtin_fmaf(bb.x, rs, acc[i][j][0]), xv.y + __builtin_fmaf(bb.y, rs, acc[i][j][1]),
+                 xv.z + __builtin_fmaf(bb.z, rs, acc[i][j][2]), xv.w + __builtin_fmaf(bb.w, rs, acc[i][j][3])};
       if constexpr (STATS) {
         s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
         q += sumsq4(v[j][0], v[j][1], v[j][2], v[j][3]);
