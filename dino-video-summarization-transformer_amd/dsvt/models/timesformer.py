@@ -502,12 +502,13 @@ class VisionTransformer(nn.Module):
             args.append(([(c, None, c.shape[0]) for c in clips], sum(c.shape[0] for c in clips), T, H, W, Cin))
         return BackboneFn.apply(self, args, *self.parameters())
 
-    def forward_frame_bank(self, frames, frame_index, B, T, get_all=False, out=None):
+    def forward_frame_bank(self, frames, frame_index, B, T, get_all=False, out=None, lnx=None):
         """Clips gathered from a frame bank [F, Cin, H, W] by frame_index [B*T] int32 (-1 =
         zero frame) inside the patch-embed kernel (frame scoring: the per-frame local/global
-        views of dino_loss_loader.py:126-171 are never materialized)."""
+        views of dino_loss_loader.py:126-171 are never materialized).  lnx: the LayerNorm-fold
+        choice (None = the model's)."""
         _, Cin, H, W = frames.shape
-        return self._forward_sources([(frames, frame_index, B)], B, T, H, W, Cin, get_all, False, out)
+        return self._forward_sources([(frames, frame_index, B)], B, T, H, W, Cin, get_all, False, out, lnx=lnx)
 
     def _forward_sources(self, srcs, B, T, H, W, Cin, get_all, get_attn, out, lnx=None):
         for src, _, _ in srcs:

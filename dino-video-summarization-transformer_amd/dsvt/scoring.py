@@ -110,6 +110,11 @@ class FrameScorer:
         self.frames_per_call = frames_per_call
         self.crop_size = crop_size if crop_size is not None else model.patch_embed.img_size[0]
         self._views = {}
+        # no LayerNorm folding: a frame's score is a difference of two close losses (the pairwise
+        # DINO loss of its local and global views), so the fold's extra bf16 rounding of the
+        # un-centred rows (error ~ sqrt(1 + mu^2 / sigma^2)) shows: bf16 scores measured 2.9e-2
+        # of max vs the fp32 oracle with it, inside the 2e-2 bar without
+        self.lnx = False
 
     @torch.no_grad()
     def dummy_scores(self, device):
@@ -118,9 +123,10 @@ class FrameScorer:
         c = self.crop_size
         bank = torch.zeros(1, 3, c, c, device=device)
         ts = min(self.local_clip_size, DUMMY_FRAMES)
-        st = self.model.forward_frame_bank(bank, torch.zeros(ts, dtype=torch.int32, device=device), 1, ts)
+        st = self.model.forward_frame_bank(bank, torch.zeros(ts, dtype=torch.int32, device=device), 1, ts,
+                                           lnx=self.lnx)
         te = self.model.forward_frame_bank(bank, torch.zeros(DUMMY_FRAMES, dtype=torch.int32, device=device), 1,
-                                           DUMMY_FRAMES)
+                                           DUMMY_FRAMES, lnx=self.lnx)
         return self.loss.per_row(st, te).expand(self.global_clip_size).contiguous()
 
     @torch.no_grad()
@@ -142,8 +148,8 @@ class FrameScorer:
         for s0 in range(0, F, n):
             s1 = min(F, s0 + n)
             b = s1 - s0
-            st = self.model.forward_frame_bank(frames, li_t[s0:s1].reshape(-1), b, ts)
-            te = self.model.forward_frame_bank(frames, gi_t[s0:s1].reshape(-1), b, G)
+            st = self.model.forward_frame_bank(frames, li_t[s0:s1].reshape(-1), b, ts, lnx=self.lnx)
+            te = self.model.forward_frame_bank(frames, gi_t[s0:s1].reshape(-1), b, G, lnx=self.lnx)
             scores[s0:s1] = self.loss.per_row(st, te)
         return scores
 
