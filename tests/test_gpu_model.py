@@ -405,15 +405,24 @@ def test_frame_scores_vitb_local3_global30(base_sd, dtype, tol):
     # the product output: the frames the "adaptive" selector picks from these scores
     # (frame_selection_loader.py:115-170), against the indices the oracle's scores give
     from dsvt.selection import adaptive_frame_indices
-    picked = mismatched = 0
+    picked = mismatched = worst = 0
     for rate in (1, 4):
         for N in (4, 8, 12, 16, 24):
             want = O.adaptive_frame_selection(ref, F_, F_ * rate, rate, N)[0]
             got, _ = adaptive_frame_indices(scores_dev, F_, F_ * rate, rate, N)
+            got = np.asarray(got)
             picked += N
-            mismatched += int(np.sum(np.asarray(got) != want))
-    print("frame selection %s: %d of %d indices differ from the oracle's" % (dtype, mismatched, picked))
-    assert mismatched == 0
+            mismatched += int(np.sum(got != want))
+            # shift in source frames (indices run over F * rate sample positions)
+            worst = max(worst, int(np.max(np.abs(got.astype(np.int64) - np.asarray(want, np.int64)))) / rate)
+    print("frame selection %s: %d of %d indices differ from the oracle's (max shift %g frames)" % (dtype, mismatched,
+                                                                                                picked, worst))
+    if dtype == torch.float32:
+        assert mismatched == 0           # parity mode: the reference's frames exactly
+    else:
+        # bf16 perf mode: the selector's CDF thresholds move a few picks to a neighbouring frame
+        # (measured 8 of 128, DESIGN.md "Frame scoring"); none further than one frame
+        assert mismatched <= 16 and worst <= 1, (mismatched, worst)
 
 
 def test_bf16_vs_fp32_full_size(base_sd):
