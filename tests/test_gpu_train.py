@@ -163,6 +163,11 @@ def test_student_grads_vit2d_bn_head(dtype, tag, monkeypatch):
     assert rel(s_out.detach().cpu().numpy(), gold[tag + "_student"]) < tol
     named = [("bb." + k, p) for k, p in net.backbone.named_parameters()] + \
             [("hd." + k, p) for k, p in net.head.named_parameters()]
+    # BatchNorm in train mode removes any shift common to the batch rows, so the gradients of
+    # the biases in front of it (the backbone's final-norm bias, each hidden Linear's bias) are
+    # zero analytically -- the reference's are rounding noise (~1e-7 of the gradient scale):
+    # those are checked absolutely against that scale instead of relatively
+    scale = max(float(np.abs(gold[k]).max()) for k in gold if k.startswith(tag + "_bb.") or k.startswith(tag + "_hd."))
     checked = 0
     for k, p in named:
         key = tag + "_" + k
@@ -170,8 +175,11 @@ def test_student_grads_vit2d_bn_head(dtype, tag, monkeypatch):
             assert p.grad is None or not p.requires_grad, k
             continue
         assert p.grad is not None, k
-        err = rel(p.grad.cpu().numpy(), gold[key])
-        assert err < tol, "%s grad rel err %.3g" % (k, err)
+        if float(np.abs(gold[key]).max()) < 1e-5 * scale:
+            assert float(p.grad.abs().max()) < tol * scale, (k, float(p.grad.abs().max()), scale)
+        else:
+            err = rel(p.grad.cpu().numpy(), gold[key])
+            assert err < tol, "%s grad rel err %.3g" % (k, err)
         checked += 1
     for k, b in net.head.named_buffers():
         want = gold[tag + "_hdbuf." + k]
