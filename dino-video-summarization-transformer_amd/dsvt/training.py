@@ -713,7 +713,10 @@ def _plain_backward(model, st, dfeat, G, ready=None):
     conv = model.patch_embed.proj
     for row0, nbs, a in st.im2col:
         r0 = row0 * Np * T
-        wgrad(dP[r0:r0 + nbs * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
+        wgrad(dP[r0:r0 + nbs * Np * T], a, G, conv.weight, view=(C, -1))
+    # the conv bias: an exact fp32 column sum of the patch rows of dX (not of their bf16 copy: with
+    # the BatchNorm head the rows' gradients largely cancel and the bf16 sum showed 4e-2)
+    _colsum(dX, G, conv.bias, rows=R, rowmap=patch_map)
     if space and st.pos_interp is not None:
         # 2-D ViT at another resolution: the resized table's gradient, then the bicubic map's transpose
         s, OH, OW, sh, sw = st.pos_interp
