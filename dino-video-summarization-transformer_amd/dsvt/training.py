@@ -850,11 +850,13 @@ def _head_backward(head, st, dlogits):
             wgrad(gb, st.a[i], G, lin.weight)
             _colsum(g, G, lin.bias)
         if i > 0:
-            nxt = torch.empty(R, lin.in_features, device=dev, dtype=mode)
-            ops.gemm_aux(gb, wt(lin.weight), None, nxt, st.pre[i - 1], EPI_DGELU)
+            # into a BatchNorm's backward: dz in fp32 (its batch-mean subtractions cancel most of dz)
+            bn_prev = st.bn[i - 1]
+            nxt = torch.empty(R, lin.in_features, device=dev, dtype=torch.float32 if bn_prev is not None else mode)
+            ops.gemm_aux(gb, wt(lin.weight), None, nxt, st.pre[i - 1], EPI_DGELU, out_f32=bn_prev is not None)
             g = nxt
-            if st.bn[i - 1] is not None:    # through BatchNorm1d (batch statistics): fp32 dx
-                bn, xhat, rstd, count = st.bn[i - 1]
+            if bn_prev is not None:          # through BatchNorm1d (batch statistics): fp32 dx
+                bn, xhat, rstd, count = bn_prev
                 gx = torch.empty(R, nxt.shape[1], device=dev, dtype=torch.float32)
                 dg = G.acc(bn.weight) if bn.affine and bn.weight.requires_grad else (None, False)
                 db = G.acc(bn.bias) if bn.affine and bn.bias.requires_grad else (None, False)

@@ -529,9 +529,16 @@ def test_dino_head_use_bn(dtype, tol, nlayers):
     assert rel(out.detach().cpu(), ref.detach().cpu()) < tol
     assert rel(xg.grad.cpu(), xr.grad.cpu()) < tol
     assert rel(ll.weight_v.grad.cpu(), ref_v.grad.cpu()) < tol
-    for m, r in zip(head.mlp, ref_mlp):
+    scale = max(float(p.grad.abs().max()) for p in ref_mlp.parameters())
+    for i, (m, r) in enumerate(zip(head.mlp, ref_mlp)):
         for name, p in m.named_parameters():
-            assert rel(p.grad.cpu(), getattr(r, name).grad.cpu()) < tol, (m, name)
+            want = getattr(r, name).grad
+            if name == "bias" and i + 1 < len(head.mlp) and isinstance(head.mlp[i + 1], nn.BatchNorm1d):
+                # a bias right before a train-mode BatchNorm: zero gradient analytically (the batch
+                # mean removes it); torch's is rounding noise -- checked against the gradient scale
+                assert float(p.grad.abs().max()) < tol * scale, (i, name)
+                continue
+            assert rel(p.grad.cpu(), want.cpu()) < tol, (m, name)
         if isinstance(m, nn.BatchNorm1d):
             assert rel(m.running_mean.cpu(), r.running_mean.cpu()) < 1e-4
             assert rel(m.running_var.cpu(), r.running_var.cpu()) < 1e-4
