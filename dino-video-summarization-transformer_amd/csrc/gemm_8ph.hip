@@ -341,6 +341,10 @@ hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_
   dim3 grid((unsigned)G), block(512);
 #define DSVT_K(E, F) gemm_8ph_kernel<E, F><<<grid, block, 0, s>>>(p)
   if (abl) {                                          // diagnostic builds: EPI_BIAS, bf16 out
+    if (abl == 16 && epi == EPI_RESID) {              // the residual GEMM's K loop alone (no epilogue)
+      gemm_8ph_kernel<EPI_RESID, true, 16><<<grid, block, 0, s>>>(p);
+      return hipGetLastError();
+    }
     if (epi != EPI_BIAS || out_f32) return hipErrorInvalidValue;
     switch (abl) {
       case 1: gemm_8ph_kernel<EPI_BIAS, false, 1><<<grid, block, 0, s>>>(p); break;
