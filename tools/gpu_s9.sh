@@ -12,4 +12,4 @@ for v in 20 26 1; do
   timeout -k 10 400 bash tools/pmc_gemm.sh $v 25104 768 768 2 || exit 1
 done
 python tools/pmc_table.py gpurun_out/pmc_gemm_v20_25104x768x768_e2 gpurun_out/pmc_gemm_v26_25104x768x768_e2 gpurun_out/pmc_gemm_v1_25104x768x768_e2 > gpurun_out/pmc9.txt 2>&1 || true
-cat gpurun_out/pmc9.txt | grep -E "^
+grep -E "^##|kernel time|WAIT|ACTIVE_INST_ANY /|MFMA busy|HBM|per CU|GB/s|TF/s" gpurun_out/pmc9.txt || true
