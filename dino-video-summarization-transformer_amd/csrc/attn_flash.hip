@@ -142,8 +142,7 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) mx = fmaxf(mx, s[qt][kt][jj]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = max_lane_groups(mx);             // VALU permlane swaps, no LDS-crossbar round trip
       const float mn = FIRST ? mx * sl2 : fmaxf(m2[qt], mx * sl2);
       float rs = 0.f;
 #pragma unroll
@@ -154,8 +153,7 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
           s[qt][kt][jj] = e;
           rs += e;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = sum_lane_groups(rs);
       if constexpr (FIRST) {
         l[qt] = rs;
 #pragma unroll

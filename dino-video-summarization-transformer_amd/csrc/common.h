@@ -50,6 +50,14 @@ __device__ __forceinline__ uint4 pack_pair_bf16(fv4 a, fv4 b) {
 }
 __device__ __forceinline__ int pair_off(int g) { return ((g & 1) << 4) | ((g >> 1) << 3); }
 
+// max over a lane's four 16-lane groups by the same two permlane swaps (every lane the same bits)
+__device__ __forceinline__ float max_lane_groups(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 // x0^2 + x1^2 + x2^2 + x3^2 as (fma(x0, x0, x1 x1)) + (fma(x2, x2, x3 x3)): written out so that no
 // template instantiation can contract it differently (-ffp-contract=fast lets the compiler fuse a
 // product into a neighbouring add where it likes; LayerNorm statistics must be the same bits
