@@ -431,9 +431,10 @@ class VisionTransformer(nn.Module):
         k = self.dsvt_streams
         if k == "auto":
             rows = B * (1 + (shape[2] // 16) * (shape[3] // 16) * shape[1])
+            # config 4 (2 joint 16x224^2 clips, 6274 rows) stays ONE call since r04: the flash kernel
+            # runs both clips' 128-query workgroups together (116 us vs 2 x 73 us one clip at a time):
+            # 602.3 / 605.4 vs 598.0 / 596.8 clips/s split in two (r03: 591-596 vs 580-584 the other way)
             k = max(1, min(3, rows // SPLIT_ROWS))
-            if k == 1 and B >= 2 and rows >= SPLIT_ROWS // 2:
-                k = 2   # e.g. config 4 (2 joint 16x224^2 clips, 6274 rows): 591-596 vs 580-584 clips/s
         k = min(int(k), B)
         # The batch is split only when this forward is not already one of several concurrent
         # calls (dino_forward / MultiCropWrapper forks): their streams already overlap, and under
