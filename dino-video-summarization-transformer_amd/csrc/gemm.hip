@@ -334,7 +334,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
   int gv = g_gemm_variant;
-  if (gv == 30 && !(!p.ln_stats && gemm_192_ok(p, epi))) gv = 0;   // forced, ineligible: auto
+  if (gv == 30 && !(!p.ln_stats && gemm_192_ok(p, epi) && (epi == EPI_RESID || !out_f32))) gv = 0;   // forced, ineligible: auto
   // DSVT_GEMM_FEW_ROWS call sites (the CLS-only tail's and the DINO head's few-row GEMMs, chosen
   // by call site so that a batch split over streams picks the same kernel as the whole batch):
   // the K-split skinny kernel (variant 50 forces it where eligible) -- bench 397.7-398.7 vs
@@ -381,6 +381,10 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // kernel's 4x more tiles win even with other streams beside it.
   if (epi == EPI_RESID) return (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
   // N = 768 bias-only (the backward's dX GEMMs): the 256x256 kernel on big calls
+#ifndef DSVT_DX192
+#define DSVT_DX192 0
+#endif
+  if (DSVT_DX192 && epi == EPI_BIAS && !out_f32 && big8 && gemm_192_ok(p, epi)) return 30;
   if (epi == EPI_BIAS && p.N < 1024) return (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }
