@@ -33,6 +33,7 @@ namespace {
 constexpr int FA_ROWB = 128;                  // bytes per staged row: 64 bf16
 constexpr int FA_TILE = 64 * FA_ROWB;         // one K or V tile, 8 KiB
 constexpr int FA_NBUF = 3;
+constexpr float FA_LAZY = 8.0f;               // running-max slack, log2 units (P <= 2^8 before 1 / l)
 
 template <int N>
 __device__ __forceinline__ void fa_vmwait() {
@@ -103,8 +104,10 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
   auto vrd = [&](int st2, int dt) { return vrd0 + st2 * 32 * FA_ROWB + ((dt ^ vf2) << 5); };
 
   const float sl2 = p.scale * 1.4426950408889634f;
-  float m2[QT], l[QT];
-  fv4 o[QT][4];
+  float m2[QT];
+  fv4 o[QT][4], lacc[QT];               // lacc: the row sums of P, accumulated by MFMA against ones
+  typedef short sv8_t __attribute__((ext_vector_type(8)));
+  const sv8_t ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};   // bf16 1.0
 
   // one 64-key tile from ring slot `buf`; FIRST: the peeled, masked tile that opens the stream
   auto tile = [&](int buf, auto first_c) {
@@ -134,7 +137,11 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
           for (int jj = 0; jj < 4; ++jj)
             s[qt][kt][jj] = (kt * 16 + 4 * g + jj) < lim ? s[qt][kt][jj] : -INFINITY;
     }
-    // online softmax (exp2 domain); s becomes P
+    // online softmax (exp2 domain) with a LAZY running max: m2 is raised -- and O / l rescaled --
+    // only when some query of the wave sees a score more than FA_LAZY (log2 units) above it, so
+    // after the first tiles the rescale multiplies are skipped; P values up to 2^FA_LAZY are exact
+    // in fp32 / representable in bf16 and the final 1 / l normalizes them.  s becomes P; the row
+    // sums come out of the P.V MFMAs (an all-ones V^T block), not VALU adds.
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       float mx = -INFINITY;
@@ -142,29 +149,25 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) mx = fmaxf(mx, s[qt][kt][jj]);
-      mx = max_lane_groups(mx);             // VALU permlane swaps, no LDS-crossbar round trip
-      const float mn = FIRST ? mx * sl2 : fmaxf(m2[qt], mx * sl2);
-      float rs = 0.f;
+      mx = max_lane_groups(mx) * sl2;       // VALU permlane swaps, no LDS-crossbar round trip
+      if constexpr (FIRST) {
+        m2[qt] = mx;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = fv4{0.f, 0.f, 0.f, 0.f};
+        lacc[qt] = fv4{0.f, 0.f, 0.f, 0.f};
+      } else if (__builtin_amdgcn_ballot_w64(mx > m2[qt] + FA_LAZY) != 0) {   // wave-uniform, rare
+        mfma_result_fence();                // o / lacc are MFMA results read by VALU under a branch
+        const float mn = fmaxf(m2[qt], mx);
+        const float alpha = __builtin_amdgcn_exp2f(m2[qt] - mn);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+        lacc[qt] *= alpha;
+        m2[qt] = mn;
+      }
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][jj], sl2, -mn));
-          s[qt][kt][jj] = e;
-          rs += e;
-        }
-      rs = sum_lane_groups(rs);
-      if constexpr (FIRST) {
-        l[qt] = rs;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = fv4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        const float alpha = __builtin_amdgcn_exp2f(m2[qt] - mn);
-        l[qt] = l[qt] * alpha + rs;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
-      }
-      m2[qt] = mn;
+        for (int jj = 0; jj < 4; ++jj) s[qt][kt][jj] = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][jj], sl2, -m2[qt]));
     }
     // O^T += V^T . P^T over two 32-key steps; k-slot (g, jj): jj < 4 -> key tile 2 st2, else 2 st2 + 1
 #pragma unroll
@@ -189,6 +192,8 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[qt], o[qt][dt], 0, 0, 0);
       }
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) lacc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[qt], lacc[qt], 0, 0, 0);
     }
   };
 
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void attn_flash_bf16(AttnParams p) {
   for (int qt = 0; qt < QT; ++qt) {
     const int64_t qo = qbase + qt * 16 + r16;
     if (qo < L) {
-      const float inv = 1.0f / l[qt];
+      const float inv = 1.0f / lacc[qt][0];   // every element of lacc holds the row sum
       bf16_t* dst = (bf16_t*)p.out + (seq * p.L + qo) * p.ld_out + h * 64 + 4 * g;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)

@@ -4,7 +4,7 @@ set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for nb in 1 2; do
+for nb in 2 1; do
   for lib in head cur head cur; do
     if [ $lib = cur ]; then unset DSVT_LIB; else export DSVT_LIB=tools/ab_lib/libdsvt_$lib.so; fi
     echo "NB=$nb $lib: $(NB=$nb timeout -k 10 120 python tools/attn_joint_bench.py 2>&1 | grep -v amdgpu | tr '\n' ' ')"
