@@ -2,7 +2,7 @@
 divided backbone, 16 clips 8x224^2), c4 (joint space-time ViT-B/16, 2 clips 16x224^2) or c5
 (Video Swin-T, 8 clips 8x224^2); bf16, random init, synthetic input.
 
-usage: python tools/cfg_bench.py c4 [--reps 5] [--warm 2] [--streams auto|1|2|3]"""
+usage: python tools/cfg_bench.py c4 [--reps 5] [--warm 2] [--streams auto|1|2|3] [--ln-fold auto|on|off]"""
 import argparse
 import os
 import sys
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--warm", type=int, default=2)
     ap.add_argument("--streams", default=None)
+    ap.add_argument("--ln-fold", choices=["auto", "on", "off"], default="auto")
     args = ap.parse_args()
     from dsvt.models import SwinTransformer3D
     from dsvt.models.timesformer import VisionTransformer
@@ -45,6 +46,7 @@ def main():
         gf = (vit_fwd_flops(8, 224, folded=True, cls_tail=m.cls_tail) if args.cfg == "c2bb" else joint_flops()) / 1e9
         if args.streams is not None:
             m.dsvt_streams = args.streams if args.streams == "auto" else int(args.streams)
+        m.ln_fold = {"auto": "auto", "on": True, "off": False}[args.ln_fold]
     m.dsvt_dtype = torch.bfloat16
     with torch.no_grad():
         for _ in range(args.warm):
