@@ -546,8 +546,9 @@ hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s) {
   }
   // contiguous sequences (joint space-time, space-only): the LDS-DMA flash kernel
   // (attn_flash.hip); variant 8 keeps the register-staged kernel below (A/B, tests)
-  // variant 11 / 12: the flash kernel with 64 / 128 queries per workgroup forced
-  if (v != 8 && attn_flash_ok(dtype, p)) return launch_attn_flash(p, s, v == 11 ? 1 : v == 12 ? 2 : 0);
+  // variants 11-15: the flash kernel's workgroup shape forced (attn_flash.hip kShapes 1-5: 4 waves
+  // x 1 / 2 query tiles, 8 waves x 3 + 2 / 2 + 1 / 2 + 2)
+  if (v != 8 && attn_flash_ok(dtype, p)) return launch_attn_flash(p, s, v >= 11 && v <= 15 ? v - 10 : 0);
   dim3 grid((unsigned)((p.seqlen + 63) / 64), (unsigned)p.heads, (unsigned)(p.nb * p.tin));
   if (dtype == 0) attn_seq_bf16<<<grid, 256, 0, s>>>(p);
   else attn_seq_f32<<<grid, 64, 0, s>>>(p);

@@ -602,7 +602,7 @@ int dsvt_set_gemm_variant(int variant) {
 }
 
 int dsvt_set_attn_variant(int variant) {
-  REQUIRE(variant >= 0 && variant <= 12, "attention variant must be 0-12");
+  REQUIRE(variant >= 0 && variant <= 15, "attention variant must be 0-15");
   set_attn_variant(variant);
   return 0;
 }

@@ -139,7 +139,7 @@ struct AttnParams {
 hipError_t launch_attn_seq(int dtype, const AttnParams& p, hipStream_t s);
 // flash attention over contiguous sequences (attn_flash.hip): joint space-time / space-only
 bool attn_flash_ok(int dtype, const AttnParams& p);
-hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s, int qt = 0);   // qt: queries / 64 per workgroup, 0 = auto
+hipError_t launch_attn_flash(const AttnParams& p, hipStream_t s, int cfg = 0);   // cfg: workgroup shape 1-5, 0 = auto
 void set_attn_variant(int v);
 // CLS query only of every spatial sequence, mean over frames -> out[b * ld_out + c] (attention.hip)
 int64_t attn_cls_ws_bytes(int64_t nseq, int64_t heads, int64_t seqlen);   // nseq = B*T

@@ -20,8 +20,9 @@ extern "C" {
 int dsvt_set_gemm_variant(int variant);
 /* bf16 short-sequence attention kernel: 0 = automatic, 1 = 16-key-tile x 4 waves, 2 = 13 x 8 waves,
  * 3 = 13 x 4 waves padded rows, 4 = streaming flash kernel, 7 = swizzled 3-tile kernel, 8 = the
- * register-staged long-sequence kernel, 11 / 12 = the flash kernel (contiguous sequences) with 64 / 128
- * queries per workgroup (5, 6, 9, 10: diagnostic builds). */
+ * register-staged long-sequence kernel, 11-15 = the flash kernel (contiguous sequences) with its
+ * workgroup shape forced: 4 waves x 1 / 2 16-query tiles (64 / 128 queries), 8 waves x 3 + 2 / 2 + 1 /
+ * 2 + 2 tiles (320 / 192 / 256 queries) (5, 6, 9, 10: diagnostic builds). */
 int dsvt_set_attn_variant(int variant);
 /* attention backward: 0 = automatic (bf16 MFMA kernel for sequences <= 256), 1 = the generic
  * two-pass VALU kernels.  Process-global. */

@@ -730,7 +730,7 @@ def test_attn_spatial_variants_repeatable(variant):
     check(back(outs[0])[:2 * L], ref, torch.bfloat16, "spatial variant %d" % variant)
 
 
-@pytest.mark.parametrize("variant", [0, 8])
+@pytest.mark.parametrize("variant", [0, 8, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("nb,L,heads", [(2, 5, 3), (1, 16, 2), (1, 17, 2), (1, 64, 2), (1, 65, 12), (2, 197, 3),
                                         (1, 208, 2), (1, 209, 2), (1, 256, 2), (1, 257, 2), (1, 300, 2),
@@ -738,7 +738,8 @@ def test_attn_spatial_variants_repeatable(variant):
 def test_attn_joint(dtype, nb, L, heads, variant):
     """L <= 256: whole-sequence LDS kernel (attn_short_bf16 in bf16); longer: the LDS-DMA flash
     kernel (attn_flash_bf16, variant 0: last partial key tile first -- 1, 44, 64, 1 valid keys
-    at L = 257, 300, 320, 449) or the register-staged one (variant 8)."""
+    at L = 257, 300, 320, 449; 11-15 its five workgroup shapes forced, whose 4- or 8-wave K/V
+    staging and per-wave query tiles differ) or the register-staged one (variant 8)."""
     from dsvt import _lib, ops
     if variant and (dtype == torch.float32 or L <= 256):
         pytest.skip("variant 8 is the bf16 long-sequence kernel")
@@ -762,12 +763,16 @@ def test_attn_joint(dtype, nb, L, heads, variant):
     check(back(out), ref, dtype, "joint")
 
 
+@pytest.mark.parametrize("variant", [0, 11, 13, 14])
 @pytest.mark.parametrize("L,hot", [(200, 190), (400, 390), (400, 10), (3137, 3000)])
-def test_attn_softmax_spike(L, hot):
+def test_attn_softmax_spike(L, hot, variant):
     """One key far above the rest: the two-pass softmax of the short kernel (L=200); in the flash
     kernel a spike in the partial last key tile (processed first: L=400 hot=390) and in a later
-    tile (hot=10, 3000: the online-softmax rescale of everything accumulated before it)."""
-    from dsvt import ops
+    tile (hot=10, 3000: the online-softmax rescale of everything accumulated before it); every
+    flash workgroup shape (variants 11, 13, 14)."""
+    from dsvt import _lib, ops
+    if variant and L <= 256:
+        pytest.skip("flash shapes: long sequences")
     nb, heads = 1, 1
     qkv = rnd((L, 192), 14, 0.5)
     qkv[:, :64] = 1.0
@@ -775,7 +780,11 @@ def test_attn_softmax_spike(L, hot):
     for dtype in DT:
         Q = to(qkv, dtype)
         out = torch.empty(L, 64, device=dev(), dtype=dtype)
-        ops.attn_joint(Q, out, nb, L, heads, 0.125)
+        _lib.call("dsvt_set_attn_variant", variant)
+        try:
+            ops.attn_joint(Q, out, nb, L, heads, 0.125)
+        finally:
+            _lib.call("dsvt_set_attn_variant", 0)
         torch.cuda.synchronize()
         q3 = back(Q)
         check(back(out), attn_ref(q3[:, :64], q3[:, 64:128], q3[:, 128:], 0.125), dtype, "spike")
@@ -861,23 +870,30 @@ def test_pair_loss_golden():
     np.testing.assert_allclose(got, np.load("tests/golden/pair_loss.npz")["loss"], rtol=2e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("variant", [0, 12, 13, 14])
 @pytest.mark.parametrize("dtype", DT)
-def test_attn_joint_config4_size(dtype):
+def test_attn_joint_config4_size(dtype, variant):
     """Config 4 at its own size (ViT-B joint space-time 16x224^2: L = 1 + 196*16 = 3137, 12 heads,
     2 clips) vs torch fp32 scaled_dot_product_attention on the same storage-rounded q/k/v;
     repeated launches are bitwise identical (the flash kernel's MFMA chains are the same
-    hazard class as the spatial kernel's)."""
+    hazard class as the spatial kernel's); the flash workgroup shapes forced (variants 12-14)."""
     import torch.nn.functional as F
-    from dsvt import ops
+    from dsvt import _lib, ops
+    if variant and dtype == torch.float32:
+        pytest.skip("flash shapes: bf16")
     nb, L, heads = 2, 3137, 12
     C = heads * 64
     gen = torch.Generator(device="cuda").manual_seed(17)
     Q = torch.randn(nb * L, 3 * C, device="cuda", generator=gen).to(dtype)
     outs = []
-    for _ in range(3):
-        out = torch.full((nb * L, C), 7.0, device="cuda", dtype=dtype)
-        ops.attn_joint(Q, out, nb, L, heads, 0.125)
-        outs.append(out)
+    _lib.call("dsvt_set_attn_variant", variant)
+    try:
+        for _ in range(3):
+            out = torch.full((nb * L, C), 7.0, device="cuda", dtype=dtype)
+            ops.attn_joint(Q, out, nb, L, heads, 0.125)
+            outs.append(out)
+    finally:
+        _lib.call("dsvt_set_attn_variant", 0)
     x = Q.float().view(nb, L, 3, heads, 64)
     ref = F.scaled_dot_product_attention(x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2),
                                          x[:, :, 2].transpose(1, 2), scale=0.125)

@@ -1,6 +1,7 @@
 """Joint space-time attention at config 4's size (2 clips x 12 heads x L = 3137, head_dim 64):
-time per launch and TFLOP/s (4 L^2 d per head) of the flash kernel (variant 0 = auto, 11 / 12 = 64 /
-128 queries per workgroup) and the register-staged kernel (variant 8), interleaved in one process."""
+time per launch and TFLOP/s (4 L^2 d per head) of the flash kernel (variant 0 = auto, 11-15 = its
+workgroup shapes: 4 waves x 1 / 2 query tiles, 8 waves x 3+2 / 2+1 / 2+2) and the register-staged kernel
+(variant 8), interleaved in one process.  NB clips (default 2), VARIANTS="0,11,..." """
 import os
 import sys
 
@@ -17,7 +18,7 @@ out = torch.empty(nb * L, C, device="cuda", dtype=torch.bfloat16)
 fl = 4.0 * nb * heads * L * L * 64
 res = {}
 for rnd in range(3):
-    for v in (0, 11, 12, 8):
+    for v in [int(x) for x in os.environ.get("VARIANTS", "0,11,12,13,14,15,8").split(",")]:
         _lib.call("dsvt_set_attn_variant", v)
         ops.attn_joint(Q, out, nb, L, heads, 0.125)
         torch.cuda.synchronize()

@@ -2,7 +2,7 @@
 over the kernel's dispatches, then derived figures (kernel time from GRBM_GUI_ACTIVE at the
 shader clock, wait / MFMA-busy fractions, HBM bytes per launch (FETCH_SIZE / WRITE_SIZE are KiB),
 bytes per CU, achieved GB/s).
-usage: python tools/pmc_table.py DIR [DIR ...] [--clock-mhz 2400] [--flop F --algo-bytes B]"""
+usage: python tools/pmc_table.py DIR [DIR ...] [--clock-mhz 2400] [--flop F --algo-bytes B] [--match NAME]"""
 import argparse
 import collections
 import csv
@@ -10,14 +10,14 @@ import glob
 import os
 
 
-def counters(d):
+def counters(d, match="gemm"):
     agg = collections.defaultdict(float)
     n = collections.defaultdict(set)
     name = None
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "gemm" not in k:
+            if match not in k:
                 continue
             name = k[:70]
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
@@ -29,11 +29,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--clock-mhz", type=float, default=2400.0)
+    ap.add_argument("--match", default="gemm", help="kernel-name substring")
     ap.add_argument("--flop", type=float, default=2.0 * 25104 * 768 * 768)
     ap.add_argument("--algo-bytes", type=float, default=25104 * 768 * (2 + 4 + 4) + 768 * 768 * 2)
     a = ap.parse_args()
     for d in a.dirs:
-        name, c = counters(d)
+        name, c = counters(d, a.match)
         if not c:
             print("## %s: no counters" % d)
             continue
