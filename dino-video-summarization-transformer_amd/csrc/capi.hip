@@ -594,9 +594,9 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 }
 
 int dsvt_set_gemm_variant(int variant) {
-  REQUIRE(variant == 0 || variant == 1 || variant == 10 || (variant >= 20 && variant <= 29 && variant != 24) ||
+  REQUIRE(variant == 0 || variant == 1 || variant == 3 || variant == 10 || (variant >= 20 && variant <= 29 && variant != 24) ||
               variant == 30 || variant == 50,
-          "gemm variant must be 0 (auto), 1, 10, 20 (21-29 but 24: ablation builds), 30 or 50");
+          "gemm variant must be 0 (auto), 1, 3, 10, 20 (21-29 but 24: ablation builds), 30 or 50");
   set_gemm_variant(variant);
   return 0;
 }

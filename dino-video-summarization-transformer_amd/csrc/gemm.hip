@@ -4,7 +4,9 @@
 //                             or the patch-embed pos/time-embed add)
 //
 // Tiling (gfx950): 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each a
-// 64x64 sub-tile = 4x4 MFMA 16x16 tiles).  K advances 128 BYTES per stage (64 bf16 or
+// 64x64 sub-tile = 4x4 MFMA 16x16 tiles); the bf16 residual epilogue also as 160x128 (MI = 5
+// fragments per wave along M: variant 3, config 4's N = 768 GEMMs, one round of 240 tiles where
+// 128x128 needs 294 = a 1.15-round grid).  K advances 128 BYTES per stage (64 bf16 or
 // 32 fp32), staged global->LDS with `global_load_lds_dwordx4` (16 B/lane, no VGPR round
 // trip) into a 2-stage ring (64 KB LDS), XOR-swizzled on the SOURCE address so the
 // ds_read_b128 fragment reads are bank-conflict free (chunk' = chunk ^ ((row>>1)&7)).
@@ -26,14 +28,15 @@ constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // A + W
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-// Issue the global->LDS copy of one [128 rows][128 bytes] tile (16 x 1 KB pieces, 4 per
+// Issue the global->LDS copy of one [32 NP rows][128 bytes] tile (4 NP x 1 KB pieces, NP per
 // wave).  Rows beyond `rows` re-read the last row (results masked in the epilogue).
+template <int NP = 4>
 __device__ __forceinline__ void stage_tile(const char* __restrict__ g, int64_t ld_bytes,
                                            int64_t row0, int64_t rows, int64_t kbyte0,
                                            char* lds_tile, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave * 4 + i;
+  for (int i = 0; i < NP; ++i) {
+    const int piece = wave * NP + i;
     const int r = piece * 8 + (lane >> 3);
     const int cl = lane & 7;
     int64_t gr = row0 + r;
@@ -50,20 +53,21 @@ __device__ __forceinline__ const char* lds_chunk(const char* tile, int r, int c)
 template <typename T> struct TileMMA;
 
 template <> struct TileMMA<bf16_t> {
-  __device__ __forceinline__ static void run(const char* At, const char* Wt, fv4 (&acc)[4][4],
+  template <int MI>
+  __device__ __forceinline__ static void run(const char* At, const char* Wt, fv4 (&acc)[MI][4],
                                              int wm, int wn, int lane) {
     const int r16 = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      sv8 a[4], b[4];
+      sv8 a[MI], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i] = *reinterpret_cast<const sv8*>(lds_chunk(At, wm * 64 + i * 16 + r16, ks * 4 + g));
+      for (int i = 0; i < MI; ++i)
+        a[i] = *reinterpret_cast<const sv8*>(lds_chunk(At, wm * 16 * MI + i * 16 + r16, ks * 4 + g));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         b[j] = *reinterpret_cast<const sv8*>(lds_chunk(Wt, wn * 64 + j * 16 + r16, ks * 4 + g));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
@@ -72,7 +76,8 @@ template <> struct TileMMA<bf16_t> {
 };
 
 template <> struct TileMMA<float> {
-  __device__ __forceinline__ static void run(const char* At, const char* Wt, fv4 (&acc)[4][4],
+  template <int MI>
+  __device__ __forceinline__ static void run(const char* At, const char* Wt, fv4 (&acc)[MI][4],
                                              int wm, int wn, int lane) {
     const int r16 = lane & 15, g = lane >> 4;
     fv4 a[4][2], b[4][2];
@@ -99,29 +104,30 @@ template <> struct TileMMA<float> {
   }
 };
 
-// The fp32 residual tile of one wave (full tiles): 16 float4 loads, issued by gemm_kernel two
+// The fp32 residual tile of one wave (full tiles): 4 MI float4 loads, issued by gemm_kernel two
 // K steps before the end of its main loop (PREF) so their latency runs under the last MFMAs.
+template <int MI>
 __device__ __forceinline__ void resid_load(const GemmParams& p, int64_t m0, int64_t n0, int wm, int wn, int lane,
-                                           float4 (&add)[4][4]) {
+                                           float4 (&add)[MI][4]) {
   const int r16 = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t orow = map_row(m0 + wm * 64 + i * 16 + r16, p.rpg, p.gstride, p.goff);
+  for (int i = 0; i < MI; ++i) {
+    const int64_t orow = map_row(m0 + wm * 16 * MI + i * 16 + r16, p.rpg, p.gstride, p.goff);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       add[i][j] = *reinterpret_cast<const float4*>(resid_src(p) + orow * p.ldo + n0 + wn * 64 + j * 16 + 4 * g);
   }
 }
 
-template <typename T, int EPI, bool OUT_F32, bool CHECK, bool PRE = false>
-__device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][4], int64_t m0, int64_t n0, int wm,
+template <typename T, int EPI, bool OUT_F32, bool CHECK, bool PRE = false, int MI = 4>
+__device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[MI][4], int64_t m0, int64_t n0, int wm,
                                              int wn, int lane, const float4 (*pre)[4] = nullptr) {
   const int r16 = lane & 15, g = lane >> 4;
-  int64_t orow[4];
-  bool vrow[4];
+  int64_t orow[MI];
+  bool vrow[MI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + wm * 64 + i * 16 + r16;
+  for (int i = 0; i < MI; ++i) {
+    const int64_t m = m0 + wm * 16 * MI + i * 16 + r16;
     vrow[i] = !CHECK || m < p.M;
     orow[i] = map_row(vrow[i] ? m : p.M - 1, p.rpg, p.gstride, p.goff);
   }
@@ -135,16 +141,16 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
       bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  float4 add[4][4];                    // residual / embedding addend per fragment
+  float4 add[MI][4];                   // residual / embedding addend per fragment
   if constexpr (PRE) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) add[i][j] = pre[i][j];
   } else if constexpr (EPI == EPI_RESID || EPI == EPI_PATCH) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t m = m0 + wm * 64 + i * 16 + r16;
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * 16 * MI + i * 16 + r16;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t n = n0 + wn * 64 + j * 16 + 4 * g;
@@ -165,15 +171,15 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
       }
     }
   }
-  float rsc[4];                        // DropPath row scales (EPI_BIAS / EPI_GELU_SAVE: the output;
+  float rsc[MI];                       // DropPath row scales (EPI_BIAS / EPI_GELU_SAVE: the output;
 #pragma unroll                         // EPI_RESID: the bias term only)
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < MI; ++i) {
     rsc[i] = 1.0f;
     if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE || EPI == EPI_RESID)
-      if (p.row_scale) rsc[i] = row_scale_of(p, m0 + wm * 64 + i * 16 + r16);
+      if (p.row_scale) rsc[i] = row_scale_of(p, m0 + wm * 16 * MI + i * 16 + r16);
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < MI; ++i) {
     if (CHECK && !vrow[i]) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -217,9 +223,11 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[4][
   }
 }
 
-template <typename T, int EPI, bool OUT_F32, bool PREF = false>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+template <typename T, int EPI, bool OUT_F32, bool PREF = false, int MI = 4>
+__global__ __launch_bounds__(256, MI == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
+  constexpr int BMv = 32 * MI;                       // tile rows
+  constexpr int A_BYTES = BMv * BKB, SBYTES = A_BYTES + TILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SBYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
@@ -228,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   const int tilesN = (int)((p.N + BN - 1) / BN);
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int64_t m0 = (int64_t)(wg / tilesN) * BM;
+  const int64_t m0 = (int64_t)(wg / tilesN) * BMv;
   const int64_t n0 = (int64_t)(wg % tilesN) * BN;
 
   const char* A = (const char*)p.A;
@@ -236,50 +244,51 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   const int64_t lda_b = p.lda * (int64_t)sizeof(T), ldw_b = p.ldw * (int64_t)sizeof(T);
   const int nk = (int)((p.K * (int64_t)sizeof(T)) / BKB);
 
-  fv4 acc[4][4];
+  fv4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
 
-  stage_tile(A, lda_b, m0, p.M, 0, smem, wave, lane);
-  stage_tile(W, ldw_b, n0, p.N, 0, smem + TILE_BYTES, wave, lane);
+  stage_tile<MI>(A, lda_b, m0, p.M, 0, smem, wave, lane);
+  stage_tile(W, ldw_b, n0, p.N, 0, smem + A_BYTES, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // PREF (fp32 residual, full tiles): the last two K steps are peeled; the residual tile's 16
   // loads are issued right after the last stage's loads, and that step waits with vmcnt(16) --
   // for the stage, not for them -- so their latency runs under the last two steps' MFMAs.
-  const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
+  const bool full = m0 + BMv <= p.M && n0 + BN <= p.N;
   const bool peel = PREF && full && nk >= 2;
   const int nmain = peel ? nk - 2 : nk;
   for (int kt = 0; kt < nmain; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    char* cur = smem + (kt & 1) * SBYTES;
     if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-      stage_tile(A, lda_b, m0, p.M, (int64_t)(kt + 1) * BKB, nxt, wave, lane);
-      stage_tile(W, ldw_b, n0, p.N, (int64_t)(kt + 1) * BKB, nxt + TILE_BYTES, wave, lane);
+      char* nxt = smem + ((kt + 1) & 1) * SBYTES;
+      stage_tile<MI>(A, lda_b, m0, p.M, (int64_t)(kt + 1) * BKB, nxt, wave, lane);
+      stage_tile(W, ldw_b, n0, p.N, (int64_t)(kt + 1) * BKB, nxt + A_BYTES, wave, lane);
     }
-    TileMMA<T>::run(cur, cur + TILE_BYTES, acc, wm, wn, lane);
+    TileMMA<T>::run(cur, cur + A_BYTES, acc, wm, wn, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   if constexpr (PREF) {
     if (peel) {
-      char* cur = smem + ((nk - 2) & 1) * STAGE_BYTES;
-      char* nxt = smem + ((nk - 1) & 1) * STAGE_BYTES;
-      stage_tile(A, lda_b, m0, p.M, (int64_t)(nk - 1) * BKB, nxt, wave, lane);
-      stage_tile(W, ldw_b, n0, p.N, (int64_t)(nk - 1) * BKB, nxt + TILE_BYTES, wave, lane);
+      char* cur = smem + ((nk - 2) & 1) * SBYTES;
+      char* nxt = smem + ((nk - 1) & 1) * SBYTES;
+      stage_tile<MI>(A, lda_b, m0, p.M, (int64_t)(nk - 1) * BKB, nxt, wave, lane);
+      stage_tile(W, ldw_b, n0, p.N, (int64_t)(nk - 1) * BKB, nxt + A_BYTES, wave, lane);
       __builtin_amdgcn_sched_barrier(0);
-      float4 xpre[4][4];
+      float4 xpre[MI][4];
       resid_load(p, m0, n0, wm, wn, lane, xpre);
       __builtin_amdgcn_sched_barrier(0);
-      TileMMA<T>::run(cur, cur + TILE_BYTES, acc, wm, wn, lane);
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      TileMMA<T>::run(cur, cur + A_BYTES, acc, wm, wn, lane);
+      if constexpr (MI == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the residual loads
+      else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       __syncthreads();
-      TileMMA<T>::run(nxt, nxt + TILE_BYTES, acc, wm, wn, lane);
+      TileMMA<T>::run(nxt, nxt + A_BYTES, acc, wm, wn, lane);
       mfma_result_fence();
-      epilogue_128<T, EPI, OUT_F32, false, true>(p, acc, m0, n0, wm, wn, lane, xpre);
+      epilogue_128<T, EPI, OUT_F32, false, true, MI>(p, acc, m0, n0, wm, wn, lane, xpre);
       return;
     }
   }
@@ -291,8 +300,16 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   // Full tiles (uniform per workgroup) take a branch-free path: no per-lane bounds branches,
   // so the compiler's vmcnt waits stay exact instead of draining after every store.
   mfma_result_fence();   // acc is read under the branches below
-  if (full) epilogue_128<T, EPI, OUT_F32, false>(p, acc, m0, n0, wm, wn, lane);
-  else epilogue_128<T, EPI, OUT_F32, true>(p, acc, m0, n0, wm, wn, lane);
+  if (full) epilogue_128<T, EPI, OUT_F32, false, false, MI>(p, acc, m0, n0, wm, wn, lane);
+  else epilogue_128<T, EPI, OUT_F32, true, false, MI>(p, acc, m0, n0, wm, wn, lane);
+}
+
+// 160x128 tiles: the bf16 residual epilogue only
+static hipError_t launch_resid160(const GemmParams& p, int epi, hipStream_t s) {
+  if (epi != EPI_RESID) return hipErrorInvalidValue;
+  const int64_t tiles = ((p.M + 159) / 160) * ((p.N + BN - 1) / BN);
+  gemm_kernel<bf16_t, EPI_RESID, true, true, 5><<<dim3((unsigned)tiles), dim3(256), 0, s>>>(p);
+  return hipGetLastError();
 }
 
 template <typename T>
@@ -327,7 +344,7 @@ static thread_local int g_gemm_variant = 0; // 0 = auto; otherwise forced (dsvt_
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
-// Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, 10 = persistent staggered 256x128
+// Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, 3 = bf16 160x128 (residual epilogue), 10 = persistent staggered 256x128
 // (gemm_big.hip), 20 = 256x256 phase-interleaved (gemm_8ph.hip), 50 = K-split skinny).
 // Measured on MI355X (tools/gemm_bench.py and same-box A/Bs of the whole step).
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
@@ -366,12 +383,21 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
     if (gv == 1 || gv == 10) return gv;
     return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   }
+  if (gv == 3 && epi != EPI_RESID) return 1;   // 160x128: the residual epilogue only
   if (gv) return gv == 50 ? 1 : gv;   // forced skinny on a shape it does not take: 128x128
   // wide bias-only projections with a bf16 output (qkv, N = 2304): the 256x256 phase-interleaved
   // kernel (v20) -- measured 895 vs 828 TF/s (global crops) and 933 vs 786 (local crops)
   // fc1 + GELU likewise (728 vs 709 TF/s global crops; its epilogue uses the general store path)
-  if ((epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.M >= 4096 && p.N >= 1024 && gemm_8ph_ok(p, epi))
+  // ... unless the 256x256 grid ends in a short second round that the 256x192 kernel's tiles fill:
+  // config 4's fc1 (M = 6274, N = 3072: 300 tiles of 256x256 -> two rounds, 400 of 256x192 -> two
+  // rounds of 3/4 the tile), chosen on ceil(tiles / 256 CUs) x tile area with a 20 % margin (no
+  // shape of the three-stream config-2 forward qualifies)
+  if ((epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.M >= 4096 && p.N >= 1024 && gemm_8ph_ok(p, epi)) {
+    const int64_t mt = (p.M + 255) / 256;
+    const int64_t c256 = (mt * ((p.N + 255) / 256) + 255) / 256 * 256, c192 = (mt * (p.N / 192) + 255) / 256 * 192;
+    if (gv == 0 && gemm_192_ok(p, epi) && c192 * 5 < c256 * 4) return 30;
     return 20;
+  }
   // fp32 residual GEMMs (N = 768: proj / temporal fc / fc2): the 256x256 kernel.  ALONE it is
   // the slower one (proj 73.6 vs 57.6 us, fc2 165 vs 138 us against the 128x128 kernel: 297
   // tiles on 256 CUs leave a 1.16-round tail), but the forward runs three backbone calls on
@@ -379,7 +405,14 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // 379.7 / 380.0 vs 360.6 / 359.7 clips/s on the bench line (same box, two interleaved rounds).
   // Below ~half a round of 256x256 tiles (config 4's single 2-clip call: 75 tiles) the 128x128
   // kernel's 4x more tiles win even with other streams beside it.
-  if (epi == EPI_RESID) return (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
+  // Below that, 128x128 tiles -- or 160x128 where their grid is a round shorter: config 4's
+  // M = 6274 (294 tiles of 128x128 = 1.15 rounds on 256 CUs -> 240 of 160x128, one round)
+  if (epi == EPI_RESID) {
+    if (big8 && gemm_8ph_ok(p, epi)) return 20;
+    const int64_t tn = (p.N + 127) / 128;
+    const int64_t c128 = (((p.M + 127) / 128) * tn + 255) / 256 * 128, c160 = (((p.M + 159) / 160) * tn + 255) / 256 * 160;
+    return c160 < c128 ? 3 : 1;
+  }
   // N = 768 bias-only (the backward's dX GEMMs): the 256x256 kernel on big calls
 #ifndef DSVT_DX192
 #define DSVT_DX192 0
@@ -393,6 +426,7 @@ hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hip
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
   if ((p.ln_stats && v != 20) || (p.stats_out && v != 20 && v != 30)) return hipErrorInvalidValue;
   if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);
+  if (v == 3) return launch_resid160(p, epi, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);
   if (v == 1) return launch_t<bf16_t>(p, epi, out_f32, s);
   return launch_t<float>(p, epi, out_f32, s);

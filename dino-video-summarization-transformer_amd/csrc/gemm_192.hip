@@ -123,9 +123,11 @@ __device__ __forceinline__ void resid192_rows(const GemmParams& p, fv4 (&acc)[4]
   }
 }
 
-// bf16 out[row(m)] = acc + bias over the wave's 64 x 96 block (the backward's N = 768 dX GEMMs):
-// 16-byte pair stores, rows past M clamped to M - 1 (their accumulators are row M - 1's: the A
-// loads are clamped) so the stores are branch-free
+// bf16 out[row(m)] = acc + bias (GELU: then the bf16-output GELU, pairwise as gemm_8ph's) over the
+// wave's 64 x 96 block (the backward's N = 768 dX GEMMs; config 4's fc1): 16-byte pair stores,
+// rows past M clamped to M - 1 (their accumulators are row M - 1's: the A loads are clamped) so the
+// stores are branch-free
+template <bool GELU>
 __device__ __forceinline__ void bias192_rows(const GemmParams& p, fv4 (&acc)[4][6], int64_t rbase, int64_t cbase,
                                              int r16, int g) {
   const bool ident = p.rpg >= p.M && p.goff == 0;
@@ -141,6 +143,14 @@ __device__ __forceinline__ void bias192_rows(const GemmParams& p, fv4 (&acc)[4][
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       acc[i][j][0] += bias4[j].x; acc[i][j][1] += bias4[j].y; acc[i][j][2] += bias4[j].z; acc[i][j][3] += bias4[j].w;
+      if constexpr (GELU) {
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const f2v v = gelu_bf16out2(f2v{acc[i][j][e], acc[i][j][e + 1]});
+          acc[i][j][e] = v.x;
+          acc[i][j][e + 1] = v.y;
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < 6; j += 2) store_pair_bf16((bf16_t*)p.out + orow * p.ldo + cbase + j * 16, acc[i][j], acc[i][j + 1], g);
@@ -281,7 +291,7 @@ __device__ __forceinline__ void tattn192(const GemmParams& p, fv4 (&acc)[4][6], 
 
 }  // namespace
 
-enum { MODE_RESID = 0, MODE_RESID_STATS = 1, MODE_TATTN = 2, MODE_BIAS = 3 };
+enum { MODE_RESID = 0, MODE_RESID_STATS = 1, MODE_TATTN = 2, MODE_BIAS = 3, MODE_GELU = 4 };
 
 // MODE_RESID_STATS: the residual epilogue also writes the bf16 rows and LN partials (FUSE 2 of
 // gemm_8ph); MODE_TATTN: the LayerNorm-folded A operand (FUSE 1 of gemm_8ph) and the temporal
@@ -291,7 +301,7 @@ __global__ __launch_bounds__(512, 1) void gemm_192_kernel(GemmParams p) {
   constexpr bool STATS = MODE == MODE_RESID_STATS;
   // VMEM stores of a full-tile epilogue (the fewest any wave issues): the four phases after it
   // let them sit between the awaited half-tile and the younger stages (see gemm_8ph.hip)
-  constexpr int S_EPI = MODE == MODE_TATTN ? 4 * 2 : MODE == MODE_BIAS ? 4 * 3 : STATS ? 4 * (6 + 3 + 1) : 4 * 6;
+  constexpr int S_EPI = MODE == MODE_TATTN ? 4 * 2 : (MODE == MODE_BIAS || MODE == MODE_GELU) ? 4 * 3 : STATS ? 4 * (6 + 3 + 1) : 4 * 6;
   __shared__ __attribute__((aligned(16))) char smem[2 * Q_BUF + (MODE == MODE_TATTN ? 8 * (Q_XCH + Q_VIM) : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -477,9 +487,9 @@ __global__ __launch_bounds__(512, 1) void gemm_192_kernel(GemmParams p) {
       const int64_t rbase = m0 + wr * 64, cbase = n0 + wc * 96;
       mfma_result_fence();
       post = rbase + 64 <= p.M;          // wave-uniform
-      if constexpr (MODE == MODE_BIAS) {
+      if constexpr (MODE == MODE_BIAS || MODE == MODE_GELU) {
         post = true;                     // clamped rows: every store issued
-        bias192_rows(p, acc, rbase, cbase, r16, g);
+        bias192_rows<MODE == MODE_GELU>(p, acc, rbase, cbase, r16, g);
       } else if constexpr (MODE == MODE_TATTN) {
         ln_affine<4, 6>(p, acc, rbase, cbase, r16, g);
         __builtin_amdgcn_sched_barrier(0);
@@ -507,11 +517,12 @@ __global__ __launch_bounds__(512, 1) void gemm_192_kernel(GemmParams p) {
 #undef Q_COMPUTE
 }
 
-// the fp32 residual epilogue only (bias added in the epilogue, times the DropPath row scale when
-// p.row_scale), N a multiple of 192 with 16-byte aligned rows, K a multiple of 64, 32-bit LDS-DMA
+// the fp32 residual epilogue (bias added in the epilogue, times the DropPath row scale when
+// p.row_scale) or bf16 bias / bias + GELU without row scales, N a multiple of 192 with 16-byte aligned rows, K a multiple of 64, 32-bit LDS-DMA
 // source offsets
 bool gemm_192_ok(const GemmParams& p, int epi) {
-  return (epi == EPI_RESID || (epi == EPI_BIAS && !p.row_scale && !p.stats_out)) && !(p.stats_out && p.row_scale) &&
+  return (epi == EPI_RESID || ((epi == EPI_BIAS || epi == EPI_GELU) && !p.row_scale && !p.stats_out)) &&
+         !(p.stats_out && p.row_scale) &&
          p.K >= 64 && p.K % 64 == 0 && p.M >= 1 && p.N >= 192 &&
          p.N % 192 == 0 && p.ldo % 8 == 0 && ((uintptr_t)p.out & 15) == 0 && ((uintptr_t)resid_src(p) & 15) == 0 &&
          (!p.bias || ((uintptr_t)p.bias & 15) == 0) && (p.M - 1) * p.lda * 2 + p.K * 2 <= (int64_t)UINT32_MAX &&
@@ -528,9 +539,10 @@ static dim3 grid_192(const GemmParams& p) {
 
 hipError_t launch_gemm_192(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
   if (!gemm_192_ok(p, epi)) return hipErrorInvalidValue;
-  if (epi == EPI_BIAS) {                              // bf16 out only (the backward's dX GEMMs)
+  if (epi == EPI_BIAS || epi == EPI_GELU) {          // bf16 out only (dX GEMMs, fc1)
     if (out_f32) return hipErrorInvalidValue;
-    gemm_192_kernel<MODE_BIAS><<<grid_192(p), dim3(512), 0, s>>>(p);
+    if (epi == EPI_GELU) gemm_192_kernel<MODE_GELU><<<grid_192(p), dim3(512), 0, s>>>(p);
+    else gemm_192_kernel<MODE_BIAS><<<grid_192(p), dim3(512), 0, s>>>(p);
     return hipGetLastError();
   }                                                   // EPI_RESID: fp32 X whatever the flag says
   if (p.stats_out && (!p.xb_out || p.N != LN_PARTS * 64 || p.row_scale)) return hipErrorInvalidValue;

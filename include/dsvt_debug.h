@@ -13,10 +13,11 @@
 extern "C" {
 #endif
 
-/* bf16 GEMM kernel: 0 = automatic, 1 = 128x128 / 4-wave kernel, 10 = persistent staggered
- * 256x128, 20 = 256x256 phase-interleaved (21-29 but 24: its diagnostic ablation builds, EPI_BIAS
- * only), 30 = 256x192 phase-interleaved (the N % 192 == 0 fp32 residual epilogue only; other
- * calls take the automatic choice), 50 = K-split skinny kernel. */
+/* bf16 GEMM kernel: 0 = automatic, 1 = 128x128 / 4-wave kernel, 3 = 160x128 / 4-wave (the fp32
+ * residual epilogue only; other calls take 1), 10 = persistent staggered 256x128, 20 = 256x256
+ * phase-interleaved (21-29 but 24: its diagnostic ablation builds, EPI_BIAS only), 30 = 256x192
+ * phase-interleaved (N % 192 == 0: the fp32 residual epilogue, bf16 bias / bias + GELU without row
+ * scales; other calls take the automatic choice), 50 = K-split skinny kernel. */
 int dsvt_set_gemm_variant(int variant);
 /* bf16 short-sequence attention kernel: 0 = automatic, 1 = 16-key-tile x 4 waves, 2 = 13 x 8 waves,
  * 3 = 13 x 4 waves padded rows, 4 = streaming flash kernel, 7 = swizzled 3-tile kernel, 8 = the

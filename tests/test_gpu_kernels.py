@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 10, 20, 30, 50])
+@pytest.fixture(params=[0, 1, 3, 10, 20, 30, 50])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -115,11 +115,13 @@ def test_gemm_skinny(M, N, K):
         _lib.call("dsvt_set_gemm_variant", 0)
 
 
-@pytest.mark.parametrize("variant", [10, 20])
-@pytest.mark.parametrize("M,N,K", [(8200, 2304, 768), (8200, 2304, 64), (6000, 3072, 128), (25104, 768, 3072)])
+@pytest.mark.parametrize("variant", [3, 10, 20, 30])
+@pytest.mark.parametrize("M,N,K", [(8200, 2304, 768), (8200, 2304, 64), (6000, 3072, 128), (25104, 768, 3072),
+                                   (6274, 3072, 768), (6274, 768, 3072)])
 def test_gemm_persistent_stream(M, N, K, variant):
     """Persistent kernels with several output tiles per workgroup (the K-tile stream crosses
-    tile boundaries; ragged last M tile), every epilogue, against torch fp32 of the bf16 operands."""
+    tile boundaries; ragged last M tile), every epilogue, against torch fp32 of the bf16 operands;
+    config 4's fc1 / fc2 shapes (M = 6274) on the 256x192 (GELU) and 160x128 (residual) kernels."""
     from dsvt import _lib, ops
     g = torch.Generator(device=dev()).manual_seed(M + N + K)
     A = (torch.randn(M, K, device=dev(), generator=g) * 0.5).to(torch.bfloat16)
@@ -164,7 +166,7 @@ def test_gelu_epilogue_accuracy():
     assert err.max() < 3e-7, err.max()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 10, 20])
+@pytest.mark.parametrize("variant", [0, 1, 10, 20, 30])
 def test_gelu_epilogue_bf16(variant):
     """The bf16-output GELU epilogue (gelu_bf16out: x * sigmoid(x * P(x^2)), every kernel that
     takes EPI_BIAS_GELU) against the exact erf GELU of the bf16-rounded input, x in [-12, 12]
@@ -172,7 +174,7 @@ def test_gelu_epilogue_bf16(variant):
     2.6e-5 bound)."""
     from dsvt import _lib, ops
     from dsvt._lib import EPI_BIAS_GELU
-    n = 64 * 256
+    n = 64 * 192                       # N % 256 == N % 192 == 0: every kernel takes it
     M = 4096 + 40                      # a ragged last 256-row tile (clamped rows in the 256x256 kernel)
     x = np.concatenate([np.linspace(-12, 12, M * 64 - 8), [0.0, 1e-6, -1e-6, 1e-3, -1e-3, 60.0, -60.0, -0.5]])
     x = x.astype(np.float32).reshape(M, 64)
@@ -217,7 +219,7 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 10, 20, 30])
+@pytest.mark.parametrize("variant", [0, 1, 3, 10, 20, 30])
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8), (16, 196, 8)])
 def test_gemm_residual_k768(variant, B, Np, T):
     """The K = 768, N = 768 residual GEMM (attn.proj / folded temporal fc shape) at the bench's
