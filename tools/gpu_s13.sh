@@ -7,4 +7,4 @@ export TMPDIR=/tmp
 rm -rf gpurun_out/c4prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c4prof -o run -- python tools/cfg_bench.py c4 --reps 10 --warm 3 > gpurun_out/c4prof.log 2>&1 || { tail -20 gpurun_out/c4prof.log; exit 1; }
 grep "c4:" gpurun_out/c4prof.log
-python tools/prof_summary.py $(ls gpurun_out/c4prof/*/run_kernel_trace.csv gpurun_out/c4prof/run_kernel_trace.csv 2>/dev/null | head -1) > gpurun_out/c4prof_summary.txt && head -24 gpurun_out/c4prof_summary.txt
+python tools/prof_summary.py gpurun_out/c4prof/run_results.db > gpurun_out/c4prof_summary.txt && head -24 gpurun_out/c4prof_summary.txt
