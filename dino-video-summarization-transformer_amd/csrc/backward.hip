@@ -181,11 +181,131 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
+// C = 768 (ViT-B), the training step's LayerNorm backward (the default, DSVT_LNB_VARIANT=2): the
+// same arithmetic as ln_bwd_kernel<DyT, true, 3, true>, with TWO rows in flight ahead of the one
+// being reduced instead of one (x, dy, dx of three rows live, dy kept as packed bf16 until used;
+// 224 VGPRs: 2 blocks per CU, 512 blocks).  Alone 59.1 -> 56.0 us at 25 104 rows (4.6 -> 4.8
+// TB/s), train step +0.3-0.7 % (tools/gpu_s17.sh, gpu_s19.sh).
+template <typename DyT>
+__global__ __launch_bounds__(256, 2) void ln_bwd768_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
+                                                        const float* __restrict__ gamma, float* __restrict__ dx,
+                                                        int64_t rows, int64_t rpg, int64_t gstride, int64_t goff,
+                                                        float eps, float* __restrict__ partial) {
+  constexpr int C = 768, NK = 12;
+  constexpr bool BF = std::is_same<DyT, bf16_t>::value;
+  constexpr int ND = BF ? 6 : 12;                 // dy registers per row (packed bf16 pairs / fp32)
+  __shared__ float red[4][2][C];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float dg[NK], db[NK], g[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    dg[k] = 0.f;
+    db[k] = 0.f;
+    g[k] = gamma[(k >> 2) * 256 + lane * 4 + (k & 3)];
+  }
+  struct RowRegs {
+    float x[NK], o[NK];
+    unsigned d[ND];
+  };
+  auto load_row = [&](int64_t r, RowRegs& R) {
+    const int64_t xr = map_row(r, rpg, gstride, goff) * C;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      load4(x + xr + i * 256 + lane * 4, R.x + 4 * i);
+      if constexpr (BF) {
+        const uint2 u = *reinterpret_cast<const uint2*>(dy + r * C + i * 256 + lane * 4);
+        R.d[2 * i] = u.x;
+        R.d[2 * i + 1] = u.y;
+      } else {
+        const float4 u = *reinterpret_cast<const float4*>(dy + r * C + i * 256 + lane * 4);
+        R.d[4 * i] = __float_as_uint(u.x); R.d[4 * i + 1] = __float_as_uint(u.y);
+        R.d[4 * i + 2] = __float_as_uint(u.z); R.d[4 * i + 3] = __float_as_uint(u.w);
+      }
+      load4(dx + xr + i * 256 + lane * 4, R.o + 4 * i);
+    }
+  };
+  auto dy_of = [&](const RowRegs& R, int k) -> float {
+    if constexpr (BF) return (k & 1) ? bf16_hi(R.d[k >> 1]) : bf16_lo(R.d[k >> 1]);
+    else return __uint_as_float(R.d[k]);
+  };
+  auto reduce_row = [&](int64_t r, RowRegs& R) {
+    const int64_t xr = map_row(r, rpg, gstride, goff) * C;
+    float cd[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) cd[k] = dy_of(R, k);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) s += R.x[k];
+    const float inv_c = 1.0f / (float)C;
+    const float mean = wave_sum_dpp(s) * inv_c;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) { R.x[k] -= mean; q += R.x[k] * R.x[k]; }
+    const float rstd = __builtin_amdgcn_rsqf(wave_sum_dpp(q) * inv_c + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const float xh = R.x[k] * rstd, gd = g[k] * cd[k];
+      R.x[k] = xh;
+      s1 += gd;
+      s2 += gd * xh;
+      dg[k] += cd[k] * xh;
+      db[k] += cd[k];
+    }
+    s1 = wave_sum_dpp(s1) * inv_c;
+    s2 = wave_sum_dpp(s2) * inv_c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      float4 o;
+      o.x = R.o[4 * i] + rstd * (g[4 * i] * cd[4 * i] - s1 - R.x[4 * i] * s2);
+      o.y = R.o[4 * i + 1] + rstd * (g[4 * i + 1] * cd[4 * i + 1] - s1 - R.x[4 * i + 1] * s2);
+      o.z = R.o[4 * i + 2] + rstd * (g[4 * i + 2] * cd[4 * i + 2] - s1 - R.x[4 * i + 2] * s2);
+      o.w = R.o[4 * i + 3] + rstd * (g[4 * i + 3] * cd[4 * i + 3] - s1 - R.x[4 * i + 3] * s2);
+      *reinterpret_cast<float4*>(dx + xr + i * 256 + lane * 4) = o;
+    }
+  };
+  const int64_t S = (int64_t)gridDim.x * 4;
+  int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  RowRegs A, B, D;
+  if (r < rows) load_row(r, A);
+  if (r + S < rows) load_row(r + S, B);
+  while (r < rows) {                     // three rows per trip: A, B, D rotate without moves
+    if (r + 2 * S < rows) load_row(r + 2 * S, D);
+    reduce_row(r, A);
+    r += S;
+    if (r >= rows) break;
+    if (r + 2 * S < rows) load_row(r + 2 * S, A);
+    reduce_row(r, B);
+    r += S;
+    if (r >= rows) break;
+    if (r + 2 * S < rows) load_row(r + 2 * S, B);
+    reduce_row(r, D);
+    r += S;
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = (k >> 2) * 256 + lane * 4 + (k & 3);
+    red[wave][0][c] = dg[k];
+    red[wave][1][c] = db[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    partial[(int64_t)blockIdx.x * 2 * C + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    partial[(int64_t)blockIdx.x * 2 * C + C + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+  }
+}
+
 // >= 4 rows per wave; at most 768 blocks = 3 per CU, what the C = 768 kernel's 163 VGPRs keep
 // resident (a 1024-block grid left a second, partial round on a third of the CUs)
+static int lnb_variant() {
+  static const int v = getenv("DSVT_LNB_VARIANT") ? atoi(getenv("DSVT_LNB_VARIANT")) : 2;   // tuning only
+  return v;
+}
+
 int ln_bwd_blocks(int64_t rows) {
+  const int64_t cap = lnb_variant() == 2 ? 512 : 768;      // ln_bwd768_kernel: 2 blocks per CU
   int64_t b = (rows + 15) / 16;
-  return (int)(b < 1 ? 1 : (b > 768 ? 768 : b));
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 
 hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
@@ -196,8 +316,13 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
                                                              goff, eps, partial)
 #define DSVT_LNB3(T) ln_bwd_kernel<T, true, 3><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, \
                                                                   gstride, goff, eps, partial)
-  static const int lnb_v = getenv("DSVT_LNB_VARIANT") ? atoi(getenv("DSVT_LNB_VARIANT")) : 1;   // tuning only
-  if (C == 768 && lnb_v == 1) {        // DPP reductions, reciprocal multiplies
+  const int lnb_v = lnb_variant();
+  if (C == 768 && lnb_v == 2) {        // two rows of look-ahead: 2 blocks per CU (224 VGPRs)
+    if (dy_dtype == 0)
+      ln_bwd768_kernel<bf16_t><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, rpg, gstride, goff, eps, partial);
+    else
+      ln_bwd768_kernel<float><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, rpg, gstride, goff, eps, partial);
+  } else if (C == 768 && lnb_v == 1) {        // DPP reductions, reciprocal multiplies
     if (dy_dtype == 0)
       ln_bwd_kernel<bf16_t, true, 3, true><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, (int)C, rpg,
                                                               gstride, goff, eps, partial);

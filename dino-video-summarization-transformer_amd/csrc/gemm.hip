@@ -376,8 +376,14 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // 256x256 kernel for the big N = 768 GEMMs: see the residual / N = 768 rules below
   const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= 128;
   if (epi == EPI_RESID && p.row_scale && gv == 20 && gemm_8ph_ok(p, epi)) return 20;
-  if (p.row_scale)              // DropPath row scales: the 128x128 and persistent kernels
+#ifndef DSVT_RESID_RS
+#define DSVT_RESID_RS 1
+#endif
+  if (p.row_scale) {            // DropPath row scales: the 128x128 and persistent kernels
+    if (epi == EPI_RESID && DSVT_RESID_RS == 20 && p.M >= 4096 && gemm_8ph_ok(p, epi)) return 20;   // A/B builds
+    if (epi == EPI_RESID && DSVT_RESID_RS == 3) return 3;
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
+  }
   if (gv >= 20 && gv <= 29) return gemm_8ph_ok(p, epi) ? gv : 1;
   if (epi >= EPI_GELU_SAVE) {   // training epilogues: 128x128 or the persistent kernel only
     if (gv == 1 || gv == 10) return gv;

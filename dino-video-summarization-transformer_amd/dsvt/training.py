@@ -15,8 +15,11 @@ kernels:
 Training-mode stochastic depth (DropPath, models/vit_utils.py:152-167) follows the
 reference's sample axes: per (b, patch) for the temporal branch (xt is [(B*N), T, C]), per
 (b, frame) for the spatial branch ([(B*T), 1+N, C]; the CLS output is the mean over frames of
-the DROPPED per-frame outputs) and per clip for the MLP, each scaled by 1/keep_prob.  The
-masks come from torch.rand on the device in that order, block by block.
+the DROPPED per-frame outputs) and per clip for the MLP, each scaled by 1/keep_prob.  All of a
+forward's masks come from ONE torch.rand draw on the device, laid out in the reference's call
+order (block by block: temporal, spatial, MLP), and the per-row scale tables of every block are
+built by batched tensor ops: a launch per mask and table was ~20 tiny kernels per block, whose
+host launch cost left the GPU idle for ~5 ms of every training step (rocprofv3 gap analysis).
 
 The gradients of every parameter are returned from Function.backward, so autograd's
 accumulation -- and DDP's bucketed all-reduce hooks -- see them like the reference's.
@@ -122,10 +125,19 @@ def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None):
     ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
 
 
-def _keep_scale(n, p, device):
-    """DropPath per-sample scale floor(keep + U[0,1)) / keep (models/vit_utils.py:152-167)."""
-    keep = 1.0 - p
-    return (torch.floor(keep + torch.rand(n, device=device, dtype=torch.float32)) / keep).contiguous()
+_KEEP = {}
+
+
+def _keep_scales(sizes, dps, device):
+    """DropPath per-sample scales floor(keep + U[0,1)) / keep (models/vit_utils.py:152-167) of
+    every drop_path call of one forward: `sizes[i]` samples at drop rate `dps[i]`, returned as one
+    flat fp32 tensor (call i's scales at offset sum(sizes[:i])) from a single torch.rand draw."""
+    key = (tuple(sizes), tuple(dps), str(device))
+    keep = _KEEP.get(key)
+    if keep is None:
+        keep = torch.tensor(np.repeat(np.asarray([1.0 - p for p in dps], np.float32), sizes), device=device)
+        _KEEP[key] = keep
+    return torch.floor(keep + torch.rand(keep.numel(), device=device, dtype=torch.float32)) / keep
 
 
 class _S:
@@ -191,25 +203,29 @@ def _block_weights(model):
 
 def _masks(model, nblk, B, Np, T, L, device):
     """DropPath scales for each block (None when inactive): temporal [B*Np], spatial [B*T]
-    (+ per-X-row bias scale [B*L]), MLP [B] (+ [B*L])."""
-    out = []
-    for blk in model.blocks[:nblk]:
-        dp = getattr(blk.drop_path, "drop_prob", 0.0)
-        if not model.training or dp <= 0.0:
-            out.append(None)
-            continue
+    (+ per-X-row bias scale [B*L]), MLP [B] (+ [B*L]) -- one draw for all active blocks, the
+    tables batched over them."""
+    act = [i for i, blk in enumerate(model.blocks[:nblk])
+           if model.training and getattr(blk.drop_path, "drop_prob", 0.0) > 0.0]
+    out = [None] * nblk
+    if not act:
+        return out
+    n = len(act)
+    chunk = B * Np + B * T + B
+    dps = [model.blocks[i].drop_path.drop_prob for i in act]
+    flat = _keep_scales([B * Np, B * T, B] * n, [p for p in dps for _ in range(3)], device).view(n, chunk)
+    t, s, mm = flat[:, :B * Np], flat[:, B * Np:B * Np + B * T], flat[:, B * Np + B * T:]
+    st = s.reshape(n, B, T)
+    rows_s = torch.empty(n, B, L, device=device, dtype=torch.float32)
+    rows_s[:, :, 0] = st.mean(2)
+    rows_s[:, :, 1:] = st.unsqueeze(2).expand(n, B, Np, T).reshape(n, B, Np * T)
+    s_cls = rows_s[:, :, 0].contiguous()                       # the CLS rows' (frame-mean) scale
+    m_rows = mm.reshape(n, B, 1).expand(n, B, L).reshape(n, B * L)
+    for j, i in enumerate(act):
         m = _S()
-        m.t = _keep_scale(B * Np, dp, device)
-        m.s = _keep_scale(B * T, dp, device)
-        m.m = _keep_scale(B, dp, device)
-        st = m.s.view(B, T)
-        rows_s = torch.empty(B, L, device=device, dtype=torch.float32)
-        rows_s[:, 0] = st.mean(1)
-        rows_s[:, 1:] = st.unsqueeze(1).expand(B, Np, T).reshape(B, Np * T)
-        m.s_rows = rows_s.reshape(-1).contiguous()
-        m.s_cls = rows_s[:, 0].contiguous()                    # the CLS rows' (frame-mean) scale
-        m.m_rows = m.m.view(B, 1).expand(B, L).reshape(-1).contiguous()
-        out.append(m)
+        m.t, m.s, m.m = t[j], s[j], mm[j]                       # contiguous rows of the draw
+        m.s_rows, m.s_cls, m.m_rows = rows_s[j].reshape(-1), s_cls[j], m_rows[j]
+        out[i] = m
     return out
 
 
@@ -539,18 +555,20 @@ def _plain_masks(model, nb, L, device):
     """DropPath scales of the joint / space-only block (timesformer.py:116-123, 184): x is
     [nb, L, C] -- nb = B clips (joint) or B*T frames (space-only) -- and each of the two
     residual branches draws one scale per sequence, attention first."""
-    out = []
-    for blk in model.blocks:
-        dp = getattr(blk.drop_path, "drop_prob", 0.0)
-        if not model.training or dp <= 0.0:
-            out.append(None)
-            continue
+    act = [i for i, blk in enumerate(model.blocks)
+           if model.training and getattr(blk.drop_path, "drop_prob", 0.0) > 0.0]
+    out = [None] * len(model.blocks)
+    if not act:
+        return out
+    n = len(act)
+    dps = [model.blocks[i].drop_path.drop_prob for i in act]
+    flat = _keep_scales([nb, nb] * n, [p for p in dps for _ in range(2)], device).view(n, 2, nb)
+    rows = flat.reshape(n, 2, nb, 1).expand(n, 2, nb, L).reshape(n, 2, nb * L)
+    for j, i in enumerate(act):
         m = _S()
-        m.a = _keep_scale(nb, dp, device)
-        m.m = _keep_scale(nb, dp, device)
-        m.a_rows = m.a.view(nb, 1).expand(nb, L).reshape(-1).contiguous()
-        m.m_rows = m.m.view(nb, 1).expand(nb, L).reshape(-1).contiguous()
-        out.append(m)
+        m.a, m.m = flat[j, 0], flat[j, 1]
+        m.a_rows, m.m_rows = rows[j, 0], rows[j, 1]
+        out[i] = m
     return out
 
 

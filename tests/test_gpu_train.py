@@ -73,13 +73,14 @@ def test_student_grads_plain_attention(gold_plain, attn, dtype, tag, monkeypatch
         masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
         state = {"off": 0, "i": 0}
 
-        def replay(n, p, device):
-            assert n == sizes[state["i"]], (n, sizes[state["i"]])
-            m = masks[state["off"]:state["off"] + n]
-            state["off"] += n
-            state["i"] += 1
+        def replay(ns, ps, device):           # one forward's masks, in the reference's call order
+            i = state["i"]
+            assert list(ns) == sizes[i:i + len(ns)], (list(ns), sizes[i:i + len(ns)])
+            m = masks[state["off"]:state["off"] + sum(ns)]
+            state["off"] += sum(ns)
+            state["i"] += len(ns)
             return torch.from_numpy(m.copy()).to(device)
-        monkeypatch.setattr(training, "_keep_scale", replay)
+        monkeypatch.setattr(training, "_keep_scales", replay)
     net = _student(dtype, tag == "drop", attn)
     crops = [torch.from_numpy(P.clip(1210 + i, (2, 3, 4, 64, 64))).cuda() for i in range(2)] + \
             [torch.from_numpy(P.clip(1220 + i, (2, 3, 4, 32, 32))).cuda() for i in range(2)]
@@ -130,13 +131,14 @@ def test_student_grads_vit2d_bn_head(dtype, tag, monkeypatch):
         masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
         state = {"off": 0, "i": 0}
 
-        def replay(n, p, device):
-            assert n == sizes[state["i"]], (n, sizes[state["i"]])
-            m = masks[state["off"]:state["off"] + n]
-            state["off"] += n
-            state["i"] += 1
+        def replay(ns, ps, device):           # one forward's masks, in the reference's call order
+            i = state["i"]
+            assert list(ns) == sizes[i:i + len(ns)], (list(ns), sizes[i:i + len(ns)])
+            m = masks[state["off"]:state["off"] + sum(ns)]
+            state["off"] += sum(ns)
+            state["i"] += len(ns)
             return torch.from_numpy(m.copy()).to(device)
-        monkeypatch.setattr(training, "_keep_scale", replay)
+        monkeypatch.setattr(training, "_keep_scales", replay)
     bb = VisionTransformer(img_size=[64], patch_size=16, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
                            qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
                            drop_path_rate=0.5 if tag == "drop" else 0.0)
@@ -217,13 +219,14 @@ def test_student_grads_match_reference(gold, dtype, tag, tail, monkeypatch):
         masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
         state = {"off": 0, "i": 0}
 
-        def replay(n, p, device):
-            assert n == sizes[state["i"]], (n, sizes[state["i"]])
-            m = masks[state["off"]:state["off"] + n]
-            state["off"] += n
-            state["i"] += 1
+        def replay(ns, ps, device):           # one forward's masks, in the reference's call order
+            i = state["i"]
+            assert list(ns) == sizes[i:i + len(ns)], (list(ns), sizes[i:i + len(ns)])
+            m = masks[state["off"]:state["off"] + sum(ns)]
+            state["off"] += sum(ns)
+            state["i"] += len(ns)
             return torch.from_numpy(m.copy()).to(device)
-        monkeypatch.setattr(training, "_keep_scale", replay)
+        monkeypatch.setattr(training, "_keep_scales", replay)
     net = _student(dtype, tag == "drop")
     net.backbone.cls_tail = tail
     crops = [torch.from_numpy(P.clip(1210 + i, (2, 3, 4, 64, 64))).cuda() for i in range(2)] + \
