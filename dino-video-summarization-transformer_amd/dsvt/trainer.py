@@ -80,6 +80,10 @@ class DINOTrainer:
         if hasattr(bb, "fold_temporal_fc"):
             bb.fold_temporal_fc = False
         self._s_params = [p for p in student.parameters()]
+        if ddp is None:          # gradients at fixed addresses: cached pointer tables (training.persistent_grad_arena)
+            for m in (getattr(student, "backbone", None), getattr(student, "head", None)):
+                if m is not None:
+                    m.dsvt_persistent_grads = True
         self._t_params = [p for p in teacher.parameters()]
 
     def step(self, images, it, check_finite=False):

@@ -66,11 +66,12 @@ class _Grads:
     buffer and whether it already holds a partial sum (False on the first write: the kernels
     then overwrite instead of accumulating, so no zero fill is needed)."""
 
-    def __init__(self, side=None, arena=None, seeded=()):
+    def __init__(self, side=None, arena=None, seeded=(), persistent=False):
         self.g = {}
         self.side = side               # weight gradients on this stream (None: the current one)
         self.arena = arena or {}       # id(p) -> preassigned buffer (dist.BlockGradReducer buckets)
         self.seeded = set(seeded)      # arena buffers that already hold a partial sum (no_sync steps)
+        self.persistent = persistent   # arena = persistent_grad_arena (hand out aliases)
         self._main = None
 
     def run_side(self, fn, inputs):
@@ -99,6 +100,10 @@ class _Grads:
             buf = self.arena.get(id(p))
             if buf is None:
                 buf = torch.empty(p.shape, device=p.device, dtype=torch.float32)
+            elif self.persistent:
+                # an alias of the persistent buffer (same storage, its own TensorImpl): autograd's
+                # AccumulateGrad then takes the returned gradient as .grad instead of cloning it
+                buf = buf.view(buf.shape)
             self.g[id(p)] = buf
             return buf, id(p) in self.seeded
         return buf, True
@@ -123,6 +128,24 @@ def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None):
     db, acc2 = G.acc(ln.bias)
     assert acc == acc2
     ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
+
+
+def persistent_grad_arena(module, params, device):
+    """Gradient buffers that live across steps (`module.dsvt_persistent_grads`, set by DINOTrainer
+    when it runs without DDP): every step's gradients land at the same addresses, so the
+    multi-tensor kernels' pointer tables (gradient clipping, AdamW; utils._tensor_list) are cache
+    hits.  A fresh pointer table per step meant a pinned host allocation + copy after the
+    backward, and the GPU sat idle ~2.5 ms of every step there (tools/gap_summary.py).  Valid
+    because the trainer drops every .grad (zero_grad(set_to_none=True)) before the next backward
+    writes the buffers again."""
+    ar = getattr(module, "_dsvt_grad_arena", None)
+    if ar is None:
+        ar = {}
+        object.__setattr__(module, "_dsvt_grad_arena", ar)
+    for p in params:
+        if p.requires_grad and id(p) not in ar:
+            ar[id(p)] = torch.empty(p.shape, device=device, dtype=torch.float32)
+    return ar
 
 
 _KEEP = {}
@@ -171,8 +194,11 @@ class BackboneFn(torch.autograd.Function):
             red.note_local()
             red = None
         arena, seeded = red.arena(dfeat.device) if red is not None else (None, ())
+        persist = red is None and getattr(model, "dsvt_persistent_grads", False)
+        if persist:
+            arena = persistent_grad_arena(model, ctx.params, dfeat.device)
         G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None,
-                   arena=arena, seeded=seeded)
+                   arena=arena, seeded=seeded, persistent=persist)
         offs = np.cumsum([0] + ctx.rows)
         for i in reversed(range(len(ctx.states))):
             # a block's gradients are final after the last group's pass over it: its bucket's
@@ -828,8 +854,11 @@ def _head_forward(head, x):
 def _head_backward(head, st, dlogits):
     mode = st.mode
     wt = head._wcache.transposed(mode)
-    G = _Grads()
     R, dev = dlogits.shape[0], dlogits.device
+    if getattr(head, "dsvt_persistent_grads", False):
+        G = _Grads(arena=persistent_grad_arena(head, list(head.parameters()), dev), persistent=True)
+    else:
+        G = _Grads()
     ll = head.last_layer
     dl = torch.empty(R, dlogits.shape[1], device=dev, dtype=mode)
     ops.cast(dlogits, dl)
