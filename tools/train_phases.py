@@ -53,8 +53,9 @@ def main():
             probe(label + " >")
             return r
         setattr(obj, name, g)
-    wrap(tr, "model", "student fwd")
-    wrap(tr, "teacher", "teacher fwd")
+    for mod, label in ((tr.student, "student fwd"), (tr.teacher, "teacher fwd")):
+        mod.register_forward_pre_hook(lambda m, a, _l=label: probe(_l + " <"))
+        mod.register_forward_hook(lambda m, a, o, _l=label: probe(_l + " >"))
     wrap(tr, "dino_loss", "loss")
     wrap(T, "clip_gradients", "clip")
     wrap(tr.optimizer, "step", "adamw")
