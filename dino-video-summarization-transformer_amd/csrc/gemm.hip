@@ -223,11 +223,21 @@ __device__ __forceinline__ void epilogue_128(const GemmParams& p, fv4 (&acc)[MI]
   }
 }
 
+template <int N>
+__device__ __forceinline__ void gk_vmwait() {
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
 template <typename T, int EPI, bool OUT_F32, bool PREF = false, int MI = 4>
 __global__ __launch_bounds__(256, MI == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   constexpr int BMv = 32 * MI;                       // tile rows
   constexpr int A_BYTES = BMv * BKB, SBYTES = A_BYTES + TILE_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SBYTES];
+  // 160x128 (one workgroup per CU): a 3-stage ring, loads two K steps ahead; 128x128: 2 stages
+  // (two workgroups per CU hide each other's waits)
+  constexpr int NST = MI == 5 ? 3 : 2;
+  constexpr int LPS = MI + 4;                        // LDS-DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NST * SBYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
@@ -250,8 +260,56 @@ __global__ __launch_bounds__(256, MI == 4 ? 2 : 1) void gemm_kernel(GemmParams p
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
 
-  stage_tile<MI>(A, lda_b, m0, p.M, 0, smem, wave, lane);
-  stage_tile(W, ldw_b, n0, p.N, 0, smem + A_BYTES, wave, lane);
+  auto stage_k = [&](int k, char* buf) {
+    stage_tile<MI>(A, lda_b, m0, p.M, (int64_t)k * BKB, buf, wave, lane);
+    stage_tile(W, ldw_b, n0, p.N, (int64_t)k * BKB, buf + A_BYTES, wave, lane);
+  };
+  if constexpr (NST == 3) {
+    const bool full3 = m0 + BMv <= p.M && n0 + BN <= p.N;
+    const bool peel3 = PREF && full3 && nk >= 2;
+    const int nmain3 = peel3 ? nk - 2 : nk;
+    stage_k(0, smem);
+    if (nk > 1) {
+      stage_k(1, smem + SBYTES);
+      gk_vmwait<LPS>();
+    } else {
+      gk_vmwait<0>();
+    }
+    __syncthreads();
+    // at the top of step kt its stage has landed for every wave; stage kt + 2 goes into the slot
+    // step kt - 1 read (released by that step's barrier)
+    for (int kt = 0; kt < nmain3; ++kt) {
+      char* cur = smem + (kt % 3) * SBYTES;
+      if (kt + 2 < nk) stage_k(kt + 2, smem + ((kt + 2) % 3) * SBYTES);
+      TileMMA<T>::run(cur, cur + A_BYTES, acc, wm, wn, lane);
+      if (kt + 2 < nk) gk_vmwait<LPS>();           // stage kt + 1 landed, kt + 2 in flight
+      else gk_vmwait<0>();
+      __syncthreads();
+    }
+    if constexpr (PREF) {
+      if (peel3) {                                 // stages nk - 2 (landed) and nk - 1 (issued)
+        char* cur = smem + ((nk - 2) % 3) * SBYTES;
+        char* nxt = smem + ((nk - 1) % 3) * SBYTES;
+        __builtin_amdgcn_sched_barrier(0);
+        float4 xpre[MI][4];
+        resid_load(p, m0, n0, wm, wn, lane, xpre);
+        __builtin_amdgcn_sched_barrier(0);
+        TileMMA<T>::run(cur, cur + A_BYTES, acc, wm, wn, lane);
+        gk_vmwait<4 * MI>();                       // stage nk - 1, not the residual loads
+        __syncthreads();
+        TileMMA<T>::run(nxt, nxt + A_BYTES, acc, wm, wn, lane);
+        mfma_result_fence();
+        epilogue_128<T, EPI, OUT_F32, false, true, MI>(p, acc, m0, n0, wm, wn, lane, xpre);
+        return;
+      }
+    }
+    mfma_result_fence();
+    if (full3) epilogue_128<T, EPI, OUT_F32, false, false, MI>(p, acc, m0, n0, wm, wn, lane);
+    else epilogue_128<T, EPI, OUT_F32, true, false, MI>(p, acc, m0, n0, wm, wn, lane);
+    return;
+  }
+
+  stage_k(0, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
