@@ -147,7 +147,8 @@ class SwinTransformerBlock3D(nn.Module):
         ops.swin_ln_rows(X, win, self.norm1, a, rows_w)
         qkv = torch.empty(rows_w, 3 * C, device=dev, dtype=mode)
         ops.gemm(a, wq, self.attn.qkv.bias, qkv)
-        o = ctx.zeros((rows_w, ldk), mode)                     # pad columns stay zero (proj K)
+        # pad columns (proj K, C = 96 -> 128) must stay zero; the attention kernel writes the rest
+        o = ctx.zeros((rows_w, ldk), mode) if ldk != C else torch.empty(rows_w, ldk, device=dev, dtype=mode)
         ops.attn_window(qkv, o, ctx.bias(self.attn, N), reg, rows_w // N, nW, N, self.num_heads, self.attn.scale)
         wpj, _ = wp(self.attn.proj.weight)
         y = torch.empty(rows_w, C, device=dev, dtype=torch.float32)
