@@ -5,7 +5,7 @@
 // Geometry: a wave owns QT 16-query tiles of one (sequence, head); a workgroup is either
 //   4 waves x QT (QT = 1 or 2: 64 / 128 queries, 48 KiB LDS, three workgroups per CU), or
 //   8 waves, waves 0-3 with QA tiles and waves 4-7 with QB (e.g. 3 + 2: 320 queries), one
-//   workgroup per CU (96 KiB LDS).  A SIMD then holds waves w and w + 4 of the workgroup, i.e.
+//   workgroup per CU (64 KiB LDS; the register count keeps a second one out).  A SIMD then holds waves w and w + 4 of the workgroup, i.e.
 //   QA + QB query tiles: the split is chosen so that the grid's per-SIMD work is even -- config 4
 //   (2 clips x 12 heads x 197 tiles) as 240 workgroups of 5 tiles per SIMD instead of 600
 //   workgroups of 2 tiles at three per CU (88 CUs carry 6 tiles per SIMD, the rest 4).
@@ -330,7 +330,12 @@ __device__ __forceinline__ void flash_run(const AttnParams& p, char* smem, const
 }
 
 constexpr int FA4_NBUF = 3;                   // 4-wave workgroups: 48 KiB, three per CU
-constexpr int FA8_NBUF = 6;                   // 8-wave: 96 KiB, so exactly one workgroup per CU
+// 8-wave: a 4-tile ring (64 KiB; > 128 VGPRs keep one workgroup per CU).  Measured, interleaved on
+// one box (tools/gpu_s27.sh): 2 clips 79.9 us at 4 tiles vs 83.3 / 84.0 / 83.4 / 85 at 3 / 5 / 6 / 9
+#ifndef DSVT_FA8_NBUF
+#define DSVT_FA8_NBUF 4
+#endif
+constexpr int FA8_NBUF = DSVT_FA8_NBUF;
 
 }  // namespace
 
