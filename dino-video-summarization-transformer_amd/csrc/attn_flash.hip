@@ -329,7 +329,10 @@ __device__ __forceinline__ void flash_run(const AttnParams& p, char* smem, const
   }
 }
 
-constexpr int FA4_NBUF = 3;                   // 4-wave workgroups: 48 KiB, three per CU
+#ifndef DSVT_FA4_NBUF
+#define DSVT_FA4_NBUF 3                       // A/B builds: 2
+#endif
+constexpr int FA4_NBUF = DSVT_FA4_NBUF;       // 4-wave workgroups: 48 KiB, three per CU
 // 8-wave: a 4-tile ring (64 KiB; > 128 VGPRs keep one workgroup per CU).  Measured, interleaved on
 // one box (tools/gpu_s27.sh): 2 clips 79.9 us at 4 tiles vs 83.3 / 84.0 / 83.4 / 85 at 3 / 5 / 6 / 9
 #ifndef DSVT_FA8_NBUF

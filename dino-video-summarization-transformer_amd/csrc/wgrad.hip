@@ -35,7 +35,10 @@ constexpr int WG_T = 256;                  // output tile: 256 n x 256 k
 constexpr int WG_ROWB = 512;               // bytes per staged row (256 bf16)
 constexpr int WG_OP = WG_BM * WG_ROWB;     // 16 KiB per operand per stage
 constexpr int WG_STAGE = 2 * WG_OP;        // [dY | X]
-constexpr int WG_NST = 4;                  // ring depth (128 KiB)
+#ifndef DSVT_WG_NST
+#define DSVT_WG_NST 4                      // A/B builds: 2
+#endif
+constexpr int WG_NST = DSVT_WG_NST;        // ring depth (128 KiB; a power of two)
 
 // byte offset of (row, column c) in a staged [32][256] operand (c % 4 == 0 for the 8-byte reads)
 __device__ __forceinline__ int wg_off(int row, int c) {
