@@ -3,14 +3,15 @@
 //   models/timesformer.py:55-87 (Attention.forward) under :120-123 (joint_space_time)
 //
 // Geometry: a wave owns QT 16-query tiles of one (sequence, head); a workgroup is either
-//   4 waves x QT (QT = 1 or 2: 64 / 128 queries, 48 KiB LDS, three workgroups per CU), or
+//   4 waves x QT (QT = 1 or 2: 64 / 128 queries, 32 KiB LDS, three workgroups per CU), or
 //   8 waves, waves 0-3 with QA tiles and waves 4-7 with QB (e.g. 3 + 2: 320 queries), one
 //   workgroup per CU (64 KiB LDS; the register count keeps a second one out).  A SIMD then holds waves w and w + 4 of the workgroup, i.e.
 //   QA + QB query tiles: the split is chosen so that the grid's per-SIMD work is even -- config 4
 //   (2 clips x 12 heads x 197 tiles) as 240 workgroups of 5 tiles per SIMD instead of 600
 //   workgroups of 2 tiles at three per CU (88 CUs carry 6 tiles per SIMD, the rest 4).
 // K/V: 64-key tiles staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB = 8 rows x 128 B per
-// wave instruction) into an NBUF-deep ring, NBUF - 1 tiles ahead, one barrier per tile.  The
+// wave instruction) into an NBUF-deep ring (2 tiles for 4 waves, 4 for 8: measured optima),
+// NBUF - 1 tiles ahead, one barrier per tile.  The
 // rows of a sequence are contiguous token rows of the [rows, 3C] qkv tensor, so the per-lane
 // DMA source offset carries the LDS swizzle (the same for every full tile: a scalar tile base +
 // a per-lane 32-bit offset):
@@ -329,10 +330,12 @@ __device__ __forceinline__ void flash_run(const AttnParams& p, char* smem, const
   }
 }
 
+// 4-wave workgroups: a 2-tile ring (32 KiB; the registers allow three per CU): 2 clips forced to
+// 64-query workgroups 86.3 vs 92.1 us with 3 tiles, 128-query 87.0 vs 87.5 (tools/gpu_s28.sh)
 #ifndef DSVT_FA4_NBUF
-#define DSVT_FA4_NBUF 3                       // A/B builds: 2
+#define DSVT_FA4_NBUF 2
 #endif
-constexpr int FA4_NBUF = DSVT_FA4_NBUF;       // 4-wave workgroups: 48 KiB, three per CU
+constexpr int FA4_NBUF = DSVT_FA4_NBUF;
 // 8-wave: a 4-tile ring (64 KiB; > 128 VGPRs keep one workgroup per CU).  Measured, interleaved on
 // one box (tools/gpu_s27.sh): 2 clips 79.9 us at 4 tiles vs 83.3 / 84.0 / 83.4 / 85 at 3 / 5 / 6 / 9
 #ifndef DSVT_FA8_NBUF

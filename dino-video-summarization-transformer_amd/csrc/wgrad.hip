@@ -36,7 +36,7 @@ constexpr int WG_ROWB = 512;               // bytes per staged row (256 bf16)
 constexpr int WG_OP = WG_BM * WG_ROWB;     // 16 KiB per operand per stage
 constexpr int WG_STAGE = 2 * WG_OP;        // [dY | X]
 #ifndef DSVT_WG_NST
-#define DSVT_WG_NST 4                      // A/B builds: 2
+#define DSVT_WG_NST 4                      // A/B builds: 2 (train step 125.0 vs 127.7, tools/gpu_s28.sh)
 #endif
 constexpr int WG_NST = DSVT_WG_NST;        // ring depth (128 KiB; a power of two)
 
