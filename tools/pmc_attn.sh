@@ -2,8 +2,8 @@
 # counter passes for the joint flash-attention kernel at config 4's size (each --pmc set its own run)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp VARIANTS=12
-OUT=gpurun_out/pmc_attn; rm -rf $OUT; mkdir -p $OUT
+export TMPDIR=/tmp VARIANTS=${VARIANTS:-13}
+OUT=gpurun_out/${PMC_OUT:-pmc_attn}; rm -rf $OUT; mkdir -p $OUT
 i=0
 for set in "GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SALU" \
@@ -15,4 +15,4 @@ for set in "GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" \
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; fi
   if [ $rc -ge 124 ]; then exit $rc; fi
 done
-python3 tools/pmc_table.py $OUT --match 'attn_flash_bf16<2>' --flop 60.5e9 --algo-bytes 38.5e6 2>&1 | tail -40 || true
+python3 tools/pmc_table.py $OUT --match "${PMC_MATCH:-attn_flash8_bf16<3, 2>}" --clock-mhz 2100 --flop 60.5e9 --algo-bytes 38.5e6 2>&1 | tail -40 || true

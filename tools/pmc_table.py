@@ -30,6 +30,8 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--clock-mhz", type=float, default=2400.0)
     ap.add_argument("--match", default="gemm", help="kernel-name substring")
+    ap.add_argument("--xcds", type=float, default=8.0,
+                    help="GRBM_GUI_ACTIVE is summed over the XCDs (MI355X_MICROARCH.md): divide by this")
     ap.add_argument("--flop", type=float, default=2.0 * 25104 * 768 * 768)
     ap.add_argument("--algo-bytes", type=float, default=25104 * 768 * (2 + 4 + 4) + 768 * 768 * 2)
     a = ap.parse_args()
@@ -38,7 +40,7 @@ def main():
         if not c:
             print("## %s: no counters" % d)
             continue
-        g = c.get("GRBM_GUI_ACTIVE", 0.0)
+        g = c.get("GRBM_GUI_ACTIVE", 0.0) / a.xcds         # kernel cycles
         us = g / a.clock_mhz
         wc = c.get("SQ_WAVE_CYCLES", 0.0)
         fetch = c.get("FETCH_SIZE", 0.0) * 1024
@@ -46,7 +48,13 @@ def main():
         print("## %s\n%s" % (d, name))
         for k in sorted(c):
             print("  %-28s %16.0f" % (k, c[k]))
-        print("  kernel time (GRBM_GUI_ACTIVE @ %.0f MHz)   %8.1f us" % (a.clock_mhz, us))
+        print("  kernel time (GRBM_GUI_ACTIVE / %g XCDs @ %.0f MHz) %8.1f us" % (a.xcds, a.clock_mhz, us))
+        if c.get("SQ_WAVES") and c.get("SQ_INSTS_VALU"):
+            print("  VALU / MFMA instructions per wave        %8.0f / %.0f" %
+                  (c["SQ_INSTS_VALU"] / c["SQ_WAVES"], c.get("SQ_INSTS_MFMA", 0) / c["SQ_WAVES"]))
+        if g and c.get("SQ_ACTIVE_INST_VALU"):
+            # quad-cycles (x4) summed over waves, per SIMD (1024), against the kernel's cycles
+            print("  VALU-active cycles per SIMD / kernel cyc %8.3f" % (c["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / g))
         if wc:
             print("  SQ_WAIT_ANY / SQ_WAVE_CYCLES             %8.3f" % (c.get("SQ_WAIT_ANY", 0) / wc))
             print("  SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES        %8.3f" % (c.get("SQ_WAIT_INST_ANY", 0) / wc))
