@@ -245,35 +245,66 @@ def test_e2e_cfg1_multicrop_head_loss(tiny_sd, dtype, tol):
     assert rel(loss_fn.center.cpu(), f["center"]) < tol
 
 
-def test_config2_chain_loss_bf16_vs_fp32(base_sd):
-    """Config-2-shaped chain (the bench's workload, 2 clips): ViT-B/16 student on 2 global
-    8x224^2 + 6 local 8x96^2 crops and teacher on the globals -> DINOHead(768 -> 65536) ->
-    DINOLoss(ncrops 8).  The fp32 parity path's loss is within 1e-3 of the torch-CPU oracle,
-    and the bf16 perf path's loss within 1e-3 (relative) of the fp32 one -- the north-star's
-    loss bar, asserted on the benchmarked mode."""
+@pytest.mark.parametrize("clips,ln_fold", [(2, "auto"), (2, True), (8, "auto")])
+def test_config2_chain_loss_bf16_vs_fp32(base_sd, monkeypatch, clips, ln_fold):
+    """Config-2 chain: ViT-B/16 student on 2 global 8x224^2 + 6 local 8x96^2 crops and teacher
+    on the globals -> DINOHead(768 -> 65536) -> DINOLoss(ncrops 8), `clips` clips per crop.  The
+    fp32 parity path's loss is within 1e-3 of the torch-CPU oracle (train_ssl.py:653-669), and the
+    bf16 perf path's loss within 1e-3 (relative) of the fp32 one -- the north-star's loss bar.
+
+    clips = 8 is the bench's own workload (bench.py: 8 multi-crop clips per GPU): its backbone
+    calls have 16 x 1569 = 25 104 and 48 x 289 = 13 872 token rows, so "auto" turns on the
+    LayerNorm fold (dsvt_gemm_lnx_fwd / dsvt_gemm_resid_stats_fwd) and the fused temporal
+    attention (dsvt_qkv_temporal_attn_fwd) exactly as in the timed step; the test asserts both
+    kernels ran.  At 2 clips "auto" leaves them off (6 276 / 3 468 rows), and True forces them on."""
     from oracle import torch_cpu as TC
+    from dsvt import ops
     from dsvt.loss import DINOLoss
     from dsvt.utils import MultiCropWrapper, dino_forward
     from dsvt.vision_transformer import DINOHead
     t_sd = P.timesformer_state(12)
     hs, ht = P.dino_head_state(7, 768, 65536), P.dino_head_state(8, 768, 65536)
-    glob = [P.clip(1201 + i, (2, 3, 8, 224, 224)) for i in range(2)]
-    loc = [P.clip(1203 + i, (2, 3, 8, 96, 96)) for i in range(6)]
+    glob = [P.clip(1201 + i, (clips, 3, 8, 224, 224)) for i in range(2)]
+    loc = [P.clip(1203 + i, (clips, 3, 8, 96, 96)) for i in range(6)]
+    calls = {"gemm_lnx": 0, "qkv_temporal_attn": 0, "gemm_resid_stats": 0}
+
+    def counted(name):
+        fn = getattr(ops, name)
+
+        def wrap(*a, **k):
+            calls[name] += 1
+            return fn(*a, **k)
+        return wrap
+    for name in calls:
+        monkeypatch.setattr(ops, name, counted(name))
 
     def net(sd, hsd, dtype):
         hd = DINOHead(768, 65536)
         hd.load_state_dict({k: torch.from_numpy(v) for k, v in hsd.items()})
         hd = hd.cuda()
         hd.dsvt_dtype = dtype
-        return MultiCropWrapper(tsf(sd, dtype), hd)
-    losses = {}
+        bb = tsf(sd, dtype)
+        bb.ln_fold = ln_fold
+        return MultiCropWrapper(bb, hd)
+    losses, logits = {}, {}
     for dtype in (torch.float32, torch.bfloat16):
         student, teacher = net(base_sd, hs, dtype), net(t_sd, ht, dtype)
         lf = DINOLoss(65536, 8, 0.04, 0.04, 0, 100).cuda()
         with torch.no_grad():
             s_out, t_out = dino_forward(student, teacher, [cu(x) for x in glob + loc])
             losses[dtype] = lf(s_out, t_out, 0).item()
+            logits[dtype] = (s_out.cpu(), t_out.cpu())
         del student, teacher
+        if dtype == torch.float32:
+            assert not any(calls.values()), calls          # the fold is a bf16-only path
+    fold_on = ln_fold is True or clips == 8
+    # per backbone call: one fused temporal kernel per block, 2 folded GEMMs (qkv, fc1) per block but
+    # the CLS-only last one (its fc1 runs on the CLS rows alone)
+    if fold_on:
+        assert calls["qkv_temporal_attn"] >= 3 * 12 and calls["gemm_lnx"] >= 3 * 11 * 2, calls
+        assert calls["gemm_resid_stats"] > 0, calls
+    else:
+        assert not any(calls.values()), calls
     # torch-CPU oracle: reference module order, one backbone call per resolution group
     cs, ct = TC.TimeSformerCPU(base_sd, 12), TC.TimeSformerCPU(t_sd, 12)
     g_in = torch.from_numpy(np.concatenate(glob))
@@ -282,8 +313,12 @@ def test_config2_chain_loss_bf16_vs_fp32(base_sd):
     t_ref = TC.DINOHeadCPU(ht)(ct.forward_features(g_in))
     ref, _ = TC.dino_loss(s_ref, t_ref, torch.zeros(1, 65536), 8, 0.04)
     ref = float(ref)
-    print("config-2 chain loss: oracle %.6f fp32 %.6f bf16 %.6f" % (ref, losses[torch.float32],
-                                                                    losses[torch.bfloat16]))
+    e_s = rel(logits[torch.bfloat16][0], logits[torch.float32][0])
+    e_t = rel(logits[torch.bfloat16][1], logits[torch.float32][1])
+    print("config-2 chain (%d clips, ln_fold %s): loss oracle %.6f fp32 %.6f bf16 %.6f; bf16 logits vs fp32: "
+          "student %.3g teacher %.3g" % (clips, ln_fold, ref, losses[torch.float32], losses[torch.bfloat16], e_s, e_t))
+    assert rel(logits[torch.float32][0], s_ref) < FP32_TOL and rel(logits[torch.float32][1], t_ref) < FP32_TOL
+    assert e_s < BF16_TOL and e_t < BF16_TOL
     assert abs(losses[torch.float32] - ref) / abs(ref) < 1e-3
     assert abs(losses[torch.bfloat16] - losses[torch.float32]) / abs(losses[torch.float32]) < 1e-3
 
@@ -425,14 +460,22 @@ def test_frame_scores_vitb_local3_global30(base_sd, dtype, tol):
         assert mismatched <= 16 and worst <= 1, (mismatched, worst)
 
 
-def test_bf16_vs_fp32_full_size(base_sd):
-    """Size-independent property at the bench shape (B=4 clips, 8x224^2): the bf16 perf path
-    tracks the fp32 parity path, whose own parity is pinned above."""
-    x = cu(P.clip(41, (4, 3, 8, 224, 224)))
+@pytest.mark.parametrize("clips", [4, 16])
+def test_bf16_vs_fp32_full_size(base_sd, clips):
+    """Size-independent property at the bench shape (8x224^2): the bf16 perf path tracks the fp32
+    parity path, whose own parity is pinned above.  16 clips is the bench's global backbone call
+    (25 104 token rows): "auto" runs it with the LayerNorm fold and the fused temporal attention,
+    as the timed step does; 4 clips (6 276 rows) runs the LayerNorm-pass path."""
+    x = cu(P.clip(41, (clips, 3, 8, 224, 224)))
     with torch.no_grad():
+        mb = tsf(base_sd, torch.bfloat16)
+        assert mb._ln_fold_on(torch.bfloat16, clips * 1569) == (clips == 16)
+        b = mb(x).cpu()
+        del mb
         a = tsf(base_sd, torch.float32)(x).cpu()
-        b = tsf(base_sd, torch.bfloat16)(x).cpu()
-    assert rel(b, a) < BF16_TOL
+    e = rel(b, a)
+    print("bf16 vs fp32 at %d clips: %.3g" % (clips, e))
+    assert e < BF16_TOL
     # batch invariance: clip 2 alone == clip 2 inside the batch (fp32)
     with torch.no_grad():
         c = tsf(base_sd, torch.float32)(x[2:3]).cpu()
