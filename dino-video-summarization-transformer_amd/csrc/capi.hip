@@ -742,13 +742,14 @@ int dsvt_bn_bwd_sums(int dtype, const void* dz, const float* xhat, int64_t R, in
   return e == hipSuccess ? 0 : hip_fail(e, "bn_bwd_sums");
 }
 
-int dsvt_bn_bwd(int dtype, const void* dz, const float* xhat, const double* sums, double count, const float* gamma,
+int dsvt_bn_bwd(int dtype, const void* dz, const float* xhat, const double* sums, const double* param_sums,
+                double count, const float* gamma,
                 const float* rstd, float* dx, float* dgamma, float* dbeta, int accumulate, int64_t R, int64_t D,
                 void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "bn_bwd: bad dtype");
   REQUIRE(dz && xhat && sums && rstd && dx && R > 0 && D > 0 && count >= 1.0, "bn_bwd: bad args");
-  hipError_t e = launch_bn_bwd_dx(dtype, dz, xhat, sums, count, gamma, rstd, dx, dgamma, dbeta, accumulate, R, D,
-                                  (hipStream_t)stream);
+  hipError_t e = launch_bn_bwd_dx(dtype, dz, xhat, sums, param_sums ? param_sums : sums, count, gamma, rstd, dx,
+                                  dgamma, dbeta, accumulate, R, D, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "bn_bwd");
 }
 

@@ -8,7 +8,8 @@
 //             mean / rstd (+ running-stat update in training)    bn_finalize
 //             y = GELU((x - mean) * rstd * gamma + beta), xhat and GELU'(.) saved for the backward
 //   backward: sums[D | D] = (sum dz, sum dz * xhat)               bn_bwd_sums (all-reduced for SyncBN)
-//             dx = gamma * rstd * (dz - sum dz / n - xhat * sum(dz xhat) / n), dgamma, dbeta
+//             dx = gamma * rstd * (dz - sum dz / n - xhat * sum(dz xhat) / n) from the reduced sums,
+//             dgamma, dbeta from the local ones
 // where dz = dL/d(BatchNorm output) (the GELU' already applied by the DGELU GEMM epilogue).
 #include "common.h"
 #include "internal.h"
@@ -102,7 +103,8 @@ __global__ void bn_bwd_dx_kernel(const T* __restrict__ dz, const float* __restri
   }
 }
 
-// dgamma (+)= sum dz * xhat, dbeta (+)= sum dz (from the all-reduced sums)
+// dgamma (+)= sum dz * xhat, dbeta (+)= sum dz -- from this process's own sums under SyncBatchNorm
+// (torch's SyncBatchNorm returns local weight / bias gradients; DDP averages them)
 __global__ void bn_param_grads_kernel(const double* __restrict__ sums, int64_t D, float* __restrict__ dgamma,
                                       float* __restrict__ dbeta, int accumulate) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -150,7 +152,8 @@ hipError_t launch_bn_bwd_sums(int dtype, const void* dz, const float* xhat, int6
   return hipGetLastError();
 }
 
-hipError_t launch_bn_bwd_dx(int dtype, const void* dz, const float* xhat, const double* sums, double count,
+hipError_t launch_bn_bwd_dx(int dtype, const void* dz, const float* xhat, const double* sums,
+                            const double* param_sums, double count,
                             const float* gamma, const float* rstd, float* dx, float* dgamma, float* dbeta,
                             int accumulate, int64_t R, int64_t D, hipStream_t s) {
   if (dtype == 0)
@@ -159,7 +162,7 @@ hipError_t launch_bn_bwd_dx(int dtype, const void* dz, const float* xhat, const 
   else
     bn_bwd_dx_kernel<float><<<elems_grid(R * D), 256, 0, s>>>((const float*)dz, xhat, sums, count, gamma, rstd, dx,
                                                               R, D);
-  if (dgamma || dbeta) bn_param_grads_kernel<<<cols_grid(D), 256, 0, s>>>(sums, D, dgamma, dbeta, accumulate);
+  if (dgamma || dbeta) bn_param_grads_kernel<<<cols_grid(D), 256, 0, s>>>(param_sums, D, dgamma, dbeta, accumulate);
   return hipGetLastError();
 }
 

@@ -249,7 +249,8 @@ hipError_t launch_bn_gelu(int dtype, const float* x, const float* mean, const fl
                           const float* beta, void* y, void* gelu_grad, float* xhat, int64_t R, int64_t D, hipStream_t s);
 hipError_t launch_bn_bwd_sums(int dtype, const void* dz, const float* xhat, int64_t R, int64_t D, double* sums,
                               hipStream_t s);
-hipError_t launch_bn_bwd_dx(int dtype, const void* dz, const float* xhat, const double* sums, double count,
+hipError_t launch_bn_bwd_dx(int dtype, const void* dz, const float* xhat, const double* sums,
+                            const double* param_sums, double count,
                             const float* gamma, const float* rstd, float* dx, float* dgamma, float* dbeta,
                             int accumulate, int64_t R, int64_t D, hipStream_t s);
 

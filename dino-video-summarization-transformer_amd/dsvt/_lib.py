@@ -12,6 +12,7 @@ BF16, F32 = 0, 1
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID = 0, 1, 2
 EPI_GELU_SAVE, EPI_DGELU = 4, 5
 GEMM_FEW_ROWS = 0x100           # OR-ed into the epilogue: a few-row GEMM (the K-split skinny kernel)
+ABI_VERSION = 2                # DSVT_ABI_VERSION of include/dsvt.h this binding is written against
 LN_FOLD_C, LN_PARTS = 768, 12   # dsvt_gemm_lnx_fwd: C of the folded LayerNorm, float2 partials per row
 TOKENS_NT, TOKENS_FRAME = 0, 1
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
@@ -39,7 +40,7 @@ SIGNATURES = {
     "dsvt_bn_finalize": (_i32, [_p, _f64, _i64, _f32, _f32, _i32, _p, _p, _p, _p, _p]),
     "dsvt_bn_gelu_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
     "dsvt_bn_bwd_sums": (_i32, [_i32, _p, _p, _i64, _i64, _p, _p]),
-    "dsvt_bn_bwd": (_i32, [_i32, _p, _p, _p, _f64, _p, _p, _p, _p, _p, _i32, _i64, _i64, _p]),
+    "dsvt_bn_bwd": (_i32, [_i32, _p, _p, _p, _p, _f64, _p, _p, _p, _p, _p, _i32, _i64, _i64, _p]),
     "dsvt_gemm_resid_stats_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _p]),
     "dsvt_gemm_lnx_fwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _p, _f32, _p, _p, _p, _p, _i64, _i64, _i64,
@@ -137,7 +138,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.dsvt_version() != 1:
+        if handle.dsvt_version() != ABI_VERSION:
             raise DsvtError("libdsvt ABI version mismatch")
         _lib = handle
     return _lib

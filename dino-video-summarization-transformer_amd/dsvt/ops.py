@@ -118,10 +118,17 @@ def qkv_temporal_attn(xb, stats, eps, folded_heads, out, M, heads, T, scale, in_
 
 
 # ---------------------------------------------------------------- DINOHead(use_bn=True)
+def _bn_synced(group):
+    """Does a SyncBatchNorm of this process group reduce over more than this process?"""
+    import torch.distributed as dist
+    return not (group is False or not (dist.is_available() and dist.is_initialized())
+                or dist.get_world_size(group) == 1)
+
+
 def _bn_allreduce(sums, count, group):
     """SyncBatchNorm: the column sums and the row count over the process group (fp64)."""
     import torch.distributed as dist
-    if group is False or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    if not _bn_synced(group):
         return count
     cnt = torch.tensor([float(count)], device=sums.device, dtype=torch.float64)
     dist.all_reduce(sums, group=group)
@@ -161,13 +168,19 @@ def bn_gelu(x, bn, out, gelu_grad=None, xhat=None, sync_group=False):
 
 
 def bn_bwd(dz, xhat, rstd, count, bn, dx, dgamma=None, dbeta=None, accumulate=False, sync_group=False):
-    """dx (fp32) of BatchNorm1d in training mode from dz = dL/d(its output); dgamma / dbeta too."""
+    """dx (fp32) of BatchNorm1d in training mode from dz = dL/d(its output); dgamma / dbeta too.
+    SyncBatchNorm: dx from the group's sums, dgamma / dbeta from this process's own (torch's
+    SyncBatchNorm backward; DDP then averages the parameter gradients over the ranks)."""
     R, D = xhat.shape
     sums = torch.empty(2 * D, device=dz.device, dtype=torch.float64)
     call("dsvt_bn_bwd_sums", _dt(dz.dtype), _ptr(dz), _ptr(xhat), R, D, _ptr(sums), _stream())
+    local = None
+    if _bn_synced(sync_group) and (dgamma is not None or dbeta is not None):
+        local = sums.clone()
     _bn_allreduce(sums, count, sync_group)
     w = bn.weight.detach() if bn.affine else None
-    call("dsvt_bn_bwd", _dt(dz.dtype), _ptr(dz), _ptr(xhat), _ptr(sums), float(count), _ptr(w), _ptr(rstd),
+    call("dsvt_bn_bwd", _dt(dz.dtype), _ptr(dz), _ptr(xhat), _ptr(sums), _ptr(local), float(count), _ptr(w),
+         _ptr(rstd),
          _ptr(dx), _ptr(dgamma), _ptr(dbeta), int(accumulate), R, D, _stream())
     return dx
 

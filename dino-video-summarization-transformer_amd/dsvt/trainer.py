@@ -86,6 +86,13 @@ class DINOTrainer:
                     m.dsvt_persistent_grads = True
         self._t_params = [p for p in teacher.parameters()]
 
+    def backward(self, loss):
+        """zero_grad(set_to_none=True) + loss.backward() (train_ssl.py:538-545).  Every .grad is
+        dropped first: the persistent gradient buffers (training.persistent_grad_arena) are then
+        free, and the backward makes them the new .grad."""
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+
     def step(self, images, it, check_finite=False):
         epoch = it // self.niter_per_ep
         for i, pg in enumerate(self.optimizer.param_groups):       # train_ssl.py:486-490
@@ -111,8 +118,7 @@ class DINOTrainer:
         loss = self.dino_loss(s_out, t_out, epoch)
         if check_finite and not math.isfinite(loss.item()):        # :530-532
             raise FloatingPointError("Loss is %s, stopping training" % loss.item())
-        self.optimizer.zero_grad(set_to_none=True)
-        loss.backward()
+        self.backward(loss)
         if self.clip_grad:
             clip_gradients(self.student, self.clip_grad)           # :547-548
         cancel_gradients_last_layer(epoch, self.student, self.freeze_last_layer)

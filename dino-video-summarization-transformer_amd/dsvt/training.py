@@ -24,6 +24,7 @@ host launch cost left the GPU idle for ~5 ms of every training step (rocprofv3 g
 The gradients of every parameter are returned from Function.backward, so autograd's
 accumulation -- and DDP's bucketed all-reduce hooks -- see them like the reference's.
 """
+import collections
 import math
 
 import numpy as np
@@ -71,7 +72,7 @@ class _Grads:
         self.side = side               # weight gradients on this stream (None: the current one)
         self.arena = arena or {}       # id(p) -> preassigned buffer (dist.BlockGradReducer buckets)
         self.seeded = set(seeded)      # arena buffers that already hold a partial sum (no_sync steps)
-        self.persistent = persistent   # arena = persistent_grad_arena (hand out aliases)
+        self.persistent = persistent   # arena = persistent_grad_arena: deliver() sets p.grad itself
         self._main = None
 
     def run_side(self, fn, inputs):
@@ -97,16 +98,36 @@ class _Grads:
     def acc(self, p):
         buf = self.g.get(id(p))
         if buf is None:
-            buf = self.arena.get(id(p))
-            if buf is None:
-                buf = torch.empty(p.shape, device=p.device, dtype=torch.float32)
-            elif self.persistent:
-                # an alias of the persistent buffer (same storage, its own TensorImpl): autograd's
-                # AccumulateGrad then takes the returned gradient as .grad instead of cloning it
-                buf = buf.view(buf.shape)
+            seeded = id(p) in self.seeded
+            if self.persistent and _own_grad(p):
+                # p.grad already holds a sum (an earlier autograd node of this backward -- the 2-D
+                # ViT's second resolution group -- or an earlier micro-step): accumulate into it
+                buf, seeded = p.grad, True
+            else:
+                buf = self.arena.get(id(p))
+                if buf is None:
+                    buf = torch.empty(p.shape, device=p.device, dtype=torch.float32)
             self.g[id(p)] = buf
-            return buf, id(p) in self.seeded
+            return buf, seeded
         return buf, True
+
+    def deliver(self, params):
+        """The gradients to return from an autograd Function's backward, one per parameter.  In
+        persistent mode the buffers become p.grad HERE (None is returned, so AccumulateGrad never
+        sees them: it would clone a buffer it cannot steal, and a second node of the same backward
+        would write the buffer the first node's sum already sits in)."""
+        out = []
+        for p in params:
+            g = self.get(p)
+            if g is None or not p.requires_grad:
+                out.append(None)
+            elif self.persistent and (p.grad is None or p.grad is g):
+                with torch.no_grad():
+                    p.grad = g
+                out.append(None)
+            else:
+                out.append(g)
+        return out
 
     def zeros(self, p):
         buf, acc = self.acc(p)
@@ -130,14 +151,26 @@ def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None):
     ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
 
 
+def _own_grad(p):
+    """p.grad can be accumulated into by the gradient kernels (fp32, contiguous, p's shape)."""
+    g = p.grad
+    return g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.shape == p.shape
+
+
 def persistent_grad_arena(module, params, device):
     """Gradient buffers that live across steps (`module.dsvt_persistent_grads`, set by DINOTrainer
     when it runs without DDP): every step's gradients land at the same addresses, so the
     multi-tensor kernels' pointer tables (gradient clipping, AdamW; utils._tensor_list) are cache
     hits.  A fresh pointer table per step meant a pinned host allocation + copy after the
-    backward, and the GPU sat idle ~2.5 ms of every step there (tools/gap_summary.py).  Valid
-    because the trainer drops every .grad (zero_grad(set_to_none=True)) before the next backward
-    writes the buffers again."""
+    backward, and the GPU sat idle ~2.5 ms of every step there (tools/gap_summary.py).
+
+    The backward sets p.grad to these buffers itself (_Grads.deliver) and accumulates into p.grad
+    when one is already there (_Grads.acc).  One loss.backward() can run several autograd nodes of
+    one module -- the 2-D ViT's MultiCropWrapper calls the backbone once per resolution group,
+    TimeSformer with concurrent_grad_groups too: the first node writes the buffers and makes them
+    p.grad, the later ones add into p.grad.  A buffer is written fresh only while its p.grad is
+    None, so the contract is the trainer's: every .grad dropped (zero_grad(set_to_none=True))
+    before the next backward, and no other reference to an old .grad kept across it."""
     ar = getattr(module, "_dsvt_grad_arena", None)
     if ar is None:
         ar = {}
@@ -148,18 +181,28 @@ def persistent_grad_arena(module, params, device):
     return ar
 
 
-_KEEP = {}
+_KEEP = collections.OrderedDict()     # (sizes, rates, device) -> keep-probability table, LRU
+_KEEP_MAX = 32
 
 
 def _keep_scales(sizes, dps, device):
     """DropPath per-sample scales floor(keep + U[0,1)) / keep (models/vit_utils.py:152-167) of
     every drop_path call of one forward: `sizes[i]` samples at drop rate `dps[i]`, returned as one
-    flat fp32 tensor (call i's scales at offset sum(sizes[:i])) from a single torch.rand draw."""
+    flat fp32 tensor (call i's scales at offset sum(sizes[:i])) from a single torch.rand draw.
+
+    The masks follow the reference's distribution and its call order and sizes (the gradient
+    goldens replay the reference's own masks through this function), but NOT its random stream:
+    the reference draws one torch.rand per drop_path call, so under the same seed the two draw
+    different masks.  Per-seed RNG parity was traded for one launch per forward."""
     key = (tuple(sizes), tuple(dps), str(device))
     keep = _KEEP.get(key)
     if keep is None:
         keep = torch.tensor(np.repeat(np.asarray([1.0 - p for p in dps], np.float32), sizes), device=device)
         _KEEP[key] = keep
+        if len(_KEEP) > _KEEP_MAX:
+            _KEEP.popitem(last=False)
+    else:
+        _KEEP.move_to_end(key)
     return torch.floor(keep + torch.rand(keep.numel(), device=device, dtype=torch.float32)) / keep
 
 
@@ -210,11 +253,7 @@ class BackboneFn(torch.autograd.Function):
             red.finish()
             red.take_seeded()          # the reduced arena views replace the local no_sync sums
         G.join()
-        out = [None, None]
-        for p in ctx.params:
-            g = G.get(p)
-            out.append(g if (g is not None and p.requires_grad) else None)
-        return tuple(out)
+        return tuple([None, None] + G.deliver(ctx.params))
 
 
 def _block_weights(model):
@@ -795,11 +834,7 @@ class HeadFn(torch.autograd.Function):
     def backward(ctx, dlogits):
         G, dx = _head_backward(ctx.head, ctx.state, dlogits.float().contiguous())
         ctx.state = None
-        out = [None, dx]
-        for p in ctx.params:
-            g = G.get(p)
-            out.append(g if (g is not None and p.requires_grad) else None)
-        return tuple(out)
+        return tuple([None, dx] + G.deliver(ctx.params))
 
 
 def _head_linears(head):

@@ -28,7 +28,10 @@
 extern "C" {
 #endif
 
-#define DSVT_ABI_VERSION 1
+/* 2 (r05): dsvt_bn_bwd takes param_sums (SyncBatchNorm's local dgamma / dbeta); DSVT_EPI_GELU_SAVE's
+ * aux holds GELU'(pre) (r04; was pre); the r03 grouped / stream-K / add-LN / row-LN GEMM entry points
+ * are gone and the variant knobs moved to dsvt_debug.h (r04) */
+#define DSVT_ABI_VERSION 2
 
 #define DSVT_BF16 0
 #define DSVT_F32 1
@@ -171,8 +174,10 @@ int dsvt_ln_fold_qkv_heads(const float *W, const float *gamma, const float *beta
  * dsvt_bn_gelu_fwd: y = GELU_erf((x - mean) * rstd * gamma + beta) in dtype, optionally GELU'(.)
  * (dtype) and xhat (fp32) for the backward.  Backward from dz = dL/d(BatchNorm output):
  * dsvt_bn_bwd_sums (sum dz, sum dz * xhat; all-reduced for SyncBatchNorm), then dsvt_bn_bwd:
- * dx = gamma * rstd * (dz - sum dz / count - xhat * sum(dz xhat) / count) (fp32), dgamma = sum
- * dz xhat, dbeta = sum dz (nullable, accumulate into them when accumulate != 0).
+ * dx = gamma * rstd * (dz - sum dz / count - xhat * sum(dz xhat) / count) (fp32) from `sums`,
+ * dgamma = sum dz xhat, dbeta = sum dz (nullable, accumulate into them when accumulate != 0) from
+ * `param_sums` -- for SyncBatchNorm the LOCAL (un-reduced) sums, as torch's SyncBatchNorm returns
+ * local weight / bias gradients that DDP then averages; NULL = `sums`.
  * ------------------------------------------------------------------------------------------ */
 int dsvt_bn_stats_fwd(const float *x, int64_t R, int64_t D, double *sums, void *stream);
 int dsvt_bn_finalize(const double *sums, double count, int64_t D, float eps, float momentum, int training,
@@ -180,7 +185,8 @@ int dsvt_bn_finalize(const double *sums, double count, int64_t D, float eps, flo
 int dsvt_bn_gelu_fwd(int dtype, const float *x, const float *mean, const float *rstd, const float *gamma,
                      const float *beta, void *y, void *gelu_grad, float *xhat, int64_t R, int64_t D, void *stream);
 int dsvt_bn_bwd_sums(int dtype, const void *dz, const float *xhat, int64_t R, int64_t D, double *sums, void *stream);
-int dsvt_bn_bwd(int dtype, const void *dz, const float *xhat, const double *sums, double count, const float *gamma,
+int dsvt_bn_bwd(int dtype, const void *dz, const float *xhat, const double *sums, const double *param_sums,
+                double count, const float *gamma,
                 const float *rstd, float *dx, float *dgamma, float *dbeta, int accumulate, int64_t R, int64_t D,
                 void *stream);
 

@@ -49,7 +49,7 @@ else:
 TOL = 1e-3
 
 
-def build(seed_bb, seed_hd):
+def build(seed_bb, seed_hd, use_bn=False):
     from dsvt.models.timesformer import VisionTransformer
     from dsvt.utils import MultiCropWrapper
     from dsvt.vision_transformer import DINOHead
@@ -59,8 +59,9 @@ def build(seed_bb, seed_hd):
                            norm_layer=partial(nn.LayerNorm, eps=1e-6), drop_path_rate=0.0,
                            num_frames=CFG["num_frames"], attention_type="divided_space_time")
     bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(seed_bb, **CFG).items()})
-    hd = DINOHead(E, OUT_DIM, **HEAD)
-    hd.load_state_dict({k: torch.from_numpy(v) for k, v in P.dino_head_state(seed_hd, E, OUT_DIM, **HEAD).items()})
+    hd = DINOHead(E, OUT_DIM, use_bn=use_bn, **HEAD)
+    sd = P.dino_head_bn_state(seed_hd, E, OUT_DIM, **HEAD) if use_bn else P.dino_head_state(seed_hd, E, OUT_DIM, **HEAD)
+    hd.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     bb.dsvt_dtype = hd.dsvt_dtype = torch.float32
     return MultiCropWrapper(bb, hd).cuda()
 
@@ -116,9 +117,18 @@ def main():
     # *_accum: gradient accumulation -- one micro-step under DDP.no_sync() (local sums only),
     # then a synchronised one; DDP averages the ACCUMULATED gradient (the overlapped
     # buckets must reduce the no_sync sums too, dist.BlockGradReducer.arena seeding)
-    modes = ("ddp", "overlap", "overlap_1stream", "ddp_accum", "overlap_accum")
+    # ddp_syncbn: DINOHead(use_bn=True) converted to SyncBatchNorm as train_ssl.py:319-321 does
+    # (--use_bn_in_head): batch statistics over both ranks, and LOCAL weight / bias gradients that
+    # DDP averages (torch's SyncBatchNorm semantics; ADVICE r04: dgamma / dbeta came out world_size
+    # times too large when taken from the all-reduced sums)
+    modes = ("ddp", "overlap", "overlap_1stream", "ddp_accum", "overlap_accum") + \
+        (("ddp_syncbn",) if SIZE == "tiny" else ())
+    bn_bufs = None
     for mode in modes:
-        student = build(4101, 4102).train()
+        student = build(4101, 4102, use_bn=mode == "ddp_syncbn").train()
+        if mode == "ddp_syncbn":
+            student = nn.SyncBatchNorm.convert_sync_batchnorm(student)
+            assert any(isinstance(m, nn.SyncBatchNorm) for m in student.head.modules())
         teacher = build(4201, 4202).eval()
         for p in teacher.parameters():
             p.requires_grad_(False)
@@ -158,15 +168,37 @@ def main():
         loss_sum = torch.tensor([float(loss.item())], dtype=torch.float64)
         dist.all_reduce(loss_sum)
         results[mode] = (grads, loss_sum, loss_fn.center.detach().cpu().numpy())
+        if mode == "ddp_syncbn":
+            bn_bufs = {n: b.detach().cpu().numpy().copy() for n, b in student.head.named_buffers()
+                       if b.dtype != torch.int64}
         info["n_params"] = len(names)
         del ddp, student
     log("phase 1 collectives done")
     if rank == 0:
         from dsvt import ops
+        allc = [torch.from_numpy(c).to(dev) for c in full]
+        if "ddp_syncbn" in results:        # single process, whole batch, plain BatchNorm1d head
+            ref = build(4101, 4102, use_bn=True).train()
+            lf = make_loss(center0)
+            lf.defer_center_update = True
+            so = ref(allc)
+            with torch.no_grad():
+                to = teacher(allc[:2])
+            loss_r = lf(so, to, 0)
+            colsum, rows = lf.last_colsum
+            ops.center_ema(lf.center, colsum, lf.center_momentum, 1.0 / rows)
+            loss_r.backward()
+            torch.cuda.synchronize()
+            g_bn = {n: p.grad.cpu().numpy().copy() for n, p in ref.named_parameters() if p.requires_grad}
+            l_bn, c_bn = loss_r, lf.center.cpu().numpy().copy()
+            for n, b in ref.head.named_buffers():
+                if n in bn_bufs:
+                    info["bn_buf_err_" + n] = e = rel(bn_bufs[n], b.cpu().numpy())
+                    assert e < 1e-4, "SyncBatchNorm running statistic %s: %.3g" % (n, e)
+            del ref, lf
         ref = build(4101, 4102).train()
         lf = make_loss(center0)
         lf.defer_center_update = True      # a single process: its center update has no all-reduce
-        allc = [torch.from_numpy(c).to(dev) for c in full]
 
         def ref_step():
             so = ref(allc)
@@ -187,13 +219,21 @@ def main():
         c_acc = lf.center.cpu().numpy().copy()
         for mode, (grads, loss_sum, center_dp) in results.items():
             accum = mode.endswith("_accum")
-            ref_g = g_acc if accum else g_one
+            ref_g = g_bn if mode == "ddp_syncbn" else g_acc if accum else g_one
             errs = {n: rel(grads[n], ref_g[n]) for n in ref_g}
+            if mode == "ddp_syncbn":
+                # a train-mode BatchNorm removes any shift common to the batch, so the gradients of
+                # the biases in front of it (the final-norm bias, the hidden Linears' biases) are
+                # zero analytically -- rounding noise in both runs: checked against the gradient scale
+                scale = max(float(np.abs(g).max()) for g in ref_g.values())
+                for n in ref_g:
+                    if float(np.abs(ref_g[n]).max()) < 1e-5 * scale:
+                        errs[n] = float(np.abs(grads[n] - ref_g[n]).max()) / scale
             worst = max(errs, key=errs.get)
             info["worst_grad_" + mode] = [worst, errs[worst]]
             info["top_" + mode] = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
             base = "ddp_accum" if accum else "ddp"
-            if mode != base:
+            if mode != base and mode != "ddp_syncbn":
                 info["vs_ddp_" + mode] = max(rel(grads[n], results[base][0][n]) for n in grads)
         for mode, (grads, loss_sum, center_dp) in results.items():
             accum = mode.endswith("_accum")
@@ -201,10 +241,10 @@ def main():
             assert info["worst_grad_" + mode][1] < TOL, "%s grad %s rel err %.3g vs single-process full batch: %s" % (
                 mode, worst, info["worst_grad_" + mode][1], info)
             l_mean = float(loss_sum.item()) / world
-            lr_ = l_acc if accum else l_ref
+            lr_ = l_bn if mode == "ddp_syncbn" else l_acc if accum else l_ref
             info["loss_" + mode] = [l_mean, float(lr_.item())]
             assert abs(l_mean - float(lr_.item())) < TOL * abs(float(lr_.item())), info["loss_" + mode]
-            ec = rel(center_dp, c_acc if accum else c_one)
+            ec = rel(center_dp, c_bn if mode == "ddp_syncbn" else c_acc if accum else c_one)
             info["center_err_" + mode] = ec
             assert ec < 1e-5, "center after the all-reduced update differs (%s): %.3g" % (mode, ec)
         del ref, lf

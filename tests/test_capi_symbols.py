@@ -55,7 +55,8 @@ def test_binding_arity_matches_header():
 
 
 def test_version_and_workspace(L):
-    assert L.dsvt_version() == 1
+    from dsvt import _lib
+    assert L.dsvt_version() == _lib.ABI_VERSION == 2
     from dsvt import _lib
     assert L.dsvt_workspace_bytes(_lib.WS_LN_GEMM, _lib.BF16, 1000, 0, 768) >= 1000 * 768 * 2
     assert L.dsvt_workspace_bytes(_lib.WS_LN_GEMM, _lib.F32, 1000, 0, 768) >= 1000 * 768 * 4

@@ -113,15 +113,21 @@ def test_student_grads_plain_attention(gold_plain, attn, dtype, tag, monkeypatch
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("tag", ["eval", "drop"])
-def test_student_grads_vit2d_bn_head(dtype, tag, monkeypatch):
+@pytest.mark.parametrize("tag,trainer", [("eval", False), ("drop", False), ("eval", True)])
+def test_student_grads_vit2d_bn_head(dtype, tag, trainer, monkeypatch):
     """The reference's default architecture family trains (--arch vit_small, train_ssl.py:248-254):
     the 2-D ViT (vision_transformer.py:134-214) through the space-only training path with one
     frame, 64^2 global and 32^2 local crops (the local calls go through interpolate_pos_encoding:
     the bicubic table and its backward, dsvt_pos_bicubic_bwd), with DINOHead(use_bn=True) (BatchNorm1d
     in train mode), MultiCropWrapper + DINOLoss -- loss, logits, every parameter gradient and the
     head's BatchNorm running statistics vs the reference's autograd (tests/golden/
-    train_grads_vit2d.npz), eval and DropPath 0.5 replaying the reference's per-image masks."""
+    train_grads_vit2d.npz), eval and DropPath 0.5 replaying the reference's per-image masks.
+
+    trainer: the backward as DINOTrainer runs it (DINOTrainer.backward, the persistent gradient
+    buffers on), twice.  The 2-D ViT goes through one autograd node PER resolution group, so one
+    backward runs two backbone nodes: the first writes the persistent buffers and makes them
+    p.grad, the second must add into them (training.persistent_grad_arena; ADVICE r04: it had
+    overwritten the first node's gradients).  Every gradient must then sit in its buffer."""
     from dsvt import training
     from dsvt.loss import DINOLoss
     from dsvt.utils import MultiCropWrapper
@@ -154,12 +160,47 @@ def test_student_grads_vit2d_bn_head(dtype, tag, monkeypatch):
         bb.eval()
     crops = [torch.from_numpy(P.clip(1250 + i, (2, 3, 64, 64))).cuda() for i in range(2)] + \
             [torch.from_numpy(P.clip(1260 + i, (2, 3, 32, 32))).cuda() for i in range(2)]
-    s_out = net(crops)
     t_out = torch.from_numpy(gold[tag + "_teacher"]).cuda()
     loss_fn = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
-    loss = loss_fn(s_out, t_out, 0)
-    loss.backward()
-    torch.cuda.synchronize()
+    if trainer:
+        from dsvt.trainer import DINOTrainer
+        tb = VisionTransformer(img_size=[64], patch_size=16, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
+                               qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6))
+        teacher = MultiCropWrapper(tb, DINOHead(64, 512, use_bn=True, hidden_dim=128, bottleneck_dim=64)).cuda()
+        tr = DINOTrainer(net, teacher, loss_fn, niter_per_ep=10, epochs=2, warmup_epochs=1)
+        assert bb.dsvt_persistent_grads and hd.dsvt_persistent_grads
+        first = {}
+        c0 = loss_fn.center.clone()
+        for it in range(2):
+            loss_fn.center.copy_(c0)             # the center moves after every loss: restart it
+            s_out = net(crops)
+            loss = loss_fn(s_out, t_out, 0)
+            tr.backward(loss)
+            torch.cuda.synchronize()
+            g_now = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
+            if it == 0:
+                first = g_now
+                bufs = {k: b.clone() for k, b in net.head.named_buffers()}
+            else:        # the second step's gradients equal the first's (same inputs, no update)
+                assert first.keys() == g_now.keys()
+                for k in first:
+                    assert rel(g_now[k].cpu().numpy(), first[k].cpu().numpy()) < 1e-6, k
+        for mod in (bb, hd):
+            arena = mod._dsvt_grad_arena
+            for p in mod.parameters():
+                if p.grad is not None:
+                    assert p.grad.data_ptr() == arena[id(p)].data_ptr()
+        # compare the first step against the goldens (the head's running statistics moved twice)
+        for k, p in net.named_parameters():
+            if k in first:
+                p.grad = first[k]
+        for k, b in net.head.named_buffers():
+            b.copy_(bufs[k])
+    else:
+        s_out = net(crops)
+        loss = loss_fn(s_out, t_out, 0)
+        loss.backward()
+        torch.cuda.synchronize()
     # bf16: the head's batch-statistics BatchNorm over 8 rows subtracts the batch mean of nearly
     # equal per-row gradients, so the bf16 roundings of the activations and GELU' survive the
     # cancellation amplified (measured up to 7.9e-2 on a first-block fc1 weight, against <= 2.1e-2
