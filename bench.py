@@ -142,20 +142,23 @@ def cpu_baseline(batches=(1, 4), reps=5):
                       % ("/".join(map(str, batches)), torch.__version__, cores, reps)}
 
 
-def pmc_traffic(kernel_prefix, path=os.path.join(ROOT, "profiles", "pmc_traffic.json")):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+def pmc_traffic(kernel_name, path=os.path.join(ROOT, "profiles", "pmc_traffic.json")):
+    """(HBM bytes per launch, source) of the dominant kernel from the committed PMC summary
     (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this same
-    bench command, gfx950 FETCH x2 correction applied); None when no summary matches."""
+    bench command, gfx950 FETCH x2 correction applied).  Matched on the FULL instantiation name
+    (dsvt.ops.gemm_kernel_name): (None, reason) when the summary has no entry for exactly that
+    kernel -- never another instantiation's counters."""
     try:
         with open(path) as f:
-            kernels = json.load(f)["kernels"]
+            doc = json.load(f)
+        kernels = doc["kernels"]
     except (OSError, ValueError, KeyError):
-        return None
-    hits = [v for k, v in kernels.items() if k.startswith(kernel_prefix)]
-    if not hits:
-        return None
-    calls = sum(h["calls"] for h in hits)
-    return round(sum(h["traffic_bytes"] * h["calls"] for h in hits) / calls)
+        return None, "no PMC summary at %s" % os.path.relpath(path, ROOT)
+    v = kernels.get(kernel_name)
+    if v is None:
+        return None, "%s has no entry for %s" % (os.path.relpath(path, ROOT), kernel_name)
+    return round(v["traffic_bytes"]), "%s (%s, %d dispatches)" % (os.path.relpath(path, ROOT),
+                                                                 doc.get("run", "rocprofv3 --pmc"), v["calls"])
 
 
 # ----------------------------------------------------------------- models / data
@@ -634,8 +637,12 @@ def main():
                 achieved, unit, pk = tb / (tms * 1e-3) / 1e9, "GB/s", HBM_PEAK_GBS
             all_ms = float(np.sum(ms))
             kname = ops.gemm_kernel_name(dom)
+            traffic, traffic_src = pmc_traffic(kname)
             roofline = {"bound": bound, "achieved": round(achieved, 1), "peak": pk, "unit": unit,
-                        "frac": round(achieved / pk, 4), "traffic": pmc_traffic(kname),
+                        "frac": round(achieved / pk, 4), "traffic": traffic, "traffic_source": traffic_src,
+                        "traffic_over_algorithmic": (round(traffic / (sum(c["mbytes"] * 1e6 * c["launches"]
+                                                                          for c in cls_out) / n), 3)
+                                                     if traffic else None),
                         "frac_attainable": round(t_att / (tms * 1e-3), 4),
                         "kernel": kname, "launches": n,
                         "avg_launch_us": round(tms / n * 1e3, 2),

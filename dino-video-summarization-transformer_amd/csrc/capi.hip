@@ -89,9 +89,17 @@ double gemm_bytes(int dtype, int epi, int out_f32, int64_t M, int64_t N, int64_t
   return b;
 }
 
+// probe tag of a GEMM launch: variant * 32 + dtype * 16 + epi * 2 + fp32-out, + 1024 * fuse (1 =
+// LayerNorm folded in, 2 = residual + LN-statistics epilogue), + 4096 when the 256x256 kernel runs its
+// N-full bf16 store path (template NFULL) -- together they name ONE template instantiation
+// (dsvt.ops.gemm_kernel_name), so the bench's PMC lookup finds that kernel's counters and no other's
 int gemm_tag(const GemmParams& p, int dtype, int epi, int out_f32) {
   const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
-  return gemm_variant_for(p, dtype, epi, out_f32) * 32 + dtype * 16 + epi * 2 + f32;
+  const int v = gemm_variant_for(p, dtype, epi, out_f32);
+  const int fuse = p.ln_stats ? 1 : (p.stats_out ? 2 : 0);
+  const int nfull = v == 20 && (fuse == 1 || (fuse == 0 && (epi == EPI_BIAS || epi == EPI_GELU) && !f32 &&
+                                               p.N % 256 == 0));
+  return v * 32 + dtype * 16 + epi * 2 + f32 + 1024 * fuse + 4096 * nfull;
 }
 
 void norm_map(int64_t& rpg, int64_t& gstride, int64_t& goff) {

@@ -18,7 +18,7 @@
 // CONSECUTIVE output columns of one row: the epilogue does 16-B (fp32) / 8-B (bf16)
 // vector loads/stores.  Workgroup ids are remapped so the N-tiles of one M-tile run on the
 // same XCD (its A panel then stays in that XCD's L2).
-#include "common.h"
+#include "gemm_epi.h"
 
 namespace dsvt {
 
@@ -229,7 +229,10 @@ __device__ __forceinline__ void gk_vmwait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
 }
 
-template <typename T, int EPI, bool OUT_F32, bool PREF = false, int MI = 4>
+// STATS (EPI_RESID, bf16, N % 128 == 0; dsvt_gemm_resid_stats_fwd): the residual epilogue that
+// also writes the updated rows' bf16 copy and LayerNorm partials (gemm_epi.h resid_stats_rows:
+// one partial per 64-column wave slab)
+template <typename T, int EPI, bool OUT_F32, bool PREF = false, int MI = 4, bool STATS = false>
 __global__ __launch_bounds__(256, MI == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   constexpr int BMv = 32 * MI;                       // tile rows
   constexpr int A_BYTES = BMv * BKB, SBYTES = A_BYTES + TILE_BYTES;
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(256, MI == 4 ? 2 : 1) void gemm_kernel(GemmParams p
   // loads are issued right after the last stage's loads, and that step waits with vmcnt(16) --
   // for the stage, not for them -- so their latency runs under the last two steps' MFMAs.
   const bool full = m0 + BMv <= p.M && n0 + BN <= p.N;
-  const bool peel = PREF && full && nk >= 2;
+  const bool peel = PREF && !STATS && full && nk >= 2;
   const int nmain = peel ? nk - 2 : nk;
   for (int kt = 0; kt < nmain; ++kt) {
     char* cur = smem + (kt & 1) * SBYTES;
@@ -358,6 +361,20 @@ __global__ __launch_bounds__(256, MI == 4 ? 2 : 1) void gemm_kernel(GemmParams p
   // Full tiles (uniform per workgroup) take a branch-free path: no per-lane bounds branches,
   // so the compiler's vmcnt waits stay exact instead of draining after every store.
   mfma_result_fence();   // acc is read under the branches below
+  if constexpr (STATS) {
+    static_assert(EPI == EPI_RESID && MI == 4, "the stats epilogue: residual, 64-row wave tiles");
+    const int g = lane >> 4;
+    float4 b4[4];
+    bias_frag4(p.bias, n0 + wn * 64, g, b4);          // N % 128 == 0: every column valid
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j][0] += b4[j].x; acc[i][j][1] += b4[j].y; acc[i][j][2] += b4[j].z; acc[i][j][3] += b4[j].w;
+      }
+    epilogue_resid_stats<MI, 4>(p, acc, m0 + wm * 16 * MI, n0 + wn * 64, lane & 15, g);
+    return;
+  }
   if (full) epilogue_128<T, EPI, OUT_F32, false, false, MI>(p, acc, m0, n0, wm, wn, lane);
   else epilogue_128<T, EPI, OUT_F32, true, false, MI>(p, acc, m0, n0, wm, wn, lane);
 }
@@ -384,7 +401,10 @@ static hipError_t launch_t(const GemmParams& p, int epi, int out_f32, hipStream_
       else gemm_kernel<T, EPI_GELU, false><<<grid, block, 0, s>>>(p);
       break;
     case EPI_RESID:   // bf16: the instantiation with the residual-tile prefetch (PREF)
-      if (sizeof(T) == 2) gemm_kernel<T, EPI_RESID, true, true><<<grid, block, 0, s>>>(p);
+      if (sizeof(T) == 2 && p.stats_out) {
+        if (p.N % 128 || p.row_scale || !p.xb_out) return hipErrorInvalidValue;
+        gemm_kernel<bf16_t, EPI_RESID, true, false, 4, true><<<grid, block, 0, s>>>(p);
+      } else if (sizeof(T) == 2) gemm_kernel<T, EPI_RESID, true, true><<<grid, block, 0, s>>>(p);
       else gemm_kernel<T, EPI_RESID, true><<<grid, block, 0, s>>>(p);
       break;
     case EPI_PATCH: gemm_kernel<T, EPI_PATCH, true><<<grid, block, 0, s>>>(p); break;
@@ -422,8 +442,13 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 #endif
   if (DSVT_RESID192 && gv == 0 && !p.ln_stats && p.M >= 4096 && gemm_192_ok(p, epi))
     return 30;
-  // the LayerNorm-folded A operand (dsvt_gemm_lnx_fwd) and the residual epilogue that writes
-  // the next LayerNorm's row statistics (dsvt_gemm_resid_stats_fwd): the 256x256 kernel only
+  // the LayerNorm-folded A operand (dsvt_gemm_lnx_fwd): the 256x256 kernel only; the residual
+  // epilogue that writes the next LayerNorm's row statistics (dsvt_gemm_resid_stats_fwd): the
+  // 256x256 kernel or (DSVT_RESID_STATS_V = 1, A/B builds; forced variant 1) the 128x128 one
+#ifndef DSVT_RESID_STATS_V
+#define DSVT_RESID_STATS_V 20
+#endif
+  if (p.stats_out && (gv == 1 || (gv == 0 && DSVT_RESID_STATS_V == 1)) && p.N % 128 == 0) return 1;
   if (p.ln_stats || p.stats_out) return 20;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
@@ -488,7 +513,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
-  if ((p.ln_stats && v != 20) || (p.stats_out && v != 20 && v != 30)) return hipErrorInvalidValue;
+  if ((p.ln_stats && v != 20) || (p.stats_out && v != 20 && v != 30 && v != 1)) return hipErrorInvalidValue;
   if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);
   if (v == 3) return launch_resid160(p, epi, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);

@@ -583,28 +583,39 @@ def probe_read(capacity=65536, with_bytes=False):
 
 
 def gemm_kernel_name(tag):
-    """probe tag (variant*32 + dtype*16 + epi*2 + f32, csrc/capi.hip gemm_tag) -> the
-    rocprofv3 kernel-name prefix of that template instantiation."""
-    variant, rest = divmod(int(tag), 32)
+    """probe tag (csrc/capi.hip gemm_tag: variant*32 + dtype*16 + epi*2 + f32, + 1024*fuse + 4096*nfull)
+    -> the rocprofv3 name of that ONE template instantiation (no argument list for the few
+    families whose mode is not in the tag: a prefix then)."""
+    tag = int(tag)
+    nfull, fuse, rest = (tag >> 12) & 1, (tag >> 10) & 3, tag & 1023
+    variant, rest = divmod(rest, 32)
     epi, f32 = (rest % 16) // 2, "true" if rest % 2 else "false"
+    P = "(dsvt::GemmParams)"
     if variant == 0:
-        return "void dsvt::gemm_kernel<float, %d, %s>" % (epi, f32)
+        return "void dsvt::gemm_kernel<float, %d, %s, false, 4, false>%s" % (epi, f32, P)
     if variant == 1:
-        # the fp32-residual launches use the instantiation with the residual-tile prefetch
-        # (csrc/gemm.hip PREF)
-        pref = epi == _lib.EPI_BIAS_RESID
-        return "void dsvt::gemm_kernel<unsigned short, %d, %s%s>" % (epi, f32, ", true" if pref else "")
-    persist = {10: "256, 128, 2, 2, 3, %d, %s, true"}
-    if variant in persist:
-        return "void dsvt::gemm_persist_kernel<" + persist[variant] % (epi, f32) + ">"
+        # the fp32-residual launches: the residual-tile prefetch (csrc/gemm.hip PREF), or the
+        # LayerNorm-statistics epilogue (STATS)
+        if fuse == 2:
+            return "void dsvt::gemm_kernel<unsigned short, 2, true, false, 4, true>" + P
+        pref = "true" if epi == _lib.EPI_BIAS_RESID else "false"
+        return "void dsvt::gemm_kernel<unsigned short, %d, %s, %s, 4, false>%s" % (epi, f32, pref, P)
+    if variant == 3:
+        return "void dsvt::gemm_kernel<unsigned short, 2, true, true, 5, false>" + P
+    if variant == 10:
+        return "void dsvt::gemm_persist_kernel<256, 128, 2, 2, 3, %d, %s, true>%s" % (epi, f32, P)
     if variant == 20:
-        return "void dsvt::gemm_8ph_kernel<%d, %s, 0, " % (epi, f32)
+        if fuse == 1:
+            return "void dsvt::gemm_8ph_kernel<%d, false, 0, true, 1>%s" % (epi, P)
+        if fuse == 2:
+            return "void dsvt::gemm_8ph_kernel<2, true, 0, false, 2>" + P
+        return "void dsvt::gemm_8ph_kernel<%d, %s, 0, %s, 0>%s" % (epi, f32, "true" if nfull else "false", P)
     if variant == 30:
         return "void dsvt::gemm_192_kernel<"
     if variant == 32:
-        return "void dsvt::gemm_192_kernel<2>"
+        return "void dsvt::gemm_192_kernel<2>" + P
     if variant == 50:
-        return "void dsvt::gemm_skinny_kernel<%d, %s>" % (epi, f32)
+        return "void dsvt::gemm_skinny_kernel<%d, %s>%s" % (epi, f32, P)
     if variant == 31:
         return "void dsvt::wgrad_kernel<0>"
     return "dsvt gemm variant %d (epilogue %d, fp32 out %s)" % (variant, epi, f32)

@@ -415,7 +415,7 @@ def test_qkv_temporal_attn(B, Np):
 
 
 @pytest.mark.parametrize("B,Np,T", [(2, 5, 3), (16, 196, 8), (48, 36, 8)])
-@pytest.mark.parametrize("variant", [0, 30])
+@pytest.mark.parametrize("variant", [0, 30, 1])
 def test_gemm_resid_stats(B, Np, T, variant):
     """dsvt_gemm_resid_stats_fwd: the residual update exactly as the plain residual GEMM on the
     same kernel (bitwise; the 256x256 one, or the 256x192 one forced), and for every updated row

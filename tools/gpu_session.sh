@@ -36,7 +36,10 @@ for stage in "$@"; do
              python tools/prof_summary.py "$OUT/c5prof" > "$OUT/c5prof_summary.txt" ;;
     pmc)     run pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
              run pmc2 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --serial --no-graph --no-train --no-other &&
-             python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" > "$OUT/pmc_summary.txt" ;;
+             python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" \
+               "$(date -u +%Y-%m-%d) bench.py --steps 3 --warmup 1 --serial --no-graph (libdsvt $(md5sum dino-video-summarization-transformer_amd/dsvt/libdsvt.so | cut -c1-12))" \
+               > "$OUT/pmc_summary.txt" &&
+             cp "$OUT/pmc_traffic.json" profiles/pmc_traffic.json ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

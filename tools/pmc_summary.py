@@ -5,7 +5,7 @@ Both counters are in KiB.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_
 exactly half the bytes of a wide coalesced streaming read, so
     traffic_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024      per dispatch.
 
-usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR [OUT_JSON]
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR [OUT_JSON [RUN_DESCRIPTION]]
 Prints a table (calls, avg fetch/write MB per dispatch, corrected traffic) and, with
 OUT_JSON, writes {kernel_name: {"traffic_bytes": .., "fetch_kib": .., "write_kib": .., "calls": ..}}
 which bench.py reads to fill roofline.traffic for its dominant kernel."""
@@ -50,6 +50,7 @@ def main():
         with open(sys.argv[3], "w") as f:
             json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                  "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 B per dispatch",
+                       "run": sys.argv[4] if len(sys.argv) > 4 else "",
                        "kernels": out}, f, indent=1)
 
 
