@@ -432,8 +432,35 @@ def other_configs(args, device):
         t = graph_timed(lambda: scorer.score(video), reps=10)
     gf = (vit_fwd_flops(3, 224) + vit_fwd_flops(30, 224)) / 1e9
     res["frame_score"] = {"value": round(64 / t, 2), "unit": "frames/s", "frames": 64, "views": "local 3 / global 30",
-                          "launch": "hip_graph (10 replays)", "eager_value": round(64 / te, 2),
+                          "launch": "hip_graph (10 replays)", "eager_value": round(64 / te, 2), "dtype": args.dtype,
                           "gflop_per_frame": round(gf, 1), "tflops": round(64 * gf / t / 1e3, 1)}
+    if dtype == torch.bfloat16:
+        # the product output is the selected frames (frame_selection_loader.py:115-170).  The fp32
+        # parity mode picks the reference's frames exactly (tests/test_gpu_model.py::
+        # test_frame_scores_vitb_local3_global30); the bf16 mode moves a few picks by one frame.
+        # Both modes are timed, and the bf16 picks are counted against the fp32 picks of the same
+        # video (rates 1 / 4, N = 4 .. 24 picks, as the test does)
+        from dsvt.selection import adaptive_frame_indices
+        with torch.no_grad():
+            s_bf = scorer.score(video).clone()
+            fm.dsvt_dtype = torch.float32
+            s_32 = scorer.score(video).clone()
+            t32 = timed(lambda: scorer.score(video), reps=2, warm=1)
+        fm.dsvt_dtype = dtype
+        picked = moved = worst = 0
+        for rate in (1, 4):
+            for n_pick in (4, 8, 12, 16, 24):
+                want, _ = adaptive_frame_indices(s_32, 64, 64 * rate, rate, n_pick)
+                got, _ = adaptive_frame_indices(s_bf, 64, 64 * rate, rate, n_pick)
+                want, got = np.asarray(want, np.int64), np.asarray(got, np.int64)
+                picked += n_pick
+                moved += int(np.sum(got != want))
+                worst = max(worst, float(np.max(np.abs(got - want))) / rate)
+        res["frame_score"].update({"picks_vs_fp32": picked, "picks_moved_vs_fp32": moved,
+                                   "pick_mismatch_rate": round(moved / picked, 4), "max_shift_frames": worst})
+        res["frame_score_fp32"] = {"value": round(64 / t32, 2), "unit": "frames/s", "frames": 64, "dtype": "fp32",
+                                   "launch": "eager (2 reps)", "tflops": round(64 * gf / t32 / 1e3, 1),
+                                   "picks": "the reference's frames (parity mode)"}
     return res
 
 

@@ -181,6 +181,70 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
+// Any C % 32 == 0 up to 2048 (the Video Swin widths: 96 / 192 / 384 / 768, 128 ... 1024, and the
+// PatchMerging norms over 4C up to 2048): one wave per row, lane owns columns k*64 + lane.
+template <typename DyT>
+__global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
+                                                          const float* __restrict__ gamma, float* __restrict__ dx,
+                                                          int64_t rows, int C, int64_t rpg, int64_t gstride,
+                                                          int64_t goff, float eps, float* __restrict__ partial) {
+  __shared__ float red[4][2][2048];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = (C + 63) >> 6;                                  // slots (<= 32)
+  float dg[32], db[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) { dg[k] = 0.f; db[k] = 0.f; }
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
+    const int64_t xr = map_row(r, rpg, gstride, goff) * C;
+    float v[32], d[32];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int c = k * 64 + lane;
+      const bool in = k < n && c < C;
+      v[k] = in ? x[xr + c] : 0.f;
+      d[k] = in ? Elem<DyT>::to_f(dy[r * C + c]) : 0.f;
+      s += v[k];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < n && k * 64 + lane < C) { v[k] -= mean; q += v[k] * v[k]; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int c = k * 64 + lane;
+      if (k < n && c < C) {
+        const float xh = v[k] * rstd, gd = gamma[c] * d[k];
+        v[k] = xh;
+        s1 += gd;
+        s2 += gd * xh;
+        dg[k] += d[k] * xh;
+        db[k] += d[k];
+      }
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int c = k * 64 + lane;
+      if (k < n && c < C) dx[xr + c] += rstd * (gamma[c] * d[k] - s1 - v[k] * s2);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const int c = k * 64 + lane;
+    if (k < n && c < C) { red[wave][0][c] = dg[k]; red[wave][1][c] = db[k]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    partial[(int64_t)blockIdx.x * 2 * C + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    partial[(int64_t)blockIdx.x * 2 * C + C + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+  }
+}
+
 // C = 768 (ViT-B), the training step's LayerNorm backward (the default, DSVT_LNB_VARIANT=2): the
 // same arithmetic as ln_bwd_kernel<DyT, true, 3, true>, with TWO rows in flight ahead of the one
 // being reduced instead of one (x, dy, dx of three rows live, dy kept as packed bf16 until used;
@@ -331,8 +395,22 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
                                                              gstride, goff, eps, partial);
   } else if (C == 768) {               // ViT-B: 3 float4 chunks per lane, a tighter register file
     if (dy_dtype == 0) DSVT_LNB3(bf16_t); else DSVT_LNB3(float);
-  } else if (C % 256 == 0 && C <= 1024) {
-    if (dy_dtype == 0) DSVT_LNB(bf16_t, true); else DSVT_LNB(float, true);
+  } else if (C % 256 == 0 && C <= 1024) {   // VEC: NI = C / 256 float4 chunks per lane
+#define DSVT_LNBN(T, NI_) ln_bwd_kernel<T, true, NI_><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, \
+                                                                        gstride, goff, eps, partial)
+    switch (C / 256) {
+      case 1: if (dy_dtype == 0) DSVT_LNBN(bf16_t, 1); else DSVT_LNBN(float, 1); break;
+      case 2: if (dy_dtype == 0) DSVT_LNBN(bf16_t, 2); else DSVT_LNBN(float, 2); break;
+      default: if (dy_dtype == 0) DSVT_LNBN(bf16_t, 4); else DSVT_LNBN(float, 4); break;   // C = 1024
+    }
+#undef DSVT_LNBN
+  } else if (C % 64 != 0 || C > 1024) {
+    if (dy_dtype == 0)
+      ln_bwd_wide_kernel<bf16_t><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, (int)C, rpg, gstride, goff,
+                                                    eps, partial);
+    else
+      ln_bwd_wide_kernel<float><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, (int)C, rpg, gstride, goff,
+                                                   eps, partial);
   } else {
     if (dy_dtype == 0) DSVT_LNB(bf16_t, false); else DSVT_LNB(float, false);
   }

@@ -142,6 +142,7 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
     }
     case DSVT_WS_PAIR_LOSS: return up(4 * M * 4);
     case DSVT_WS_LN_BWD: return up((int64_t)ln_bwd_blocks(M) * 2 * K * 4);          // M = rows, K = C
+    case DSVT_WS_ATTN_WIN_BWD: return up(attn_window_bwd_groups(M, N) * N * K * K * 4);   // M = nwin, N = heads, K = N tokens
     case DSVT_WS_COLSUM: return up(colsum_parts(M) * N * 4);                        // M = rows, N = C
     case DSVT_WS_ATTN_BWD: return up(M * 3 * N * 4 + M * (N / 64) * K * 2 * 4);     // M = nb*tin, N = C, K = seqlen
     case DSVT_WS_EMBED_BWD: return up((M + N + 2 + M * N) * K * 4);                 // M = Np, N = T, K = C
@@ -701,7 +702,7 @@ int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float
                        int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
   REQUIRE(dy_dtype == DSVT_BF16 || dy_dtype == DSVT_F32, "layernorm_bwd: bad dy dtype");
   REQUIRE(x && dy && gamma && dx && dgamma && dbeta, "layernorm_bwd: null pointer");
-  REQUIRE(rows > 0 && C % 64 == 0 && C > 0 && C <= 1024, "layernorm_bwd: need 0 < C <= 1024, C %% 64 == 0");
+  REQUIRE(rows > 0 && C % 32 == 0 && C > 0 && C <= 2048, "layernorm_bwd: need 0 < C <= 2048, C %% 32 == 0");
   REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, 1, rows, 0, C),
           "layernorm_bwd: workspace too small");
   norm_map(rpg, gstride, goff);
@@ -1018,11 +1019,46 @@ int dsvt_swin_merge_ln_fwd(int dtype, const float* x, const float* gamma, const 
   return e == hipSuccess ? 0 : hip_fail(e, "swin_merge_ln");
 }
 
-int dsvt_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C, void* stream) {
+int dsvt_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C,
+                            const float* row_scale, int64_t group, void* stream) {
   REQUIRE(X && y && idx && aligned16(X) && aligned16(y) && rows > 0 && C > 0 && C % 4 == 0,
           "window_scatter_add: bad args");
-  hipError_t e = launch_window_scatter_add(X, y, idx, rows, C, (hipStream_t)stream);
+  REQUIRE(!row_scale || group > 0, "window_scatter_add: row_scale needs group > 0");
+  hipError_t e = launch_window_scatter_add(X, y, idx, rows, C, row_scale, group, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "window_scatter_add");
+}
+
+int dsvt_swin_gather_rows(int dtype, const float* x, const int32_t* idx, const float* row_scale, int64_t group,
+                          void* out, int64_t rows, int64_t C, int64_t ldo, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "swin_gather_rows: bad dtype");
+  REQUIRE(x && out && rows > 0 && C > 0 && ldo >= C, "swin_gather_rows: bad args");
+  REQUIRE(!row_scale || group > 0, "swin_gather_rows: row_scale needs group > 0");
+  hipError_t e = launch_swin_gather_rows(dtype, x, idx, row_scale, group, out, rows, C, ldo, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "swin_gather_rows");
+}
+
+int dsvt_attn_window_bwd(int dtype, const void* qkv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                         const float* bias, const int32_t* region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads,
+                         int64_t head_dim, float scale, void* dqkv, int64_t ld_dqkv, float* dbias, void* workspace,
+                         int64_t workspace_bytes, void* stream) {
+  REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "attn_window_bwd: bad dtype");
+  REQUIRE(qkv && o && dout && bias && region && dqkv && dbias, "attn_window_bwd: null pointer");
+  REQUIRE(head_dim == 32, "attn_window_bwd: head_dim must be 32 (Video Swin)");
+  REQUIRE(nwin > 0 && nwc > 0 && N > 0 && N <= 128 && heads > 0, "attn_window_bwd: need 0 < N <= 128");
+  REQUIRE(ldo >= heads * 32 && lddo >= heads * 32 && ld_dqkv >= 3 * heads * 32, "attn_window_bwd: bad ldo / lddo / ld_dqkv");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_ATTN_WIN_BWD, dtype, nwin, heads, N),
+          "attn_window_bwd: workspace too small");
+  const int64_t C = heads * 32;
+  hipError_t e = launch_attn_window_bwd(dtype, qkv, o, ldo, dout, lddo, bias, region, nwin, nwc, N, heads, C, scale,
+                                        dqkv, ld_dqkv, dbias, (float*)workspace, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "attn_window_bwd");
+}
+
+int dsvt_relpos_bias_bwd(const float* dbias, const int64_t* index, int64_t nmax, int64_t N, int64_t heads,
+                         int64_t entries, float* dtable, int accumulate, void* stream) {
+  REQUIRE(dbias && index && dtable && N > 0 && N <= nmax && heads > 0 && entries > 0, "relpos_bias_bwd: bad args");
+  hipError_t e = launch_relpos_bias_bwd(dbias, index, nmax, N, heads, entries, dtable, accumulate, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "relpos_bias_bwd");
 }
 
 int dsvt_relpos_bias_fwd(const float* table, const int64_t* index, int64_t nmax, int64_t N, int64_t heads, float* out,

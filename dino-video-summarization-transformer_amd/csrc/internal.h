@@ -219,7 +219,17 @@ hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, co
 hipError_t launch_swin_merge_ln(int dtype, const float* x, const float* gamma, const float* beta, void* out, int64_t B,
                                 int64_t D, int64_t H, int64_t W, int64_t C, float eps, hipStream_t s);
 hipError_t launch_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C,
-                                     hipStream_t s);
+                                     const float* row_scale, int64_t group, hipStream_t s);
+// Video Swin training (swin_bwd.hip)
+int64_t attn_window_bwd_groups(int64_t nwin, int64_t heads);
+hipError_t launch_swin_gather_rows(int dtype, const float* x, const int32_t* idx, const float* row_scale,
+                                   int64_t group, void* out, int64_t rows, int64_t C, int64_t ldo, hipStream_t s);
+hipError_t launch_attn_window_bwd(int dtype, const void* qkv, const void* o, int64_t ldo, const void* dout,
+                                  int64_t lddo, const float* bias, const int32_t* region, int64_t nwin, int64_t nwc,
+                                  int64_t N, int64_t heads, int64_t C, float scale, void* dqkv, int64_t lddq,
+                                  float* dbias, float* workspace, hipStream_t s);
+hipError_t launch_relpos_bias_bwd(const float* dbias, const int64_t* index, int64_t nmax, int64_t N, int64_t heads,
+                                  int64_t entries, float* dtable, int accumulate, hipStream_t s);
 hipError_t launch_relpos_bias(const float* table, const int64_t* index, int64_t nmax, int64_t N, int64_t heads,
                               float* out, hipStream_t s);
 hipError_t launch_attn_window(int dtype, const void* qkv, void* out, int64_t ldo, const float* bias,

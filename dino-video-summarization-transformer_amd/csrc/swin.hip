@@ -247,17 +247,23 @@ hipError_t launch_swin_merge_ln(int dtype, const float* x, const float* gamma, c
 }
 
 // ---------------------------------------------------------------- window reverse + residual
-// X[idx[m]] += y[m] for idx[m] >= 0 (window rows -> token rows; every token row has exactly one
-// window row, so the adds never collide).  C % 4 == 0.
+// X[idx[m]] += s[m / group] * y[m] for idx[m] >= 0 (window rows -> token rows; every token row
+// has exactly one window row, so the adds never collide; s: the training DropPath scale of the
+// row's sample, nullable = 1).  C % 4 == 0.
 __global__ __launch_bounds__(256) void window_scatter_add_kernel(float* __restrict__ X, const float* __restrict__ y,
-                                                                 const int32_t* __restrict__ idx, int64_t rows, int C) {
+                                                                 const int32_t* __restrict__ idx, int64_t rows, int C,
+                                                                 const float* __restrict__ row_scale, int64_t group) {
   const int c4 = C / 4;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows * c4; i += (int64_t)gridDim.x * 256) {
     const int64_t m = i / c4;
     const int c = (int)(i % c4) * 4;
     const int32_t dst = idx[m];
     if (dst < 0) continue;
-    const float4 v = *reinterpret_cast<const float4*>(y + m * C + c);
+    float4 v = *reinterpret_cast<const float4*>(y + m * C + c);
+    if (row_scale) {
+      const float sc = row_scale[m / group];
+      v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+    }
     float4* xo = reinterpret_cast<float4*>(X + (int64_t)dst * C + c);
     float4 xv = *xo;
     xv.x += v.x; xv.y += v.y; xv.z += v.z; xv.w += v.w;
@@ -266,10 +272,11 @@ __global__ __launch_bounds__(256) void window_scatter_add_kernel(float* __restri
 }
 
 hipError_t launch_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_t rows, int64_t C,
-                                     hipStream_t s) {
+                                     const float* row_scale, int64_t group, hipStream_t s) {
   int64_t blocks = (rows * C / 4 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  window_scatter_add_kernel<<<(unsigned)(blocks < 1 ? 1 : blocks), 256, 0, s>>>(X, y, idx, rows, (int)C);
+  window_scatter_add_kernel<<<(unsigned)(blocks < 1 ? 1 : blocks), 256, 0, s>>>(X, y, idx, rows, (int)C, row_scale,
+                                                                                group);
   return hipGetLastError();
 }
 

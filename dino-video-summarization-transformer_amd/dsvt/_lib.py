@@ -18,7 +18,7 @@ TOKENS_NT, TOKENS_FRAME = 0, 1
 PROBE_GEMM, PROBE_ATTN_SPATIAL, PROBE_ATTN_TEMPORAL, PROBE_NORM, PROBE_LOSS = 1, 2, 4, 8, 16
 WS_LN_GEMM, WS_PATCH_EMBED, WS_ATTN_SPATIAL, WS_DINO_LOSS, WS_PAIR_LOSS = 1, 2, 3, 4, 5
 WS_LN_BWD, WS_COLSUM, WS_ATTN_BWD, WS_EMBED_BWD = 6, 7, 8, 9
-WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_ATTN_CLS, WS_ATTN_CLS_BWD = 10, 11, 12, 14, 15
+WS_SELECT, WS_AUGMENT, WS_WGRAD, WS_ATTN_CLS, WS_ATTN_CLS_BWD, WS_ATTN_WIN_BWD = 10, 11, 12, 14, 15, 16
 
 _i32, _i64, _f32, _f64, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 
@@ -98,7 +98,11 @@ SIGNATURES = {
                                          _i64, _p, _p, _i64, _p]),
     "dsvt_swin_ln_rows_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),
     "dsvt_swin_merge_ln_fwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
-    "dsvt_window_scatter_add": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "dsvt_window_scatter_add": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64, _p]),
+    "dsvt_swin_gather_rows": (_i32, [_i32, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _p]),
+    "dsvt_attn_window_bwd": (_i32, [_i32, _p, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p,
+                                    _i64, _p, _p, _i64, _p]),
+    "dsvt_relpos_bias_bwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _p, _i32, _p]),
     "dsvt_relpos_bias_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p]),
     "dsvt_attn_window_fwd": (_i32, [_i32, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_cast_pad_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _p]),

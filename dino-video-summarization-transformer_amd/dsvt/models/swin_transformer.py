@@ -1,8 +1,8 @@
 """Video Swin Transformer backbone (config 5) on libdsvt.so -- drop-in for
 models/swin_transformer.py of the reference (`SwinTransformer3D` :463-687 and its parts), with
 the same constructor signatures and state_dict keys (incl. the `relative_position_index`
-buffers), so checkpoints load unchanged.  Inference forward only (training DropPath / backward
-are implemented for the TimeSformer hot path).
+buffers), so checkpoints load unchanged.  Inference forward here; training (DropPath, the
+backward of every layer) in dsvt/swin_training.py.
 
 Layout: the residual stream of a stage is fp32 X [B, D, H, W, C] (channels last).  Each block:
   norm1 + zero pad + cyclic roll + window_partition   -> ONE gather-LayerNorm kernel through an
@@ -233,6 +233,17 @@ class _SwinCtx:
     def __init__(self, model, mode, device):
         self.model, self.mode, self.device = model, mode, device
         self.wp = model._wcache.padded(mode)
+        self.wpt = model._wcache.padded_transposed(mode)      # training: W^T for the dX GEMMs
+
+    def merge_idx(self, B, D, H, W):
+        """PatchMerging's 2x2 gather as a device row map (training, dsvt.swin_training.merge_map)."""
+        key = ("merge", B, D, H, W, self.device)
+        ent = self.model._aux.get(key)
+        if ent is None:
+            from ..swin_training import merge_map
+            ent = torch.from_numpy(merge_map(B, D, H, W)).to(self.device)
+            self.model._aux[key] = ent
+        return ent
 
     def maps(self, B, D, H, W, ws, ss):
         key = ("maps", B, D, H, W, ws, ss, self.device)
@@ -362,12 +373,20 @@ class SwinTransformer3D(nn.Module):
         """swin_transformer.py:668-682 -> pooled features [B, num_features] fp32."""
         if not x.is_cuda or not self.norm.weight.is_cuda:
             raise DsvtError("dsvt SwinTransformer3D runs only on the GPU (no CPU fallback)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("dsvt Swin backward is not implemented: run under torch.no_grad()")
-        if self.training and self._drop[2] > 0:
-            raise NotImplementedError("training-mode DropPath is not implemented for dsvt Swin; call .eval()")
         if self.patch_embed.norm is not None:
             raise NotImplementedError("patch_norm=True is not supported by the dsvt Swin forward")
+        if self.training and (self._drop[0] > 0 or self._drop[1] > 0):
+            raise NotImplementedError("training-mode dropout (drop_rate / attn_drop_rate > 0) is not in dsvt; "
+                                      "stochastic depth (drop_path_rate) is")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            # training (the --arch swin student, train_ssl.py:237-239): one autograd node per call
+            from ..swin_training import SwinFn
+            return SwinFn.apply(self, x, *self.parameters())
+        if self.training and self._drop[2] > 0:
+            # train mode with DropPath but nothing to differentiate (a train-mode teacher under
+            # no_grad): the masked training forward without saved activations
+            from ..swin_training import swin_train_forward
+            return swin_train_forward(self, x, save=False)[0]
         mode = self.dsvt_dtype
         ctx = _SwinCtx(self, mode, x.device)
         x = x.float().contiguous()

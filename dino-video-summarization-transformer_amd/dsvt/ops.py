@@ -648,9 +648,42 @@ def swin_merge_ln(x, ln, out, B, D, H, W):
     return out
 
 
-def window_scatter_add(X, y, idx):
-    call("dsvt_window_scatter_add", _ptr(X), _ptr(y), _ptr(idx), y.shape[0], y.shape[1], _stream())
+def window_scatter_add(X, y, idx, row_scale=None, group=1):
+    """X[idx[m]] += s[m // group] * y[m] (idx[m] >= 0; row_scale None = 1)."""
+    _check(X, torch.float32, "X")
+    _check(y, torch.float32, "y")
+    if idx.dtype != torch.int32 or idx.numel() != y.shape[0]:
+        raise _lib.DsvtError("window_scatter_add: idx must be int32 with one entry per row of y")
+    call("dsvt_window_scatter_add", _ptr(X), _ptr(y), _ptr(idx), y.shape[0], y.shape[1], _ptr(row_scale),
+         int(group), _stream())
     return X
+
+
+def swin_gather_rows(x, idx, out, rows, row_scale=None, group=1):
+    """out[m] = dtype(s[m // group] * x[idx[m]]), zero rows for idx < 0 and zero columns past x's
+    width (idx None = identity)."""
+    _check(x, torch.float32, "x")
+    if idx is not None and (idx.dtype != torch.int32 or idx.numel() < rows):
+        raise _lib.DsvtError("swin_gather_rows: idx must be int32 with >= rows entries")
+    call("dsvt_swin_gather_rows", _dt(out.dtype), _ptr(x), _ptr(idx), _ptr(row_scale), int(group), _ptr(out), rows,
+         x.shape[-1], out.shape[-1], _stream())
+    return out
+
+
+def attn_window_bwd(qkv, o, dout, bias, region, dqkv, dbias, nwin, nwc, N, heads, scale):
+    """WindowAttention3D backward: dqkv (qkv's layout) and the score-bias gradient dbias [heads, N, N]."""
+    ws = _ws(_lib.WS_ATTN_WIN_BWD, qkv.dtype, nwin, heads, N, qkv.device)
+    call("dsvt_attn_window_bwd", _dt(qkv.dtype), _ptr(qkv), _ptr(o), o.shape[-1], _ptr(dout), dout.shape[-1],
+         _ptr(bias), _ptr(region), nwin, nwc, N, heads, 32, float(scale), _ptr(dqkv), dqkv.shape[-1], _ptr(dbias), _ptr(ws),
+         ws.numel() * 4, _stream())
+    return dqkv
+
+
+def relpos_bias_bwd(dbias, index, N, dtable, accumulate=False):
+    """relative_position_bias_table gradient from the score-bias gradient (deterministic gather)."""
+    call("dsvt_relpos_bias_bwd", _ptr(dbias), _ptr(index), index.shape[-1], N, dtable.shape[1], dtable.shape[0],
+         _ptr(dtable), int(accumulate), _stream())
+    return dtable
 
 
 def relpos_bias(table, index, N, out):

@@ -105,6 +105,26 @@ class WeightCache:
             return out, ldk
         return get
 
+    def padded_transposed(self, mode):
+        """W^T [K, N] as [K, ldn] in the storage dtype with zero columns N..ldn-1 (ldn = N rounded up
+        to the MFMA K tile): the B operand of an input-gradient GEMM dX = dY . W whose dY width N
+        needs padding (the Video Swin C = 96 stage, train_ssl.py --arch swin).  Returns (wt, ldn)."""
+        def get(p):
+            t = p.detach()
+            N = t.shape[0]
+            q = 64 if mode == torch.bfloat16 else 32
+            ldn = (N + q - 1) // q * q
+            key = (id(p), "padT", mode)
+            ent = self._c.get(key)
+            if ent is not None and ent[0] == p._version and ent[1] == p.data_ptr():
+                self._sync(ent)
+                return ent[2], ldn
+            out = torch.empty(t.shape[1], ldn, device=t.device, dtype=mode)
+            ops.cast_pad(t.t().contiguous().float(), out)
+            self._c[key] = (p._version, p.data_ptr(), out) + self._event()
+            return out, ldn
+        return get
+
     def transposed(self, mode):
         """W^T [in, out] in the storage dtype (dsvt cast-transpose kernel), cached like the
         casts: the B operand of the backward's input-gradient GEMMs dX = dY . W."""

@@ -74,6 +74,7 @@ extern "C" {
 #define DSVT_WS_WGRAD 12       /* M = rows, N, K: the weight gradient is [N, K] */
 #define DSVT_WS_ATTN_CLS 14    /* M = B*T sequences, N = heads, K = keys per sequence 1 + (L-1)/T */
 #define DSVT_WS_ATTN_CLS_BWD 15 /* M = B*T sequences, N = heads */
+#define DSVT_WS_ATTN_WIN_BWD 16 /* M = windows, N = heads, K = tokens per window */
 
 int dsvt_version(void);
 const char *dsvt_last_error(void);
@@ -462,9 +463,32 @@ int dsvt_swin_ln_rows_fwd(int dtype, const float *x, const int32_t *idx, const f
 /* PatchMerging (:293-315): 2x2 gather (x0, x1, x2, x3 order, zero pad) + LayerNorm(4C). */
 int dsvt_swin_merge_ln_fwd(int dtype, const float *x, const float *gamma, const float *beta, void *out,
                            int64_t B, int64_t D, int64_t H, int64_t W, int64_t C, float eps, void *stream);
-/* X[idx[m]] += y[m] (idx[m] >= 0): window_reverse + reverse roll + crop + residual (:241-251). */
+/* X[idx[m]] += s[m / group] * y[m] (idx[m] >= 0): window_reverse + reverse roll + crop + residual
+ * (:241-251); row_scale (nullable = 1): the training DropPath scale of the row's sample (:263, x =
+ * shortcut + drop_path(x)), window rows of one sample in runs of `group`.  Also the reverse of any
+ * row gather (the PatchMerging 2x2 gather's gradient). */
 int dsvt_window_scatter_add(float *X, const float *y, const int32_t *idx, int64_t rows, int64_t C,
-                            void *stream);
+                            const float *row_scale, int64_t group, void *stream);
+/* ---- Video Swin training (swin_bwd.hip; the --arch swin student, train_ssl.py:237-239) ----------
+ * out[m] = dtype(s[m / group] * x[idx[m]]) for c < C, zero for idx[m] < 0 and columns C..ldo-1 (idx
+ * NULL = identity, row_scale NULL = 1): window_partition of a token gradient (the window-row gradient
+ * of the attention branch), row-scaled / K-padded casts, the PatchMerging 2x2 gather (:300-310). */
+int dsvt_swin_gather_rows(int dtype, const float *x, const int32_t *idx, const float *row_scale, int64_t group,
+                          void *out, int64_t rows, int64_t C, int64_t ldo, void *stream);
+/* WindowAttention3D backward (:139-171): dqkv [nwin*N, 3C] (qkv's layout) from the forward's qkv,
+ * its output o [nwin*N, ldo] and dout [nwin*N, lddo] (the gradient of o); P recomputed with the
+ * relative-position bias and the shift mask (-100 across regions); dqkv rows ld_dqkv apart (>= 3C:
+ * room for the zero K padding the next GEMM needs).  dbias [heads][N][N] fp32 = the
+ * gradient of the bias added to the scores, summed over the windows in a fixed order (written, not
+ * accumulated).  workspace >= dsvt_workspace_bytes(DSVT_WS_ATTN_WIN_BWD, ., nwin, heads, N). */
+int dsvt_attn_window_bwd(int dtype, const void *qkv, const void *o, int64_t ldo, const void *dout, int64_t lddo,
+                         const float *bias, const int32_t *region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads,
+                         int64_t head_dim, float scale, void *dqkv, int64_t ld_dqkv, float *dbias, void *workspace,
+                         int64_t workspace_bytes, void *stream);
+/* relative_position_bias_table gradient (:152-156 backward): dtable[e][h] (+)= sum over i, j < N with
+ * index[i*nmax + j] == e of dbias[h][i][j]; entries = rows of the table.  Deterministic (no atomics). */
+int dsvt_relpos_bias_bwd(const float *dbias, const int64_t *index, int64_t nmax, int64_t N, int64_t heads,
+                         int64_t entries, float *dtable, int accumulate, void *stream);
 /* out[h][i][j] = table[index[i*nmax + j]][h], i, j < N (:152-156, the [:N, :N] slice). */
 int dsvt_relpos_bias_fwd(const float *table, const int64_t *index, int64_t nmax, int64_t N,
                          int64_t heads, float *out, void *stream);

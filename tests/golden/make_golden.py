@@ -271,6 +271,79 @@ def swin_base_cases():
     return {"base": out, "keys_base": np.array(sorted(m.state_dict().keys()))}
 
 
+SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
+
+
+def swin_grads_cases():
+    """Video Swin TRAINING (the --arch swin student, train_ssl.py:237-239; models/swin_transformer.py):
+    a small SwinTransformer3D (C 64, depths 2-2, heads 2-4: head_dim 32, window (2, 7, 7)) under
+    MultiCropWrapper as it calls the backbone (one call per resolution) -> DINOHead -> DINOLoss,
+    backward: loss, student logits, every parameter gradient.  2 global 8x60^2 crops (15 x 15
+    tokens: window padding, shifted windows with the -100 mask, an odd PatchMerging; stage 2 at 8 x
+    8: padded again) and 2 local 4x36^2 crops (D = 1: the window shrinks in time, stage 2 at 5 x 5
+    fits one window: no shift); eval and DropPath 0.5, the masks recorded in call order (timm
+    DropPath stubbed with models/vit_utils.DropPath, whose forward is patched to record)."""
+    import torch.distributed as dist
+    import models.vit_utils as ref_vu
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29536")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    for name in ("timm", "timm.models", "timm.models.layers"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["timm.models.layers"].DropPath = ref_vu.DropPath
+    sys.modules["timm.models.layers"].trunc_normal_ = ref_vu.trunc_normal_
+    import models.swin_transformer as ref_swin
+    TL = _extract(os.path.join(REF, "train_ssl.py"), ["DINOLoss"])["DINOLoss"]
+    res = {}
+    for tag, dpr in (("eval", 0.0), ("drop", 0.5)):
+        bb = ref_swin.SwinTransformer3D(drop_path_rate=dpr, **SWIN_TRAIN)
+        sd = P.swin_state(1401, {k: v.shape for k, v in bb.state_dict().items()})
+        missing, unexpected = bb.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+        assert not unexpected and all("relative_position_index" in k for k in missing)
+        hd = ref_vit.DINOHead(128, 512, hidden_dim=128, bottleneck_dim=64)
+        _load(hd, P.dino_head_state(1402, 128, 512, hidden_dim=128, bottleneck_dim=64))
+        masks = []
+        gen = torch.Generator().manual_seed(1403)
+        orig = ref_vu.DropPath.forward
+
+        def dp_forward(self, x):
+            if self.drop_prob == 0. or not self.training:
+                return x
+            keep = 1 - self.drop_prob
+            r = torch.floor(keep + torch.rand((x.shape[0],), generator=gen, dtype=x.dtype))
+            masks.append((r / keep).numpy().astype(np.float32))
+            return x.div(keep) * r.view((x.shape[0],) + (1,) * (x.ndim - 1))
+        ref_vu.DropPath.forward = dp_forward
+        try:
+            if tag == "eval":
+                bb.eval()
+            else:
+                bb.train()         # a statement: the reference's train() returns None
+            hd.train()
+            g_in = [torch.from_numpy(P.clip(1410 + i, (2, 3, 8, 60, 60))) for i in range(2)]
+            l_in = [torch.from_numpy(P.clip(1420 + i, (2, 3, 4, 36, 36))) for i in range(2)]
+            s_out = hd(torch.cat([bb(torch.cat(g_in)), bb(torch.cat(l_in))]))
+            t_out = torch.from_numpy(P.uniform(1430, (4, 512)))
+            lf = TL(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2)
+            loss = lf(s_out, t_out, 0)
+            loss.backward()
+        finally:
+            ref_vu.DropPath.forward = orig
+        res[tag + "_loss"] = np.float32(loss.item())
+        res[tag + "_student"] = s_out.detach().numpy()
+        res[tag + "_teacher"] = t_out.numpy()
+        for k, p in bb.named_parameters():
+            res[tag + "_bb." + k] = p.grad.numpy().copy()
+        for k, p in hd.named_parameters():
+            if p.grad is not None:
+                res[tag + "_hd." + k] = p.grad.numpy().copy()
+        if masks:
+            res[tag + "_masks"] = np.concatenate(masks)
+            res[tag + "_mask_sizes"] = np.array([len(m) for m in masks], np.int32)
+    return res
+
+
 def run(m, x, **kw):
     with torch.no_grad():
         return m.forward_features(torch.from_numpy(x), **kw).numpy()
@@ -664,7 +737,7 @@ def views_edge_cases():
 GROUPS = {"selection": selection_cases, "augment": augment_cases, "train_step": train_step_cases,
           "train_step_fp16": train_step_fp16_cases, "train_grads_plain": train_grads_plain_cases,
           "views_edge": views_edge_cases, "train_grads_vit2d": train_grads_vit2d_cases,
-          "swin_base": swin_base_cases}
+          "swin_base": swin_base_cases, "swin_grads": swin_grads_cases}
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:             # regenerate only the named fixture groups

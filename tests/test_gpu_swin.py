@@ -116,3 +116,146 @@ def test_swin_ln_rows_gather(dtype, C, ldo):
     err = (out.float() - ref).abs().max().item()
     assert err < (2e-5 if dtype == torch.float32 else 3e-2), err
     assert (out[~valid].float() == 0).all() and (out[:, C:].float() == 0).all()
+
+
+# ------------------------------------------------------------------------------ Swin training
+SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tag", ["eval", "drop"])
+def test_swin_student_grads_match_reference(dtype, tag, monkeypatch):
+    """The --arch swin student trains (train_ssl.py:237-239; models/swin_transformer.py): a small
+    SwinTransformer3D (C 64, depths 2-2, heads 2-4, window (2, 7, 7)) under MultiCropWrapper ->
+    DINOHead -> DINOLoss, loss.backward() -- loss, logits and every parameter gradient (incl. the
+    relative-position bias tables, the PatchMerging norm / reduction and the Conv3d patch embed)
+    against the reference's own autograd (tests/golden/swin_grads.npz: window padding, the shifted
+    windows' mask, an odd merge, windows clamped in time; eval and DropPath 0.5 with the
+    reference's masks replayed).  fp32 1e-3, bf16 4e-2 (relative to max |ref| per tensor)."""
+    from dsvt import training
+    from dsvt.loss import DINOLoss
+    from dsvt.models import SwinTransformer3D
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+    gold = dict(np.load("tests/golden/swin_grads.npz"))
+    if tag == "drop":
+        masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
+        state = {"off": 0, "i": 0}
+
+        def replay(ns, ps, device):           # one forward's masks, in the reference's call order
+            i = state["i"]
+            assert list(ns) == sizes[i:i + len(ns)], (list(ns), sizes[i:i + len(ns)])
+            m = masks[state["off"]:state["off"] + sum(ns)]
+            state["off"] += sum(ns)
+            state["i"] += len(ns)
+            return torch.from_numpy(m.copy()).to(device)
+        monkeypatch.setattr(training, "_keep_scales", replay)
+        import dsvt.swin_training as ST
+        monkeypatch.setattr(ST, "_keep_scales", replay)
+    bb = SwinTransformer3D(drop_path_rate=0.5 if tag == "drop" else 0.0, **SWIN_TRAIN)
+    sd = P.swin_state(1401, {k: v.shape for k, v in bb.state_dict().items()})
+    missing, unexpected = bb.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and all("relative_position_index" in k for k in missing)
+    hd = DINOHead(128, 512, hidden_dim=128, bottleneck_dim=64)
+    hd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                        P.dino_head_state(1402, 128, 512, hidden_dim=128, bottleneck_dim=64).items()})
+    bb.dsvt_dtype = hd.dsvt_dtype = dtype
+    net = MultiCropWrapper(bb, hd).cuda()
+    net.train()
+    if tag == "eval":
+        bb.eval()
+    crops = [torch.from_numpy(P.clip(1410 + i, (2, 3, 8, 60, 60))).cuda() for i in range(2)] + \
+            [torch.from_numpy(P.clip(1420 + i, (2, 3, 4, 36, 36))).cuda() for i in range(2)]
+    s_out = net(crops)
+    t_out = torch.from_numpy(gold[tag + "_teacher"]).cuda()
+    loss_fn = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    loss = loss_fn(s_out, t_out, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    tol = TOL[dtype] if dtype == torch.float32 else 4e-2
+    assert abs(loss.item() - float(gold[tag + "_loss"])) < tol * abs(float(gold[tag + "_loss"]))
+    assert _rel(s_out.detach().cpu().numpy(), gold[tag + "_student"]) < tol
+    checked, errs = 0, {}
+    for pre, mod in (("bb.", bb), ("hd.", hd)):
+        for k, p in mod.named_parameters():
+            key = tag + "_" + pre + k
+            if key not in gold:
+                assert p.grad is None or not p.requires_grad, k
+                continue
+            assert p.grad is not None, key
+            errs[key] = _rel(p.grad.cpu().numpy(), gold[key])
+            checked += 1
+    bad = sorted(((e, k) for k, e in errs.items() if e >= tol), reverse=True)
+    assert not bad, "%d gradients off: %s" % (len(bad), bad)
+    worst = max((e, k) for k, e in errs.items())
+    if tag == "drop":
+        assert state["i"] == len(sizes), "mask draws %d of %d" % (state["i"], len(sizes))
+    print("swin train grads", tag, dtype, "worst %.3g (%s)" % worst)
+    assert checked >= 40
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-12))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,shifted", [(98, True), (49, False), (25, True), (128, True)])
+def test_attn_window_bwd_vs_autograd(dtype, N, shifted):
+    """dsvt_attn_window_bwd against torch fp64 autograd of the reference's WindowAttention3D math
+    (:139-171: q.k * scale + bias + -100 across shift regions, softmax, P.V): dq, dk, dv and the
+    score-bias gradient summed over the windows; then the relative-position table gradient
+    (dsvt_relpos_bias_bwd) against autograd of the table gather."""
+    from dsvt import ops
+    torch.manual_seed(N)
+    heads, nwin, nwc, C = 3, 6, 3, 96
+    dev = torch.device("cuda")
+    qkv = torch.randn(nwin * N, 3 * C, device=dev)
+    dout = torch.randn(nwin * N, C, device=dev)
+    reg = torch.randint(0, 3, (nwc, N), device=dev, dtype=torch.int32) if shifted else \
+        torch.zeros(nwc, N, device=dev, dtype=torch.int32)
+    wd, wh, ww = 2, 8, 8                       # a relative-position index over an N <= 128 window
+    nmax = wd * wh * ww
+    coords = torch.stack(torch.meshgrid(torch.arange(wd), torch.arange(wh), torch.arange(ww), indexing="ij")).flatten(1)
+    rel = (coords[:, :, None] - coords[:, None, :]).permute(1, 2, 0).contiguous()
+    rel[:, :, 0] += wd - 1
+    rel[:, :, 1] += wh - 1
+    rel[:, :, 2] += ww - 1
+    rel[:, :, 0] *= (2 * wh - 1) * (2 * ww - 1)
+    rel[:, :, 1] *= 2 * ww - 1
+    index = rel.sum(-1).to(dev)
+    entries = (2 * wd - 1) * (2 * wh - 1) * (2 * ww - 1)
+    table = (0.5 * torch.randn(entries, heads, device=dev))
+    scale = 32 ** -0.5
+    # reference in fp64 on the storage-dtype-rounded inputs
+    q_in = qkv.to(dtype).double().requires_grad_(True)
+    tab = table.double().requires_grad_(True)
+    x = q_in.view(nwin, N, 3, heads, 32).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    bias = tab[index[:N, :N].reshape(-1)].reshape(N, N, heads).permute(2, 0, 1)
+    s = (q * scale) @ k.transpose(-2, -1) + bias.unsqueeze(0)
+    r = reg.long()
+    mask = torch.where(r[:, :, None] != r[:, None, :], -100.0, 0.0).double()       # [nwc, N, N]
+    s = s + mask[torch.arange(nwin, device=dev) % nwc].unsqueeze(1)
+    o = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(nwin * N, C)
+    do_in = dout.to(dtype).double()
+    (o * do_in).sum().backward()
+    # dsvt
+    qkv_s = qkv.to(dtype).contiguous()
+    bias_f = torch.empty(heads, N, N, device=dev)
+    ops.relpos_bias(table, index, N, bias_f)
+    o_s = torch.empty(nwin * N, C, device=dev, dtype=dtype)
+    ops.attn_window(qkv_s, o_s, bias_f, reg, nwin, nwc, N, heads, scale)
+    dqkv = torch.zeros(nwin * N, 3 * C + 32, device=dev, dtype=dtype)      # a padded row stride
+    dbias = torch.empty(heads, N, N, device=dev)
+    ops.attn_window_bwd(qkv_s, o_s, dout.to(dtype).contiguous(), bias_f, reg, dqkv, dbias, nwin, nwc, N, heads, scale)
+    dtab = torch.full((entries, heads), 7.0, device=dev)
+    ops.relpos_bias_bwd(dbias, index, N, dtab, accumulate=False)
+    torch.cuda.synchronize()
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    got = dqkv[:, :3 * C].double().cpu()
+    assert _rel(got, q_in.grad.cpu()) < tol
+    assert torch.all(dqkv[:, 3 * C:] == 0)
+    assert _rel(dtab.cpu(), tab.grad.cpu()) < tol

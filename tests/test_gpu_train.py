@@ -471,7 +471,10 @@ def test_attn_joint_bwd_vs_autograd(dtype, tol, L, attn_bwd_variant):
     assert rel(dq.float().cpu(), q32.grad.cpu()) < tol
 
 
-@pytest.mark.parametrize("C,dy_dtype", [(64, torch.float32), (768, torch.float32), (768, torch.bfloat16)])
+@pytest.mark.parametrize("C,dy_dtype", [(64, torch.float32), (768, torch.float32), (768, torch.bfloat16),
+                                        (96, torch.bfloat16), (384, torch.float32), (1536, torch.bfloat16),
+                                        (2048, torch.float32), (256, torch.bfloat16), (512, torch.float32),
+                                        (1024, torch.bfloat16)])
 def test_layernorm_bwd_rowmap_vs_autograd(C, dy_dtype):
     """dX[row(m)] += dLN for the patch rows of a [B, 1 + Np*T, C] token tensor; dgamma/dbeta."""
     from dsvt import ops
