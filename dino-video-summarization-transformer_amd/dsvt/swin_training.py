@@ -217,7 +217,7 @@ def swin_train_forward(model, x, save=True):
         st.layers.append((blocks, mS))
     C = X.shape[1]
     Y = torch.empty_like(X)
-    ops.layernorm(X, X.shape[0], C, model.norm.weight, model.norm.bias, model.norm.eps, Y)
+    ops.swin_ln_rows(X, None, model.norm, Y, X.shape[0])          # any C (a C = 96 last stage too)
     out = torch.empty(B, C, device=x.device, dtype=torch.float32)
     ops.frame_mean(Y, out, B, D * H * W, C)                 # AdaptiveAvgPool3d((1, 1, 1))
     st.X, st.DHW = X, D * H * W

@@ -196,7 +196,9 @@ class MultiCropWrapper(nn.Module):
                     o.record_stream(cur)
             return self.head(torch.cat(outs) if len(outs) > 1 else outs[0])
         total = sum(inp.shape[0] for inp in x)
-        feats = torch.empty(total, self.backbone.embed_dim, device=x[0].device, dtype=torch.float32)
+        # num_features: the backbone's output width (a Swin's is embed_dim * 2^(stages - 1))
+        feats = torch.empty(total, getattr(self.backbone, "num_features", self.backbone.embed_dim), device=x[0].device,
+                            dtype=torch.float32)
         jobs, start, row = [], 0, 0
         for end in idx_crops:
             group = x[start:end]

@@ -272,6 +272,7 @@ def swin_base_cases():
 
 
 SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
+SWIN_TRAIN96 = dict(embed_dim=96, depths=[2], num_heads=[3])     # Swin-T's C = 96 stage: K padding
 
 
 def swin_grads_cases():
@@ -296,13 +297,14 @@ def swin_grads_cases():
     import models.swin_transformer as ref_swin
     TL = _extract(os.path.join(REF, "train_ssl.py"), ["DINOLoss"])["DINOLoss"]
     res = {}
-    for tag, dpr in (("eval", 0.0), ("drop", 0.5)):
-        bb = ref_swin.SwinTransformer3D(drop_path_rate=dpr, **SWIN_TRAIN)
+    for tag, dpr, cfg in (("eval", 0.0, SWIN_TRAIN), ("drop", 0.5, SWIN_TRAIN), ("c96", 0.5, SWIN_TRAIN96)):
+        bb = ref_swin.SwinTransformer3D(drop_path_rate=dpr, **cfg)
         sd = P.swin_state(1401, {k: v.shape for k, v in bb.state_dict().items()})
         missing, unexpected = bb.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
         assert not unexpected and all("relative_position_index" in k for k in missing)
-        hd = ref_vit.DINOHead(128, 512, hidden_dim=128, bottleneck_dim=64)
-        _load(hd, P.dino_head_state(1402, 128, 512, hidden_dim=128, bottleneck_dim=64))
+        nf = bb.num_features
+        hd = ref_vit.DINOHead(nf, 512, hidden_dim=128, bottleneck_dim=64)
+        _load(hd, P.dino_head_state(1402, nf, 512, hidden_dim=128, bottleneck_dim=64))
         masks = []
         gen = torch.Generator().manual_seed(1403)
         orig = ref_vu.DropPath.forward
@@ -316,7 +318,7 @@ def swin_grads_cases():
             return x.div(keep) * r.view((x.shape[0],) + (1,) * (x.ndim - 1))
         ref_vu.DropPath.forward = dp_forward
         try:
-            if tag == "eval":
+            if dpr == 0.0:
                 bb.eval()
             else:
                 bb.train()         # a statement: the reference's train() returns None

@@ -120,11 +120,12 @@ def test_swin_ln_rows_gather(dtype, C, ldo):
 
 # ------------------------------------------------------------------------------ Swin training
 SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
+SWIN_TRAIN96 = dict(embed_dim=96, depths=[2], num_heads=[3])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("tag", ["eval", "drop"])
+@pytest.mark.parametrize("tag", ["eval", "drop", "c96"])
 def test_swin_student_grads_match_reference(dtype, tag, monkeypatch):
     """The --arch swin student trains (train_ssl.py:237-239; models/swin_transformer.py): a small
     SwinTransformer3D (C 64, depths 2-2, heads 2-4, window (2, 7, 7)) under MultiCropWrapper ->
@@ -132,15 +133,17 @@ def test_swin_student_grads_match_reference(dtype, tag, monkeypatch):
     relative-position bias tables, the PatchMerging norm / reduction and the Conv3d patch embed)
     against the reference's own autograd (tests/golden/swin_grads.npz: window padding, the shifted
     windows' mask, an odd merge, windows clamped in time; eval and DropPath 0.5 with the
-    reference's masks replayed).  fp32 1e-3, bf16 4e-2 (relative to max |ref| per tensor)."""
+    reference's masks replayed); c96: Swin-T's C = 96 stage (one stage, DropPath 0.5), whose K
+    dimensions (96, 288) the MFMA tile does not divide -- the zero-padded operands of the forward
+    and backward GEMMs.  fp32 1e-3, bf16 4e-2 (relative to max |ref| per tensor)."""
     from dsvt import training
     from dsvt.loss import DINOLoss
     from dsvt.models import SwinTransformer3D
     from dsvt.utils import MultiCropWrapper
     from dsvt.vision_transformer import DINOHead
     gold = dict(np.load("tests/golden/swin_grads.npz"))
-    if tag == "drop":
-        masks, sizes = gold["drop_masks"], list(gold["drop_mask_sizes"])
+    if tag != "eval":
+        masks, sizes = gold[tag + "_masks"], list(gold[tag + "_mask_sizes"])
         state = {"off": 0, "i": 0}
 
         def replay(ns, ps, device):           # one forward's masks, in the reference's call order
@@ -153,14 +156,17 @@ def test_swin_student_grads_match_reference(dtype, tag, monkeypatch):
         monkeypatch.setattr(training, "_keep_scales", replay)
         import dsvt.swin_training as ST
         monkeypatch.setattr(ST, "_keep_scales", replay)
-    bb = SwinTransformer3D(drop_path_rate=0.5 if tag == "drop" else 0.0, **SWIN_TRAIN)
+    bb = SwinTransformer3D(drop_path_rate=0.0 if tag == "eval" else 0.5, **(SWIN_TRAIN96 if tag == "c96" else SWIN_TRAIN))
     sd = P.swin_state(1401, {k: v.shape for k, v in bb.state_dict().items()})
     missing, unexpected = bb.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
     assert not unexpected and all("relative_position_index" in k for k in missing)
-    hd = DINOHead(128, 512, hidden_dim=128, bottleneck_dim=64)
+    nf = bb.num_features
+    hd = DINOHead(nf, 512, hidden_dim=128, bottleneck_dim=64)
     hd.load_state_dict({k: torch.from_numpy(v) for k, v in
-                        P.dino_head_state(1402, 128, 512, hidden_dim=128, bottleneck_dim=64).items()})
+                        P.dino_head_state(1402, nf, 512, hidden_dim=128, bottleneck_dim=64).items()})
     bb.dsvt_dtype = hd.dsvt_dtype = dtype
+    if tag == "c96":
+        hd.dsvt_dtype = torch.float32      # a 96-wide head input is no bf16 MFMA K tile; the backbone is the subject
     net = MultiCropWrapper(bb, hd).cuda()
     net.train()
     if tag == "eval":
@@ -189,10 +195,10 @@ def test_swin_student_grads_match_reference(dtype, tag, monkeypatch):
     bad = sorted(((e, k) for k, e in errs.items() if e >= tol), reverse=True)
     assert not bad, "%d gradients off: %s" % (len(bad), bad)
     worst = max((e, k) for k, e in errs.items())
-    if tag == "drop":
+    if tag != "eval":
         assert state["i"] == len(sizes), "mask draws %d of %d" % (state["i"], len(sizes))
     print("swin train grads", tag, dtype, "worst %.3g (%s)" % worst)
-    assert checked >= 40
+    assert checked >= (20 if tag == "c96" else 40)
 
 
 def _rel(a, b):
@@ -259,3 +265,61 @@ def test_attn_window_bwd_vs_autograd(dtype, N, shifted):
     assert _rel(got, q_in.grad.cpu()) < tol
     assert torch.all(dqkv[:, 3 * C:] == 0)
     assert _rel(dtab.cpu(), tab.grad.cpu()) < tol
+
+
+@pytest.mark.gpu
+def test_swin_trainer_steps_bf16():
+    """DINOTrainer steps (train_ssl.py:466-573 loop body: student forward + teacher forward, DINO
+    loss, backward into the persistent gradient buffers -- the Swin student goes through one
+    autograd node per resolution group --, clipping, AdamW, EMA) with the Swin student / teacher
+    of --arch swin at small widths: finite losses, every student parameter updated, the teacher
+    moved by the EMA, and the step's gradients equal to a plain loss.backward() of the same step."""
+    from dsvt.loss import DINOLoss
+    from dsvt.models import SwinTransformer3D
+    from dsvt.trainer import DINOTrainer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+
+    def net(seed):
+        bb = SwinTransformer3D(drop_path_rate=0.0, **SWIN_TRAIN)
+        sd = P.swin_state(seed, {k: v.shape for k, v in bb.state_dict().items()})
+        bb.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+        hd = DINOHead(128, 512, hidden_dim=128, bottleneck_dim=64)
+        bb.dsvt_dtype = hd.dsvt_dtype = torch.bfloat16
+        return MultiCropWrapper(bb, hd).cuda()
+    student, teacher = net(1501), net(1501)
+    student.train()
+    teacher.eval()
+    crops = [torch.from_numpy(P.clip(1510 + i, (2, 3, 8, 60, 60))).cuda() for i in range(2)] + \
+            [torch.from_numpy(P.clip(1520 + i, (2, 3, 4, 36, 36))).cuda() for i in range(2)]
+    # reference gradients of the first step: plain autograd accumulation, no persistent buffers
+    ref = net(1501)
+    ref.train()
+    ref.load_state_dict(student.state_dict())
+    lf_r = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    with torch.no_grad():
+        t_out = teacher(crops[:2])
+    lf_r(ref(crops), t_out, 0).backward()
+    g_ref = {k: p.grad.clone() for k, p in ref.named_parameters() if p.grad is not None}
+    lf = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    tr = DINOTrainer(student, teacher, lf, epochs=2, niter_per_ep=4, warmup_epochs=1, lr=1e-3)
+    p0 = {k: p.detach().clone() for k, p in student.named_parameters()}
+    t0 = {k: p.detach().clone() for k, p in teacher.named_parameters()}
+    orig_step = tr.optimizer.step
+    seen = {}
+
+    def step_spy(*a, **k):                   # the first step's gradients, before clipping's effect is applied by AdamW
+        if not seen:
+            seen.update({n: p.grad.clone() for n, p in student.named_parameters() if p.grad is not None})
+        return orig_step(*a, **k)
+    tr.clip_grad = 0                         # compare raw gradients (no clipping)
+    tr.optimizer.step = step_spy
+    losses = [float(tr.step(crops, it)) for it in (4, 5)]
+    torch.cuda.synchronize()
+    assert all(np.isfinite(losses)), losses
+    for k in g_ref:
+        assert _rel(seen[k].cpu().numpy(), g_ref[k].cpu().numpy()) < 1e-5, k
+    for k, p in student.named_parameters():
+        if p.requires_grad and k in seen:
+            assert not torch.equal(p.detach(), p0[k]), k
+    assert any(not torch.equal(p.detach(), t0[k]) for k, p in teacher.named_parameters())
