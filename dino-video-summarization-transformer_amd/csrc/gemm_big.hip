@@ -41,7 +41,9 @@ __device__ __forceinline__ void wait_stages(int k) {
 // Before storing tile t it issues the first stages of tile t+1 into the (free) LDS ring, so
 // the loads fly under the store tail; STAGGER delays the second-resident half of the grid by
 // ~half a tile so the two workgroups of a CU alternate MFMA loop and store tail.
-template <int BM, int BN, int WM, int WN, int NST, int EPI, bool OUT_F32, bool STAGGER>
+// STATS (EPI_RESID, 64-column wave tiles): the residual epilogue that also writes the updated
+// rows' bf16 copy and LayerNorm partials (dsvt_gemm_resid_stats_fwd; gemm_epi.h resid_stats_rows)
+template <int BM, int BN, int WM, int WN, int NST, int EPI, bool OUT_F32, bool STAGGER, bool STATS = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParams p) {
   constexpr int NW = WM * WN;
   constexpr int A_BYTES = BM * BIG_ROWB, B_BYTES = BN * BIG_ROWB, ST_BYTES = A_BYTES + B_BYTES;
@@ -161,8 +163,24 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
     }
     // ---- direct epilogue of tile (cm0, cn0)
     mfma_result_fence();
-    epilogue_direct<MI, NJ, EPI, OUT_F32, false, false, false, false, true>(p, acc, cm0 + wm * WTM, cn0 + wn * WTN,
-                                                                          r16, g);
+    if constexpr (STATS) {
+      static_assert(EPI == EPI_RESID && NJ == 4, "the stats epilogue: residual, 64-column wave slabs");
+      float4 b4[4];
+      bias_frag4(p.bias, cn0 + wn * WTN, g, b4);           // N % BN == 0: every column valid
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          acc[i][j][0] += b4[j].x; acc[i][j][1] += b4[j].y; acc[i][j][2] += b4[j].z; acc[i][j][3] += b4[j].w;
+        }
+#ifndef DSVT_PERSIST_STATS_W
+#define DSVT_PERSIST_STATS_W 2   // rows of X in flight (3 spills)
+#endif
+      epilogue_resid_stats<MI, NJ, DSVT_PERSIST_STATS_W>(p, acc, cm0 + wm * WTM, cn0 + wn * WTN, r16, g);
+    } else {
+      epilogue_direct<MI, NJ, EPI, OUT_F32, false, false, false, false, true>(p, acc, cm0 + wm * WTM,
+                                                                            cn0 + wn * WTN, r16, g);
+    }
     if (tn >= t_end) break;
     t = tn;
   }
@@ -181,6 +199,11 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
   GemmParams q = p;
   if (const char* e = getenv("DSVT_TILE_GROUP")) q.tile_group = atoi(e);
 #define DSVT_K(E, F) gemm_persist_kernel<BM, BN, WM, WN, NST, E, F, STAGGER><<<grid, block, 0, s>>>(q)
+  if (p.stats_out) {
+    if (epi != EPI_RESID || p.N % BN || p.row_scale || !p.xb_out) return hipErrorInvalidValue;
+    gemm_persist_kernel<BM, BN, WM, WN, NST, EPI_RESID, true, STAGGER, true><<<grid, block, 0, s>>>(q);
+    return hipGetLastError();
+  }
   switch (epi) {
     case EPI_BIAS: if (out_f32) DSVT_K(EPI_BIAS, true); else DSVT_K(EPI_BIAS, false); break;
     case EPI_GELU: if (out_f32) DSVT_K(EPI_GELU, true); else DSVT_K(EPI_GELU, false); break;

@@ -492,14 +492,13 @@ __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ
 // wave's 64-column slab (stats_out[row][cbase / 64]).  The X loads run a rolling window of W rows
 // ahead of the stores like the plain residual epilogue; FULL (wave-uniform): no row past M, no
 // per-lane bounds branch around the stores (which would make the compiler drain vmcnt).
-template <int MI, int NJ, bool FULL>
-__device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
-                                                 int r16, int g) {
-  static_assert(NJ == 4, "64-column wave slab");
 #ifndef DSVT_STATS_W
 #define DSVT_STATS_W 3
 #endif
-  constexpr int W = DSVT_STATS_W;
+template <int MI, int NJ, bool FULL, int W = DSVT_STATS_W>
+__device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
+                                                 int r16, int g) {
+  static_assert(NJ == 4, "64-column wave slab");
   const bool ident = p.rpg >= p.M && p.goff == 0;
   const int part = (int)(cbase >> 6);
   auto orow_of = [&](int i) -> int64_t {
@@ -544,11 +543,11 @@ __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)
   }
 }
 
-template <int MI, int NJ>
+template <int MI, int NJ, int W = DSVT_STATS_W>
 __device__ __forceinline__ void epilogue_resid_stats(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                      int64_t cbase, int r16, int g) {
-  if (rbase + MI * 16 <= p.M) resid_stats_rows<MI, NJ, true>(p, acc, rbase, cbase, r16, g);
-  else resid_stats_rows<MI, NJ, false>(p, acc, rbase, cbase, r16, g);
+  if (rbase + MI * 16 <= p.M) resid_stats_rows<MI, NJ, true, W>(p, acc, rbase, cbase, r16, g);
+  else resid_stats_rows<MI, NJ, false, W>(p, acc, rbase, cbase, r16, g);
 }
 
 }  // namespace dsvt

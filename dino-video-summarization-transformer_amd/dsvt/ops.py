@@ -603,7 +603,8 @@ def gemm_kernel_name(tag):
     if variant == 3:
         return "void dsvt::gemm_kernel<unsigned short, 2, true, true, 5, false>" + P
     if variant == 10:
-        return "void dsvt::gemm_persist_kernel<256, 128, 2, 2, 3, %d, %s, true>%s" % (epi, f32, P)
+        return "void dsvt::gemm_persist_kernel<256, 128, 2, 2, 3, %d, %s, true, %s>%s" % (
+            epi, f32, "true" if fuse == 2 else "false", P)
     if variant == 20:
         if fuse == 1:
             return "void dsvt::gemm_8ph_kernel<%d, false, 0, true, 1>%s" % (epi, P)
