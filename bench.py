@@ -255,19 +255,21 @@ def train_bench(args, device, rank, world, steps, warmup):
     # the reference's own configuration: the teacher left in train mode (DropPath 0.1 active,
     # never .eval()'d: train_ssl.py:330-333), run under no_grad after the student -- the masked
     # training forward without saved activations (training.backbone_forward_nosave)
-    teacher.train()
-    trainer.step(crops, 2000 + warmup + steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    for i in range(steps):
-        trainer.step(crops, 2001 + warmup + steps + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed_tt = ddist.max_over_ranks(time.perf_counter() - t1, device)
-    teacher.eval()
+    elapsed_tt = float("nan")
+    if not getattr(args, "no_teacher_train", False):      # tools/train_step.py traces skip it
+        teacher.train()
+        trainer.step(crops, 2000 + warmup + steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(steps):
+            trainer.step(crops, 2001 + warmup + steps + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed_tt = ddist.max_over_ranks(time.perf_counter() - t1, device)
+        teacher.eval()
     g, l = vit_fwd_flops(8, 224), vit_fwd_flops(8, 96)
     fwd_s = 2 * g + 6 * l + 8 * head_flops()
     clip_gf = (2 * g + 2 * head_flops() + 3 * fwd_s) / 1e9      # teacher fwd + student fwd + 2x-fwd backward

@@ -701,7 +701,8 @@ int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float
                        int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* dgamma, float* dbeta,
                        int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
   REQUIRE(dy_dtype == DSVT_BF16 || dy_dtype == DSVT_F32, "layernorm_bwd: bad dy dtype");
-  REQUIRE(x && dy && gamma && dx && dgamma && dbeta, "layernorm_bwd: null pointer");
+  REQUIRE(x && dy && gamma && dx, "layernorm_bwd: null pointer");
+  REQUIRE((dgamma == nullptr) == (dbeta == nullptr), "layernorm_bwd: dgamma and dbeta both or neither");
   REQUIRE(rows > 0 && C % 32 == 0 && C > 0 && C <= 2048, "layernorm_bwd: need 0 < C <= 2048, C %% 32 == 0");
   REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, 1, rows, 0, C),
           "layernorm_bwd: workspace too small");
@@ -714,9 +715,22 @@ int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float
                   hipError_t e;
                   if ((e = launch_ln_bwd(dy_dtype, x, dy, gamma, dx, rows, C, rpg, gstride, goff, eps, part, s)))
                     return e;
+                  if (!dgamma) return hipSuccess;            // partials left for dsvt_layernorm_bwd_params
                   if ((e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s))) return e;
                   return launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
                 });
+}
+
+int dsvt_layernorm_bwd_params(int64_t rows, int64_t C, const void* workspace, int64_t workspace_bytes, float* dgamma,
+                              float* dbeta, int accumulate, void* stream) {
+  REQUIRE(dgamma && dbeta && workspace && rows > 0 && C > 0 && C <= 2048, "layernorm_bwd_params: bad args");
+  REQUIRE(workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, 1, rows, 0, C), "layernorm_bwd_params: workspace too small");
+  const float* part = (const float*)workspace;
+  const int nb = ln_bwd_blocks(rows);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s);
+  if (e == hipSuccess) e = launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
+  return e == hipSuccess ? 0 : hip_fail(e, "layernorm_bwd_params");
 }
 
 // ---- DINOHead(use_bn=True): BatchNorm1d + GELU (head_bn.hip)

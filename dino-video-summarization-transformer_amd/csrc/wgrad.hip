@@ -57,8 +57,27 @@ __device__ __forceinline__ void wg_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-typedef __attribute__((address_space(3))) sv4* LDS4;
 typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+
+// ds_read_b64_tr_b16 as inline asm: the builtin makes the compiler drain every in-flight LDS-DMA
+// (s_waitcnt vmcnt(0) -- the stages prefetched three ahead included) before the first read of each
+// stage, which serialized the loads with the math; the asm form is not tracked, so the counted
+// vmcnt waits above stay the only ones and wg_lgkm_wait orders the results before their use
+__device__ __forceinline__ sv4 wg_tr_read(const char* lds) {
+  sv4 r;
+  const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+// s_waitcnt lgkmcnt(0) tied to the 24 fragment halves, so no use of them is scheduled above it
+__device__ __forceinline__ void wg_lgkm_wait(sv4 (&b)[8], sv4 (&a)[16]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]),
+                 "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]),
+                 "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]),
+                 "+v"(a[15]));
+}
 
 }  // namespace
 
@@ -145,20 +164,24 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) fa[i] = sv8{(short)i, 1, 2, 3, 4, 5, 6, (short)it};
     } else {
+      sv4 hb[8], ha[16];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = wn * 64 + j * 16 + cq;
-        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(ty + wg_off(ra, c)));
-        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(ty + wg_off(rb, c)));
-        fb[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        hb[2 * j] = wg_tr_read(ty + wg_off(ra, c));
+        hb[2 * j + 1] = wg_tr_read(ty + wg_off(rb, c));
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int c = wk * 128 + i * 16 + cq;
-        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(tx + wg_off(ra, c)));
-        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(tx + wg_off(rb, c)));
-        fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        ha[2 * i] = wg_tr_read(tx + wg_off(ra, c));
+        ha[2 * i + 1] = wg_tr_read(tx + wg_off(rb, c));
       }
+      wg_lgkm_wait(hb, ha);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = __builtin_shufflevector(hb[2 * j], hb[2 * j + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = __builtin_shufflevector(ha[2 * i], ha[2 * i + 1], 0, 1, 2, 3, 4, 5, 6, 7);
     }
     const int64_t m0 = (s_begin + it) * WG_BM;
     if (m0 + WG_BM > p.M) {                                   // last stage: dY rows past M -> 0

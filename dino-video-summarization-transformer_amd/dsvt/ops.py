@@ -435,13 +435,21 @@ def gemm_rowscale(a, w, bias, out, row_scale, group, aux=None, epilogue=_lib.EPI
 
 
 def layernorm_bwd(x, dy, gamma, eps, dx, rows, dgamma, dbeta, rowmap=None, accumulate=True):
-    """dx[row(m)] += dLN(x[row(m)], dy[m]); dgamma / dbeta (+)= the affine-parameter grads."""
+    """dx[row(m)] += dLN(x[row(m)], dy[m]); dgamma / dbeta (+)= the affine-parameter grads.
+    dgamma = dbeta = None: their partial sums are left in the returned workspace for
+    layernorm_bwd_params (returns ws then, else dx)."""
     C = x.shape[-1]
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
     ws = _ws(_lib.WS_LN_BWD, torch.float32, rows, 0, C, x.device)
     call("dsvt_layernorm_bwd", _dt(dy.dtype), _ptr(x), _ptr(dy), _ptr(gamma), _ptr(dx), rows, C, rpg, gs, go,
          float(eps), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ptr(ws), ws.numel() * 4, _stream())
-    return dx
+    return ws if dgamma is None else dx
+
+
+def layernorm_bwd_params(ws, rows, C, dgamma, dbeta, accumulate=True):
+    """dgamma / dbeta (+)= the partial sums a layernorm_bwd(dgamma=None) left in ws."""
+    call("dsvt_layernorm_bwd_params", rows, C, _ptr(ws), ws.numel() * 4, _ptr(dgamma), _ptr(dbeta), int(accumulate),
+         _stream())
 
 
 def colsum(y, out, rows=None, rowmap=None, row_scale=None, accumulate=True):

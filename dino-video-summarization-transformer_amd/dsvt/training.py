@@ -26,6 +26,7 @@ accumulation -- and DDP's bucketed all-reduce hooks -- see them like the referen
 """
 import collections
 import math
+import os
 
 import numpy as np
 import torch
@@ -144,11 +145,35 @@ def _colsum(y, G, p, **kw):
     ops.colsum(y, buf, accumulate=acc, **kw)
 
 
+# the LayerNorm-parameter reductions and the dX-chain bias column sums on the weight-gradient
+# stream (1) or inline on the dX chain (0: the round-4 schedule, kept for same-box A/Bs)
+_SIDE_PARAMS = os.environ.get("DSVT_TRAIN_SIDE_PARAMS", "1") != "0"
+
+
+def _colsum_side(y, G, p, row_scale=None):
+    """A bias gradient (column sums of y, optionally row-scaled) on the weight-gradient stream.  y
+    must not be rewritten afterwards (the storage-dtype copies of dX are fresh buffers)."""
+    buf, acc = G.acc(p)
+    if not _SIDE_PARAMS:
+        ops.colsum(y, buf, accumulate=acc, row_scale=row_scale)
+        return
+    G.run_side(lambda: ops.colsum(y, buf, accumulate=acc, row_scale=row_scale),
+               (y,) if row_scale is None else (y, row_scale))
+
+
 def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None):
+    """dx += the LayerNorm input gradient on the current stream (the dX chain); the dgamma / dbeta
+    reduction of its per-block partials runs on the weight-gradient stream (nothing on the dX chain
+    waits for it: four small launches per LayerNorm off the critical path)."""
     dg, acc = G.acc(ln.weight)
     db, acc2 = G.acc(ln.bias)
     assert acc == acc2
-    ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
+    if G.side is None or not _SIDE_PARAMS:
+        ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
+        return
+    ws = ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, None, None, rowmap=rowmap, accumulate=acc)
+    C = x.shape[-1]
+    G.run_side(lambda: ops.layernorm_bwd_params(ws, rows, C, dg, db, accumulate=acc), (ws,))
 
 
 def _own_grad(p):
@@ -533,11 +558,13 @@ def _divided_backward(model, st, dfeat, G, ready=None):
         ops.cast_rows(dX, dXb, rows)
         if mk is None:
             dXs = dXb
-            _colsum(dX, G, fc2.bias)
         else:
             dXs = torch.empty(rows, C, device=dev, dtype=mode)
             ops.cast_rows(dX, dXs, rows, row_scale=mk.m, group=L)
-            _colsum(dX, G, fc2.bias, row_scale=mk.m_rows)
+        # the bias gradients from the storage-dtype copies (as every other Linear's: the wgrad
+        # kernel's fused column sum), on the weight-gradient stream instead of an fp32 pass over dX
+        # on the dX chain
+        _colsum_side(dXs, G, fc2.bias)
         wgrad(dXb, S.h, G, fc2.weight)
         dpre = torch.empty(rows, fc1.out_features, device=dev, dtype=mode)
         ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
@@ -551,7 +578,7 @@ def _divided_backward(model, st, dfeat, G, ready=None):
         dXb = torch.empty(rows, C, device=dev, dtype=mode)
         ops.cast_rows(dX, dXb, rows)
         wgrad(dXb, S.o_s, G, blk.attn.proj.weight)
-        _colsum(dX, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_rows)
+        _colsum_side(dXb, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_rows)
         do = torch.empty(rows, C, device=dev, dtype=mode)
         ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)
         dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
@@ -755,11 +782,10 @@ def _plain_backward(model, st, dfeat, G, ready=None):
         ops.cast_rows(dX, dXb, rows)
         if mk is None:
             dXs = dXb
-            _colsum(dX, G, fc2.bias)
         else:
             dXs = torch.empty(rows, C, device=dev, dtype=mode)
             ops.cast_rows(dX, dXs, rows, row_scale=mk.m, group=L)
-            _colsum(dX, G, fc2.bias, row_scale=mk.m_rows)
+        _colsum_side(dXs, G, fc2.bias)
         wgrad(dXb, S.h, G, fc2.weight)
         dpre = torch.empty(rows, fc1.out_features, device=dev, dtype=mode)
         ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
@@ -772,7 +798,7 @@ def _plain_backward(model, st, dfeat, G, ready=None):
         dXb = torch.empty(rows, C, device=dev, dtype=mode)
         ops.cast_rows(dX, dXb, rows)
         wgrad(dXb, S.o, G, blk.attn.proj.weight)
-        _colsum(dX, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.a_rows)
+        _colsum_side(dXb, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.a_rows)
         do = torch.empty(rows, C, device=dev, dtype=mode)
         if mk is None:
             ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)

@@ -357,6 +357,11 @@ int dsvt_layernorm_bwd(int dy_dtype, const float *x, const void *dy, const float
                        int64_t rows, int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps,
                        float *dgamma, float *dbeta, int accumulate, void *workspace,
                        int64_t workspace_bytes, void *stream);
+/* dgamma = dbeta = NULL in dsvt_layernorm_bwd: the affine-parameter partial sums stay in its workspace
+ * and this finishes them (fixed order, (+)= into dgamma / dbeta) -- on another stream if the caller
+ * likes (the training backward runs them beside the dX chain), after the dsvt_layernorm_bwd. */
+int dsvt_layernorm_bwd_params(int64_t rows, int64_t C, const void *workspace, int64_t workspace_bytes, float *dgamma,
+                              float *dbeta, int accumulate, void *stream);
 /* bias gradient: out[c] (+)= sum_m row_scale[m] * y[row(m)][c]  (y in dtype, row stride ld;
  * row_scale nullable = 1). */
 int dsvt_colsum_bwd(int dtype, const void *y, int64_t rows, int64_t C, int64_t ld, int64_t rpg,

@@ -20,6 +20,8 @@ if __name__ == "__main__":
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--serial-teacher", dest="concurrent_teacher", action="store_false")
     ap.add_argument("--concurrent-groups", dest="concurrent_groups", action="store_true")
+    ap.add_argument("--no-teacher-train", action="store_true",
+                    help="skip the teacher-train-mode leg (the trace then ends with the timed steps)")
     ap.add_argument("--host-time", action="store_true",
                     help="also report the host-side enqueue time of each step (no sync inside the step)")
     a = ap.parse_args()
