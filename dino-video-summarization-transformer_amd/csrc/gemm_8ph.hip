@@ -57,6 +57,32 @@ __device__ __forceinline__ void p8_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifndef DSVT_8PH_ASM_RD
+#define DSVT_8PH_ASM_RD 1
+#endif
+// Fragment reads as inline-asm ds_read_b128 at an immediate offset (DSVT_8PH_ASM_RD, default):
+// with plain LDS loads the compiler drained every in-flight LDS-DMA stage (s_waitcnt vmcnt(0),
+// two K-tiles of prefetch) at the K-loop head of the residual / GELU-save instantiations.  The
+// asm reads are not tracked: the phase's own counted vmcnt wait + barrier order them after the
+// DMA they read, and p8_tie* (lgkmcnt(0) tied to the fragments) orders their use.
+template <int OFF>
+__device__ __forceinline__ sv8 p8_rd(unsigned a) {
+  sv8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+__device__ __forceinline__ unsigned p8_lds(const char* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+__device__ __forceinline__ void p8_tie4(sv8 (&f)[2][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0][0]), "+v"(f[0][1]), "+v"(f[1][0]), "+v"(f[1][1]));
+}
+__device__ __forceinline__ void p8_tie8(sv8 (&f)[4][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(f[0][0]), "+v"(f[0][1]), "+v"(f[1][0]), "+v"(f[1][1]), "+v"(f[2][0]), "+v"(f[2][1]),
+                 "+v"(f[3][0]), "+v"(f[3][1]));
+}
+
 }  // namespace
 
 // ABL (diagnostic builds, benchmarking only; 0 = normal): bit 0 no wave-row stagger, bit 1 no
@@ -161,12 +187,31 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
   const int rdA = (wr * 64 + r16) * P8_ROWB, rdB = (wc * 32 + r16) * P8_ROWB;
   const int cs0 = (g ^ xs) << 4, cs1 = ((4 + g) ^ xs) << 4;
   sv8 fa[4][2], fbl[2][2], fbr[2][2];
+#if DSVT_8PH_ASM_RD
+#define P8_RD(DST, H, BASE, CB, N)                                                                     \
+  {                                                                                                    \
+    const unsigned b_ = p8_lds(smem + (CB) + (BASE)), a0_ = b_ + cs0, a1_ = b_ + cs1;                  \
+    DST[0][0] = p8_rd<(H) * P8_HALF>(a0_);                                                             \
+    DST[0][1] = p8_rd<(H) * P8_HALF>(a1_);                                                             \
+    DST[1][0] = p8_rd<(H) * P8_HALF + 16 * P8_ROWB>(a0_);                                              \
+    DST[1][1] = p8_rd<(H) * P8_HALF + 16 * P8_ROWB>(a1_);                                              \
+    if constexpr ((N) == 4) {                                                                          \
+      DST[(N) - 2][0] = p8_rd<(H) * P8_HALF + 32 * P8_ROWB>(a0_);                                      \
+      DST[(N) - 2][1] = p8_rd<(H) * P8_HALF + 32 * P8_ROWB>(a1_);                                      \
+      DST[(N) - 1][0] = p8_rd<(H) * P8_HALF + 48 * P8_ROWB>(a0_);                                      \
+      DST[(N) - 1][1] = p8_rd<(H) * P8_HALF + 48 * P8_ROWB>(a1_);                                      \
+    }                                                                                                  \
+  }
+#define P8_TIE(STMT) STMT
+#else
 #define P8_RD(DST, H, BASE, CB, N)                                                                     \
   _Pragma("unroll") for (int f_ = 0; f_ < (N); ++f_) {                                                \
     const char* s_ = smem + (CB) + (H) * P8_HALF + (BASE) + f_ * 16 * P8_ROWB;                        \
     DST[f_][0] = *reinterpret_cast<const sv8*>(s_ + cs0);                                             \
     DST[f_][1] = *reinterpret_cast<const sv8*>(s_ + cs1);                                             \
   }
+#define P8_TIE(STMT)
+#endif
 #define P8_MFMA(I0, J0, FB)                                                                            \
   {                                                                                                    \
     if (!(ABL & 8)) __builtin_amdgcn_s_setprio(1);                                                     \
@@ -191,10 +236,11 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     else if (S_EPI > 0 && post) vm_wait<8 + S_EPI>();      \
     else vm_wait<8>();                                     \
   }
-#define P8_COMPUTE(MFMA_STMT)                              \
+#define P8_COMPUTE(MFMA_STMT, TIE)                         \
   {                                                        \
     p8_barrier();                                          \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
+    TIE;                                                   \
     __builtin_amdgcn_sched_barrier(0);                     \
     MFMA_STMT;                                             \
     p8_barrier();                                          \
@@ -269,21 +315,21 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
     P8_RD(fa, H_AT, rdA, cb, 4);
     if (v1) P8_STAGE(H_BR, oBR, W, sb1, kb1);
     P8_WAIT(v1);
-    P8_COMPUTE(P8_MFMA(0, 0, fbl));
+    P8_COMPUTE(P8_MFMA(0, 0, fbl), P8_TIE((p8_tie4(fbl), p8_tie8(fa))));
     // phase 1: read BR, stage AB(j+1), quadrant (AT, BR)
     P8_RD(fbr, H_BR, rdB, cb, 2);
     if (v1) P8_STAGE(H_AB, oAB, A, sb1, kb1);
     P8_WAIT(v1);
-    P8_COMPUTE(P8_MFMA(0, 2, fbr));
+    P8_COMPUTE(P8_MFMA(0, 2, fbr), P8_TIE(p8_tie4(fbr)));
     // phase 2: read AB, stage AT(j+2), quadrant (AB, BR)
     P8_RD(fa, H_AB, rdA, cb, 4);
     if (v2) P8_STAGE(H_AT, oAT, A, sb2, kb2);
     P8_WAIT(v2);
-    P8_COMPUTE(P8_MFMA(4, 2, fbr));
+    P8_COMPUTE(P8_MFMA(4, 2, fbr), P8_TIE(p8_tie8(fa)));
     // phase 3: no reads, stage BL(j+2), quadrant (AB, BL)
     if (v2) P8_STAGE(H_BL, oBL, W, sb2, kb2);
     P8_WAIT(v2);
-    P8_COMPUTE(P8_MFMA(4, 0, fbl));
+    P8_COMPUTE(P8_MFMA(4, 0, fbl), );
 
     post = false;
     if (++kc == nk) {                     // tile done: register epilogue
@@ -322,6 +368,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmParams p) {
 #undef P8_MFMA
 #undef P8_WAIT
 #undef P8_COMPUTE
+#undef P8_TIE
 }
 
 // K a multiple of 64, 32-bit LDS-DMA source offsets, no patch-embed epilogue.  (The GELU

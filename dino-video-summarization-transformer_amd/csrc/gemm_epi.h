@@ -33,6 +33,45 @@ __device__ __forceinline__ void store_pair_bf16(bf16_t* span, fv4 a, fv4 b, int 
   }
 }
 
+// The DropPath row scales of a wave's `rows` output rows from [rbase, rbase + rows): with at least
+// that many rows per scale group (every training shape: a clip's 1 + N*T tokens), the span covers
+// at most two groups, whose two scales come from SCALAR loads (lgkmcnt, inline asm) -- a per-lane
+// vector load of the scale in the epilogue left a VMEM load pending on the path back to the K
+// loop's head, and the compiler then drained every in-flight LDS-DMA stage there (s_waitcnt
+// vmcnt(0)) on every K step.  Rows past M take row M - 1's scale (the clamped rows rewrite it).
+__device__ __forceinline__ float sload_f32(const float* base, uint32_t idx) {
+  const uint64_t a = (uint64_t)(uintptr_t)(base + idx);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const uint64_t u = ((uint64_t)hi << 32) | lo;
+  float v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
+  return v;
+}
+
+struct WaveRowScale {
+  float s0 = 1.0f, s1 = 1.0f;
+  int64_t bound = 0;                   // rows < bound take s0
+  bool on = false, vec = false;
+  __device__ __forceinline__ WaveRowScale(const GemmParams& p, int64_t rbase, int rows, bool use) {
+    if (!use || p.row_scale == nullptr) return;
+    on = true;
+    const int64_t grp = p.rs_group;
+    if (grp < rows) { vec = true; return; }
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rbase < p.M ? rbase : p.M - 1));
+    const uint32_t rl = (uint32_t)(rbase + rows - 1 < p.M ? rbase + rows - 1 : p.M - 1);
+    const uint32_t c0 = r0 / (uint32_t)grp, c1 = __builtin_amdgcn_readfirstlane(rl) / (uint32_t)grp;
+    s0 = sload_f32(p.row_scale, c0);
+    s1 = sload_f32(p.row_scale, c1);
+    bound = (int64_t)(c0 + 1) * grp;
+  }
+  __device__ __forceinline__ float at(const GemmParams& p, int64_t m) const {
+    if (!on) return 1.0f;
+    m = m < p.M ? m : p.M - 1;
+    if (vec) return p.row_scale[(uint32_t)m / (uint32_t)p.rs_group];
+    return m < bound ? s0 : s1;
+  }
+};
+
 // Direct (register) epilogue shared by the big and persistent kernels.
 // BIAS_IN_ACC: the accumulators started from the bias (gemm_8ph.hip), none is added here.
 // NOFAST: skip the full-tile 16-byte pair-store path (its cross-lane packing keeps more values
@@ -48,18 +87,16 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
   constexpr bool RS = ROWSCALE && (EPI == EPI_BIAS || EPI == EPI_GELU_SAVE);
-  float rsc[RS ? MI : 1];
   const bool scaled = RS && p.row_scale != nullptr;          // workgroup-uniform
-  if constexpr (RS) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i) rsc[i] = scaled ? row_scale_of(p, rbase + i * 16 + r16) : 1.0f;
-  }
+  const bool rres = EPI == EPI_RESID && p.row_scale != nullptr;   // workgroup-uniform
+  // (evaluated where each path uses it: a scale loaded up front but unused on the path taken
+  // stays a pending load at the K-loop head, see WaveRowScale)
+  const WaveRowScale wrs(p, rbase, MI * 16, RS || rres);
   // bias: scalar loads for a full 64-column wave slab (no vmcnt wait behind the in-flight
   // prefetch of the next tile); per-lane vector loads only at a ragged N edge
   float4 bias4[NJ];
   // EPI_RESID with DropPath row scales (training): the bias is NOT in the accumulators (the
-  // kernel leaves it out), it is added here as s[m] * bias like the 128x128 kernel does
-  const bool rres = EPI == EPI_RESID && p.row_scale != nullptr;   // workgroup-uniform
+  // kernel leaves it out), it is added here as s[m] * bias like the 128x128 kernel does (rres)
   if (BIAS_IN_ACC && !rres) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) bias4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -74,6 +111,11 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
       const int64_t n = cbase + j * 16 + 4 * g;
       bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // consumed here, on this (ragged-N) path: the per-lane bounds branches below may skip every
+    // use, and a load left pending on the way back to the K loop makes the compiler drain the
+    // in-flight LDS-DMA stages at its head on every K step (see WaveRowScale)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
   }
   // training epilogues (bf16 aux operand): GELU with the pre-activation saved, and GELU backward
   // PAIR_AUX (the 256x256 kernel; the persistent 256x128 one spills with it), bf16 output, full
@@ -108,7 +150,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         float rs = 1.0f;
-        if constexpr (RS) rs = scaled ? row_scale_of(p, rbase + i * 16 + r16 < p.M ? rbase + i * 16 + r16 : p.M - 1) : 1.0f;
+        if constexpr (RS) rs = wrs.at(p, rbase + i * 16 + r16);
 #pragma unroll
         for (int jp = 0; jp < NJ / 2; ++jp) {
           const int j = 2 * jp;
@@ -177,7 +219,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           for (int j = 0; j < NJ; ++j) load4((const bf16_t*)p.aux + orow * p.ld_aux + cbase + j * 16 + 4 * g, pre[j]);
         }
         float rs = 1.0f;
-        if constexpr (RS) rs = scaled ? row_scale_of(p, m) : 1.0f;
+        if constexpr (RS) rs = wrs.at(p, m);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int64_t n = cbase + j * 16 + 4 * g;
@@ -225,7 +267,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           store4((bf16_t*)p.aux + orow * p.ld_aux + n, gp[0], gp[1], gp[2], gp[3]);
           if constexpr (RS) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] *= rsc[i];
+            for (int e = 0; e < 4; ++e) v[e] *= wrs.at(p, m);
           }
         } else {
           float pre[4];
@@ -258,7 +300,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
           if constexpr (RS) {
             if (scaled && EPI != EPI_GELU) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[i][j][e] *= rsc[i];
+              for (int e = 0; e < 4; ++e) acc[i][j][e] *= wrs.at(p, m);
             }
           }
         }
@@ -346,7 +388,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
         float rs2[2] = {1.0f, 1.0f};
         if (rres) {
 #pragma unroll
-          for (int ii = 0; ii < 2; ++ii) rs2[ii] = row_scale_of(p, rbase + (i + ii) * 16 + r16);
+          for (int ii = 0; ii < 2; ++ii) rs2[ii] = wrs.at(p, rbase + (i + ii) * 16 + r16);
         }
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
@@ -366,7 +408,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int64_t m = rbase + i * 16 + r16;
-    const float rsr = rres ? row_scale_of(p, m) : 1.0f;
+    const float rsr = rres ? wrs.at(p, m) : 1.0f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       float4 bb = bias4[j];
@@ -378,7 +420,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
       }
       if constexpr (RS) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] *= rsc[i];
+        for (int e = 0; e < 4; ++e) acc[i][j][e] *= wrs.at(p, m);
       }
     }
     if (m >= p.M) continue;

@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../dino-video-summarization-transformer_amd/csrc"
 make -s
 FLAGS="$1"
-mkdir -p build/ab ../../tools/ab_lib
+rm -rf build/ab; mkdir -p build/ab ../../tools/ab_lib   # no stale objects of an earlier A/B
 for f in ${AB_SRCS:-gemm gemm_big gemm_8ph gemm_192}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS -c $f.hip -o build/ab/$f.o
 done
