@@ -94,7 +94,14 @@ struct WgradParams {
 // ABL (diagnostic builds, tools/wgrad_bench.py only; 0 = normal): bit 0 no loads after the
 // prologue (stale stages), bit 1 no MFMA (fragments kept live), bit 2 no fragment reads.
 // (Measured and dropped: staggering the two wave rows a barrier apart, 2 barriers per stage,
-// -4 %; staging X through registers beside the LDS-DMA of dY, -6 %.)
+// -4 %; staging X through registers beside the LDS-DMA of dY, -6 %; r05, after the asm reads:
+// each stage in two k-halves, the second half's reads in flight under the first half's MFMAs
+// (lgkmcnt(8) / lgkmcnt(0)): qkv 127.4 vs 124.2 us, train step 134.8 / 135.0 vs 135.0 / 134.7;
+// the gemm_8ph schedule -- two phases per stage, reads -> barrier -> 16 MFMA -> barrier, wave row
+// 1 one barrier behind, the stage DMA in phase 1: qkv 140.4 vs 125.0 us, train 132.1 / 131.7 vs
+// 134.6 / 134.8.  Alone the kernel runs ~0.45 of its MFMA time (PMC: MFMA busy 0.33 of the
+// chip's SIMD cycles at 216 of 256 CUs, LDS array 15 % busy, 0 bank conflicts, 43 % of wave
+// cycles in s_waitcnt); tools/pmc_wgrad.sh.)
 template <int ABL = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[WG_NST * WG_STAGE];
