@@ -261,6 +261,184 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WgradParams p) {
   }
 }
 
+// Two workgroups per CU (DSVT_WGRAD_HALF): a 128 (k) x 256 (n) output tile per 256-thread
+// workgroup -- 4 waves, each the same 128 x 64 block and fragment code as above, all on k rows
+// 0..127 -- with a 3-stage ring of 24 KiB stages (X rows of 256 B, dY rows of 512 B), 72 KiB per
+// workgroup.  The two workgroups of a CU synchronize only themselves, so one's fragment reads and
+// loads run under the other's MFMAs instead of all eight waves of the 256 x 256 tile reading,
+// then computing, between one barrier and the next.  1.5x the L2 -> LDS bytes per FLOP, which
+// costs more than the overlap buys on the full-chip grids (qkv 133.4 vs 127.4 us, fc2 145.7 vs
+// 137.8; train step 136.0 / 135.8 vs 137.1 / 137.8 with it everywhere) but not on the 768 x 768
+// weights, whose 9 tiles x 8 slices hold 72 CUs: proj 90.8 vs 105.6 us.  Default (2): there only.
+namespace {
+constexpr int WH_K = 128, WH_N = 256;       // tile: k x n
+constexpr int WH_XROWB = 256;               // bytes per staged X row (128 bf16)
+constexpr int WH_XOP = WG_BM * WH_XROWB;    // 8 KiB
+constexpr int WH_YOP = WG_BM * WG_ROWB;     // 16 KiB
+constexpr int WH_STAGE = WH_YOP + WH_XOP;   // [dY | X] 24 KiB
+constexpr int WH_NST = 3;
+
+__device__ __forceinline__ int wh_xoff(int row, int c) {      // 256-B rows, 16 chunks, same XOR
+  return row * WH_XROWB + ((((c >> 3) ^ ((row & 7) << 1))) << 4) + ((c & 7) << 1);
+}
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void wgrad_half_kernel(WgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[WH_NST * WH_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int wn = wave;                          // the wave's n columns wn*64 ..
+  const int tiles = p.tilesN * p.tilesK;
+  const int per_x = (int)(gridDim.x >> 3);
+  const int t = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+  if (t >= tiles * p.S) return;
+  const int sl = t / tiles, tile = t - sl * tiles;
+  const int64_t n0 = (int64_t)(tile / p.tilesK) * WH_N, k0 = (int64_t)(tile % p.tilesK) * WH_K;
+  const int64_t steps = (p.M + WG_BM - 1) / WG_BM;
+  const int64_t s_begin = sl * steps / p.S, s_end = (sl + 1) * steps / p.S;
+  const int nst = (int)(s_end - s_begin);
+
+  // DMA roles: dY -- 4 wave-instructions of 2 rows x 512 B; X -- 2 of 4 rows x 256 B
+  int yrow[4], xrow[2];
+  int64_t cy[4], cx[2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    yrow[q] = (wave * 4 + q) * 2 + (lane >> 5);
+    const int lc = (lane & 31) ^ ((yrow[q] & 7) << 1);
+    const int64_t cn = n0 + lc * 8;
+    cy[q] = cn < p.N ? cn : p.N - 8;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    xrow[q] = (wave * 2 + q) * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ ((xrow[q] & 7) << 1);
+    const int64_t ck = k0 + lc * 8;
+    cx[q] = ck < p.K ? ck : p.K - 8;
+  }
+  auto stage = [&](int buf, int64_t step) {
+    const int64_t m0 = step * WG_BM;
+    char* base = smem + buf * WH_STAGE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int64_t m = m0 + yrow[q];
+      m = m < p.M ? m : p.M - 1;                               // clamped; zeroed in registers
+      __builtin_amdgcn_global_load_lds((const void*)(p.dy + m * p.ldy + cy[q]),
+                                       LDS_PTR(base + (wave * 4 + q) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      int64_t m = m0 + xrow[q];
+      m = m < p.M ? m : p.M - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(p.x + m * p.ldx + cx[q]),
+                                       LDS_PTR(base + WH_YOP + (wave * 2 + q) * 1024), 16, 0, 0);
+    }
+  };
+
+  fv4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+  const bool do_cs = p.db != nullptr && k0 == 0;               // workgroup-uniform
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf2_t ones = {(__bf16)1.0f, (__bf16)1.0f};
+
+  for (int i = 0; i < WH_NST - 1 && i < nst; ++i) stage(i, s_begin + i);
+  const int ra = 4 * g + (r16 >> 2), rb = ra + 16, cq = 4 * (r16 & 3);
+  int buf = 0;
+  for (int it = 0; it < nst; ++it) {
+    if (it + 1 < nst) wg_vm_wait<6>();                         // stage it+1 may stay in flight
+    else wg_vm_wait<0>();
+    wg_barrier();                 // stage `it` landed for every wave; stage it-1 read by every wave
+    if (it + WH_NST - 1 < nst) {
+      const int nb = buf == 0 ? WH_NST - 1 : buf - 1;           // (it + 2) % 3
+      stage(nb, s_begin + it + WH_NST - 1);
+    }
+    const char* ty = smem + buf * WH_STAGE;
+    const char* tx = ty + WH_YOP;
+    buf = buf == WH_NST - 1 ? 0 : buf + 1;
+    sv4 hb[8], ha[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = wn * 64 + j * 16 + cq;
+      hb[2 * j] = wg_tr_read(ty + wg_off(ra, c));
+      hb[2 * j + 1] = wg_tr_read(ty + wg_off(rb, c));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = i * 16 + cq;
+      ha[2 * i] = wg_tr_read(tx + wh_xoff(ra, c));
+      ha[2 * i + 1] = wg_tr_read(tx + wh_xoff(rb, c));
+    }
+    wg_lgkm_wait(hb, ha);
+    sv8 fb[4], fa[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = __builtin_shufflevector(hb[2 * j], hb[2 * j + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = __builtin_shufflevector(ha[2 * i], ha[2 * i + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+    const int64_t m0 = (s_begin + it) * WG_BM;
+    if (m0 + WG_BM > p.M) {                                   // last stage: dY rows past M -> 0
+      const int valid = (int)(p.M - m0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int row = (e < 4 ? 4 * g + e : 16 + 4 * g + e - 4);
+          if (row >= valid) fb[j][e] = 0;
+        }
+    }
+    if (do_cs) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 u = __builtin_bit_cast(uint4, fb[j]);
+        float s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.x), ones, cs[j], false);
+        s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.y), ones, s, false);
+        s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.z), ones, s, false);
+        cs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.w), ones, s, false);
+      }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  mfma_result_fence();
+  const bool direct = p.S == 1;
+  float* out = p.out + (direct ? 0 : (int64_t)sl * p.N * p.K);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = n0 + wn * 64 + j * 16 + r16;
+    if (n >= p.N) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t k = k0 + i * 16 + 4 * g;
+      if (k >= p.K) continue;
+      float4* o = reinterpret_cast<float4*>(out + n * p.K + k);
+      const fv4 a = acc[i][j];
+      if (direct && p.accumulate) {
+        const float4 old = *o;
+        *o = make_float4(old.x + a[0], old.y + a[1], old.z + a[2], old.w + a[3]);
+      } else {
+        *o = make_float4(a[0], a[1], a[2], a[3]);
+      }
+    }
+  }
+  if (do_cs) {
+    float* dbo = p.db + (direct ? 0 : (int64_t)sl * p.N);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = cs[j];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int64_t n = n0 + wn * 64 + j * 16 + r16;
+      if (g == 0 && n < p.N) dbo[n] = (direct && p.accumulate) ? dbo[n] + v : v;
+    }
+  }
+}
+
 // dst (+)= sum over the S slices of the partials, in slice order (float4 per thread); the
 // workgroups past `gblocks` do the same for the bias partials (one launch for both)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int64_t S, int64_t n4,
@@ -306,12 +484,24 @@ int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K) {
 hipError_t launch_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* G, float* db, int64_t M,
                         int64_t N, int64_t K, int accumulate, float* partial, hipStream_t s) {
   const int64_t S = wgrad_slices(M, N, K);
-  const int tilesN = (int)((N + WG_T - 1) / WG_T), tilesK = (int)((K + WG_T - 1) / WG_T);
   float* dbp = db == nullptr ? nullptr : (S > 1 ? partial + S * N * K : db);
+  static const int abl = getenv("DSVT_WGRAD_ABL") ? atoi(getenv("DSVT_WGRAD_ABL")) : 0;   // diagnostics only
+#ifndef DSVT_WGRAD_HALF
+#define DSVT_WGRAD_HALF 2   // A/B (train step, 3 interleaved rounds): 138.0 / 137.9 / 138.2 vs 137.4 / 136.8 / 136.7
+#endif
+  static const int half = getenv("DSVT_WGRAD_HALF") ? atoi(getenv("DSVT_WGRAD_HALF")) : DSVT_WGRAD_HALF;
+  // 2: only where the 256 x 256 grid holds fewer than half the CUs (the 768 x 768 weights: 9 tiles)
+  const int64_t tiles256 = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
+  if (abl == 0 && (half == 1 || (half == 2 && tiles256 * S < 128))) {
+    const int tilesN = (int)((N + WH_N - 1) / WH_N), tilesK = (int)((K + WH_K - 1) / WH_K);
+    WgradParams p{dy, ldy, x, ldx, S > 1 ? partial : G, dbp, M, N, K, (int)S, tilesN, tilesK, accumulate};
+    const int64_t total = (int64_t)tilesN * tilesK * S;
+    wgrad_half_kernel<<<dim3((unsigned)((total + 7) / 8 * 8)), 256, 0, s>>>(p);
+  } else {
+  const int tilesN = (int)((N + WG_T - 1) / WG_T), tilesK = (int)((K + WG_T - 1) / WG_T);
   WgradParams p{dy, ldy, x, ldx, S > 1 ? partial : G, dbp, M, N, K, (int)S, tilesN, tilesK, accumulate};
   const int64_t total = (int64_t)tilesN * tilesK * S;
   const dim3 grid((unsigned)((total + 7) / 8 * 8));
-  static const int abl = getenv("DSVT_WGRAD_ABL") ? atoi(getenv("DSVT_WGRAD_ABL")) : 0;   // diagnostics only
   switch (abl) {
     case 1: wgrad_kernel<1><<<grid, 512, 0, s>>>(p); break;
     case 2: wgrad_kernel<2><<<grid, 512, 0, s>>>(p); break;
@@ -319,6 +509,7 @@ hipError_t launch_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t 
     case 4: wgrad_kernel<4><<<grid, 512, 0, s>>>(p); break;
     case 6: wgrad_kernel<6><<<grid, 512, 0, s>>>(p); break;
     default: wgrad_kernel<0><<<grid, 512, 0, s>>>(p); break;
+  }
   }
   if (S > 1) {
     const int64_t n4 = N * K / 4, d4 = db ? N / 4 : 0;
