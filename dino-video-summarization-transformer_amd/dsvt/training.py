@@ -246,10 +246,31 @@ class BackboneFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, groups, *params):
         feats, states = [], []
-        for srcs, B, T, H, W, Cin in groups:      # in order: the DropPath masks are drawn per group
-            f, st = _backbone_forward(model, srcs, B, T, H, W, Cin)
+        dev = groups[0][0][0][0].device
+        # the groups' forwards on concurrent streams (group 0 on the current one, the rest on one
+        # side stream), like the inference path's backbone calls: one group's partly-filled last
+        # wave of GEMM tiles runs beside the other's.  The host still enqueues the groups in order,
+        # so the DropPath draws -- and the results -- are those of the sequential forward; the
+        # backward stays on the current stream (the saved activations were joined below).
+        fork = len(groups) > 1 and dev.type == "cuda" and _FWD_FORK
+        if fork:
+            from .utils import side_stream, stream_slot
+            _refresh_forward_weights(model)       # the bf16 weight copies, before the fork
+            cur = torch.cuda.current_stream(dev)
+            side = side_stream(dev, ("train_fwd_group", stream_slot(dev)))
+            side.wait_stream(cur)
+        for gi, (srcs, B, T, H, W, Cin) in enumerate(groups):   # in order: DropPath masks per group
+            if fork and gi > 0:
+                with torch.cuda.stream(side):
+                    f, st = _backbone_forward(model, srcs, B, T, H, W, Cin)
+            else:
+                f, st = _backbone_forward(model, srcs, B, T, H, W, Cin)
             feats.append(f)
             states.append(st)
+        if fork:
+            cur.wait_stream(side)
+            for f in feats[1:]:
+                f.record_stream(cur)
         ctx.model, ctx.states, ctx.params = model, states, params
         ctx.rows = [f.shape[0] for f in feats]
         return feats[0] if len(feats) == 1 else torch.cat(feats)
@@ -327,6 +348,18 @@ def backbone_forward_nosave(model, srcs, B, T, H, W, Cin):
     defect 2) and runs under torch.no_grad() (:527), so nothing is ever differentiated."""
     feats, _ = _backbone_forward(model, srcs, B, T, H, W, Cin, save=False)
     return feats
+
+
+# the training forward's resolution groups on concurrent streams (1) or one after the other (0)
+_FWD_FORK = os.environ.get("DSVT_TRAIN_FWD_FORK", "1") != "0"
+
+
+def _refresh_forward_weights(model):
+    """The storage-dtype weight copies the training forward multiplies by (what
+    _backbone_forward / _plain_forward refresh first)."""
+    ws = _block_weights(model) if model.attention_type == 'divided_space_time' else _plain_weights(model)
+    model._wcache.refresh(ws + [model.patch_embed.proj.weight], model.dsvt_dtype,
+                          flat={id(model.patch_embed.proj.weight)})
 
 
 def _backbone_forward(model, srcs, B, T, H, W, Cin, save=True):
