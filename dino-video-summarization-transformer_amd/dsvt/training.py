@@ -83,13 +83,15 @@ class _Grads:
         if self.side is None:
             fn()
             return
+        cur = torch.cuda.current_stream(self.side.device)   # the stream that produced the inputs
         if self._main is None:
-            self._main = torch.cuda.current_stream(self.side.device)
-        self.side.wait_stream(self._main)
+            self._main = cur
+        self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
             fn()
         for t in inputs:
-            t.record_stream(self.side)
+            if t is not None:
+                t.record_stream(self.side)
 
     def join(self):
         """The current stream waits for every side-stream product (before the grads are used)."""
@@ -289,6 +291,12 @@ class BackboneFn(torch.autograd.Function):
         G = _Grads(side=_wgrad_stream(dfeat.device) if getattr(model, "dsvt_wgrad_stream", True) else None,
                    arena=arena, seeded=seeded, persistent=persist)
         offs = np.cumsum([0] + ctx.rows)
+        if (_BWD_FORK and red is None and G.side is not None and _SIDE_PARAMS and len(ctx.states) == 2
+                and model.attention_type == 'divided_space_time' and dfeat.is_cuda):
+            _backward_two_groups(model, ctx.states, [dfeat[offs[i]:offs[i + 1]] for i in range(2)], G)
+            ctx.states = [None, None]
+            G.join()
+            return tuple([None, None] + G.deliver(ctx.params))
         for i in reversed(range(len(ctx.states))):
             # a block's gradients are final after the last group's pass over it: its bucket's
             # all-reduce starts then, under the backward of the blocks below
@@ -300,6 +308,49 @@ class BackboneFn(torch.autograd.Function):
             red.take_seeded()          # the reduced arena views replace the local no_sync sums
         G.join()
         return tuple([None, None] + G.deliver(ctx.params))
+
+
+# the two resolution groups' backward dX chains on concurrent streams, block by block (1), or
+# one group after the other (0, the default: 140.0 / 140.6 vs 133.9 / 134.0 clips/s with the
+# interleave -- three streams of GEMMs beside the weight-gradient stream lose more to contention
+# than the chains' tails leave idle; the forward's fork, with no third stream, wins 2.5 %)
+_BWD_FORK = os.environ.get("DSVT_TRAIN_BWD_FORK", "0") != "0"
+
+
+def _backward_two_groups(model, states, dfeats, G):
+    """Group 1's backward on the side stream its forward ran on, group 0's on the current
+    stream, advanced block by block in turn (host order: group 0's block, then group 1's), so
+    each chain's GEMM tails and small kernels run beside the other's and both feed the one
+    weight-gradient stream in a fixed order.  Every parameter-gradient write goes through that
+    stream (the weight / bias products, the LayerNorm-parameter reductions, the embedding sums),
+    so nothing accumulates into a shared buffer from two streams."""
+    from .utils import side_stream, stream_slot
+    dev = dfeats[0].device
+    cur = torch.cuda.current_stream(dev)
+    side = side_stream(dev, ("train_fwd_group", stream_slot(dev)))
+    G._main = cur
+    if not _FWD_FORK:
+        # group 1's saved activations were allocated on the current stream: mark their use on the
+        # side stream, or the allocator could hand their memory out again while it still reads them
+        for obj in [states[1]] + list(states[1].blocks) + [m for m in states[1].masks if m is not None]:
+            for t in vars(obj).values():
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(side)
+        for _, _, a in states[1].im2col:
+            a.record_stream(side)
+    g0 = _divided_backward_steps(model, states[0], dfeats[0], G)
+    g1 = _divided_backward_steps(model, states[1], dfeats[1], G)
+    live0 = next(g0, None) is not None               # the W^T refresh happens in this first step
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        live1 = next(g1, None) is not None
+    while live0 or live1:
+        if live0:
+            live0 = next(g0, None) is not None
+        if live1:
+            with torch.cuda.stream(side):
+                live1 = next(g1, None) is not None
+    cur.wait_stream(side)
 
 
 def _block_weights(model):
@@ -518,11 +569,10 @@ def _tail_backward(blk, S, mk, dXc, wt, G, B, T, L, C, rows, mode, dev):
     ops.cast_rows(dXc, dXb, B)
     if mk is None:
         dXs = dXb
-        _colsum(dXc, G, fc2.bias)
     else:
         dXs = torch.empty(B, C, device=dev, dtype=mode)
         ops.cast_rows(dXc, dXs, B, row_scale=mk.m, group=1)
-        _colsum(dXc, G, fc2.bias, row_scale=mk.m)
+    _colsum_side(dXs, G, fc2.bias)           # (dXc itself is updated below: the fresh copies)
     wgrad(dXb, S.h, G, fc2.weight)
     dpre = torch.empty(B, fc1.out_features, device=dev, dtype=mode)
     ops.gemm_aux(dXs, wt(fc2.weight), None, dpre, S.pre, EPI_DGELU)
@@ -533,7 +583,7 @@ def _tail_backward(blk, S, mk, dXc, wt, G, B, T, L, C, rows, mode, dev):
     dXb = torch.empty(B, C, device=dev, dtype=mode)            # fresh: the fc2 wgrad may still read the last
     ops.cast_rows(dXc, dXb, B)
     wgrad(dXb, S.o_cls, G, blk.attn.proj.weight)
-    _colsum(dXc, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_cls)
+    _colsum_side(dXb, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_cls)
     do = torch.empty(B, C, device=dev, dtype=mode)
     ops.gemm(dXb, wt(blk.attn.proj.weight), None, do)
     dqkv = torch.empty(rows, 3 * C, device=dev, dtype=mode)
@@ -559,6 +609,16 @@ def _divided_backward(model, st, dfeat, G, ready=None):
     optimizer step: G runs them on a second stream, overlapping the dX chain (GEMM tails,
     LayerNorm and attention backward, casts, the split-K reductions).  `ready(k)` is called when
     block k's gradients are complete (k = depth: the embeddings and the final norm)."""
+    for _ in _divided_backward_steps(model, st, dfeat, G, ready):
+        pass
+    return G
+
+
+def _divided_backward_steps(model, st, dfeat, G, ready=None):
+    """_divided_backward as a generator that yields after every block (and after the
+    embeddings): BackboneFn.backward interleaves two resolution groups' dX chains this way, each
+    on its own stream, their weight-gradient products enqueued block by block on the one side
+    stream."""
     mode, B, T, Np, L, C = st.mode, st.B, st.T, st.Np, st.L, st.C
     rows, R = B * L, B * Np * T
     dev = dfeat.device
@@ -584,6 +644,7 @@ def _divided_backward(model, st, dfeat, G, ready=None):
                 setattr(S, k, None)
             if ready is not None:
                 ready(bi)
+            yield bi
             continue
         # ---- MLP
         fc1, fc2 = blk.mlp.fc1, blk.mlp.fc2
@@ -626,11 +687,12 @@ def _divided_backward(model, st, dfeat, G, ready=None):
             setattr(S, k, None)        # free this block's activations as soon as it is done
         if ready is not None:
             ready(bi)
+        yield bi
     # ---- patch embedding + token embeddings (timesformer.py:201-209, 288-323)
     _embed_backward(model, st, dX, G, B, T, Np, L, C, R, mode, dev, patch_map)
     if ready is not None:
         ready(depth)
-    return G
+    yield depth
 
 
 def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map):
@@ -664,6 +726,13 @@ def _embed_backward(model, st, dX, G, B, T, Np, L, C, R, mode, dev, patch_map):
     for row0, nb, a in st.im2col:
         r0 = row0 * Np * T
         wgrad(dP[r0:r0 + nb * Np * T], a, G, conv.weight, view=(C, -1), bias=conv.bias)
+    if _SIDE_PARAMS and G.side is not None:
+        # on the weight-gradient stream like every other parameter gradient: two groups' chains
+        # may run concurrently (BackboneFn.backward), and these sums accumulate into shared tables
+        G.run_side(lambda: ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed),
+                                         G.zeros(model.time_embed), G.zeros(model.cls_token)),
+                   (dX, st.pidx, st.tidx))
+        return
     ops.embed_bwd(dX, B, Np, T, st.pidx, st.tidx, G.zeros(model.pos_embed), G.zeros(model.time_embed),
                   G.zeros(model.cls_token))
 
