@@ -461,10 +461,13 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   const bool big8 = p.M >= 4096 && ((p.M + 255) / 256) * ((p.N + 255) / 256) >= 128;
   if (epi == EPI_RESID && p.row_scale && gv == 20 && gemm_8ph_ok(p, epi)) return 20;
 #ifndef DSVT_RESID_RS
-#define DSVT_RESID_RS 1
+// the training residual GEMMs with DropPath row scales: the 256x256 kernel (20) since r05's
+// K-loop drain fix and the forward's group fork (train step 140.2 / 140.8 vs 139.6 / 139.7 on
+// the 128x128 kernel, 1; neutral before the fork)
+#define DSVT_RESID_RS 20
 #endif
   if (p.row_scale) {            // DropPath row scales: the 128x128 and persistent kernels
-    if (epi == EPI_RESID && DSVT_RESID_RS == 20 && p.M >= 4096 && gemm_8ph_ok(p, epi)) return 20;   // A/B builds
+    if (epi == EPI_RESID && DSVT_RESID_RS == 20 && p.M >= 4096 && gemm_8ph_ok(p, epi)) return 20;
     if (epi == EPI_RESID && DSVT_RESID_RS == 3) return 3;
     return (epi != EPI_RESID && p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
   }
