@@ -250,11 +250,17 @@ __global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const float* __restric
 // being reduced instead of one (x, dy, dx of three rows live, dy kept as packed bf16 until used;
 // 224 VGPRs: 2 blocks per CU, 512 blocks).  Alone 59.1 -> 56.0 us at 25 104 rows (4.6 -> 4.8
 // TB/s), train step +0.3-0.7 % (tools/gpu_s17.sh, gpu_s19.sh).
+// dxb (optional): the updated dx rows also stored as bf16 -- the copy the next GEMMs of the dX chain
+// read -- at row (r / og) * (og - osk) + r % og - osk of dxb for the rows with r % og >= osk (og
+// = rows, osk = 0: the same rows; og = L, osk = 1: the patch rows of [B, L] token rows, compact),
+// instead of a cast_rows pass re-reading dx.
 template <typename DyT>
 __global__ __launch_bounds__(256, 2) void ln_bwd768_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
                                                         const float* __restrict__ gamma, float* __restrict__ dx,
                                                         int64_t rows, int64_t rpg, int64_t gstride, int64_t goff,
-                                                        float eps, float* __restrict__ partial) {
+                                                        float eps, float* __restrict__ partial,
+                                                        bf16_t* __restrict__ dxb = nullptr, int64_t og = 1,
+                                                        int64_t osk = 0) {
   constexpr int C = 768, NK = 12;
   constexpr bool BF = std::is_same<DyT, bf16_t>::value;
   constexpr int ND = BF ? 6 : 12;                 // dy registers per row (packed bf16 pairs / fp32)
@@ -318,6 +324,9 @@ __global__ __launch_bounds__(256, 2) void ln_bwd768_kernel(const float* __restri
     }
     s1 = wave_sum_dpp(s1) * inv_c;
     s2 = wave_sum_dpp(s2) * inv_c;
+    const int64_t rr = r % og;
+    const bool cp = dxb != nullptr && rr >= osk;                 // wave-uniform
+    bf16_t* const ob = dxb + ((r / og) * (og - osk) + rr - osk) * C;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       float4 o;
@@ -326,6 +335,8 @@ __global__ __launch_bounds__(256, 2) void ln_bwd768_kernel(const float* __restri
       o.z = R.o[4 * i + 2] + rstd * (g[4 * i + 2] * cd[4 * i + 2] - s1 - R.x[4 * i + 2] * s2);
       o.w = R.o[4 * i + 3] + rstd * (g[4 * i + 3] * cd[4 * i + 3] - s1 - R.x[4 * i + 3] * s2);
       *reinterpret_cast<float4*>(dx + xr + i * 256 + lane * 4) = o;
+      if (cp)
+        *reinterpret_cast<uint2*>(ob + i * 256 + lane * 4) = make_uint2(cvt_pk_bf16(o.x, o.y), cvt_pk_bf16(o.z, o.w));
     }
   };
   const int64_t S = (int64_t)gridDim.x * 4;
@@ -370,6 +381,19 @@ int ln_bwd_blocks(int64_t rows) {
   const int64_t cap = lnb_variant() == 2 ? 512 : 768;      // ln_bwd768_kernel: 2 blocks per CU
   int64_t b = (rows + 15) / 16;
   return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+hipError_t launch_ln_bwd_cast(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx,
+                              int64_t rows, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* partial,
+                              void* dxb, int64_t og, int64_t osk, hipStream_t s) {
+  const int nb = ln_bwd_blocks(rows);
+  if (dy_dtype == 0)
+    ln_bwd768_kernel<bf16_t><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, rpg, gstride, goff, eps, partial,
+                                                (bf16_t*)dxb, og, osk);
+  else
+    ln_bwd768_kernel<float><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, rpg, gstride, goff, eps, partial,
+                                               (bf16_t*)dxb, og, osk);
+  return hipGetLastError();
 }
 
 hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,

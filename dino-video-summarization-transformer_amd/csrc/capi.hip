@@ -721,6 +721,33 @@ int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float
                 });
 }
 
+int dsvt_layernorm_bwd_cast(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx, int64_t rows,
+                            int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* dgamma,
+                            float* dbeta, int accumulate, void* dxb, int64_t og, int64_t osk, void* workspace,
+                            int64_t workspace_bytes, void* stream) {
+  REQUIRE(dy_dtype == DSVT_BF16 || dy_dtype == DSVT_F32, "layernorm_bwd_cast: bad dy dtype");
+  REQUIRE(x && dy && gamma && dx && dxb, "layernorm_bwd_cast: null pointer");
+  REQUIRE((dgamma == nullptr) == (dbeta == nullptr), "layernorm_bwd_cast: dgamma and dbeta both or neither");
+  REQUIRE(rows > 0 && C == 768, "layernorm_bwd_cast: C = 768 only");
+  REQUIRE(og >= 1 && osk >= 0 && osk < og, "layernorm_bwd_cast: need 0 <= osk < og");
+  REQUIRE(workspace && workspace_bytes >= dsvt_workspace_bytes(DSVT_WS_LN_BWD, 1, rows, 0, C),
+          "layernorm_bwd_cast: workspace too small");
+  norm_map(rpg, gstride, goff);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const int nb = ln_bwd_blocks(rows);
+  return probed(DSVT_PROBE_NORM, (double)rows * C * (14 + esize(dy_dtype)), s, "dsvt_layernorm_bwd_cast",
+                [&]() -> hipError_t {
+                  hipError_t e;
+                  if ((e = launch_ln_bwd_cast(dy_dtype, x, dy, gamma, dx, rows, rpg, gstride, goff, eps, part,
+                                              dxb, og, osk, s)))
+                    return e;
+                  if (!dgamma) return hipSuccess;
+                  if ((e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s))) return e;
+                  return launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
+                });
+}
+
 int dsvt_layernorm_bwd_params(int64_t rows, int64_t C, const void* workspace, int64_t workspace_bytes, float* dgamma,
                               float* dbeta, int accumulate, void* stream) {
   REQUIRE(dgamma && dbeta && workspace && rows > 0 && C > 0 && C <= 2048, "layernorm_bwd_params: bad args");

@@ -75,6 +75,8 @@ SIGNATURES = {
     "dsvt_layernorm_bwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _p, _i32, _p, _i64,
                                   _p]),
     "dsvt_layernorm_bwd_params": (_i32, [_i64, _i64, _p, _i64, _p, _p, _i32, _p]),
+    "dsvt_layernorm_bwd_cast": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _p, _i32, _p,
+                                       _i64, _i64, _p, _i64, _p]),
     "dsvt_colsum_bwd": (_i32, [_i32, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p, _i32, _p, _i64, _p]),
     "dsvt_attn_temporal_bwd": (_i32, [_i32, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_attn_spatial_bwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p]),

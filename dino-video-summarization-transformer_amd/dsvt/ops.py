@@ -434,15 +434,23 @@ def gemm_rowscale(a, w, bias, out, row_scale, group, aux=None, epilogue=_lib.EPI
     return out
 
 
-def layernorm_bwd(x, dy, gamma, eps, dx, rows, dgamma, dbeta, rowmap=None, accumulate=True):
+def layernorm_bwd(x, dy, gamma, eps, dx, rows, dgamma, dbeta, rowmap=None, accumulate=True, cast_to=None,
+                  cast_map=None):
     """dx[row(m)] += dLN(x[row(m)], dy[m]); dgamma / dbeta (+)= the affine-parameter grads.
     dgamma = dbeta = None: their partial sums are left in the returned workspace for
-    layernorm_bwd_params (returns ws then, else dx)."""
+    layernorm_bwd_params (returns ws then, else dx).  cast_to (bf16, C = 768): the updated rows
+    also stored there through cast_map = (og, osk) (dsvt_layernorm_bwd_cast; default the same rows)."""
     C = x.shape[-1]
     rpg, gs, go = rowmap if rowmap is not None else (0, 0, 0)
     ws = _ws(_lib.WS_LN_BWD, torch.float32, rows, 0, C, x.device)
-    call("dsvt_layernorm_bwd", _dt(dy.dtype), _ptr(x), _ptr(dy), _ptr(gamma), _ptr(dx), rows, C, rpg, gs, go,
-         float(eps), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ptr(ws), ws.numel() * 4, _stream())
+    if cast_to is not None:
+        og, osk = cast_map if cast_map is not None else (rows, 0)
+        call("dsvt_layernorm_bwd_cast", _dt(dy.dtype), _ptr(x), _ptr(dy), _ptr(gamma), _ptr(dx), rows, C, rpg, gs,
+             go, float(eps), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ptr(cast_to), og, osk, _ptr(ws),
+             ws.numel() * 4, _stream())
+    else:
+        call("dsvt_layernorm_bwd", _dt(dy.dtype), _ptr(x), _ptr(dy), _ptr(gamma), _ptr(dx), rows, C, rpg, gs, go,
+             float(eps), _ptr(dgamma), _ptr(dbeta), int(accumulate), _ptr(ws), ws.numel() * 4, _stream())
     return ws if dgamma is None else dx
 
 

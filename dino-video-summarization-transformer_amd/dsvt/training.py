@@ -163,19 +163,29 @@ def _colsum_side(y, G, p, row_scale=None):
                (y,) if row_scale is None else (y, row_scale))
 
 
-def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None):
+# the LayerNorm backward storing the next GEMMs' bf16 dX copy itself (dsvt_layernorm_bwd_cast)
+# instead of a cast pass: off -- 136.2 / 136.7 vs 136.7 / 137.1 clips/s with it (same box)
+_LN_CAST = os.environ.get("DSVT_TRAIN_LN_CAST", "0") != "0"
+
+
+def _ln_bwd(x, dy, ln, dx, rows, G, rowmap=None, cast_to=None, cast_map=None):
     """dx += the LayerNorm input gradient on the current stream (the dX chain); the dgamma / dbeta
     reduction of its per-block partials runs on the weight-gradient stream (nothing on the dX chain
-    waits for it: four small launches per LayerNorm off the critical path)."""
+    waits for it: four small launches per LayerNorm off the critical path).  cast_to: a bf16
+    buffer the kernel also stores the updated rows into (C = 768, identity x map; cast_map as in
+    ops.layernorm_bwd) -- returns True when it did, and the caller's cast pass is not needed."""
     dg, acc = G.acc(ln.weight)
     db, acc2 = G.acc(ln.bias)
     assert acc == acc2
-    if G.side is None or not _SIDE_PARAMS:
-        ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, dg, db, rowmap=rowmap, accumulate=acc)
-        return
-    ws = ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, None, None, rowmap=rowmap, accumulate=acc)
     C = x.shape[-1]
-    G.run_side(lambda: ops.layernorm_bwd_params(ws, rows, C, dg, db, accumulate=acc), (ws,))
+    if not (_LN_CAST and cast_to is not None and cast_to.dtype == torch.bfloat16 and C == 768 and rowmap is None):
+        cast_to = None
+    side = G.side is not None and _SIDE_PARAMS
+    ws = ops.layernorm_bwd(x, dy, ln.weight, ln.eps, dx, rows, None if side else dg, None if side else db,
+                           rowmap=rowmap, accumulate=acc, cast_to=cast_to, cast_map=cast_map)
+    if side:
+        G.run_side(lambda: ops.layernorm_bwd_params(ws, rows, C, dg, db, accumulate=acc), (ws,))
+    return cast_to is not None
 
 
 def _own_grad(p):
@@ -666,11 +676,12 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
         da = torch.empty(rows, C, device=dev, dtype=mode)       # LN input gradient (storage dtype)
         ops.gemm(dpre, wt(fc1.weight), None, da)
         del dpre
-        _ln_bwd(S.X2, da, blk.norm2, dX, rows, G)
         # ---- spatial: a fresh buffer, not dXb again -- the fc2 weight gradient may still be
-        # reading dXb on the side stream (record_stream guards reuse after free, not rewrites)
+        # reading dXb on the side stream (record_stream guards reuse after free, not rewrites);
+        # the LayerNorm backward stores the updated rows into it (no cast pass)
         dXb = torch.empty(rows, C, device=dev, dtype=mode)
-        ops.cast_rows(dX, dXb, rows)
+        if not _ln_bwd(S.X2, da, blk.norm2, dX, rows, G, cast_to=dXb):
+            ops.cast_rows(dX, dXb, rows)
         wgrad(dXb, S.o_s, G, blk.attn.proj.weight)
         _colsum_side(dXb, G, blk.attn.proj.bias, row_scale=None if mk is None else mk.s_rows)
         do = torch.empty(rows, C, device=dev, dtype=mode)
@@ -681,8 +692,10 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
         wgrad(dqkv, S.a_s, G, blk.attn.qkv.weight, bias=blk.attn.qkv.bias)
         ops.gemm(dqkv, wt(blk.attn.qkv.weight), None, da)
         del dqkv, do
-        _ln_bwd(S.X1, da, blk.norm1, dX, rows, G)
-        _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map)
+        dY = torch.empty(R, C, device=dev, dtype=mode)           # the temporal branch's dX rows
+        fused = _ln_bwd(S.X1, da, blk.norm1, dX, rows, G, cast_to=dY, cast_map=(L, 1))
+        _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map,
+                           dY=dY if fused else None)
         for k in list(vars(S)):
             setattr(S, k, None)        # free this block's activations as soon as it is done
         if ready is not None:
@@ -695,12 +708,14 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
     yield depth
 
 
-def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map):
-    """Backward of the temporal branch (patch rows of X only, timesformer.py:127-137): adds into dX."""
+def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map, dY=None):
+    """Backward of the temporal branch (patch rows of X only, timesformer.py:127-137): adds into dX.
+    dY: the patch rows of dX in the storage dtype when the caller's LayerNorm backward stored them."""
     heads = blk.attn.num_heads
     ta = blk.temporal_attn
-    dY = torch.empty(R, C, device=dev, dtype=mode)
-    ops.cast_rows(dX, dY, R, rowmap=patch_map)
+    if dY is None:
+        dY = torch.empty(R, C, device=dev, dtype=mode)
+        ops.cast_rows(dX, dY, R, rowmap=patch_map)
     wgrad(dY, S.u, G, blk.temporal_fc.weight, bias=blk.temporal_fc.bias)
     du = torch.empty(R, C, device=dev, dtype=mode)
     if mk is None:

@@ -362,6 +362,14 @@ int dsvt_layernorm_bwd(int dy_dtype, const float *x, const void *dy, const float
  * likes (the training backward runs them beside the dX chain), after the dsvt_layernorm_bwd. */
 int dsvt_layernorm_bwd_params(int64_t rows, int64_t C, const void *workspace, int64_t workspace_bytes, float *dgamma,
                               float *dbeta, int accumulate, void *stream);
+/* dsvt_layernorm_bwd for C = 768 that also stores each updated dx row as bf16 into dxb [*, 768]
+ * (the copy the next GEMMs of the dX chain read): token row r goes to dxb row
+ * (r / og) * (og - osk) + r % og - osk when r % og >= osk (og = rows, osk = 0: the same rows;
+ * og = L, osk = 1: the patch rows of [B, L] token rows, compact), replacing a cast pass over dx. */
+int dsvt_layernorm_bwd_cast(int dy_dtype, const float *x, const void *dy, const float *gamma, float *dx, int64_t rows,
+                            int64_t C, int64_t rpg, int64_t gstride, int64_t goff, float eps, float *dgamma,
+                            float *dbeta, int accumulate, void *dxb, int64_t og, int64_t osk, void *workspace,
+                            int64_t workspace_bytes, void *stream);
 /* bias gradient: out[c] (+)= sum_m row_scale[m] * y[row(m)][c]  (y in dtype, row stride ld;
  * row_scale nullable = 1). */
 int dsvt_colsum_bwd(int dtype, const void *y, int64_t rows, int64_t C, int64_t ld, int64_t rpg,

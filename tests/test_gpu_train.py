@@ -501,6 +501,38 @@ def test_layernorm_bwd_rowmap_vs_autograd(C, dy_dtype):
     assert rel(dg.cpu(), g32.grad.cpu()) < 1e-4 and rel(db.cpu(), b32.grad.cpu()) < 1e-4
 
 
+@pytest.mark.parametrize("B,L", [(3, 21), (16, 1569), (48, 289)])
+@pytest.mark.parametrize("dy_dtype", [torch.bfloat16, torch.float32])
+def test_layernorm_bwd_cast_matches_cast_pass(B, L, dy_dtype):
+    """dsvt_layernorm_bwd_cast (C = 768): dx and dgamma / dbeta bitwise those of
+    dsvt_layernorm_bwd, and the bf16 copy bitwise a cast_rows pass over the updated dx -- of
+    every row (og = rows, osk = 0) and of the patch rows, compact (og = L, osk = 1: the temporal
+    branch's input), at the train step's global / local shapes and a small ragged one."""
+    from dsvt import ops
+    C, rows = 768, B * L
+    g = torch.Generator(device="cuda").manual_seed(12)
+    X = torch.randn(rows, C, device="cuda", generator=g) * 2 + 0.3
+    gamma = torch.randn(C, device="cuda", generator=g)
+    dy = torch.randn(rows, C, device="cuda", generator=g).to(dy_dtype)
+    dX0 = torch.randn(rows, C, device="cuda", generator=g)
+    dX_ref = dX0.clone()
+    dg_ref, db_ref = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    ops.layernorm_bwd(X, dy, gamma, 1e-6, dX_ref, rows, dg_ref, db_ref)
+    for og, osk, nout in ((rows, 0, rows), (L, 1, B * (L - 1))):
+        dX = dX0.clone()
+        dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        out = torch.full((nout, C), float("nan"), device="cuda").to(torch.bfloat16)
+        ops.layernorm_bwd(X, dy, gamma, 1e-6, dX, rows, dg, db, cast_to=out, cast_map=(og, osk))
+        exp = torch.empty(nout, C, device="cuda", dtype=torch.bfloat16)
+        if osk == 0:
+            ops.cast_rows(dX_ref, exp, rows)
+        else:
+            ops.cast_rows(dX_ref, exp, nout, rowmap=(L - 1, L, 1))
+        torch.cuda.synchronize()
+        assert torch.equal(dX, dX_ref) and torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
+        assert torch.equal(out, exp), (og, osk)
+
+
 @pytest.mark.parametrize("M", [300, 4037, 4613])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
 def test_gelu_save_and_dgelu_epilogues(dtype, tol, M):
