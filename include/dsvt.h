@@ -30,7 +30,8 @@ extern "C" {
 
 /* 2 (r05): dsvt_bn_bwd takes param_sums (SyncBatchNorm's local dgamma / dbeta); DSVT_EPI_GELU_SAVE's
  * aux holds GELU'(pre) (r04; was pre); the r03 grouped / stream-K / add-LN / row-LN GEMM entry points
- * are gone and the variant knobs moved to dsvt_debug.h (r04) */
+ * are gone and the variant knobs moved to dsvt_debug.h (r04).  Added in 2, existing calls unchanged:
+ * dsvt_layernorm_bwd_params / _cast, the Swin training entries. */
 #define DSVT_ABI_VERSION 2
 
 #define DSVT_BF16 0
