@@ -463,12 +463,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // M-slices: tiles x S <= 256 workgroups (one per CU, one round), each slice >= 8 stages, and
 // at most 8 slices: every slice adds an N x K fp32 partial written and re-read, and in the
 // training step these products run on a side stream beside the dX chain, so total traffic
-// counts more than filling the chip (train step: cap 8 > 6, 10, 12, 16 > uncapped (28 for the
-// 768 x 768 weights) > 4 > 2; tools/train_step.py, DSVT_WGRAD_MAXS)
+// counts more than filling the chip (r04 train step: cap 8 > 6, 10, 12, 16 > uncapped (28 for the
+// 768 x 768 weights) > 4 > 2; tools/train_step.py, DSVT_WGRAD_MAXS).  r05, after the kernel's
+// drain fix (interleaved, tools/ab_train.sh): 12 137.5 / 137.6 / 137.6 / 137.5, 16 137.5 / 138.0,
+// 8 136.5 / 136.9, 28 136.8 / 136.5, 6 133.9 / 134.2, 4 123.4 / 123.8 -> 12 (only the 768 x 768
+// weights, 9 tiles, reach it; their grid stays on the two-per-CU kernel, 108 < 128 workgroups)
 int64_t wgrad_slices(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
   const int64_t steps = (M + WG_BM - 1) / WG_BM;
-  static const int64_t max_s = getenv("DSVT_WGRAD_MAXS") ? atoll(getenv("DSVT_WGRAD_MAXS")) : 8;
+  static const int64_t max_s = getenv("DSVT_WGRAD_MAXS") ? atoll(getenv("DSVT_WGRAD_MAXS")) : 12;
   int64_t S = 256 / tiles;
   if (S > max_s) S = max_s;
   if (S > steps / 8) S = steps / 8;
