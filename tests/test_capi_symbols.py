@@ -99,6 +99,22 @@ def test_validation_rejects_before_launch(L):
     # LayerNorm width limits
     rc = L.dsvt_layernorm_fwd(_lib.BF16, 0, fake, fake, fake, fake, 4, 100, 0, 0, 0, ctypes.c_float(1e-6), None)
     assert rc == 1
+    # LayerNorm backward: the fused bf16 copy is C = 768 only, with 0 <= osk < og; the split
+    # parameter reduction needs its outputs and a workspace
+    f = ctypes.c_float(1e-6)
+    rc = L.dsvt_layernorm_bwd_cast(_lib.BF16, fake, fake, fake, fake, 100, 512, 0, 0, 0, f, None, None, 1, fake, 100,
+                                   0, fake, 1 << 24, None)
+    assert rc == 1 and b"C = 768" in L.dsvt_last_error()
+    rc = L.dsvt_layernorm_bwd_cast(_lib.BF16, fake, fake, fake, fake, 100, 768, 0, 0, 0, f, None, None, 1, fake, 10,
+                                   10, fake, 1 << 24, None)
+    assert rc == 1 and b"osk" in L.dsvt_last_error()
+    rc = L.dsvt_layernorm_bwd_cast(_lib.BF16, fake, fake, fake, fake, 100, 768, 0, 0, 0, f, fake, None, 1, fake, 10,
+                                   1, fake, 1 << 24, None)
+    assert rc == 1 and b"both or neither" in L.dsvt_last_error()
+    rc = L.dsvt_layernorm_bwd_params(100, 768, fake, 1 << 24, None, fake, 1, None)
+    assert rc == 1 and b"bad args" in L.dsvt_last_error()
+    rc = L.dsvt_layernorm_bwd_params(100, 768, fake, 16, fake, fake, 1, None)
+    assert rc == 1 and b"workspace" in L.dsvt_last_error()
     # frame selection: N out of range; a score that indexes past the unsampled video
     rc = L.dsvt_select_frames(fake, 10, 10, 20, 2, 0, fake, fake, None, fake, 1 << 20, None)
     assert rc == 1 and b"N" in L.dsvt_last_error()
