@@ -634,6 +634,11 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
     dev = dfeat.device
     model._wcache.refresh(_block_weights(model), mode, transposed=True)   # all stale W^T copies, one launch
     wt = model._wcache.transposed(mode)
+    if _tfold_on(mode, G):
+        # every block's folded temporal_fc . attn.proj weight, formed on the weight-gradient
+        # stream while the chain starts (the chain's reads wait on its event: WeightCache._sync)
+        G.run_side(lambda: [model._wcache.folded_t(mode, b.temporal_fc, b.temporal_attn.proj)
+                            for b in model.blocks], ())
     patch_map = (Np * T, L, 1)
     # final norm on the CLS rows (timesformer.py:342-345)
     if st.tail:                       # st.X: the compact CLS rows of the CLS-only last block
@@ -649,7 +654,8 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
         ta = blk.temporal_attn
         if getattr(S, "tail", False):
             dX = _tail_backward(blk, S, mk, dXc, wt, G, B, T, L, C, rows, mode, dev)
-            _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map)
+            _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map,
+                               wcache=model._wcache)
             for k in list(vars(S)):
                 setattr(S, k, None)
             if ready is not None:
@@ -695,7 +701,7 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
         dY = torch.empty(R, C, device=dev, dtype=mode)           # the temporal branch's dX rows
         fused = _ln_bwd(S.X1, da, blk.norm1, dX, rows, G, cast_to=dY, cast_map=(L, 1))
         _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map,
-                           dY=dY if fused else None)
+                           dY=dY if fused else None, wcache=model._wcache)
         for k in list(vars(S)):
             setattr(S, k, None)        # free this block's activations as soon as it is done
         if ready is not None:
@@ -708,7 +714,19 @@ def _divided_backward_steps(model, st, dfeat, G, ready=None):
     yield depth
 
 
-def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map, dY=None):
+# the temporal branch's dX through temporal_fc and attn.proj as ONE GEMM by their folded weight on
+# the dX chain, the intermediate (for attn.proj's weight / bias gradients) on the weight-gradient
+# stream (1, bf16 mode), or both GEMMs on the chain (0, the default: 139.6 / 139.0 vs 142.9 /
+# 142.9 clips/s with the fold -- the extra GEMM on the weight-gradient stream costs the chain more
+# through contention than the one it saves)
+_TFOLD = os.environ.get("DSVT_TRAIN_TFOLD", "0") != "0"
+
+
+def _tfold_on(mode, G):
+    return _TFOLD and mode == torch.bfloat16 and G.side is not None
+
+
+def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patch_map, dY=None, wcache=None):
     """Backward of the temporal branch (patch rows of X only, timesformer.py:127-137): adds into dX.
     dY: the patch rows of dX in the storage dtype when the caller's LayerNorm backward stored them."""
     heads = blk.attn.num_heads
@@ -717,14 +735,35 @@ def _temporal_backward(blk, S, mk, dX, wt, G, B, T, Np, L, C, R, mode, dev, patc
         dY = torch.empty(R, C, device=dev, dtype=mode)
         ops.cast_rows(dX, dY, R, rowmap=patch_map)
     wgrad(dY, S.u, G, blk.temporal_fc.weight, bias=blk.temporal_fc.bias)
-    du = torch.empty(R, C, device=dev, dtype=mode)
-    if mk is None:
-        ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
-    else:
-        ops.gemm_rowscale(dY, wt(blk.temporal_fc.weight), None, du, mk.t, T)
-    wgrad(du, S.o_t, G, ta.proj.weight, bias=ta.proj.bias)
     do_t = torch.empty(R, C, device=dev, dtype=mode)
-    ops.gemm(du, wt(ta.proj.weight), None, do_t)
+    if wcache is not None and _tfold_on(mode, G):
+        # do_t = s_t * (dY . Wfc . Wproj): the chain skips the intermediate
+        wf = wcache.folded_t(mode, blk.temporal_fc, ta.proj)
+        if mk is None:
+            ops.gemm(dY, wf, None, do_t)
+        else:
+            ops.gemm_rowscale(dY, wf, None, do_t, mk.t, T)
+        buf, acc = G.acc(ta.proj.weight)
+        dbuf, acc_b = G.acc(ta.proj.bias)
+        assert acc == acc_b
+        wfc = wt(blk.temporal_fc.weight)
+
+        def side_du():           # du = s_t * (dY . Wfc) and the attn.proj gradients from it
+            du = torch.empty(R, C, device=dev, dtype=mode)
+            if mk is None:
+                ops.gemm(dY, wfc, None, du)
+            else:
+                ops.gemm_rowscale(dY, wfc, None, du, mk.t, T)
+            ops.wgrad(du, S.o_t, buf, accumulate=acc, db=dbuf)
+        G.run_side(side_du, (dY, S.o_t, wfc) if mk is None else (dY, S.o_t, wfc, mk.t))
+    else:
+        du = torch.empty(R, C, device=dev, dtype=mode)
+        if mk is None:
+            ops.gemm(dY, wt(blk.temporal_fc.weight), None, du)
+        else:
+            ops.gemm_rowscale(dY, wt(blk.temporal_fc.weight), None, du, mk.t, T)
+        wgrad(du, S.o_t, G, ta.proj.weight, bias=ta.proj.bias)
+        ops.gemm(du, wt(ta.proj.weight), None, do_t)
     dqkv_t = torch.empty(R, 3 * C, device=dev, dtype=mode)
     ops.attn_temporal_bwd(S.qkv_t, do_t, dqkv_t, B * Np, T, heads, ta.scale)
     wgrad(dqkv_t, S.a_t, G, ta.qkv.weight, bias=ta.qkv.bias)

@@ -171,6 +171,25 @@ class WeightCache:
         self._c[key] = (stamp, (w, b32)) + self._event()
         return w, b32
 
+    def folded_t(self, mode, outer, inner):
+        """(Wo.Wi)^T [in_i, out_o] in `mode`: the B operand of dX_inner_input = dY_outer . Wo . Wi
+        (the backward of two nn.Linear with nothing between them in ONE GEMM), formed in fp32 and
+        cast-transposed, cached until either weight changes."""
+        params = (outer.weight, inner.weight)
+        stamp = tuple((p._version, p.data_ptr()) for p in params)
+        key = ("fold_t", id(outer), id(inner), mode)
+        ent = self._c.get(key)
+        if ent is not None and ent[0] == stamp:
+            self._sync(ent)
+            return ent[1]
+        wo, wi = (p.detach().float().contiguous() for p in params)
+        w32 = torch.empty(wo.shape[0], wi.shape[1], device=wo.device, dtype=torch.float32)
+        ops.gemm(wo, wi.t().contiguous(), None, w32)     # W[m][n] = sum_k Wo[m][k] Wi[k][n]
+        out = torch.empty(wi.shape[1], wo.shape[0], device=wo.device, dtype=mode)
+        ops.cast_transpose(w32, out)
+        self._c[key] = (stamp, out) + self._event()
+        return out
+
     def ln_folded(self, linear, ln, heads=0):
         """(Wf, wsum, bias_f) of nn.Linear `linear` after nn.LayerNorm `ln` for the LayerNorm-folded
         GEMM (dsvt_gemm_lnx_fwd): Wf = bf16(W * gamma), wsum = its row sums, bias_f = b + W . beta,
