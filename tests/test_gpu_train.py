@@ -752,6 +752,49 @@ def _step_nets():
     return nets
 
 
+def test_train_mode_teacher_concurrent_equals_sequential():
+    """A train-mode teacher with DropPath (the reference's setup, never .eval()'d) runs on its own
+    stream beside the student, enqueued after it: the host-side RNG draws keep the student-first
+    order, so two DINOTrainer steps are bitwise those of the sequential order (same seeds)."""
+    from dsvt.loss import DINOLoss
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.trainer import DINOTrainer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+    cfg = dict(embed_dim=64, num_heads=1, depth=2, img_size=48, num_frames=2)
+
+    def nets():
+        out = []
+        for _ in range(2):
+            bb = VisionTransformer(img_size=48, patch_size=16, num_classes=0, embed_dim=64, depth=2, num_heads=1,
+                                   mlp_ratio=4, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6),
+                                   drop_path_rate=0.3, num_frames=2, attention_type="divided_space_time")
+            bb.load_state_dict({k: torch.from_numpy(v) for k, v in P.timesformer_state(1411, **cfg).items()})
+            hd = DINOHead(64, 128, norm_last_layer=True, hidden_dim=64, bottleneck_dim=32)
+            hd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                                P.dino_head_state(1412, 64, 128, hidden_dim=64, bottleneck_dim=32).items()})
+            bb.dsvt_dtype = hd.dsvt_dtype = torch.float32
+            out.append(MultiCropWrapper(bb, hd).cuda().train())
+        return out
+    results = []
+    for concurrent in (False, True):
+        student, teacher = nets()
+        tr = DINOTrainer(student, teacher, DINOLoss(128, 4, 0.04, 0.04, 0, 2).cuda(), epochs=2, niter_per_ep=2,
+                         warmup_epochs=1, batch_size_per_gpu=2, world_size=1, concurrent_teacher=concurrent)
+        teacher.train()
+        losses = []
+        for it in range(2):
+            crops = [torch.from_numpy(P.clip(1520 + 10 * it + i, (2, 3, 2, 48, 48))).cuda() for i in range(2)] + \
+                    [torch.from_numpy(P.clip(1525 + 10 * it + i, (2, 3, 2, 32, 32))).cuda() for i in range(2)]
+            torch.manual_seed(77 + it)
+            losses.append(tr.step(crops, it).detach().clone())
+        torch.cuda.synchronize()
+        results.append((losses, [p.detach().clone() for p in list(student.parameters()) + list(teacher.parameters())]))
+    (l0, p0), (l1, p1) = results
+    assert all(torch.equal(a, b) for a, b in zip(l0, l1)), (l0, l1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
 def test_train_steps_match_reference():
     """a17: four whole SSL steps (train_ssl.py:466-573, 2 epochs x 2 iterations) of
     dsvt.trainer.DINOTrainer against the reference's own train_one_epoch run on the same
