@@ -752,6 +752,21 @@ def _step_nets():
     return nets
 
 
+@pytest.mark.parametrize("sched", ["bwd_fork", "tfold", "ln_cast", "no_side_params", "no_fwd_fork"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_student_grads_alternative_schedules(gold, dtype, sched, monkeypatch):
+    """The training path's measured-and-kept-off (or -on) schedule switches still give the
+    reference's gradients: the two groups' backward chains interleaved on two streams
+    (DSVT_TRAIN_BWD_FORK), the folded temporal_fc . attn.proj dX GEMM (DSVT_TRAIN_TFOLD), the
+    LayerNorm backward storing the bf16 dX copy (DSVT_TRAIN_LN_CAST), the parameter reductions on
+    the dX chain (DSVT_TRAIN_SIDE_PARAMS=0), the groups' forwards in order (DSVT_TRAIN_FWD_FORK=0)."""
+    from dsvt import training
+    flag, value = {"bwd_fork": ("_BWD_FORK", True), "tfold": ("_TFOLD", True), "ln_cast": ("_LN_CAST", True),
+                   "no_side_params": ("_SIDE_PARAMS", False), "no_fwd_fork": ("_FWD_FORK", False)}[sched]
+    monkeypatch.setattr(training, flag, value)
+    test_student_grads_match_reference(gold, dtype, "drop", True, monkeypatch)
+
+
 def test_train_mode_teacher_concurrent_equals_sequential():
     """A train-mode teacher with DropPath (the reference's setup, never .eval()'d) runs on its own
     stream beside the student, enqueued after it: the host-side RNG draws keep the student-first
