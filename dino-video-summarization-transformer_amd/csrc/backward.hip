@@ -23,6 +23,7 @@
 //   ema / sumsq / scale    multi-tensor teacher EMA (train_ssl.py:555-558) and per-tensor
 //                          gradient norm clipping (utils/utils.py:102-111)
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -843,7 +844,7 @@ __global__ __launch_bounds__(256) void attn_temporal_bwd_reg(const bf16_t* __res
 
 hipError_t launch_attn_temporal_bwd(int dtype, const void* qkv, const void* dout, void* dqkv, int64_t nseq, int64_t T,
                                     int64_t heads, int64_t C, float scale, hipStream_t s) {
-  if (dtype == 0 && T <= 8 && g_attn_bwd_variant == 0) {
+  if (dtype == 0 && T <= 8 && (g_attn_bwd_variant == 0 || g_attn_bwd_variant == 2)) {
     const int64_t groups = nseq * heads;
     const unsigned blocks = (unsigned)((groups * 16 + 255) / 256);
     if (T <= 4)
@@ -1243,12 +1244,264 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_short_bf16(AttnBwdParams 
   }
 }
 
+// The same math with HALF the LDS (variant 2): phase 1 keeps only K and V of the whole sequence in
+// LDS (each wave's Q / dO tile comes straight from global memory in MFMA fragment layout), phase 2
+// only Q and dO (K / V tiles from global), restaged in between -- 66 KB instead of 130, so two
+// 4-wave workgroups share a CU and one's staging runs under the other's MFMAs.  Alone 152.5 vs
+// 158.0 us at the train step's global shape (tools/attn_bwd_bench.py); in the step 141.2 / 141.1
+// vs 142.2 / 141.8 clips/s (DSVT_ATTN_BWD_SPLIT=1): selectable (variant 2), off by default.
+template <int NKT, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_split_bf16(AttnBwdParams p) {
+  constexpr int NKP = (NKT + 1) / 2, SN = 2 * NKP, LP = NKP * 32;
+  constexpr int NT = 64 * NW, PCS = (LP * 8 + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) bf16_t sm[2][LP * BKV];   // phase 1: K, V; phase 2: Q, dO
+  __shared__ float m2s[LP], dds[LP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.x;
+  const int64_t seq = blockIdx.y, b = seq / p.tin, t = seq % p.tin;
+  const int L = (int)p.seqlen;
+  const bf16_t* qkv = (const bf16_t*)p.qkv;
+  const bf16_t* dout = (const bf16_t*)p.dout;
+  const int64_t C = p.C;
+  const float ssc = p.seq_scale ? p.seq_scale[seq] : 1.0f;
+  const float sl2 = p.scale * 1.4426950408889634f;
+  auto dscale = [&](int r) { return ssc * ((r == 0 && p.cls_aux) ? p.cls_scale : 1.0f); };
+  auto scale8 = [&](uint4& v, float sc) {
+    unsigned* u = reinterpret_cast<unsigned*>(&v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) u[e] = pack_bf16x2(bf16_lo(u[e]) * sc, bf16_hi(u[e]) * sc);
+  };
+  // two tensors of the whole sequence into sm[0] / sm[1]: K, V (qd = false) or Q, scaled dO
+  auto stage2 = [&](bool qd) {
+#pragma unroll
+    for (int i = 0; i < PCS; ++i) {
+      const int pc = tid + NT * i, r = pc >> 3, ch = pc & 7;
+      if (r < LP) {
+        uint4 va = make_uint4(0, 0, 0, 0), vb = va;
+        if (r < L) {
+          const int64_t row = brow(p, b, t, r);
+          const bf16_t* src = qkv + row * p.ld_qkv + h * 64 + ch * 8;
+          if (qd) {
+            va = *reinterpret_cast<const uint4*>(src);
+            vb = *reinterpret_cast<const uint4*>(dout + row * p.ld_dout + h * 64 + ch * 8);
+            const float sc = dscale(r);
+            if (sc != 1.0f) scale8(vb, sc);
+          } else {
+            va = *reinterpret_cast<const uint4*>(src + C);
+            vb = *reinterpret_cast<const uint4*>(src + 2 * C);
+          }
+        }
+        *reinterpret_cast<uint4*>(&sm[0][r * BKV + ch * 8]) = va;
+        *reinterpret_cast<uint4*>(&sm[1][r * BKV + ch * 8]) = vb;
+      }
+    }
+  };
+  // one 16-row tile's MFMA fragments (row r16 of the tile, columns 8g.. and 32 + 8g..) from global
+  auto frag_g = [&](const bf16_t* base, int64_t ld, int64_t off, int row, bool sc_d, sv8& f0, sv8& f1) {
+    uint4 a = make_uint4(0, 0, 0, 0), c = a;
+    if (row < L) {
+      const bf16_t* src = base + brow(p, b, t, row) * ld + off + g * 8;
+      a = *reinterpret_cast<const uint4*>(src);
+      c = *reinterpret_cast<const uint4*>(src + 32);
+      if (sc_d) {
+        const float sc = dscale(row);
+        if (sc != 1.0f) { scale8(a, sc); scale8(c, sc); }
+      }
+    }
+    f0 = __builtin_bit_cast(sv8, a);
+    f1 = __builtin_bit_cast(sv8, c);
+  };
+  const int nkt = (L + 15) >> 4;
+  typedef __attribute__((address_space(3))) sv4* LDS4;
+
+  stage2(false);
+  __syncthreads();
+  {
+    const bf16_t* Ks = sm[0];
+    const bf16_t* Vs = sm[1];
+    // ================= phase 1: dQ, row statistics
+    for (int qt = wave; qt < nkt; qt += NW) {
+      sv8 qf0, qf1, df0, df1;
+      frag_g(qkv, p.ld_qkv, h * 64, qt * 16 + r16, false, qf0, qf1);
+      frag_g(dout, p.ld_dout, h * 64, qt * 16 + r16, true, df0, df1);
+      fv4 s[SN], dp[SN];
+#pragma unroll
+      for (int kt = 0; kt < SN; ++kt) {
+        const bf16_t* kr = Ks + (kt * 16 + r16) * BKV + g * 8;
+        const bf16_t* vr = Vs + (kt * 16 + r16) * BKV + g * 8;
+        fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(kr), qf0, z, 0, 0, 0);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(kr + 32), qf1, z, 0, 0, 0);
+        fv4 y = fv4{0.f, 0.f, 0.f, 0.f};
+        y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(vr), df0, y, 0, 0, 0);
+        dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(vr + 32), df1, y, 0, 0, 0);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < SN; ++kt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[kt][j] = (kt * 16 + 4 * g + j < L) ? s[kt][j] : -INFINITY;
+        mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mxs = mx * sl2;
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s[kt][j] = __builtin_amdgcn_exp2f(fmaf(s[kt][j], sl2, -mxs));
+          rs += s[kt][j];
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      const float inv = 1.0f / rs;
+      float D = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s[kt][j] *= inv;
+          D = fmaf(s[kt][j], dp[kt][j], D);
+        }
+      D += __shfl_xor(D, 16, 64);
+      D += __shfl_xor(D, 32, 64);
+      fv4 dq[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) dq[d] = fv4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kp = 0; kp < NKP; ++kp) {
+        sv8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (short)f2bf(s[2 * kp][j] * (dp[2 * kp][j] - D));
+          pb[4 + j] = (short)f2bf(s[2 * kp + 1][j] * (dp[2 * kp + 1][j] - D));
+        }
+        const int kr0 = kp * 32 + 4 * g + (r16 >> 2), kr1 = kr0 + 16;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int col = dt * 16 + 4 * (r16 & 3);
+          const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ks + kr0 * BKV + col));
+          const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ks + kr1 * BKV + col));
+          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                                           pb, dq[dt], 0, 0, 0);
+        }
+      }
+      mfma_result_fence();
+      const int qo = qt * 16 + r16;
+      if (g == 0) {
+        m2s[qo] = qo < L ? mxs + __log2f(rs) : INFINITY;
+        dds[qo] = qo < L ? D : 0.f;
+      }
+      if (qo < L) {
+        if (qo == 0 && p.cls_aux) {
+          float* dst = p.cls_aux + seq * 3 * C + h * 64 + 4 * g;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            store4(dst + dt * 16, dq[dt][0] * p.scale, dq[dt][1] * p.scale, dq[dt][2] * p.scale, dq[dt][3] * p.scale);
+        } else {
+          bf16_t* dst = (bf16_t*)p.dqkv + brow(p, b, t, qo) * p.ld_dqkv + h * 64 + 4 * g;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            store4(dst + dt * 16, dq[dt][0] * p.scale, dq[dt][1] * p.scale, dq[dt][2] * p.scale, dq[dt][3] * p.scale);
+        }
+      }
+    }
+  }
+  for (int q = nkt * 16 + tid; q < LP; q += NT) { m2s[q] = INFINITY; dds[q] = 0.f; }
+  __syncthreads();                       // every phase-1 read of K, V done; statistics visible
+  stage2(true);
+  __syncthreads();
+  const bf16_t* Qs = sm[0];
+  const bf16_t* Ds = sm[1];
+  // ================= phase 2: dK, dV
+  for (int kt = wave; kt < nkt; kt += NW) {
+    sv8 kf0, kf1, vf0, vf1;
+    frag_g(qkv, p.ld_qkv, C + h * 64, kt * 16 + r16, false, kf0, kf1);
+    frag_g(qkv, p.ld_qkv, 2 * C + h * 64, kt * 16 + r16, false, vf0, vf1);
+    fv4 dk[4], dv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) { dk[d] = fv4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+#pragma unroll
+    for (int qp = 0; qp < NKP; ++qp) {
+      fv4 P[2], dS[2];
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        const int q0 = (2 * qp + hq) * 16;
+        const bf16_t* qr = Qs + (q0 + r16) * BKV + g * 8;
+        const bf16_t* dr = Ds + (q0 + r16) * BKV + g * 8;
+        fv4 z = fv4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(qr), kf0, z, 0, 0, 0);
+        const fv4 sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(qr + 32), kf1, z, 0, 0, 0);
+        fv4 y = fv4{0.f, 0.f, 0.f, 0.f};
+        y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(dr), vf0, y, 0, 0, 0);
+        const fv4 dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const sv8*>(dr + 32), vf1, y, 0, 0, 0);
+        const float4 m2 = *reinterpret_cast<const float4*>(&m2s[q0 + 4 * g]);
+        const float4 dd = *reinterpret_cast<const float4*>(&dds[q0 + 4 * g]);
+        const float mm[4] = {m2.x, m2.y, m2.z, m2.w}, D4[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          P[hq][j] = __builtin_amdgcn_exp2f(fmaf(sc[j], sl2, -mm[j]));
+          dS[hq][j] = P[hq][j] * (dpv[j] - D4[j]);
+        }
+      }
+      sv8 pb, sb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(P[0][j]);
+        pb[4 + j] = (short)f2bf(P[1][j]);
+        sb[j] = (short)f2bf(dS[0][j]);
+        sb[4 + j] = (short)f2bf(dS[1][j]);
+      }
+      const int qr0 = qp * 32 + 4 * g + (r16 >> 2), qr1 = qr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 dlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ds + qr0 * BKV + col));
+        const sv4 dhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Ds + qr1 * BKV + col));
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(dlo, dhi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                                         pb, dv[dt], 0, 0, 0);
+        const sv4 qlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Qs + qr0 * BKV + col));
+        const sv4 qhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS4)(Qs + qr1 * BKV + col));
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(qlo, qhi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                                         sb, dk[dt], 0, 0, 0);
+      }
+    }
+    mfma_result_fence();
+    const int ko = kt * 16 + r16;
+    if (ko < L) {
+      if (ko == 0 && p.cls_aux) {
+        float* dst = p.cls_aux + seq * 3 * C + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          store4(dst + C + dt * 16, dk[dt][0] * p.scale, dk[dt][1] * p.scale, dk[dt][2] * p.scale, dk[dt][3] * p.scale);
+          store4(dst + 2 * C + dt * 16, dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+        }
+      } else {
+        bf16_t* dst = (bf16_t*)p.dqkv + brow(p, b, t, ko) * p.ld_dqkv + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          store4(dst + C + dt * 16, dk[dt][0] * p.scale, dk[dt][1] * p.scale, dk[dt][2] * p.scale, dk[dt][3] * p.scale);
+          store4(dst + 2 * C + dt * 16, dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+        }
+      }
+    }
+  }
+}
+
 void set_attn_bwd_variant(int v) { g_attn_bwd_variant = v; }
 
 hipError_t launch_attn_bwd_generic(int dtype, const AttnBwdParams& p, hipStream_t s) {
   const int64_t items = p.nb * p.tin * p.heads * p.seqlen;
   const unsigned blocks = (unsigned)((items * 16 + 255) / 256);
-  if (dtype == 0 && p.seqlen <= 256 && g_attn_bwd_variant == 0) {
+  static const int split_env = getenv("DSVT_ATTN_BWD_SPLIT") ? atoi(getenv("DSVT_ATTN_BWD_SPLIT")) : 0;
+  const bool split = g_attn_bwd_variant == 2 || (g_attn_bwd_variant == 0 && split_env);
+  if (dtype == 0 && p.seqlen > 64 && p.seqlen <= 208 && split) {
+    dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
+    attn_bwd_split_bf16<13, 4><<<grid, 256, 0, s>>>(p);
+  } else if (dtype == 0 && p.seqlen <= 256 && (g_attn_bwd_variant == 0 || g_attn_bwd_variant == 2)) {
     dim3 grid((unsigned)p.heads, (unsigned)(p.nb * p.tin));
     if (p.seqlen <= 64) attn_bwd_short_bf16<4, 4><<<grid, 256, 0, s>>>(p);
     else if (p.seqlen <= 208) attn_bwd_short_bf16<13, 8><<<grid, 512, 0, s>>>(p);

@@ -617,7 +617,8 @@ int dsvt_set_attn_variant(int variant) {
 }
 
 int dsvt_set_attn_bwd_variant(int variant) {
-  REQUIRE(variant == 0 || variant == 1, "attention backward variant must be 0 (auto) or 1 (generic VALU)");
+  REQUIRE(variant >= 0 && variant <= 2,
+          "attention backward variant must be 0 (auto), 1 (generic VALU) or 2 (half-LDS MFMA, 64 < L <= 208)");
   set_attn_bwd_variant(variant);
   return 0;
 }

@@ -26,7 +26,8 @@ int dsvt_set_gemm_variant(int variant);
  * 2 + 2 tiles (320 / 192 / 256 queries) (5, 6, 9, 10: diagnostic builds). */
 int dsvt_set_attn_variant(int variant);
 /* attention backward: 0 = automatic (bf16 MFMA kernel for sequences <= 256), 1 = the generic
- * two-pass VALU kernels.  Process-global. */
+ * two-pass VALU kernels, 2 = the half-LDS two-workgroups-per-CU MFMA kernel for 64 < L <= 208
+ * (else as 0).  Process-global. */
 int dsvt_set_attn_bwd_variant(int variant);
 
 #ifdef __cplusplus

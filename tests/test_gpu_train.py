@@ -348,9 +348,10 @@ def test_attn_spatial_cls_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled):
     assert torch.equal(dq, dq2)
 
 
-@pytest.fixture(params=[0, 1], ids=["auto", "generic"])
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "generic", "split"])
 def attn_bwd_variant(request):
-    """bf16: the MFMA whole-sequence kernel (auto, L <= 256) and the generic VALU kernels."""
+    """bf16: the MFMA whole-sequence kernel (auto, L <= 256), the generic VALU kernels, and the
+    half-LDS two-per-CU MFMA kernel (split, 64 < L <= 208)."""
     from dsvt import _lib
     _lib.call("dsvt_set_attn_bwd_variant", request.param)
     yield request.param
@@ -381,13 +382,15 @@ def test_attn_spatial_bwd_vs_autograd(dtype, tol, B, T, Np, H, scaled, attn_bwd_
     assert rel(outs[0].float().cpu(), q32.grad.cpu()) < tol
 
 
-def test_attn_bwd_bench_shape_repeatable():
+@pytest.mark.parametrize("variant", [0, 2], ids=["auto", "split"])
+def test_attn_bwd_bench_shape_repeatable(variant):
     """The two attention backward kernels of the train step at the bench's global group (16 clips x
-    8 x 224^2, 12 heads, bf16): spatial attn_bwd_short_bf16 (128 frame sequences of 197 tokens,
-    DropPath sequence scales) and temporal attn_temporal_bwd_reg<8> (3136 patch sequences of 8):
-    three launches each bitwise identical and finite (the MFMA-hazard class of DESIGN §3 at the
-    occupancy the step runs them at), and against torch fp32 autograd."""
-    from dsvt import ops
+    8 x 224^2, 12 heads, bf16): spatial attn_bwd_short_bf16 / attn_bwd_split_bf16 (128 frame
+    sequences of 197 tokens, DropPath sequence scales) and temporal attn_temporal_bwd_reg<8> (3136
+    patch sequences of 8): three launches each bitwise identical and finite (the MFMA-hazard class
+    of DESIGN §3 at the occupancy the step runs them at), and against torch fp32 autograd."""
+    from dsvt import ops, _lib
+    _lib.call("dsvt_set_attn_bwd_variant", variant)
     B, T, Np, H = 16, 8, 196, 12
     C, L = H * 64, 1 + Np * T
     g = torch.Generator(device="cuda").manual_seed(11)
@@ -425,6 +428,7 @@ def test_attn_bwd_bench_shape_repeatable():
                                        x[:, :, 2].transpose(1, 2), scale=0.125)
     o.transpose(1, 2).reshape(nseq * T, C).backward(dt.float())
     assert rel(outs[0].float().cpu(), q32.grad.cpu()) < 3e-2
+    _lib.call("dsvt_set_attn_bwd_variant", 0)
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
