@@ -688,11 +688,15 @@ def test_ema_and_clip_multi_tensor():
     shapes = [(5000,), (3, 7), (64, 64), (1,), (4097,)]
     st = [torch.randn(s, device="cuda", generator=g) for s in shapes]
     te = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    # 4-byte-offset views take the kernels' scalar path (the float4 path needs 16-B alignment)
+    st.append(torch.randn(9001, device="cuda", generator=g)[1:])
+    te.append(torch.randn(9003, device="cuda", generator=g)[3:])
     ref = [0.996 * b + 0.004 * a for a, b in zip(st, te)]
     ema_update_(te, st, 0.996)
     for a, b in zip(te, ref):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
     grads = [torch.randn(s, device="cuda", generator=g) * (3.0 if i % 2 else 0.01) for i, s in enumerate(shapes)]
+    grads.append(torch.randn(12289, device="cuda", generator=g)[1:] * 3.0)
     exp = []
     for x in grads:
         nrm = x.norm(2)
@@ -702,7 +706,7 @@ def test_ema_and_clip_multi_tensor():
     torch.cuda.synchronize()
     for a, b in zip(grads, exp):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-7)
-    assert norms.shape == (len(shapes),)
+    assert norms.shape == (len(shapes) + 1,)
 
 
 def test_adamw_matches_torch():
@@ -718,13 +722,15 @@ def test_adamw_matches_torch():
     runs = []
     for cls in (AdamW, torch.optim.AdamW):
         ps = [torch.nn.Parameter(x.clone()) for x in p0]
+        # a 4-byte-offset view parameter (scalar path of the float4 kernel)
+        ps.append(torch.nn.Parameter(torch.cat([p0[1][:1], p0[3]])[1:]))
         opt = cls([{"params": ps[:3]}, {"params": ps[3:], "weight_decay": 0.0}])
         for it in range(3):
             for i, pg in enumerate(opt.param_groups):
                 pg["lr"] = 1e-3 * (it + 1)
                 if i == 0:
                     pg["weight_decay"] = 0.04 + 0.1 * it
-            for p, gr in zip(ps, grads[it]):
+            for p, gr in zip(ps, grads[it] + [grads[it][3] * 0.5]):
                 p.grad = gr.clone()
             if it == 0:
                 ps[4].grad = None
