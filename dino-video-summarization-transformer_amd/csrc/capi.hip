@@ -97,7 +97,7 @@ int gemm_tag(const GemmParams& p, int dtype, int epi, int out_f32) {
   const int f32 = (epi == EPI_RESID || epi == EPI_PATCH) ? 1 : (out_f32 ? 1 : 0);
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
   const int fuse = p.ln_stats ? 1 : (p.stats_out ? 2 : 0);
-  const int nfull = v == 20 && (fuse == 1 || (fuse == 0 && (epi == EPI_BIAS || epi == EPI_GELU) && !f32 &&
+  const int nfull = (v == 20 || v == 40) && (fuse == 1 || (fuse == 0 && (epi == EPI_BIAS || epi == EPI_GELU) && !f32 &&
                                                p.N % 256 == 0));
   return v * 32 + dtype * 16 + epi * 2 + f32 + 1024 * fuse + 4096 * nfull;
 }
@@ -604,8 +604,8 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 
 int dsvt_set_gemm_variant(int variant) {
   REQUIRE(variant == 0 || variant == 1 || variant == 3 || variant == 10 || (variant >= 20 && variant <= 29 && variant != 24) ||
-              variant == 30 || variant == 50,
-          "gemm variant must be 0 (auto), 1, 3, 10, 20 (21-29 but 24: ablation builds), 30 or 50");
+              variant == 30 || (variant >= 40 && variant <= 46 && variant != 43) || variant == 50,
+          "gemm variant must be 0 (auto), 1, 3, 10, 20 (21-29 but 24: ablation builds), 30, 40 (41, 42, 44-46: ablation builds) or 50");
   set_gemm_variant(variant);
   return 0;
 }

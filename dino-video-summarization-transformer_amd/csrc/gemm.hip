@@ -450,6 +450,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 #endif
   if (p.stats_out && (gv == 1 || (gv == 0 && DSVT_RESID_STATS_V == 1)) && p.N % 128 == 0) return 1;
   if (p.stats_out && (gv == 10 || (gv == 0 && DSVT_RESID_STATS_V == 10)) && p.N % 128 == 0) return 10;
+  if (gv >= 40 && gv <= 49) return gemm_4w_ok(p, epi, out_f32) ? gv : (p.ln_stats || p.stats_out) ? 20 : 1;
   if (p.ln_stats || p.stats_out) return 20;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
@@ -517,7 +518,8 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
-  if ((p.ln_stats && v != 20) || (p.stats_out && v != 20 && v != 30 && v != 1 && v != 10)) return hipErrorInvalidValue;
+  if ((p.ln_stats && v != 20 && v != 40) || (p.stats_out && v != 20 && v != 30 && v != 1 && v != 10 && v != 40))
+    return hipErrorInvalidValue;
   if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);
   if (v == 3) return launch_resid160(p, epi, s);
   if (v >= 2) return launch_gemm_big(p, v, epi, out_f32, s);

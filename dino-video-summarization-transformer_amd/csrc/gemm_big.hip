@@ -232,6 +232,13 @@ hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f3
     case 28: return launch_gemm_8ph(p, epi, out_f32, s, 32);
     case 29: return launch_gemm_8ph(p, epi, out_f32, s, 64);
     case 30: return launch_gemm_192(p, epi, out_f32, s);
+    // 40 = gemm_4w.hip (41, 42, 44-46: its diagnostic ablation builds)
+    case 40: return launch_gemm_4w(p, epi, out_f32, s);
+    case 41: return launch_gemm_4w(p, epi, out_f32, s, 2);
+    case 42: return launch_gemm_4w(p, epi, out_f32, s, 4);
+    case 44: return launch_gemm_4w(p, epi, out_f32, s, 16);
+    case 45: return launch_gemm_4w(p, epi, out_f32, s, 18);
+    case 46: return launch_gemm_4w(p, epi, out_f32, s, 26);
     default: return hipErrorInvalidValue;
   }
 }

@@ -537,9 +537,10 @@ __device__ __forceinline__ void ln_affine(const GemmParams& p, fv4 (&acc)[MI][NJ
 #ifndef DSVT_STATS_W
 #define DSVT_STATS_W 3
 #endif
-template <int MI, int NJ, bool FULL, int W = DSVT_STATS_W>
+// BIAS (gemm_4w.hip, whose accumulators start from zero): bias4 added to each row as it is formed
+template <int MI, int NJ, bool FULL, int W = DSVT_STATS_W, bool BIAS = false>
 __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase, int64_t cbase,
-                                                 int r16, int g) {
+                                                 int r16, int g, const float4* bias4 = nullptr) {
   static_assert(NJ == 4, "64-column wave slab");
   const bool ident = p.rpg >= p.M && p.goff == 0;
   const int part = (int)(cbase >> 6);
@@ -564,7 +565,9 @@ __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const float4 xv = x[i % W][j];
-      v[j] = fv4{xv.x + acc[i][j][0], xv.y + acc[i][j][1], xv.z + acc[i][j][2], xv.w + acc[i][j][3]};
+      fv4 a = acc[i][j];
+      if constexpr (BIAS) a += fv4{bias4[j].x, bias4[j].y, bias4[j].z, bias4[j].w};
+      v[j] = fv4{xv.x + a[0], xv.y + a[1], xv.z + a[2], xv.w + a[3]};
       s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
       q += sumsq4(v[j][0], v[j][1], v[j][2], v[j][3]);
     }
@@ -582,14 +585,15 @@ __device__ __forceinline__ void resid_stats_rows(const GemmParams& p, fv4 (&acc)
       // the four lanes of the row store the same 8 bytes (no per-lane branch)
       *reinterpret_cast<float2*>(p.stats_out + (orow * LN_PARTS + part) * 2) = make_float2(s, q);
     }
+    if constexpr (BIAS) __builtin_amdgcn_sched_barrier(0);   // one row's accumulators live at a time
   }
 }
 
-template <int MI, int NJ, int W = DSVT_STATS_W>
+template <int MI, int NJ, int W = DSVT_STATS_W, bool BIAS = false>
 __device__ __forceinline__ void epilogue_resid_stats(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
-                                                     int64_t cbase, int r16, int g) {
-  if (rbase + MI * 16 <= p.M) resid_stats_rows<MI, NJ, true, W>(p, acc, rbase, cbase, r16, g);
-  else resid_stats_rows<MI, NJ, false, W>(p, acc, rbase, cbase, r16, g);
+                                                     int64_t cbase, int r16, int g, const float4* bias4 = nullptr) {
+  if (rbase + MI * 16 <= p.M) resid_stats_rows<MI, NJ, true, W, BIAS>(p, acc, rbase, cbase, r16, g, bias4);
+  else resid_stats_rows<MI, NJ, false, W, BIAS>(p, acc, rbase, cbase, r16, g, bias4);
 }
 
 }  // namespace dsvt

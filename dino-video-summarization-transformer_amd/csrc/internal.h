@@ -74,6 +74,8 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32);  // 
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s);
 hipError_t launch_gemm_8ph(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);  // variant 20
 bool gemm_8ph_ok(const GemmParams& p, int epi);
+hipError_t launch_gemm_4w(const GemmParams& p, int epi, int out_f32, hipStream_t s, int abl = 0);   // variant 40
+bool gemm_4w_ok(const GemmParams& p, int epi, int out_f32);
 hipError_t launch_gemm_192(const GemmParams& p, int epi, int out_f32, hipStream_t s);    // variant 30
 bool gemm_192_ok(const GemmParams& p, int epi);
 // the LayerNorm-folded temporal qkv GEMM with the T = 8 attention in its epilogue (gemm_192.hip)

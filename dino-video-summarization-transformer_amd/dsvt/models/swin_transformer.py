@@ -255,14 +255,22 @@ class _SwinCtx:
         return ent
 
     def bias(self, attn, N):
+        """The [heads, N, N] relative-position bias of one attention module at window size N, cached
+        per (module, N) and recomputed IN PLACE when the table changes (its version counter or
+        storage: every optimizer / EMA step in training) -- one tensor per entry, so the cache does
+        not grow with the steps.  The rewrite is enqueued on the current stream after that step's
+        update of the table, i.e. after every reader of the previous values."""
         t = attn.relative_position_bias_table
-        key = ("bias", id(attn), N, t._version, t.data_ptr())
+        key = ("bias", id(attn), N)
+        stamp = (t._version, t.data_ptr())
         ent = self.model._aux.get(key)
         if ent is None:
-            ent = torch.empty(attn.num_heads, N, N, device=self.device, dtype=torch.float32)
-            ops.relpos_bias(t.detach().contiguous(), attn.relative_position_index.contiguous(), N, ent)
+            ent = [None, torch.empty(attn.num_heads, N, N, device=self.device, dtype=torch.float32)]
             self.model._aux[key] = ent
-        return ent
+        if ent[0] != stamp:
+            ops.relpos_bias(t.detach().contiguous(), attn.relative_position_index.contiguous(), N, ent[1])
+            ent[0] = stamp
+        return ent[1]
 
     def zeros(self, shape, dtype):
         return torch.zeros(shape, device=self.device, dtype=dtype)

@@ -627,6 +627,12 @@ def gemm_kernel_name(tag):
         if fuse == 2:
             return "void dsvt::gemm_8ph_kernel<2, true, 0, false, 2>" + P
         return "void dsvt::gemm_8ph_kernel<%d, %s, 0, %s, 0>%s" % (epi, f32, "true" if nfull else "false", P)
+    if variant == 40:
+        if fuse == 1:
+            return "void dsvt::gemm_4w_kernel<%d, false, 0, true, 1>%s" % (epi, P)
+        if fuse == 2:
+            return "void dsvt::gemm_4w_kernel<2, true, 0, false, 2>" + P
+        return "void dsvt::gemm_4w_kernel<%d, %s, 0, %s, 0>%s" % (epi, f32, "true" if nfull else "false", P)
     if variant == 30:
         return "void dsvt::gemm_192_kernel<"
     if variant == 32:

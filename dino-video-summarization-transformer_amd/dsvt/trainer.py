@@ -25,18 +25,34 @@ from .training import np_cosine_scheduler
 from .utils import cancel_gradients_last_layer, clip_gradients, ema_update_, get_params_groups
 
 
-def _draws_rng(model):
-    """True when a forward of `model` draws random numbers: train mode with an active DropPath
-    or dropout.  Such a teacher must run AFTER the student, as in the reference
-    (train_ssl.py:523-527), so a seeded run draws the masks in the same order."""
-    if not model.training:
+class _TeacherStepSettings:
+    """The teacher backbone's step-time settings, applied for the duration of the teacher call
+    only (set permanently they also changed later uses of the same teacher object,
+    e.g. eval or kNN feature extraction).  Inside a training step:
+    - no batch split over streams of its own: the teacher runs beside the student on its own
+      stream (146.6 / 146.7 vs 143.7 / 143.6 clips/s with the inference path's automatic 3-way
+      split -- five streams contend, as in the forward bench);
+    - no temporal_attn.proj -> temporal_fc fold: the EMA changes the weights every step, so the
+      fold (an fp32 768^3 product per block, redone each step) costs more than the extra bf16 GEMM
+      of the unfolded pair it saves."""
+
+    SETTINGS = (("dsvt_streams", 1), ("fold_temporal_fc", False))
+
+    def __init__(self, teacher):
+        self.bb = getattr(teacher, "backbone", teacher)
+        self.saved = []
+
+    def __enter__(self):
+        self.saved = [(k, getattr(self.bb, k)) for k, _ in self.SETTINGS if hasattr(self.bb, k)]
+        for k, v in self.SETTINGS:
+            if hasattr(self.bb, k):
+                setattr(self.bb, k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved:
+            setattr(self.bb, k, v)
         return False
-    for m in model.modules():
-        if m.training and (getattr(m, "drop_prob", 0.0) or 0.0) > 0.0:
-            return True
-        if isinstance(m, torch.nn.Dropout) and m.training and m.p > 0.0:
-            return True
-    return False
 
 
 class DINOTrainer:
@@ -73,17 +89,7 @@ class DINOTrainer:
             raise ValueError("optimizer must be 'dsvt' or 'torch'")
         for p in teacher.parameters():
             p.requires_grad_(False)
-        # the EMA changes the teacher's weights every step, so folding temporal_attn.proj into
-        # temporal_fc (an fp32 768^3 product per block, redone each step) costs more than the
-        # extra bf16 GEMM of the unfolded pair it saves
-        bb = getattr(teacher, "backbone", teacher)
-        if hasattr(bb, "fold_temporal_fc"):
-            bb.fold_temporal_fc = False
-        # the teacher's forward runs beside the student's (its own stream): no further batch split
-        # over streams of its own (146.6 / 146.7 vs 143.7 / 143.6 clips/s with the inference
-        # path's automatic 3-way split -- five streams contend, as in the forward bench)
-        if hasattr(bb, "dsvt_streams"):
-            bb.dsvt_streams = 1
+        self._teacher_settings = _TeacherStepSettings(teacher)
         self._s_params = [p for p in student.parameters()]
         if ddp is None:          # gradients at fixed addresses: cached pointer tables (training.persistent_grad_arena)
             for m in (getattr(student, "backbone", None), getattr(student, "head", None)):
@@ -116,13 +122,13 @@ class DINOTrainer:
             side.wait_stream(main)
             # (student first for any teacher: 143.6 / 143.8 vs 143.1 / 143.3 clips/s teacher-first)
             s_out = self.model(images)                             # :523
-            with torch.cuda.stream(side), torch.no_grad():
+            with torch.cuda.stream(side), torch.no_grad(), self._teacher_settings:
                 t_out = self.teacher(images[:self.n_global])       # :527 (teacher on global views)
             main.wait_stream(side)
             t_out.record_stream(main)
         else:
             s_out = self.model(images)                             # :523
-            with torch.no_grad():
+            with torch.no_grad(), self._teacher_settings:
                 t_out = self.teacher(images[:self.n_global])       # :527 (teacher on global views)
         loss = self.dino_loss(s_out, t_out, epoch)
         if check_finite and not math.isfinite(loss.item()):        # :530-532

@@ -28,10 +28,13 @@
 extern "C" {
 #endif
 
-/* 2 (r05): dsvt_bn_bwd takes param_sums (SyncBatchNorm's local dgamma / dbeta); DSVT_EPI_GELU_SAVE's
- * aux holds GELU'(pre) (r04; was pre); the r03 grouped / stream-K / add-LN / row-LN GEMM entry points
- * are gone and the variant knobs moved to dsvt_debug.h (r04).  Added in 2, existing calls unchanged:
- * dsvt_layernorm_bwd_params / _cast, the Swin training entries. */
+/* 2 (r05): dsvt_bn_bwd takes param_sums (SyncBatchNorm's local dgamma / dbeta); dsvt_window_scatter_add
+ * takes (row_scale, group) BEFORE stream -- a version-1 caller would pass its stream as row_scale;
+ * DSVT_EPI_GELU_SAVE's aux holds GELU'(pre) (r04; was pre); the r03 grouped / stream-K / add-LN /
+ * row-LN GEMM entry points are gone and the variant knobs moved to dsvt_debug.h (r04).  Added in 2:
+ * dsvt_layernorm_bwd_params / _cast, the Swin training entries.  tests/test_capi_symbols.py freezes
+ * every entry point's parameter count per ABI version: a signature change without a version bump
+ * fails it. */
 #define DSVT_ABI_VERSION 2
 
 #define DSVT_BF16 0

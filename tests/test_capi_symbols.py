@@ -138,3 +138,22 @@ def test_ops_raise_with_dsvt_error(L):
     from dsvt import ops, DsvtError
     with pytest.raises(DsvtError):
         ops.cast(torch.zeros(8), torch.zeros(8, dtype=torch.bfloat16))   # CPU tensors: no fallback
+
+
+def test_signatures_frozen_per_abi_version(L):
+    """Every entry point's parameter count is frozen per ABI version (tests/golden/abi_arity.json):
+    changing a signature -- as r05 did to dsvt_window_scatter_add without recording it -- or
+    removing an entry point fails here until DSVT_ABI_VERSION is bumped and the table regenerated
+    (a new entry point may be added within a version)."""
+    import json
+    frozen = json.load(open(os.path.join(ROOT, "tests", "golden", "abi_arity.json")))
+    assert L.dsvt_version() == frozen["abi_version"], "ABI version bumped: regenerate abi_arity.json"
+    for hdr, path in (("dsvt.h", HEADER), ("dsvt_debug.h", DEBUG_HEADER)):
+        src = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+        now = {}
+        for m in re.finditer(r"\b(dsvt_\w+)\s*\(([^)]*)\)", src):
+            now[m.group(1)] = len([p for p in m.group(2).split(",") if p.strip() and p.strip() != "void"])
+        for name, n in frozen[hdr].items():
+            assert name in now, "%s removed from %s within ABI version %d" % (name, hdr, frozen["abi_version"])
+            assert now[name] == n, "%s: %d parameters, frozen %d at ABI version %d" % (name, now[name], n,
+                                                                                       frozen["abi_version"])

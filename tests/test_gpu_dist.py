@@ -68,3 +68,33 @@ def test_bench_refuses_more_ranks_than_gpus():
     assert r.returncode != 0
     assert "GPU" in (r.stderr + r.stdout)
     assert '"metric"' not in r.stdout
+
+
+def test_bench_multi_gpu_path_rehearsal(tmp_path):
+    """the exact path the driver's 8-GPU SCALE run takes -- `bench.py --gpus N`
+    -> launch_ranks -> torch.distributed.run -> per-rank init_from_env(device) -> probe + HIP-graph
+    capture per rank -> max_over_ranks -> the wrap_ddp train leg (per-block gradient buckets) --
+    executed with 2 ranks on the box's one GPU (gloo: RCCL refuses two ranks per device).  One
+    JSON line from rank 0, dp2 everywhere, a finite loss, both ranks' exit status 0."""
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("needs a GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    log = os.path.join(LOGDIR if os.path.isdir(LOGDIR) else str(tmp_path), "bench_dp2_rehearsal.log")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--shared-gpu",
+           "--steps", "2", "--warmup", "1", "--train-steps", "1", "--no-other", "--no-cpu-baseline"]
+    with open(log, "w") as f:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=f, text=True, timeout=420)
+    assert r.returncode == 0, "bench --gpus 2 exited %d; stderr in %s:\n%s" % (
+        r.returncode, log, open(log).read()[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    print("dp2 rehearsal:", {k: out[k] for k in ("value", "n_gpus", "world_size", "backend", "loss")},
+          out["train_step"]["value"], out["train_step"]["parallelism"])
+    assert out["n_gpus"] == 2 and out["world_size"] == 2 and out["backend"] == "gloo"
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 2 * out["config"]["clips_per_gpu"]
+    ts = out["train_step"]
+    assert ts["n_gpus"] == 2 and ts["parallelism"].startswith("dp2") and "per-block buckets" in ts["parallelism"]
+    import math
+    assert math.isfinite(out["loss"]) and math.isfinite(ts["loss"]) and out["value"] > 0 and ts["value"] > 0

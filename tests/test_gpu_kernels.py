@@ -39,7 +39,7 @@ def check(got, ref, dtype, what=""):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 3, 10, 20, 30, 50])
+@pytest.fixture(params=[0, 1, 3, 10, 20, 30, 40, 50])
 def gemm_variant(request):
     """Every bf16 GEMM kernel variant is checked (the fp32 path has one kernel)."""
     from dsvt import _lib
@@ -219,7 +219,7 @@ def test_gemm_residual_rowmap(dtype, B, Np, T, gemm_variant):
     np.testing.assert_array_equal(back(X)[np.arange(B) * L], x0[np.arange(B) * L])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 10, 20, 30])
+@pytest.mark.parametrize("variant", [0, 1, 3, 10, 20, 30, 40])
 @pytest.mark.parametrize("B,Np,T", [(3, 5, 4), (4, 49, 8), (16, 196, 8)])
 def test_gemm_residual_k768(variant, B, Np, T):
     """The K = 768, N = 768 residual GEMM (attn.proj / folded temporal fc shape) at the bench's
@@ -304,7 +304,8 @@ def test_ln_fold_weights():
 
 @pytest.mark.parametrize("B,Np,T", [(2, 5, 3), (4, 49, 8), (16, 196, 8)])
 @pytest.mark.parametrize("epi", [0, 1])
-def test_gemm_lnx(B, Np, T, epi):
+@pytest.mark.parametrize("variant", [0, 20, 40])
+def test_gemm_lnx(B, Np, T, epi, variant):
     """dsvt_gemm_lnx_fwd (the LayerNorm folded into qkv / fc1) against LayerNorm -> Linear in
     float64 on the same fp32 rows: every row (the spatial qkv / fc1) and the patch rows through the
     temporal row map (temporal qkv); rows whose means are about their spread; bias and GELU
@@ -335,12 +336,17 @@ def test_gemm_lnx(B, Np, T, epi):
     b64 = back(lin.bias.detach()).astype(np.float64)
     lnx = _ln_ref(x.astype(np.float64), back(ln.weight.detach()), back(ln.bias.detach()))
     patch = (np.arange(R) // (Np * T)) * L + 1 + np.arange(R) % (Np * T)
+    from dsvt import _lib
     for M, rowmap, src in ((rows, None, np.arange(rows)), (R, (Np * T, L, 1), patch)):
         outs = []
-        for _ in range(2):
-            out = torch.full((M, N), float("nan"), device=dev(), dtype=torch.bfloat16)
-            ops.gemm_lnx(xb, st, ln.eps, folded, out, M, in_rowmap=rowmap, epilogue=epi)
-            outs.append(out)
+        _lib.call("dsvt_set_gemm_variant", variant)
+        try:
+            for _ in range(2):
+                out = torch.full((M, N), float("nan"), device=dev(), dtype=torch.bfloat16)
+                ops.gemm_lnx(xb, st, ln.eps, folded, out, M, in_rowmap=rowmap, epilogue=epi)
+                outs.append(out)
+        finally:
+            _lib.call("dsvt_set_gemm_variant", 0)
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1])
         ref = lnx[src] @ w64.T + b64
@@ -415,7 +421,7 @@ def test_qkv_temporal_attn(B, Np):
 
 
 @pytest.mark.parametrize("B,Np,T", [(2, 5, 3), (16, 196, 8), (48, 36, 8)])
-@pytest.mark.parametrize("variant", [0, 30, 1, 10])
+@pytest.mark.parametrize("variant", [0, 30, 1, 10, 40])
 def test_gemm_resid_stats(B, Np, T, variant):
     """dsvt_gemm_resid_stats_fwd: the residual update exactly as the plain residual GEMM on the
     same kernel (bitwise; the 256x256 one, or the 256x192 one forced), and for every updated row

@@ -323,3 +323,11 @@ def test_swin_trainer_steps_bf16():
         if p.requires_grad and k in seen:
             assert not torch.equal(p.detach(), p0[k]), k
     assert any(not torch.equal(p.detach(), t0[k]) for k, p in teacher.named_parameters())
+    # the relative-position bias cache must not grow with the steps (AdamW and the
+    # EMA bump every table's version); after the first step every entry is recomputed in place
+    sizes = []
+    for it in (6, 7, 0, 1):
+        tr.step(crops, it)
+        torch.cuda.synchronize()
+        sizes.append((len(student.backbone._aux), len(teacher.backbone._aux)))
+    assert len(set(sizes)) == 1, sizes

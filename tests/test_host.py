@@ -154,3 +154,30 @@ def test_trainer_schedules_match_reference_run():
     np.testing.assert_allclose(tr.lr_schedule, gold["lr"], rtol=1e-12)
     np.testing.assert_allclose(tr.wd_schedule, gold["wd"], rtol=1e-12)
     np.testing.assert_allclose(tr.momentum_schedule, gold["momentum"], rtol=1e-12)
+
+
+def test_teacher_step_settings_are_scoped():
+    """DINOTrainer's teacher-call settings (no stream split, no temporal fc fold) hold only inside
+    the call and are restored after it, also when the call raises."""
+    from dsvt.trainer import _TeacherStepSettings
+
+    class BB(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.dsvt_streams, self.fold_temporal_fc = "auto", True
+
+    class Wrap(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.backbone = BB()
+    t = Wrap()
+    ts = _TeacherStepSettings(t)
+    with ts:
+        assert t.backbone.dsvt_streams == 1 and t.backbone.fold_temporal_fc is False
+    assert t.backbone.dsvt_streams == "auto" and t.backbone.fold_temporal_fc is True
+    try:
+        with ts:
+            raise RuntimeError("inside")
+    except RuntimeError:
+        pass
+    assert t.backbone.dsvt_streams == "auto" and t.backbone.fold_temporal_fc is True
