@@ -94,6 +94,20 @@ __device__ __forceinline__ void w4_mfma(fv4& c, const sv8& a, const sv8& b) {
 __device__ __forceinline__ void w4_mfma0(fv4& c, const sv8& a, const sv8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
 }
+// untracked global loads (inline asm): the compiler's own wait for a tracked load issued after
+// LDS-DMA is vmcnt(0) -- it does not count the DMA in order with loads -- which drains every stage
+// in flight; these are waited for by a counted w4_vm_wait at their use instead
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v_t w4_gld2(const void* a) {
+  f2v_t r;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ fv4 w4_gld4(const void* a) {
+  fv4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(a));
+  return r;
+}
 // chunk position of row-quad q (rows 4q .. 4q+3 of a 16-row block): swz = {0, 2, 3, 1}
 __device__ __forceinline__ int w4_swz(int q) { return (0x78 >> (2 * q)) & 3; }
 
@@ -119,7 +133,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
   constexpr bool CLAMPED = NFULL && (EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32;
   // post-epilogue boundary waits: 0 = the 32 store instructions of the CLAMPED path counted in,
   // 1 = the epilogue loaded (and so waited for every older stage): no wait, 2 = conservative
-  constexpr int POST = (FUSE == 0 && CLAMPED) ? 0 : (FUSE != 0 || EPI == EPI_RESID) ? 1 : 2;
+  // (FUSE 1: its statistics / wsum / bias loads are prefetched in the tile's last step and consumed
+  // before the epilogue's stores, so it is mode 0 too)
+  constexpr int POST = ((FUSE == 0 || FUSE == 1) && CLAMPED) ? 0 : (FUSE == 2 || EPI == EPI_RESID) ? 1 : 2;
   constexpr int S_EPI = 32;
   __shared__ __attribute__((aligned(16))) char smem[W4_NBUF * W4_STAGE];
 
@@ -214,9 +230,43 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
 
   int post = 0;                          // boundaries left that follow an epilogue's stores
 
+  // FUSE 1: the epilogue's loads (the rows' 3 LN partials per lane group, wsum and the folded bias
+  // of the wave's columns), issued at the start of the tile's last step -- BEFORE that step's DMA
+  // -- so waiting for them drains no stage the DMA issued since (an epilogue load after them
+  // drained all NBUF - 1 stages in flight, like every load in the 256x256 kernel's epilogue)
+  f2v_t pst[8][3];
+  fv4 pws[2][4], pbf[2][4];
+  auto prefetch = [&](int64_t rbase, int64_t cbase) {
+    if constexpr (FUSE == 1) {
+      int le;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(le));
+      const int r16e = le & 15, ge = le >> 4;
+      const uint32_t a_rpg = (uint32_t)(p.a_rpg < p.M ? p.a_rpg : p.M), a_gs = (uint32_t)p.a_gstride;
+      const uint32_t a_go = (uint32_t)p.a_goff, mlast = (uint32_t)(p.M - 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t m = (uint32_t)(rbase + i * 16 + r16e);
+        m = m < mlast ? m : mlast;
+        const uint32_t xr = (m / a_rpg) * a_gs + a_go + m % a_rpg;   // rows < 2^31 (host-checked)
+        const float2* sp = reinterpret_cast<const float2*>(p.ln_stats) + (uint64_t)(xr * LN_PARTS + 3 * ge);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pst[i][k] = w4_gld2(sp + k);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t n = cbase + h * 64 + j * 16 + 4 * ge;
+          pws[h][j] = w4_gld4(p.ln_wsum + n);
+          pbf[h][j] = w4_gld4(p.bias + n);
+        }
+    }
+  };
+
   // one step: boundary, then 64 MFMAs on (FA, FB) with stage u + 1's reads into (NA, NB) and
   // stage u + NBUF's DMA into stage u's buffer interleaved
-  auto step = [&](auto first, auto rd, int u, sv8 (&FA)[8], sv8 (&FB)[8], sv8 (&NA)[8], sv8 (&NB)[8]) {
+  auto step = [&](auto first, auto rd, int u, sv8 (&FA)[8], sv8 (&FB)[8], sv8 (&NA)[8], sv8 (&NB)[8],
+                  int64_t pre_r = -1, int64_t pre_c = 0) {
     if (POST == 0 && post > 0) {
       --post;
       w4_vm_wait<W4_VM + S_EPI>();
@@ -227,6 +277,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
     }
     w4_tie(FA, FB);
     w4_barrier();
+    if constexpr (!decltype(rd)::value) {  // the tile's last step: the epilogue's loads
+      prefetch(pre_r, pre_c);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const int nbuf = (u + 1) % W4_NBUF, dbuf = u % W4_NBUF;
     const uint32_t na = rdA + (uint32_t)(nbuf * W4_STAGE), nb = rdB + (uint32_t)(nbuf * W4_STAGE);
     w4_for<64>([&](auto nc) {
@@ -260,8 +314,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
     }
     // the tile's last step leaves the next stage's fragments to after the epilogue (the
     // epilogue gets the 128 fragment registers)
+    int64_t m0, n0;
+    tile_mn(tlc, m0, n0);
     step(F_{}, T_{}, u, fa0, fb0, fa1, fb1);
-    step(F_{}, F_{}, u + 1, fa1, fb1, fa0, fb0);
+    step(F_{}, F_{}, u + 1, fa1, fb1, fa0, fb0, m0 + wr * 128, n0 + wc * 128);
     u += 2;
     // tile done: register epilogue.  Its lane constants come from an opaque copy of the lane id,
     // so the compiler cannot hoist their (row-map, address) arithmetic out of the tile loop and
@@ -269,8 +325,6 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
     int lane_e;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
     const int r16 = lane_e & 15, g = lane_e >> 4;
-    int64_t m0, n0;
-    tile_mn(tlc, m0, n0);
     const int64_t rbase = m0 + wr * 128, cbase = n0 + wc * 128;
     mfma_result_fence();
     if constexpr ((ABL & 16) != 0) {
@@ -284,7 +338,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
       // the bias is not in the accumulators (every tile starts from C = 0): added a row at a time
       // as the rows are formed (one row's accumulators live in VGPRs at a time)
       auto bias_of = [&](int64_t cb, float4 (&b4)[4]) {
-        if (cb + 64 <= p.N) {
+        // N % 256 == 0 (CLAMPED): always the scalar-load path.  A vector load on a path not taken
+        // left pending at the join made the compiler drain vmcnt(0) -- every in-flight DMA stage --
+        // in each epilogue half (33 of 102 us at the qkv shape)
+        if (CLAMPED || cb + 64 <= p.N) {
           bias_frag4(p.bias, cb, g, b4);
         } else {
 #pragma unroll
@@ -294,9 +351,106 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
           }
         }
       };
+      auto bias_f4 = [&](int64_t cb, float4 (&b4)[4]) { bias_frag4(p.bias, cb, g, b4); };
+      // FUSE 2 on a tile full in M (N % 256 == 0): the residual update X[row] += acc + bias, its
+      // bf16 copy and LN partials (resid_stats_rows' arithmetic, bitwise), with the X loads as
+      // untracked asm (a rolling window of W4_XW rows) and counted waits: the compiler's own waits
+      // for them were vmcnt(0), 17 per tile.  Per row: 4 loads, then 7 stores (4 X, 2 bf16, 1 stats).
+      auto resid_stats_full = [&](fv4 (&a)[8][4], int64_t rb, int64_t cb, int r16x, int gx, const float4 (&b4)[4]) {
+        constexpr int XW = 3;
+        int64_t rpg = p.rpg;
+        asm volatile("" : "+s"(rpg));
+        const bool ident = rpg >= p.M && p.goff == 0;
+        const int part = (int)(cb >> 6);
+        const float* xs = resid_src(p);
+        auto orow_of = [&](int i) -> int64_t {
+          const int64_t m = rb + i * 16 + r16x;
+          return ident ? m : map_row(m, rpg, p.gstride, p.goff);
+        };
+        fv4 x[XW][4];
+        auto load_row = [&](int i) {
+          const float* src = xs + orow_of(i) * p.ldo + cb + 4 * gx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[i % XW][j] = w4_gld4(src + j * 16);
+        };
+#pragma unroll
+        for (int i = 0; i < XW; ++i) load_row(i);
+        w4_for<8>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          // VMEM ops issued after row i's loads when row i is consumed: the loads of rows i+1 ..
+          // min(i+XW-1, 7) (4 each) and the 7 stores of each row k < i issued after them -- rows
+          // 0 .. i-1 for a prologue row (i < XW), else the XW rows i-XW .. i-1 (row i's loads were
+          // issued in row i-XW, before its stores).  Extra ops only make the wait longer.
+          constexpr int later_loads = 4 * ((i + XW - 1 < 8 ? i + XW - 1 : 7) - i);
+          constexpr int later_stores = 7 * (i < XW ? i : XW);
+          w4_vm_wait<later_loads + later_stores>();
+          asm volatile("" : "+v"(x[i % XW][0]), "+v"(x[i % XW][1]), "+v"(x[i % XW][2]), "+v"(x[i % XW][3]));
+          const int64_t orow = orow_of(i);
+          fv4 v[4];
+          float sm = 0.f, q = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const fv4 xv = x[i % XW][j];
+            fv4 av = a[i][j];
+            av += fv4{b4[j].x, b4[j].y, b4[j].z, b4[j].w};
+            v[j] = fv4{xv[0] + av[0], xv[1] + av[1], xv[2] + av[2], xv[3] + av[3]};
+            sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+            q += sumsq4(v[j][0], v[j][1], v[j][2], v[j][3]);
+          }
+          if constexpr (i + XW < 8) load_row(i + XW);
+          sm = sum_lane_groups(sm);
+          q = sum_lane_groups(q);
+          float* dst = (float*)p.out + orow * p.ldo + cb + 4 * gx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) *reinterpret_cast<fv4*>(dst + j * 16) = v[j];
+          bf16_t* xbo = (bf16_t*)p.xb_out + orow * p.ldo + cb;
+          store_pair_bf16(xbo, v[0], v[1], gx);
+          store_pair_bf16(xbo + 32, v[2], v[3], gx);
+          *reinterpret_cast<float2*>(p.stats_out + (orow * LN_PARTS + part) * 2) = make_float2(sm, q);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      };
       if constexpr (FUSE == 1) {
-        ln_affine<8, 4>(p, acc[0], rbase, cbase, r16, g);
-        ln_affine<8, 4>(p, acc[1], rbase, cbase + 64, r16, g);
+        // acc <- rstd * (acc - mu * wsum[n]) + bias_f[n] (ln_affine, on the prefetched loads): wait
+        // for them -- only the last step's 8 DMA ops were issued after them -- tied to every value
+        asm volatile("s_waitcnt vmcnt(%24)"
+                     : "+v"(pst[0][0]), "+v"(pst[0][1]), "+v"(pst[0][2]), "+v"(pst[1][0]), "+v"(pst[1][1]),
+                       "+v"(pst[1][2]), "+v"(pst[2][0]), "+v"(pst[2][1]), "+v"(pst[2][2]), "+v"(pst[3][0]),
+                       "+v"(pst[3][1]), "+v"(pst[3][2]), "+v"(pst[4][0]), "+v"(pst[4][1]), "+v"(pst[4][2]),
+                       "+v"(pst[5][0]), "+v"(pst[5][1]), "+v"(pst[5][2]), "+v"(pst[6][0]), "+v"(pst[6][1]),
+                       "+v"(pst[6][2]), "+v"(pst[7][0]), "+v"(pst[7][1]), "+v"(pst[7][2])
+                     : "i"((ABL & 2) ? 0 : 8));
+        asm volatile("" : "+v"(pws[0][0]), "+v"(pws[0][1]), "+v"(pws[0][2]), "+v"(pws[0][3]), "+v"(pws[1][0]),
+                          "+v"(pws[1][1]), "+v"(pws[1][2]), "+v"(pws[1][3]), "+v"(pbf[0][0]), "+v"(pbf[0][1]),
+                          "+v"(pbf[0][2]), "+v"(pbf[0][3]), "+v"(pbf[1][0]), "+v"(pbf[1][1]), "+v"(pbf[1][2]),
+                          "+v"(pbf[1][3]));
+        __builtin_amdgcn_sched_barrier(0);
+        const float invk = p.ln_invk;
+        float mu[8], rs[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float sm = (pst[i][0].x + pst[i][1].x) + pst[i][2].x;
+          float q = (pst[i][0].y + pst[i][1].y) + pst[i][2].y;
+          sm = sum_lane_groups(sm);
+          q = sum_lane_groups(q);
+          const float m_ = sm * invk;
+          const float var = fmaxf(__builtin_fmaf(-m_, m_, q * invk), 0.f);   // explicit: no contraction freedom
+          rs[i] = 1.0f / sqrtf(var + p.ln_eps);
+          mu[i] = -m_ * rs[i];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const fv4 w4 = pws[h][j], b4 = pbf[h][j];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              acc[h][i][j][0] = fmaf(rs[i], acc[h][i][j][0], fmaf(mu[i], w4[0], b4[0]));
+              acc[h][i][j][1] = fmaf(rs[i], acc[h][i][j][1], fmaf(mu[i], w4[1], b4[1]));
+              acc[h][i][j][2] = fmaf(rs[i], acc[h][i][j][2], fmaf(mu[i], w4[2], b4[2]));
+              acc[h][i][j][3] = fmaf(rs[i], acc[h][i][j][3], fmaf(mu[i], w4[3], b4[3]));
+            }
+          }
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -304,8 +458,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
         const int64_t cb = cbase + 64 * h;
         if constexpr (FUSE == 2) {
           float4 b4[4];
-          bias_of(cb, b4);
-          epilogue_resid_stats<8, 4, DSVT_STATS_W, true>(p, acc[h], rbase, cb, r16, g, b4);
+          bias_f4(cb, b4);
+          if (rbase + 128 <= p.M) resid_stats_full(acc[h], rbase, cb, r16, g, b4);
+          else epilogue_resid_stats<8, 4, DSVT_STATS_W, true>(p, acc[h], rbase, cb, r16, g, b4);
         } else if constexpr (CLAMPED) {
           // bias / GELU, bf16 out, N % 256 == 0: 16-byte pair stores, rows past M clamped to M - 1
           // (their accumulators are row M - 1's: identical rewrites)
@@ -374,6 +529,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
 // bf16 output and N % 256 == 0 (the 16-byte store path), or the fp32 residual
 bool gemm_4w_ok(const GemmParams& p, int epi, int out_f32) {
   const bool nfull_bf16 = (epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.N % 256 == 0;
+  if (p.stats_out && p.N % 256) return false;          // the 128-column wave slab of the stats epilogue
   return p.K >= 32 * W4_NBUF && p.K % 64 == 0 && p.M >= 1 && p.N >= 1 && (nfull_bf16 || epi == EPI_RESID) &&
          !p.row_scale && (p.M - 1) * p.lda * 2 + p.K * 2 <= (int64_t)UINT32_MAX &&
          (p.N - 1) * p.ldw * 2 + p.K * 2 <= (int64_t)UINT32_MAX;
@@ -405,7 +561,7 @@ hipError_t launch_gemm_4w(const GemmParams& p, int epi, int out_f32, hipStream_t
     return hipGetLastError();
   }
   if (p.stats_out) {                                  // residual + LN inputs (dsvt_gemm_resid_stats_fwd)
-    if (epi != EPI_RESID || !p.xb_out || p.N % 128) return hipErrorInvalidValue;
+    if (epi != EPI_RESID || !p.xb_out || p.N % 256) return hipErrorInvalidValue;
     gemm_4w_kernel<EPI_RESID, true, 0, false, 2><<<grid, block, 0, s>>>(p);
     return hipGetLastError();
   }

@@ -456,8 +456,45 @@ def test_frame_scores_vitb_local3_global30(base_sd, dtype, tol):
         assert mismatched == 0           # parity mode: the reference's frames exactly
     else:
         # bf16 perf mode: the selector's CDF thresholds move a few picks to a neighbouring frame
-        # (measured 8 of 128, DESIGN.md "Frame scoring"); none further than one frame
-        assert mismatched <= 16 and worst <= 1, (mismatched, worst)
+        # (measured 8 of 128 on this video, DESIGN.md "Frame scoring"); none further than one frame.
+        # The bound is the one the bench video is held to below (<= 12 of 128 = 9.4 %, one frame).
+        assert mismatched <= 12 and worst <= 1, (mismatched, worst)
+
+
+def test_frame_pick_mismatch_bench_video():
+    """the bf16 picks on the bench's OWN frame-scoring video (bench.py
+    other_configs: random-init ViT-B under torch seed 2, F = 64 frames of torch.randn, local 3 /
+    global 30, rates 1 and 4, N = 4 .. 24 picks) against the fp32 parity mode's picks of the same
+    video -- the number the bench line reports as picks_moved_vs_fp32 -- held to the same bound as
+    the reference-weight video above (<= 12 of 128, one frame), and printed."""
+    from functools import partial
+
+    import torch.nn as nn
+    from dsvt.models.timesformer import VisionTransformer
+    from dsvt.scoring import FrameScorer
+    from dsvt.selection import adaptive_frame_indices
+    torch.manual_seed(2)
+    fm = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
+                           norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=8,
+                           attention_type="divided_space_time").cuda().eval()
+    video = torch.randn(64, 3, 224, 224, device="cuda")
+    scorer = FrameScorer(fm, local_clip_size=3, global_clip_size=30)
+    with torch.no_grad():
+        fm.dsvt_dtype = torch.bfloat16
+        s_bf = scorer.score(video).clone()
+        fm.dsvt_dtype = torch.float32
+        s_32 = scorer.score(video).clone()
+    picked = moved = worst = 0
+    for rate in (1, 4):
+        for n_pick in (4, 8, 12, 16, 24):
+            want, _ = adaptive_frame_indices(s_32, 64, 64 * rate, rate, n_pick)
+            got, _ = adaptive_frame_indices(s_bf, 64, 64 * rate, rate, n_pick)
+            want, got = np.asarray(want, np.int64), np.asarray(got, np.int64)
+            picked += n_pick
+            moved += int(np.sum(got != want))
+            worst = max(worst, float(np.max(np.abs(got - want))) / rate)
+    print("bench video: bf16 moved %d of %d picks vs fp32 (max shift %g frames)" % (moved, picked, worst))
+    assert picked == 128 and moved <= 12 and worst <= 1, (moved, worst)
 
 
 @pytest.mark.parametrize("clips", [4, 16])
