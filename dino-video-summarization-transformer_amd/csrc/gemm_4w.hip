@@ -137,6 +137,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
   // before the epilogue's stores, so it is mode 0 too)
   constexpr int POST = ((FUSE == 0 || FUSE == 1) && CLAMPED) ? 0 : (FUSE == 2 || EPI == EPI_RESID) ? 1 : 2;
   constexpr int S_EPI = 32;
+  // the bias comes in by the last step's prefetch (untracked loads, one counted wait) wherever the
+  // wave's 128 columns are inside N: the scalar-load path (bias_frag4) serialized ~32 scalar
+  // cache round trips per epilogue (30 of 101 us at the qkv shape)
+  constexpr bool PRE_BIAS = CLAMPED || FUSE == 2;
   __shared__ __attribute__((aligned(16))) char smem[W4_NBUF * W4_STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -237,10 +241,17 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
   f2v_t pst[8][3];
   fv4 pws[2][4], pbf[2][4];
   auto prefetch = [&](int64_t rbase, int64_t cbase) {
+    int le;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(le));
+    const int ge = le >> 4;
+    if constexpr (FUSE != 1 && PRE_BIAS) {   // the bias of the wave's 128 columns (N % 256 == 0;
+#pragma unroll                             // gemm_4w_ok: a bias is present -- no branch around the loads)
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pbf[h][j] = w4_gld4(p.bias + cbase + h * 64 + j * 16 + 4 * ge);
+    }
     if constexpr (FUSE == 1) {
-      int le;
-      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(le));
-      const int r16e = le & 15, ge = le >> 4;
+      const int r16e = le & 15;
       const uint32_t a_rpg = (uint32_t)(p.a_rpg < p.M ? p.a_rpg : p.M), a_gs = (uint32_t)p.a_gstride;
       const uint32_t a_go = (uint32_t)p.a_goff, mlast = (uint32_t)(p.M - 1);
 #pragma unroll
@@ -277,7 +288,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
     }
     w4_tie(FA, FB);
     w4_barrier();
-    if constexpr (!decltype(rd)::value) {  // the tile's last step: the epilogue's loads
+    // the tile's last step: the epilogue's loads (never in a build without the epilogue: an
+    // untracked load must be waited for before its registers can be reused -- the ABL 16 build
+    // that prefetched into dead registers faulted on the GPU)
+    if constexpr (!decltype(rd)::value && (ABL & 16) == 0) {
       prefetch(pre_r, pre_c);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -351,7 +365,17 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
           }
         }
       };
-      auto bias_f4 = [&](int64_t cb, float4 (&b4)[4]) { bias_frag4(p.bias, cb, g, b4); };
+      if constexpr (FUSE != 1 && PRE_BIAS) {   // the prefetched bias: only the last step's 8 DMA ops came after it
+        asm volatile("s_waitcnt vmcnt(%8)"
+                     : "+v"(pbf[0][0]), "+v"(pbf[0][1]), "+v"(pbf[0][2]), "+v"(pbf[0][3]), "+v"(pbf[1][0]),
+                       "+v"(pbf[1][1]), "+v"(pbf[1][2]), "+v"(pbf[1][3])
+                     : "i"((ABL & 2) ? 0 : 8));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      auto bias_f4 = [&](int h, float4 (&b4)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b4[j] = make_float4(pbf[h][j][0], pbf[h][j][1], pbf[h][j][2], pbf[h][j][3]);
+      };
       // FUSE 2 on a tile full in M (N % 256 == 0): the residual update X[row] += acc + bias, its
       // bf16 copy and LN partials (resid_stats_rows' arithmetic, bitwise), with the X loads as
       // untracked asm (a rolling window of W4_XW rows) and counted waits: the compiler's own waits
@@ -458,9 +482,13 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
         const int64_t cb = cbase + 64 * h;
         if constexpr (FUSE == 2) {
           float4 b4[4];
-          bias_f4(cb, b4);
+          bias_f4(h, b4);
           if (rbase + 128 <= p.M) resid_stats_full(acc[h], rbase, cb, r16, g, b4);
-          else epilogue_resid_stats<8, 4, DSVT_STATS_W, true>(p, acc[h], rbase, cb, r16, g, b4);
+          else {                          // an M-edge tile (rows past M): the shared epilogue, an
+            GemmParams pe = p;            // opaque row-map divisor (not hoisted into the K loop)
+            asm volatile("" : "+s"(pe.rpg));
+            epilogue_resid_stats<8, 4, DSVT_STATS_W, true>(pe, acc[h], rbase, cb, r16, g, b4);
+          }
         } else if constexpr (CLAMPED) {
           // bias / GELU, bf16 out, N % 256 == 0: 16-byte pair stores, rows past M clamped to M - 1
           // (their accumulators are row M - 1's: identical rewrites)
@@ -469,7 +497,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) b4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
           } else {
-            bias_of(cb, b4);
+            bias_f4(h, b4);
           }
           // (an opaque copy of the row map: its division constants are formed here, per tile, not
           // hoisted out of the tile loop and held -- or spilled -- through the K loop)
@@ -525,12 +553,14 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
   w4_vm_wait<0>();                        // no LDS-DMA may land after the workgroup has left
 }
 
-// K a multiple of 64 with at least NBUF stages, 32-bit LDS-DMA source offsets; bias / GELU with a
-// bf16 output and N % 256 == 0 (the 16-byte store path), or the fp32 residual
+// K a multiple of 64 with at least NBUF stages, 32-bit LDS-DMA source offsets, a bias (prefetched
+// unconditionally); bias / GELU with a bf16 output and N % 256 == 0 (the 16-byte store path), or
+// the fp32 residual
 bool gemm_4w_ok(const GemmParams& p, int epi, int out_f32) {
   const bool nfull_bf16 = (epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.N % 256 == 0;
   if (p.stats_out && p.N % 256) return false;          // the 128-column wave slab of the stats epilogue
   return p.K >= 32 * W4_NBUF && p.K % 64 == 0 && p.M >= 1 && p.N >= 1 && (nfull_bf16 || epi == EPI_RESID) &&
+         p.bias != nullptr &&
          !p.row_scale && (p.M - 1) * p.lda * 2 + p.K * 2 <= (int64_t)UINT32_MAX &&
          (p.N - 1) * p.ldw * 2 + p.K * 2 <= (int64_t)UINT32_MAX;
 }
