@@ -451,6 +451,15 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (p.stats_out && (gv == 1 || (gv == 0 && DSVT_RESID_STATS_V == 1)) && p.N % 128 == 0) return 1;
   if (p.stats_out && (gv == 10 || (gv == 0 && DSVT_RESID_STATS_V == 10)) && p.N % 128 == 0) return 10;
   if (gv >= 40 && gv <= 49) return gemm_4w_ok(p, epi, out_f32) ? gv : (p.ln_stats || p.stats_out) ? 20 : 1;
+  // the 4-wave 256x256 kernel (gemm_4w.hip, r06) where it takes the call: the LayerNorm-folded
+  // qkv / fc1, the residual + LN-statistics GEMMs and the plain bias / GELU GEMMs below --
+  // tools/gemm4w_bench.py, same box: lnx qkv 97.0 vs 110.8 us, lnx fc1 137.2 vs 157.5, qkv 90.7 vs
+  // 106.8, fc1 125.7 vs 140.8, proj + stats 76.1 vs 80.2, fc2 + stats 174.8 vs 173.4 (global rows)
+#ifndef DSVT_GEMM4W
+#define DSVT_GEMM4W 1
+#endif
+  const bool use4w = DSVT_GEMM4W && gv == 0 && p.M >= 4096 && gemm_4w_ok(p, epi, out_f32);
+  if ((p.ln_stats || p.stats_out) && use4w) return 40;
   if (p.ln_stats || p.stats_out) return 20;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
@@ -490,7 +499,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
     const int64_t mt = (p.M + 255) / 256;
     const int64_t c256 = (mt * ((p.N + 255) / 256) + 255) / 256 * 256, c192 = (mt * (p.N / 192) + 255) / 256 * 192;
     if (gv == 0 && gemm_192_ok(p, epi) && c192 * 5 < c256 * 4) return 30;
-    return 20;
+    return use4w ? 40 : 20;
   }
   // fp32 residual GEMMs (N = 768: proj / temporal fc / fc2): the 256x256 kernel.  ALONE it is
   // the slower one (proj 73.6 vs 57.6 us, fc2 165 vs 138 us against the 128x128 kernel: 297

@@ -7,11 +7,11 @@ cd "$(dirname "$0")/../dino-video-summarization-transformer_amd/csrc"
 make -s
 FLAGS="$1"
 rm -rf build/ab; mkdir -p build/ab ../../tools/ab_lib   # no stale objects of an earlier A/B
-for f in ${AB_SRCS:-gemm gemm_big gemm_8ph gemm_192}; do
+for f in ${AB_SRCS:-gemm gemm_big gemm_8ph gemm_4w gemm_192}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS -c $f.hip -o build/ab/$f.o
 done
 objs=""
-for f in gemm wgrad gemm_big gemm_8ph gemm_192 norm attention attn_flash dino_loss head_bn backward swin swin_bwd select augment capi; do
+for f in gemm wgrad gemm_big gemm_8ph gemm_4w gemm_192 norm attention attn_flash dino_loss head_bn backward swin swin_bwd select augment capi; do
   if [ -f build/ab/$f.o ]; then objs="$objs build/ab/$f.o"; else objs="$objs build/$f.o"; fi
 done
 NAME=${2:-ab}
