@@ -135,7 +135,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
   // 1 = the epilogue loaded (and so waited for every older stage): no wait, 2 = conservative
   // (FUSE 1: its statistics / wsum / bias loads are prefetched in the tile's last step and consumed
   // before the epilogue's stores, so it is mode 0 too)
-  constexpr int POST = ((FUSE == 0 || FUSE == 1) && CLAMPED) ? 0 : (FUSE == 2 || EPI == EPI_RESID) ? 1 : 2;
+  // (plain EPI_RESID: 2 -- a wave whose 128 rows all lie past M loads nothing, so nothing of its
+  // epilogue drains the stages in flight)
+  constexpr int POST = ((FUSE == 0 || FUSE == 1) && CLAMPED) ? 0 : FUSE == 2 ? 1 : 2;
   constexpr int S_EPI = 32;
   // the bias comes in by the last step's prefetch (untracked loads, one counted wait) wherever the
   // wave's 128 columns are inside N: the scalar-load path (bias_frag4) serialized ~32 scalar
