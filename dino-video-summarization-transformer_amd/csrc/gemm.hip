@@ -452,13 +452,19 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (p.stats_out && (gv == 10 || (gv == 0 && DSVT_RESID_STATS_V == 10)) && p.N % 128 == 0) return 10;
   if (gv >= 40 && gv <= 49) return gemm_4w_ok(p, epi, out_f32) ? gv : (p.ln_stats || p.stats_out) ? 20 : 1;
   // the 4-wave 256x256 kernel (gemm_4w.hip, r06) where it takes the call: the LayerNorm-folded
-  // qkv / fc1, the residual + LN-statistics GEMMs and the plain bias / GELU GEMMs below --
-  // tools/gemm4w_bench.py, same box: lnx qkv 97.0 vs 110.8 us, lnx fc1 137.2 vs 157.5, qkv 90.7 vs
-  // 106.8, fc1 125.7 vs 140.8, proj + stats 76.1 vs 80.2, fc2 + stats 174.8 vs 173.4 (global rows)
+  // qkv / fc1 and the plain bias / GELU GEMMs below -- tools/gemm4w_bench.py, same box: lnx qkv
+  // 97.0 vs 110.8 us, lnx fc1 137.2 vs 157.5, qkv 90.7 vs 106.8, fc1 125.7 vs 140.8 (global rows);
+  // fwd+loss (tools/r5_ab.sh, two interleaved rounds) 410.0 / 408.7 clips/s with the folded GEMMs on
+  // it vs 405.3 / 404.8 without.  The residual + statistics GEMMs stay on the 8-wave kernel: alone
+  // on par (proj + stats 76.1 vs 80.2 us, fc2 + stats 174.8 vs 173.4), in the step 397.0 / 397.6
+  // with them on the 4-wave kernel -- its epilogue keeps fewer X loads in flight per CU
 #ifndef DSVT_GEMM4W
-#define DSVT_GEMM4W 1
+#define DSVT_GEMM4W 5
 #endif
-  const bool use4w = DSVT_GEMM4W && gv == 0 && p.M >= 4096 && gemm_4w_ok(p, epi, out_f32);
+  // (A/B builds: DSVT_GEMM4W is a mask -- 1 the LayerNorm-folded GEMMs, 2 the residual + statistics
+  // GEMMs, 4 the plain bias / GELU GEMMs)
+  const bool use4w = DSVT_GEMM4W && gv == 0 && p.M >= 4096 && gemm_4w_ok(p, epi, out_f32) &&
+                     (DSVT_GEMM4W & (p.ln_stats ? 1 : p.stats_out ? 2 : 4));
   if ((p.ln_stats || p.stats_out) && use4w) return 40;
   if (p.ln_stats || p.stats_out) return 20;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
