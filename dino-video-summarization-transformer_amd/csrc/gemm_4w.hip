@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
       // untracked asm (a rolling window of W4_XW rows) and counted waits: the compiler's own waits
       // for them were vmcnt(0), 17 per tile.  Per row: 4 loads, then 7 stores (4 X, 2 bf16, 1 stats).
       auto resid_stats_full = [&](fv4 (&a)[8][4], int64_t rb, int64_t cb, int r16x, int gx, const float4 (&b4)[4]) {
-        constexpr int XW = 3;
+        constexpr int XW = 4;
         int64_t rpg = p.rpg;
         asm volatile("" : "+s"(rpg));
         const bool ident = rpg >= p.M && p.goff == 0;
