@@ -527,7 +527,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 #define DSVT_DX192 0
 #endif
   if (DSVT_DX192 && epi == EPI_BIAS && !out_f32 && big8 && gemm_192_ok(p, epi)) return 30;
-  if (epi == EPI_BIAS && p.N < 1024) return (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
+  if (epi == EPI_BIAS && p.N < 1024) return (big8 && use4w) ? 40 : (big8 && gemm_8ph_ok(p, epi)) ? 20 : 1;
   return (p.M >= 2048 && p.N % 128 == 0 && p.K <= 1024) ? 10 : 1;
 }
 

@@ -246,11 +246,15 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
     int le;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(le));
     const int ge = le >> 4;
-    if constexpr (FUSE != 1 && PRE_BIAS) {   // the bias of the wave's 128 columns (N % 256 == 0;
-#pragma unroll                             // gemm_4w_ok: a bias is present -- no branch around the loads)
+    if constexpr (FUSE != 1 && PRE_BIAS) {   // the bias of the wave's 128 columns (N % 256 == 0).
+      // No branch around the loads (a join would let the compiler copy a pending register): without
+      // a bias they read W's first N floats (valid memory: N * K bf16 >= N floats) and the epilogue
+      // selects zeros
+      const float* bsrc = p.bias ? p.bias : (const float*)p.W;
+#pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) pbf[h][j] = w4_gld4(p.bias + cbase + h * 64 + j * 16 + 4 * ge);
+        for (int j = 0; j < 4; ++j) pbf[h][j] = w4_gld4(bsrc + cbase + h * 64 + j * 16 + 4 * ge);
     }
     if constexpr (FUSE == 1) {
       const int r16e = le & 15;
@@ -374,9 +378,12 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
                      : "i"((ABL & 2) ? 0 : 8));
         __builtin_amdgcn_sched_barrier(0);
       }
+      const bool has_bias = p.bias != nullptr;   // kernel-argument uniform: a select, no branch
       auto bias_f4 = [&](int h, float4 (&b4)[4]) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b4[j] = make_float4(pbf[h][j][0], pbf[h][j][1], pbf[h][j][2], pbf[h][j][3]);
+        for (int j = 0; j < 4; ++j)
+          b4[j] = has_bias ? make_float4(pbf[h][j][0], pbf[h][j][1], pbf[h][j][2], pbf[h][j][3])
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
       };
       // FUSE 2 on a tile full in M (N % 256 == 0): the residual update X[row] += acc + bias, its
       // bf16 copy and LN partials (resid_stats_rows' arithmetic, bitwise), with the X loads as
@@ -555,14 +562,14 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmParams p) {
   w4_vm_wait<0>();                        // no LDS-DMA may land after the workgroup has left
 }
 
-// K a multiple of 64 with at least NBUF stages, 32-bit LDS-DMA source offsets, a bias (prefetched
-// unconditionally); bias / GELU with a bf16 output and N % 256 == 0 (the 16-byte store path), or
-// the fp32 residual
+// K a multiple of 64 with at least NBUF stages, 32-bit LDS-DMA source offsets; bias / GELU with a
+// bf16 output and N % 256 == 0 (the 16-byte store path; a bias or none: prefetched unconditionally),
+// or the fp32 residual (with a bias unless the statistics epilogue)
 bool gemm_4w_ok(const GemmParams& p, int epi, int out_f32) {
   const bool nfull_bf16 = (epi == EPI_BIAS || epi == EPI_GELU) && !out_f32 && p.N % 256 == 0;
   if (p.stats_out && p.N % 256) return false;          // the 128-column wave slab of the stats epilogue
   return p.K >= 32 * W4_NBUF && p.K % 64 == 0 && p.M >= 1 && p.N >= 1 && (nfull_bf16 || epi == EPI_RESID) &&
-         p.bias != nullptr &&
+         (p.bias != nullptr || nfull_bf16 || p.stats_out) &&
          !p.row_scale && (p.M - 1) * p.lda * 2 + p.K * 2 <= (int64_t)UINT32_MAX &&
          (p.N - 1) * p.ldw * 2 + p.K * 2 <= (int64_t)UINT32_MAX;
 }

@@ -115,6 +115,29 @@ def test_gemm_skinny(M, N, K):
         _lib.call("dsvt_set_gemm_variant", 0)
 
 
+@pytest.mark.parametrize("variant", [0, 20, 40])
+@pytest.mark.parametrize("M,N,K", [(4700, 768, 3072), (25104, 768, 2304), (300, 2304, 768)])
+def test_gemm_no_bias_bf16(variant, M, N, K):
+    """bias = None on the bf16 store path (the backward's dX GEMMs, N = 768): the 4-wave kernel
+    prefetches from W then selects zeros -- against float64, and bitwise equal to variant 20 where
+    both run (same K order; no bias to round in)."""
+    from dsvt import _lib, ops
+    a, w = rnd((M, K), 91), rnd((N, K), 92, 0.03)
+    A, W = to(a, torch.bfloat16), to(w, torch.bfloat16)
+    outs = {}
+    for v in sorted({variant, 20}):
+        _lib.call("dsvt_set_gemm_variant", v)
+        try:
+            out = torch.full((M, N), float("nan"), device=dev(), dtype=torch.bfloat16)
+            ops.gemm(A, W, None, out)
+        finally:
+            _lib.call("dsvt_set_gemm_variant", 0)
+        torch.cuda.synchronize()
+        outs[v] = out
+    check(back(outs[variant]), back(A) @ back(W).T, torch.bfloat16, "no-bias v%d" % variant)
+    assert torch.equal(outs[variant], outs[20])
+
+
 @pytest.mark.parametrize("variant", [3, 10, 20, 30])
 @pytest.mark.parametrize("M,N,K", [(8200, 2304, 768), (8200, 2304, 64), (6000, 3072, 128), (25104, 768, 3072),
                                    (6274, 3072, 768), (6274, 768, 3072)])
