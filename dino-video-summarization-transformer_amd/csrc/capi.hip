@@ -603,9 +603,11 @@ int dsvt_center_ema(float* center, const float* colsum, int64_t D, float momentu
 }
 
 int dsvt_set_gemm_variant(int variant) {
-  REQUIRE(variant == 0 || variant == 1 || variant == 3 || variant == 10 || (variant >= 20 && variant <= 29 && variant != 24) ||
-              variant == 30 || (variant >= 40 && variant <= 46 && variant != 43) || variant == 50,
-          "gemm variant must be 0 (auto), 1, 3, 10, 20 (21-29 but 24: ablation builds), 30, 40 (41, 42, 44-46: ablation builds) or 50");
+  REQUIRE(variant == 0 || variant == 1 || variant == 3 || (variant >= 10 && variant <= 15) ||
+              (variant >= 20 && variant <= 29 && variant != 24) || variant == 30 ||
+              (variant >= 40 && variant <= 46 && variant != 43) || variant == 50,
+          "gemm variant must be 0 (auto), 1, 3, 10-15, 20 (21-29 but 24: ablation builds), 30, 40 (41, 42, 44-46: "
+          "ablation builds) or 50");
   set_gemm_variant(variant);
   return 0;
 }

@@ -423,7 +423,7 @@ static thread_local int g_gemm_variant = 0; // 0 = auto; otherwise forced (dsvt_
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
 // Kernel choice (0 = fp32 128x128, 1 = bf16 128x128, 3 = bf16 160x128 (residual epilogue), 10 = persistent staggered 256x128
-// (gemm_big.hip), 20 = 256x256 phase-interleaved (gemm_8ph.hip), 50 = K-split skinny).
+// (gemm_big.hip; 11-15 its 128x64 / 64x64 instantiations), 20 = 256x256 phase-interleaved (gemm_8ph.hip), 50 = K-split skinny).
 // Measured on MI355X (tools/gemm_bench.py and same-box A/Bs of the whole step).
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   if (dtype != 0) return 0;
@@ -467,6 +467,17 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
                      (DSVT_GEMM4W & (p.ln_stats ? 1 : p.stats_out ? 2 : 4));
   if ((p.ln_stats || p.stats_out) && use4w) return 40;
   if (p.ln_stats || p.stats_out) return 20;
+  // small GEMMs -- Video Swin's stages 3-4 (M = 3136 / 784 rows: 42-300 tiles of 128x128 leave most
+  // CUs idle) and its narrow stage 1-2 layers (N = 96-576): the persistent kernel with 64x64 tiles
+  // (variant 12).  tools/r6_swin_gemm.sh, same box, us: stage-3 qkv 10.8 vs 14.5, fc2 13.6 vs 19.2,
+  // stage-4 fc2 20.1 vs 38.8, proj 8.3 vs 12.5, stage-1 qkv 15.9 vs 23.0, fc1 17.9 vs 24.2.  Not
+  // the DINO ViT's GEMMs (M >= 4096 and N >= 768) nor its head (M < 512 rows)
+#ifndef DSVT_SMALL_GEMM
+#define DSVT_SMALL_GEMM 1
+#endif
+  if (DSVT_SMALL_GEMM && gv == 0 && !p.row_scale && p.K % 32 == 0 && p.M >= 512 && (p.M < 4096 || p.N <= 576) &&
+      (epi == EPI_BIAS || epi == EPI_GELU || epi == EPI_RESID))
+    return 12;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of
   // fc2 through GELU': the 256x256 kernel with the branch-free training epilogue -- measured
   // 195 vs 254 us (persistent 256x128) and 215 vs 231 us at 25104 x 3072 x 768 (tools/aux_bench.py)

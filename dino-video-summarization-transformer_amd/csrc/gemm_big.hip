@@ -20,20 +20,24 @@ constexpr int BIG_ROWB = 64;   // bytes per tile row per stage (32 bf16)
 
 __device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
-// s_waitcnt vmcnt(n) leaving lgkmcnt / expcnt untouched (gfx9 encoding; n < 16)
+// s_waitcnt vmcnt(n) leaving lgkmcnt / expcnt untouched (gfx9 encoding: vmcnt[3:0] at bits 3:0,
+// vmcnt[5:4] at bits 15:14; n < 64)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 16, "vmcnt immediate");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
 }
 
-// s_waitcnt vmcnt(k * PS) for a runtime k in [0, 3] (instantiates only encodable immediates)
-template <int PS>
+// s_waitcnt vmcnt(min(k, K) * PS) for a wave-uniform runtime k >= 0 (one immediate per depth)
+template <int PS, int K>
 __device__ __forceinline__ void wait_stages(int k) {
-  if constexpr (3 * PS < 16) { if (k >= 3) { wait_vm<3 * PS>(); return; } }
-  if constexpr (2 * PS < 16) { if (k >= 2) { wait_vm<2 * PS>(); return; } }
-  if (k >= 1) { wait_vm<PS>(); return; }
-  wait_vm<0>();
+  static_assert(K * PS < 64, "vmcnt immediate");
+  if constexpr (K == 0) {
+    wait_vm<0>();
+  } else {
+    if (k >= K) { wait_vm<K * PS>(); return; }
+    wait_stages<PS, K - 1>(k);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -50,7 +54,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
   constexpr int WTM = BM / WM, WTN = BN / WN, MI = WTM / 16, NJ = WTN / 16;
   constexpr int A_PIECES = A_BYTES / 1024 / NW, B_PIECES = B_BYTES / 1024 / NW;
   constexpr int PER_STAGE = A_PIECES + B_PIECES;
-  static_assert(NST >= 3 && NST <= 5 && (NST - 2) * PER_STAGE < 16, "ring depth");
+  static_assert(NST >= 3 && NST <= 16 && (NST - 2) * PER_STAGE < 64, "ring depth");
   __shared__ __attribute__((aligned(16))) char smem[NST * ST_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -135,7 +139,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
     sv8 fa[MI], fb[NJ];
     for (int kt = 0; kt < nk; ++kt) {
       const int ahead = nk - 1 - kt < NST - 2 ? nk - 1 - kt : NST - 2;
-      wait_stages<PER_STAGE>(ahead);
+      wait_stages<PER_STAGE, NST - 2>(ahead);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -192,7 +196,8 @@ template <int BM, int BN, int WM, int WN, bool STAGGER, int NST = 3>
 static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hipStream_t s) {
   const int64_t tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int64_t lds = (int64_t)NST * (BM + BN) * BIG_ROWB;
-  int64_t G = lds > 80 * 1024 ? 256 : 512;           // resident workgroups: 1 or 2 per CU
+  // resident workgroups: 1 or 2 per CU, up to 4 for the small-tile instantiations (LDS <= 40 KB)
+  int64_t G = lds > 80 * 1024 ? 256 : lds > 40 * 1024 ? 512 : 1024;
   const int64_t per_x = (tiles + 7) / 8;
   if (per_x * 8 < G) G = per_x * 8;
   dim3 grid((unsigned)G), block(64 * WM * WN);
@@ -200,9 +205,12 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
   if (const char* e = getenv("DSVT_TILE_GROUP")) q.tile_group = atoi(e);
 #define DSVT_K(E, F) gemm_persist_kernel<BM, BN, WM, WN, NST, E, F, STAGGER><<<grid, block, 0, s>>>(q)
   if (p.stats_out) {
-    if (epi != EPI_RESID || p.N % BN || p.row_scale || !p.xb_out) return hipErrorInvalidValue;
-    gemm_persist_kernel<BM, BN, WM, WN, NST, EPI_RESID, true, STAGGER, true><<<grid, block, 0, s>>>(q);
-    return hipGetLastError();
+    if constexpr (BN / WN == 64) {     // the stats epilogue: 64-column wave slabs
+      if (epi != EPI_RESID || p.N % BN || p.row_scale || !p.xb_out) return hipErrorInvalidValue;
+      gemm_persist_kernel<BM, BN, WM, WN, NST, EPI_RESID, true, STAGGER, true><<<grid, block, 0, s>>>(q);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
   }
   switch (epi) {
     case EPI_BIAS: if (out_f32) DSVT_K(EPI_BIAS, true); else DSVT_K(EPI_BIAS, false); break;
@@ -222,6 +230,14 @@ static hipError_t launch_persist_t(const GemmParams& p, int epi, int out_f32, hi
 hipError_t launch_gemm_big(const GemmParams& p, int variant, int epi, int out_f32, hipStream_t s) {
   switch (variant) {
     case 10: return launch_persist_t<256, 128, 2, 2, true>(p, epi, out_f32, s);
+    // small tiles for the small GEMMs (Video Swin stages 3-4: M = 784 / 3136 rows, 42-300 tiles of
+    // 128x128 leave most CUs idle): 128x64 and 64x64, 5-stage rings
+    case 11: return launch_persist_t<128, 64, 2, 2, false, 5>(p, epi, out_f32, s);
+    case 12: return launch_persist_t<64, 64, 2, 2, false, 5>(p, epi, out_f32, s);
+    // ... with deep rings (more bytes in flight per workgroup: a small grid has ~1 per CU)
+    case 13: return launch_persist_t<64, 64, 2, 2, false, 10>(p, epi, out_f32, s);
+    case 14: return launch_persist_t<128, 64, 2, 2, false, 6>(p, epi, out_f32, s);
+    case 15: return launch_persist_t<64, 64, 2, 2, false, 14>(p, epi, out_f32, s);
     case 20: return launch_gemm_8ph(p, epi, out_f32, s);
     case 21: return launch_gemm_8ph(p, epi, out_f32, s, 1);
     case 22: return launch_gemm_8ph(p, epi, out_f32, s, 2);

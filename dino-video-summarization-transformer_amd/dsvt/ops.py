@@ -621,6 +621,9 @@ def gemm_kernel_name(tag):
     if variant == 10:
         return "void dsvt::gemm_persist_kernel<256, 128, 2, 2, 3, %d, %s, true, %s>%s" % (
             epi, f32, "true" if fuse == 2 else "false", P)
+    if 11 <= variant <= 15:
+        bm, nst = {11: (128, 5), 12: (64, 5), 13: (64, 10), 14: (128, 6), 15: (64, 14)}[variant]
+        return "void dsvt::gemm_persist_kernel<%d, 64, 2, 2, %d, %d, %s, false, false>%s" % (bm, nst, epi, f32, P)
     if variant == 20:
         if fuse == 1:
             return "void dsvt::gemm_8ph_kernel<%d, false, 0, true, 1>%s" % (epi, P)
