@@ -1072,6 +1072,19 @@ int dsvt_window_scatter_add(float* X, const float* y, const int32_t* idx, int64_
   return e == hipSuccess ? 0 : hip_fail(e, "window_scatter_add");
 }
 
+int dsvt_gemm_resid_rows_fwd(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, float* X,
+                             int64_t ldx, const int32_t* idx, int64_t M, int64_t N, int64_t K, void* stream) {
+  if (int e = check_gemm(DSVT_BF16, EPI_RESID, A, lda, W, ldw, bias, X, ldx, M, N, K)) return e;
+  REQUIRE(idx, "gemm_resid_rows: idx is null");
+  int64_t rpg = 0, gstride = 0, goff = 0;
+  norm_map(rpg, gstride, goff);
+  GemmParams p{A, lda, W, ldw, bias, X, ldx, M, N, K, rpg, gstride, goff, nullptr, nullptr, nullptr, nullptr, 1};
+  p.row_idx = idx;
+  return probed(DSVT_PROBE_GEMM, 2.0 * M * N * K, (hipStream_t)stream, "dsvt_gemm_resid_rows_fwd",
+                [&] { return launch_gemm(p, DSVT_BF16, EPI_RESID, 1, (hipStream_t)stream); },
+                gemm_tag(p, DSVT_BF16, EPI_RESID, 1), gemm_bytes(DSVT_BF16, EPI_RESID, 1, M, N, K));
+}
+
 int dsvt_swin_gather_rows(int dtype, const float* x, const int32_t* idx, const float* row_scale, int64_t group,
                           void* out, int64_t rows, int64_t C, int64_t ldo, void* stream) {
   REQUIRE(dtype == DSVT_BF16 || dtype == DSVT_F32, "swin_gather_rows: bad dtype");

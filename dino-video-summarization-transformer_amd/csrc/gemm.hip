@@ -426,6 +426,8 @@ void set_gemm_variant(int v) { g_gemm_variant = v; }
 // (gemm_big.hip; 11-15 its 128x64 / 64x64 instantiations), 20 = 256x256 phase-interleaved (gemm_8ph.hip), 50 = K-split skinny).
 // Measured on MI355X (tools/gemm_bench.py and same-box A/Bs of the whole step).
 int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
+  // the index-mapped residual epilogue (dsvt_gemm_resid_rows_fwd): the 64x64 persistent kernel
+  if (p.row_idx) return (dtype == 0 && epi == EPI_RESID && p.K % 32 == 0 && !p.stats_out && !p.ln_stats) ? 12 : -1;
   if (dtype != 0) return 0;
   if (epi == EPI_PATCH) return 1;
   int gv = g_gemm_variant;
@@ -544,6 +546,7 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 
 hipError_t launch_gemm(const GemmParams& p, int dtype, int epi, int out_f32, hipStream_t s) {
   const int v = gemm_variant_for(p, dtype, epi, out_f32);
+  if (v < 0 || (p.row_idx && (v < 10 || v > 15))) return hipErrorInvalidValue;
   if ((p.ln_stats && v != 20 && v != 40) || (p.stats_out && v != 20 && v != 30 && v != 1 && v != 10 && v != 40))
     return hipErrorInvalidValue;
   if (v == 50) return launch_gemm_skinny(p, epi, out_f32, s);

@@ -182,8 +182,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_persist_kernel(GemmParam
 #endif
       epilogue_resid_stats<MI, NJ, DSVT_PERSIST_STATS_W>(p, acc, cm0 + wm * WTM, cn0 + wn * WTN, r16, g);
     } else {
-      epilogue_direct<MI, NJ, EPI, OUT_F32, false, false, false, false, true>(p, acc, cm0 + wm * WTM,
-                                                                            cn0 + wn * WTN, r16, g);
+      epilogue_direct<MI, NJ, EPI, OUT_F32, false, false, false, false, true, false, false, true>(
+          p, acc, cm0 + wm * WTM, cn0 + wn * WTN, r16, g);
     }
     if (tn >= t_end) break;
     t = tn;

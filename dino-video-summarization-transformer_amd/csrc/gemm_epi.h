@@ -82,7 +82,7 @@ struct WaveRowScale {
 // (the A loads of those rows are clamped to it), so the extra stores rewrite identical bytes,
 // and no per-lane bounds branch around the stores (which makes the compiler drain vmcnt)
 template <int MI, int NJ, int EPI, bool OUT_F32, int NT = 0, bool NOSTORE = false, bool BIAS_IN_ACC = false,
-          bool NOFAST = false, bool ROWSCALE = false, bool NFULL = false, bool PAIR_AUX = false>
+          bool NOFAST = false, bool ROWSCALE = false, bool NFULL = false, bool PAIR_AUX = false, bool ROWIDX = false>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[MI][NJ], int64_t rbase,
                                                 int64_t cbase, int r16, int g) {
   using OutT = typename std::conditional<(EPI == EPI_RESID || EPI == EPI_PATCH || OUT_F32), float, bf16_t>::type;
@@ -343,9 +343,15 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
   if constexpr (EPI == EPI_RESID && MI % 2 == 0 && MI >= 4 && DSVT_RESID_PIPE && BIAS_IN_ACC) {
     if (!rres && rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {   // the bias is in acc: add X only
       const bool idm = p.rpg >= p.M && p.goff == 0;
+      const bool use_idx = ROWIDX && p.row_idx;   // GemmParams::row_idx (the persistent kernels only)
+      int64_t ridx[MI];
+      if (use_idx) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) ridx[i] = p.row_idx[rbase + i * 16 + r16];
+      }
       auto row_off = [&](int i) -> int64_t {
         const int64_t m = rbase + i * 16 + r16;
-        return (idm ? m : map_row(m, p.rpg, p.gstride, p.goff)) * p.ldo + cbase + 4 * g;
+        return (use_idx ? ridx[i] : idm ? m : map_row(m, p.rpg, p.gstride, p.goff)) * p.ldo + cbase + 4 * g;
       };
       constexpr int W = DSVT_RESID_PIPE > 0 ? DSVT_RESID_PIPE : 1;   // rows of X in flight (a rolling window)
       float4 x[W][NJ];
@@ -374,13 +380,20 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
   // their stores (one HBM round trip per row pair instead of per fragment), branch-free
   if constexpr (EPI == EPI_RESID && MI % 2 == 0) {
     if (rbase + MI * 16 <= p.M && cbase + NJ * 16 <= p.N) {
+      const bool use_idx = ROWIDX && p.row_idx;
+      int64_t ridx[MI];                // the index map's rows, all loaded before the first X load
+      if (use_idx) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) ridx[i] = p.row_idx[rbase + i * 16 + r16];
+      }
 #pragma unroll
       for (int i = 0; i < MI; i += 2) {
         float* xr[2];
         float4 x[2][NJ];
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii) {
-          const int64_t off = map_row(rbase + (i + ii) * 16 + r16, p.rpg, p.gstride, p.goff) * p.ldo + cbase + 4 * g;
+          const int64_t orow = use_idx ? ridx[i + ii] : map_row(rbase + (i + ii) * 16 + r16, p.rpg, p.gstride, p.goff);
+          const int64_t off = orow * p.ldo + cbase + 4 * g;
           xr[ii] = (float*)p.out + off;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) x[ii][j] = *reinterpret_cast<const float4*>(resid_src(p) + off + j * 16);
@@ -397,9 +410,9 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
             float4 bb = bias4[j];
             bb.x *= rs2[ii]; bb.y *= rs2[ii]; bb.z *= rs2[ii]; bb.w *= rs2[ii];
             const fv4 a = acc[i + ii][j];
-            *reinterpret_cast<float4*>(xr[ii] + j * 16) =
-                make_float4(x[ii][j].x + a[0] + bb.x, x[ii][j].y + a[1] + bb.y, x[ii][j].z + a[2] + bb.z,
-                            x[ii][j].w + a[3] + bb.w);
+            *reinterpret_cast<float4*>(xr[ii] + j * 16) =      // x + (A.W^T + b), as the reference adds
+                make_float4(x[ii][j].x + (a[0] + bb.x), x[ii][j].y + (a[1] + bb.y), x[ii][j].z + (a[2] + bb.z),
+                            x[ii][j].w + (a[3] + bb.w));
           }
       }
       return;
@@ -424,7 +437,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, fv4 (&acc)[
       }
     }
     if (m >= p.M) continue;
-    const int64_t orow = map_row(m, p.rpg, p.gstride, p.goff);
+    const int64_t orow = (ROWIDX && EPI == EPI_RESID && p.row_idx) ? (int64_t)p.row_idx[m] : map_row(m, p.rpg, p.gstride, p.goff);
     if constexpr ((EPI == EPI_BIAS || EPI == EPI_GELU) && !OUT_F32 && NJ % 2 == 0) {
 #pragma unroll
       for (int j = 0; j < NJ; j += 2) {

@@ -48,6 +48,10 @@ struct GemmParams {
   float* stats_out = nullptr;
   // temporal attention epilogue (launch_gemm_tattn): softmax scale
   float attn_scale = 0.f;
+  // EPI_RESID output rows through an index instead of the affine map: row(m) = row_idx[m] (every
+  // entry >= 0, no two equal; dsvt_gemm_resid_rows_fwd: Video Swin's window_reverse + residual add).
+  // The persistent kernels only (variants 10-15).
+  const int32_t* row_idx = nullptr;
 };
 
 // float2 (sum, sum of squares) partials per token row: one per 64-column slab of C = 768

@@ -526,7 +526,28 @@ __global__ void frame_mean_kernel(const float* __restrict__ x, float* __restrict
   }
 }
 
+// Many rows per mean (Video Swin's AdaptiveAvgPool3d over D*H*W = 98 token rows per clip): one
+// workgroup per (b, 64 columns), each of its 4 waves sums every 4th row, the 4 partials are added
+// in wave order through LDS (one fixed summation order).  The kernel above walks all T rows in one
+// thread: 24 us for config 5's [8 x 98, 768].
+__global__ __launch_bounds__(256) void frame_mean_split_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               int Tf, int64_t rowlen) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t b = blockIdx.y, i = (int64_t)blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (i < rowlen)
+    for (int t = wave; t < Tf; t += 4) s += x[(b * Tf + t) * rowlen + i];
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && i < rowlen) y[b * rowlen + i] = (((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]) / Tf;
+}
+
 hipError_t launch_frame_mean(const float* x, float* y, int64_t B, int64_t T, int64_t rowlen, hipStream_t s) {
+  if (T > 16) {
+    frame_mean_split_kernel<<<dim3((unsigned)((rowlen + 63) / 64), (unsigned)B), 256, 0, s>>>(x, y, (int)T, rowlen);
+    return hipGetLastError();
+  }
   unsigned bx = (unsigned)((rowlen + 255) / 256);
   if (bx > 1024) bx = 1024;
   frame_mean_kernel<<<dim3(bx, (unsigned)B), 256, 0, s>>>(x, y, (int)T, rowlen);

@@ -102,6 +102,7 @@ SIGNATURES = {
     "dsvt_swin_ln_rows_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),
     "dsvt_swin_merge_ln_fwd": (_i32, [_i32, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_window_scatter_add": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64, _p]),
+    "dsvt_gemm_resid_rows_fwd": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _p]),
     "dsvt_swin_gather_rows": (_i32, [_i32, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _p]),
     "dsvt_attn_window_bwd": (_i32, [_i32, _p, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p,
                                     _i64, _p, _p, _i64, _p]),

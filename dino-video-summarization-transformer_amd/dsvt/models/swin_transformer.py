@@ -13,6 +13,7 @@ Layout: the residual stream of a stage is fp32 X [B, D, H, W, C] (channels last)
 PatchMerging is a 2x2 gather + LayerNorm(4C) kernel and the reduction GEMM; the head is the
 final LayerNorm and the average pool over (D, H, W).
 """
+import os
 from functools import lru_cache, reduce
 from operator import mul
 
@@ -151,9 +152,13 @@ class SwinTransformerBlock3D(nn.Module):
         o = ctx.zeros((rows_w, ldk), mode) if ldk != C else torch.empty(rows_w, ldk, device=dev, dtype=mode)
         ops.attn_window(qkv, o, ctx.bias(self.attn, N), reg, rows_w // N, nW, N, self.num_heads, self.attn.scale)
         wpj, _ = wp(self.attn.proj.weight)
-        y = torch.empty(rows_w, C, device=dev, dtype=torch.float32)
-        ops.gemm(o, wpj, self.attn.proj.bias, y, out_f32=True)
-        ops.window_scatter_add(X, y, win)
+        if mode == torch.bfloat16 and ctx.no_pad(B, D, H, W, window_size, shift_size):
+            # window_reverse + residual add in the proj GEMM's epilogue (X[win[m]] += ...)
+            ops.gemm_resid_rows(o, wpj, self.attn.proj.bias, X, win)
+        else:
+            y = torch.empty(rows_w, C, device=dev, dtype=torch.float32)
+            ops.gemm(o, wpj, self.attn.proj.bias, y, out_f32=True)
+            ops.window_scatter_add(X, y, win)
         rows = X.shape[0]
         w1, ldk1 = wp(self.mlp.fc1.weight)
         a2 = torch.empty(rows, ldk1, device=dev, dtype=mode)
@@ -252,7 +257,14 @@ class _SwinCtx:
             win, reg, nW, N = window_maps(B, D, H, W, tuple(ws), tuple(ss))
             ent = (torch.from_numpy(win).to(self.device), torch.from_numpy(reg).to(self.device), nW, N)
             self.model._aux[key] = ent
+            self.model._aux[("nopad",) + key[1:]] = bool((win >= 0).all())
         return ent
+
+    def no_pad(self, B, D, H, W, ws, ss):
+        """True when the window map of maps(...) has no padding rows (-1): every window row is a
+        token row (decided on the host when the map is built)."""
+        self.maps(B, D, H, W, ws, ss)
+        return self.model._aux[("nopad", B, D, H, W, ws, ss, self.device)]
 
     def bias(self, attn, N):
         """The [heads, N, N] relative-position bias of one attention module at window size N, cached
@@ -310,6 +322,7 @@ class SwinTransformer3D(nn.Module):
         self.avg_pool = torch.nn.AdaptiveAvgPool3d((1, 1, 1))
         self._freeze_stages()
         self.dsvt_dtype = _DEFAULT_DTYPE[0]
+        self.dsvt_streams = "auto"       # inference: clip chunks on concurrent streams (_split_count)
         self._wcache = WeightCache()
         self._aux = {}
         self._drop = (drop_rate, attn_drop_rate, drop_path_rate)
@@ -398,6 +411,65 @@ class SwinTransformer3D(nn.Module):
         mode = self.dsvt_dtype
         ctx = _SwinCtx(self, mode, x.device)
         x = x.float().contiguous()
+        B = x.shape[0]
+        out = torch.empty(B, self.num_features, device=x.device, dtype=torch.float32)
+        k = self._split_count(B)
+        from ..utils import fork_depth
+        if k > 1 and fork_depth() == 0:
+            # the clips are independent: k chunks on k HIP streams, one chunk's small, latency-bound
+            # kernels (stages 3-4: 784-3136 rows) beside another's (opt-in, see _split_count)
+            from ..utils import run_concurrent, stream_slot
+            bounds = [B * i // k for i in range(k + 1)]
+            for b0, b1 in zip(bounds[:-1], bounds[1:]):
+                self._prepare_chunk(ctx, b1 - b0, x.shape[2:])    # caches filled before the fork
+            run_concurrent([(lambda b0=b0, b1=b1: self._forward_chunk(ctx, x[b0:b1], out[b0:b1]))
+                            for b0, b1 in zip(bounds[:-1], bounds[1:])], x.device,
+                           slot0=("swin", stream_slot(x.device)))
+            return out
+        return self._forward_chunk(ctx, x, out)
+
+    def _split_count(self, B):
+        """Streams of one inference forward: dsvt_streams, at most B ("auto": env DSVT_SWIN_STREAMS,
+        else 1)."""
+        k = self.dsvt_streams
+        if k == "auto":
+            k = os.environ.get("DSVT_SWIN_STREAMS", "auto")
+        # auto = ONE stream: config 5 (8 clips) replays at 7044-7110 clips/s unsplit vs 6908-6928 in two
+        # chunks and 5734-6474 in four (tools/r6_g9.sh, HIP graph, same box) -- the chunks' halved
+        # GEMMs lose more than the overlap recovers
+        k = 1 if k == "auto" else int(k)
+        return max(1, min(k, B))
+
+    def _stage_geometry(self, D0, H0, W0):
+        """(D, H, W) of the token grid after the patch embedding, and of each stage."""
+        pd, ph, pw = self.patch_size
+        D, H, W = -(-D0 // pd), -(-H0 // ph), -(-W0 // pw)
+        dims = []
+        for layer in self.layers:
+            dims.append((H, W))
+            if layer.downsample is not None:
+                H, W = (H + 1) // 2, (W + 1) // 2
+        return D, dims
+
+    def _prepare_chunk(self, ctx, B, spatial):
+        """The bf16 weight copies, window maps and relative-position biases a chunk of B clips
+        reads, made on the current stream (a chunk forked onto another stream must not be the
+        first to build a cache entry that a concurrent chunk reads)."""
+        ctx.wp(self.patch_embed.proj.weight, flat=True)
+        D, dims = self._stage_geometry(*spatial)
+        for layer, (H, W) in zip(self.layers, dims):
+            for blk in layer.blocks:
+                ws, ss = get_window_size((D, H, W), blk.window_size, blk.shift_size)
+                _, _, _, N = ctx.maps(B, D, H, W, ws, ss)
+                ctx.bias(blk.attn, N)
+                for lin in (blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2):
+                    ctx.wp(lin.weight)
+            if layer.downsample is not None:
+                ctx.wp(layer.downsample.reduction.weight)
+
+    def _forward_chunk(self, ctx, x, out):
+        """The inference forward of clips x [B, Cin, D0, H0, W0] fp32 into out [B, num_features]."""
+        mode = ctx.mode
         B, Cin, D0, H0, W0 = x.shape
         pd, ph, pw = self.patch_size
         D, H, W = -(-D0 // pd), -(-H0 // ph), -(-W0 // pw)
@@ -412,7 +484,6 @@ class SwinTransformer3D(nn.Module):
         C = X.shape[1]
         Y = torch.empty_like(X)
         ops.swin_ln_rows(X, None, self.norm, Y, X.shape[0])      # any C <= 2048
-        out = torch.empty(B, C, device=x.device, dtype=torch.float32)
         ops.frame_mean(Y, out, B, D * H * W, C)                 # AdaptiveAvgPool3d((1, 1, 1))
         return out
 

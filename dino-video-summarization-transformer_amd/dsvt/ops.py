@@ -685,6 +685,20 @@ def window_scatter_add(X, y, idx, row_scale=None, group=1):
     return X
 
 
+def gemm_resid_rows(a, w, bias, X, idx):
+    """X[idx[m]] += a[m] . w^T + bias (bf16; every idx[m] >= 0 and distinct): attn.proj with the
+    window_reverse + residual add in its epilogue (dsvt_gemm_resid_rows_fwd)."""
+    _check(a, torch.bfloat16, "A")
+    _check(w, torch.bfloat16, "W")
+    _check(X, torch.float32, "X")
+    if idx.dtype != torch.int32 or idx.numel() < a.shape[0]:
+        raise _lib.DsvtError("gemm_resid_rows: idx must be int32 with one entry per row of A")
+    K = a.shape[-1]
+    call("dsvt_gemm_resid_rows_fwd", _ptr(a), K, _ptr(w), w.shape[1], _ptr(bias), _ptr(X), X.shape[-1], _ptr(idx),
+         a.shape[0], w.shape[0], K, _stream())
+    return X
+
+
 def swin_gather_rows(x, idx, out, rows, row_scale=None, group=1):
     """out[m] = dtype(s[m // group] * x[idx[m]]), zero rows for idx < 0 and zero columns past x's
     width (idx None = identity)."""

@@ -486,6 +486,12 @@ int dsvt_swin_merge_ln_fwd(int dtype, const float *x, const float *gamma, const 
  * row gather (the PatchMerging 2x2 gather's gradient). */
 int dsvt_window_scatter_add(float *X, const float *y, const int32_t *idx, int64_t rows, int64_t C,
                             const float *row_scale, int64_t group, void *stream);
+/* attn.proj with the window_reverse + residual add in its epilogue (bf16; swin_transformer.py:170-171
+ * then :241-251, :269): X[idx[m]] += A[m] . W^T + bias for m < M -- dsvt_gemm_fwd into an fp32 [M, N]
+ * buffer followed by dsvt_window_scatter_add, without the buffer.  Every idx[m] must be >= 0 and
+ * distinct (a window map without padding rows; with padding use the two-call form). */
+int dsvt_gemm_resid_rows_fwd(const void *A, int64_t lda, const void *W, int64_t ldw, const float *bias, float *X,
+                             int64_t ldx, const int32_t *idx, int64_t M, int64_t N, int64_t K, void *stream);
 /* ---- Video Swin training (swin_bwd.hip; the --arch swin student, train_ssl.py:237-239) ----------
  * out[m] = dtype(s[m / group] * x[idx[m]]) for c < C, zero for idx[m] < 0 and columns C..ldo-1 (idx
  * NULL = identity, row_scale NULL = 1): window_partition of a token gradient (the window-row gradient

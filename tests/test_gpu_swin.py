@@ -118,6 +118,34 @@ def test_swin_ln_rows_gather(dtype, C, ldo):
     assert (out[~valid].float() == 0).all() and (out[:, C:].float() == 0).all()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(3136, 384, 384), (784, 768, 768), (6272, 96, 128), (1000, 192, 192)])
+def test_gemm_resid_rows_matches_two_call_form(M, N, K):
+    """dsvt_gemm_resid_rows_fwd (attn.proj with window_reverse + residual in the epilogue) against
+    the two-call form it replaces -- dsvt_gemm_fwd into an fp32 buffer, then
+    dsvt_window_scatter_add -- BITWISE (same kernel, x + (A.W^T + b) in both), through a random
+    permutation of the rows (Video Swin-T's stage shapes; M = 1000: a ragged last tile); and
+    against an fp32 torch reference."""
+    from dsvt import ops
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g)
+    X0 = torch.randn(M, N, device="cuda", generator=g)
+    idx = torch.randperm(M, device="cuda", generator=g).to(torch.int32)
+    X1 = X0.clone()
+    ops.gemm_resid_rows(a, w, b, X1, idx)
+    X2 = X0.clone()
+    y = torch.empty(M, N, device="cuda")
+    ops.gemm(a, w, b, y, out_f32=True)
+    ops.window_scatter_add(X2, y, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(X1, X2)
+    ref = X0.clone()
+    ref[idx.long()] += a.float() @ w.float().t() + b
+    assert (X1 - ref).abs().max().item() < 2e-3
+
+
 # ------------------------------------------------------------------------------ Swin training
 SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
 SWIN_TRAIN96 = dict(embed_dim=96, depths=[2], num_heads=[3])
@@ -297,8 +325,10 @@ def test_swin_trainer_steps_bf16():
     ref.train()
     ref.load_state_dict(student.state_dict())
     lf_r = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()
+    teacher.backbone.dsvt_streams = 1       # as the trainer's teacher call runs it (trainer._TeacherStepSettings)
     with torch.no_grad():
         t_out = teacher(crops[:2])
+    teacher.backbone.dsvt_streams = "auto"
     lf_r(ref(crops), t_out, 0).backward()
     g_ref = {k: p.grad.clone() for k, p in ref.named_parameters() if p.grad is not None}
     lf = DINOLoss(512, 4, 0.04, 0.04, 0, 10, student_temp=0.1, global_crops=2).cuda()

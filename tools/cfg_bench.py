@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--warm", type=int, default=2)
     ap.add_argument("--streams", default=None)
     ap.add_argument("--ln-fold", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--graph", action="store_true", help="also time HIP-graph replays (as bench.py does)")
     args = ap.parse_args()
     from dsvt.models import SwinTransformer3D
     from dsvt.models.timesformer import VisionTransformer
@@ -57,6 +58,25 @@ def main():
             m(x)
         torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / args.reps
+    if args.graph:
+        with torch.no_grad():
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                m(x)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                m(x)
+            g.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.reps):
+                g.replay()
+            torch.cuda.synchronize()
+        tg = (time.perf_counter() - t0) / args.reps
+        print("%s graph: %.2f clips/s, %.3f ms per replay" % (args.cfg, n / tg, tg * 1e3))
     print("%s: %.2f clips/s, %.3f ms per call, %.1f TFLOP/s executed (%.1f %% of the bf16 peak)"
           % (args.cfg, n / t, t * 1e3, n * gf / t / 1e3, 100 * n * gf / t / 1e3 / PEAK_TFLOPS["bf16"]))
 
