@@ -1140,6 +1140,30 @@ int dsvt_attn_window_fwd(int dtype, const void* qkv, void* out, int64_t ldo, con
   });
 }
 
+int64_t dsvt_attn_window_bias_frag_floats(int64_t N, int64_t heads) {
+  return (N > 0 && N <= 128 && heads > 0) ? attn_window_frag_floats(N, heads) : -1;
+}
+
+int dsvt_attn_window_bias_frag(const float* bias, int64_t N, int64_t heads, float* frag, void* stream) {
+  REQUIRE(bias && frag && aligned16(frag), "attn_window_bias_frag: bad pointer");
+  REQUIRE(N > 0 && N <= 128 && heads > 0, "attn_window_bias_frag: need 0 < N <= 128");
+  hipError_t e = launch_attn_window_bias_frag(bias, N, heads, frag, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "attn_window_bias_frag");
+}
+
+int dsvt_attn_window_frag_fwd(const void* qkv, void* out, int64_t ldo, const float* frag, const int32_t* region,
+                              int64_t nwin, int64_t nwc, int64_t N, int64_t heads, float scale, void* stream) {
+  REQUIRE(qkv && out && frag && region && aligned16(qkv) && aligned16(out) && aligned16(frag),
+          "attn_window_frag: bad pointer");
+  REQUIRE(nwin > 0 && nwc > 0 && N > 0 && N <= 128 && heads > 0, "attn_window_frag: need 0 < N <= 128");
+  REQUIRE(ldo >= heads * 32 && ldo % 8 == 0, "attn_window_frag: ldo must be >= 32 heads and a multiple of 8");
+  const double flops = 4.0 * nwin * heads * (double)N * N * 32;
+  return probed(DSVT_PROBE_ATTN_SPATIAL, flops, (hipStream_t)stream, "dsvt_attn_window_frag_fwd", [&] {
+    return launch_attn_window_frag(qkv, out, ldo, frag, region, nwin, nwc, N, heads, heads * 32, scale,
+                                   (hipStream_t)stream);
+  });
+}
+
 int dsvt_select_frames(const double* loss, int64_t n_loss, int64_t n_frames, int64_t n_unsampled, int64_t rate,
                        int64_t N, int64_t* indices, int32_t* frame_pos, double* cdf_out, void* workspace,
                        size_t workspace_bytes, void* stream) {

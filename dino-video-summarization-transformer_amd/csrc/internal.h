@@ -245,6 +245,13 @@ hipError_t launch_attn_window(int dtype, const void* qkv, void* out, int64_t ldo
                               const int32_t* region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C,
                               float scale, hipStream_t s);
 hipError_t launch_cast_pad(int dtype, const float* x, void* y, int64_t N, int64_t K, int64_t ldk, hipStream_t s);
+// bf16 window attention with the bias in MFMA-fragment order (attn_window_bias_frag: [heads][ceil(N/16)][8][64]
+// float4) and the out columns C..ldo-1 zeroed
+int64_t attn_window_frag_floats(int64_t N, int64_t heads);
+hipError_t launch_attn_window_bias_frag(const float* bias, int64_t N, int64_t heads, float* frag, hipStream_t s);
+hipError_t launch_attn_window_frag(const void* qkv, void* out, int64_t ldo, const float* frag, const int32_t* region,
+                                   int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C, float scale,
+                                   hipStream_t s);
 
 // frame selection (select.hip)
 int64_t select_frames_ws_bytes(int64_t n, int64_t n_unsampled);

@@ -464,6 +464,158 @@ __global__ __launch_bounds__(256) void attn_window_bf16(WinAttnParams p) {
   }
 }
 
+// The same with the relative-position bias read in MFMA-fragment order and the window's region ids
+// in LDS.  attn_window_bf16 reads the [heads][N][N] bias and the region row per score element:
+// 64 scattered 4-byte loads per lane per 16-query tile (every wave load touching 16 rows), which
+// made it VMEM-issue bound (config 5: 31 us at stage 1 vs ~5 us of qkv / out traffic).  Here the
+// bias of tile (qt, kt) is one contiguous 1 KB block, lane l holding bias[qt*16 + l%16][kt*16 +
+// 4(l/16) .. +3] (attn_window_bias_frag builds it once per table): 8 coalesced 16-byte loads per
+// lane per tile.  Same arithmetic as attn_window_bf16 (bitwise-equal outputs).  The workgroups
+// of head 0 also zero the out columns C..ldo-1 (the proj GEMM's K padding).
+__global__ __launch_bounds__(256) void attn_window_frag_bf16(WinAttnParams p) {
+  constexpr int SN = 8, LPW = 128;
+  __shared__ __attribute__((aligned(16))) bf16_t kv[2][LPW * WROW];
+  __shared__ __attribute__((aligned(16))) int rg[LPW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.x;
+  const int64_t win = blockIdx.y;
+  const int N = (int)p.N;
+  const int64_t C = p.C;
+  const bf16_t* qkv = (const bf16_t*)p.qkv + win * N * 3 * C;
+  const int32_t* reg = p.region + (win % p.nwc) * N;
+  for (int pc = tid; pc < LPW * 4; pc += 256) {
+    const int r = pc >> 2, ch = pc & 3;
+    uint4 k4 = make_uint4(0, 0, 0, 0), v4 = k4;
+    if (r < N) {
+      const bf16_t* src = qkv + (int64_t)r * 3 * C + C + h * 32 + ch * 8;
+      k4 = *reinterpret_cast<const uint4*>(src);
+      v4 = *reinterpret_cast<const uint4*>(src + C);
+    }
+    *reinterpret_cast<uint4*>(&kv[0][r * WROW + ch * 8]) = k4;
+    *reinterpret_cast<uint4*>(&kv[1][r * WROW + ch * 8]) = v4;
+  }
+  if (tid < LPW) rg[tid] = reg[tid < N ? tid : N - 1];
+  if (h == 0 && p.ldo > C) {                       // zero K padding of the window's out rows
+    const int pad8 = (int)((p.ldo - C) >> 3);
+    for (int e = tid; e < N * pad8; e += 256)
+      *reinterpret_cast<uint4*>((bf16_t*)p.out + (win * N + e / pad8) * p.ldo + C + (e % pad8) * 8) =
+          make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  const bf16_t* Ks = kv[0];
+  const bf16_t* Vs = kv[1];
+  const int nqt = (N + 15) >> 4;
+  const float4* fb = reinterpret_cast<const float4*>(p.bias) + (int64_t)h * nqt * SN * 64;
+  const float l2e = 1.4426950408889634f;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    int qi = qt * 16 + r16;
+    const int qc = qi < N ? qi : N - 1;
+    const sv8 qf = *reinterpret_cast<const sv8*>(qkv + (int64_t)qc * 3 * C + h * 32 + g * 8);
+    float4 bq[SN];
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) bq[kt] = fb[(qt * SN + kt) * 64 + lane];
+    fv4 s[SN];
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+      const sv8 kf = *reinterpret_cast<const sv8*>(Ks + (kt * 16 + r16) * WROW + g * 8);
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, fv4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    const int rq = rg[qc];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt) {
+      const int4 rk = *reinterpret_cast<const int4*>(&rg[kt * 16 + 4 * g]);
+      const float bb[4] = {bq[kt].x, bq[kt].y, bq[kt].z, bq[kt].w};
+      const int rr[4] = {rk.x, rk.y, rk.z, rk.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kt * 16 + 4 * g + j;
+        float v = s[kt][j] * p.scale + bb[j] + ((rr[j] != rq) ? -100.0f : 0.0f);
+        v = key < N ? v * l2e : -INFINITY;
+        s[kt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < SN; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[kt][j] = __builtin_amdgcn_exp2f(s[kt][j] - mx);
+        rs += s[kt][j];
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    fv4 o[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kp = 0; kp < SN / 2; ++kp) {
+      sv8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[2 * kp][j]);
+        pb[4 + j] = (short)f2bf(s[2 * kp + 1][j]);
+      }
+      const int vr0 = kp * 32 + 4 * g + (r16 >> 2), vr1 = vr0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 16 + 4 * (r16 & 3);
+        const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr0 * WROW + col));
+        const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) sv4*)(Vs + vr1 * WROW + col));
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), pb,
+                                                        o[dt], 0, 0, 0);
+      }
+    }
+    mfma_result_fence();
+    if (qi < N) {
+      const float inv = 1.0f / rs;
+      bf16_t* dst = (bf16_t*)p.out + (win * N + qi) * p.ldo + h * 32 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        store4(dst + dt * 16, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    }
+  }
+}
+
+// frag[h][qt][kt][lane] (float4) = bias[h][qt*16 + lane%16][kt*16 + 4(lane/16) + 0..3], zero past N
+__global__ __launch_bounds__(256) void attn_window_bias_frag_kernel(const float* __restrict__ bias, int N, int nqt,
+                                                                    int64_t total, float4* __restrict__ frag) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int lane = (int)(e & 63), kt = (int)((e >> 6) & 7);
+    const int64_t t = e >> 9;                        // h * nqt + qt
+    const int qt = (int)(t % nqt), h = (int)(t / nqt);
+    const int q = qt * 16 + (lane & 15), k0 = kt * 16 + 4 * (lane >> 4);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      v[j] = (q < N && k0 + j < N) ? bias[((int64_t)h * N + q) * N + k0 + j] : 0.f;
+    frag[e] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+int64_t attn_window_frag_floats(int64_t N, int64_t heads) { return heads * ((N + 15) / 16) * 8 * 64 * 4; }
+
+hipError_t launch_attn_window_bias_frag(const float* bias, int64_t N, int64_t heads, float* frag, hipStream_t s) {
+  const int64_t total = attn_window_frag_floats(N, heads) / 4;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  attn_window_bias_frag_kernel<<<(unsigned)blocks, 256, 0, s>>>(bias, (int)N, (int)((N + 15) / 16), total,
+                                                                 (float4*)frag);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_window_frag(const void* qkv, void* out, int64_t ldo, const float* frag, const int32_t* region,
+                                   int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C, float scale,
+                                   hipStream_t s) {
+  WinAttnParams p{qkv, out, frag, region, nwin, nwc, N, heads, C, scale, ldo};
+  attn_window_frag_bf16<<<dim3((unsigned)heads, (unsigned)nwin), 256, 0, s>>>(p);
+  return hipGetLastError();
+}
+
 // fp32 VALU: one thread per (window, head, query), K/V rows read through L2
 __global__ __launch_bounds__(256) void attn_window_f32(WinAttnParams p) {
   const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;

@@ -109,6 +109,9 @@ SIGNATURES = {
     "dsvt_relpos_bias_bwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _p, _i32, _p]),
     "dsvt_relpos_bias_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p]),
     "dsvt_attn_window_fwd": (_i32, [_i32, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p]),
+    "dsvt_attn_window_bias_frag_floats": (_i64, [_i64, _i64]),
+    "dsvt_attn_window_bias_frag": (_i32, [_p, _i64, _i64, _p, _p]),
+    "dsvt_attn_window_frag_fwd": (_i32, [_p, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "dsvt_cast_pad_fwd": (_i32, [_i32, _p, _p, _i64, _i64, _i64, _p]),
     "dsvt_select_frames": (_i32, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
     "dsvt_gather_rows": (_i32, [_p, _i64, _p, _i64, _p, _p]),

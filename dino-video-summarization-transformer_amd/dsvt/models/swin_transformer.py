@@ -148,9 +148,14 @@ class SwinTransformerBlock3D(nn.Module):
         ops.swin_ln_rows(X, win, self.norm1, a, rows_w)
         qkv = torch.empty(rows_w, 3 * C, device=dev, dtype=mode)
         ops.gemm(a, wq, self.attn.qkv.bias, qkv)
-        # pad columns (proj K, C = 96 -> 128) must stay zero; the attention kernel writes the rest
-        o = ctx.zeros((rows_w, ldk), mode) if ldk != C else torch.empty(rows_w, ldk, device=dev, dtype=mode)
-        ops.attn_window(qkv, o, ctx.bias(self.attn, N), reg, rows_w // N, nW, N, self.num_heads, self.attn.scale)
+        if mode == torch.bfloat16:   # the fragment-order kernel also zeroes the K padding (C = 96 -> 128)
+            o = torch.empty(rows_w, ldk, device=dev, dtype=mode)
+            ops.attn_window_frag(qkv, o, ctx.bias_frag(self.attn, N), reg, rows_w // N, nW, N, self.num_heads,
+                                 self.attn.scale)
+        else:
+            # pad columns (proj K) must stay zero; the attention kernel writes the rest
+            o = ctx.zeros((rows_w, ldk), mode) if ldk != C else torch.empty(rows_w, ldk, device=dev, dtype=mode)
+            ops.attn_window(qkv, o, ctx.bias(self.attn, N), reg, rows_w // N, nW, N, self.num_heads, self.attn.scale)
         wpj, _ = wp(self.attn.proj.weight)
         if mode == torch.bfloat16 and ctx.no_pad(B, D, H, W, window_size, shift_size):
             # window_reverse + residual add in the proj GEMM's epilogue (X[win[m]] += ...)
@@ -234,6 +239,11 @@ class PatchEmbed3D(nn.Module):
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
 
 
+def _lib_frag_floats(N, heads):
+    from .._lib import lib
+    return lib().dsvt_attn_window_bias_frag_floats(int(N), int(heads))
+
+
 class _SwinCtx:
     def __init__(self, model, mode, device):
         self.model, self.mode, self.device = model, mode, device
@@ -272,17 +282,29 @@ class _SwinCtx:
         storage: every optimizer / EMA step in training) -- one tensor per entry, so the cache does
         not grow with the steps.  The rewrite is enqueued on the current stream after that step's
         update of the table, i.e. after every reader of the previous values."""
+        return self._bias_entry(attn, N)[1]
+
+    def bias_frag(self, attn, N):
+        """bias(attn, N) in MFMA-fragment order (ops.attn_window_frag's operand), kept with it."""
+        return self._bias_entry(attn, N)[2]
+
+    def _bias_entry(self, attn, N):
         t = attn.relative_position_bias_table
         key = ("bias", id(attn), N)
         stamp = (t._version, t.data_ptr())
         ent = self.model._aux.get(key)
         if ent is None:
-            ent = [None, torch.empty(attn.num_heads, N, N, device=self.device, dtype=torch.float32)]
+            b = torch.empty(attn.num_heads, N, N, device=self.device, dtype=torch.float32)
+            ent = [None, b, None]
+            if self.mode == torch.bfloat16:
+                ent[2] = torch.empty(_lib_frag_floats(N, attn.num_heads), device=self.device, dtype=torch.float32)
             self.model._aux[key] = ent
         if ent[0] != stamp:
             ops.relpos_bias(t.detach().contiguous(), attn.relative_position_index.contiguous(), N, ent[1])
+            if ent[2] is not None:
+                ops.attn_window_bias_frag(ent[1], N, attn.num_heads, ent[2])
             ent[0] = stamp
-        return ent[1]
+        return ent
 
     def zeros(self, shape, dtype):
         return torch.zeros(shape, device=self.device, dtype=dtype)

@@ -731,6 +731,28 @@ def relpos_bias(table, index, N, out):
     return out
 
 
+def attn_window_bias_frag(bias, N, heads, frag=None):
+    """The [heads, N, N] relative-position bias in MFMA-fragment order (attn_window_frag's operand)."""
+    n = _lib.lib().dsvt_attn_window_bias_frag_floats(int(N), int(heads))
+    if n < 0:
+        raise _lib.DsvtError("attn_window_bias_frag: need 0 < N <= 128")
+    if frag is None:
+        frag = torch.empty(n, device=bias.device, dtype=torch.float32)
+    elif frag.numel() != n:
+        raise _lib.DsvtError("attn_window_bias_frag: frag must hold %d floats" % n)
+    call("dsvt_attn_window_bias_frag", _ptr(bias), int(N), int(heads), _ptr(frag), _stream())
+    return frag
+
+
+def attn_window_frag(qkv, out, frag, region, nwin, nwc, N, heads, scale):
+    """bf16 window attention reading the fragment-ordered bias; zeroes out's columns past heads*32."""
+    _check(qkv, torch.bfloat16, "qkv")
+    _check(out, torch.bfloat16, "out")
+    call("dsvt_attn_window_frag_fwd", _ptr(qkv), _ptr(out), out.shape[-1], _ptr(frag), _ptr(region), nwin, nwc, N,
+         heads, float(scale), _stream())
+    return out
+
+
 def attn_window(qkv, out, bias, region, nwin, nwc, N, heads, scale):
     call("dsvt_attn_window_fwd", _dt(qkv.dtype), _ptr(qkv), _ptr(out), out.shape[-1], _ptr(bias), _ptr(region), nwin,
          nwc, N, heads, 32, float(scale), _stream())

@@ -128,9 +128,15 @@ def _block_fwd(blk, X, B, D, H, W, ctx, scales, save):
     ops.swin_ln_rows(X, win, blk.norm1, a, rows_w)
     qkv = torch.empty(rows_w, 3 * C, device=dev, dtype=mode)
     ops.gemm(a, wq, blk.attn.qkv.bias, qkv)
-    o = torch.zeros(rows_w, ldk, device=dev, dtype=mode) if ldk != C else torch.empty(rows_w, C, device=dev, dtype=mode)
     bias = ctx.bias(blk.attn, N)
-    ops.attn_window(qkv, o, bias, reg, rows_w // N, nW, N, blk.num_heads, blk.attn.scale)
+    if mode == torch.bfloat16:       # fragment-order bias; the kernel zeroes the K padding
+        o = torch.empty(rows_w, ldk, device=dev, dtype=mode)
+        ops.attn_window_frag(qkv, o, ctx.bias_frag(blk.attn, N), reg, rows_w // N, nW, N, blk.num_heads,
+                             blk.attn.scale)
+    else:
+        o = torch.zeros(rows_w, ldk, device=dev, dtype=mode) if ldk != C else torch.empty(rows_w, C, device=dev,
+                                                                                          dtype=mode)
+        ops.attn_window(qkv, o, bias, reg, rows_w // N, nW, N, blk.num_heads, blk.attn.scale)
     wpj, _ = ctx.wp(blk.attn.proj.weight)
     y = torch.empty(rows_w, C, device=dev, dtype=torch.float32)
     ops.gemm(o, wpj, blk.attn.proj.bias, y, out_f32=True)

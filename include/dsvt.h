@@ -521,6 +521,13 @@ int dsvt_relpos_bias_fwd(const float *table, const int64_t *index, int64_t nmax,
 int dsvt_attn_window_fwd(int dtype, const void *qkv, void *out, int64_t ldo, const float *bias,
                          const int32_t *region, int64_t nwin, int64_t nwc, int64_t N, int64_t heads,
                          int64_t head_dim, float scale, void *stream);
+/* The bf16 form with the bias in MFMA-fragment order: frag (dsvt_attn_window_bias_frag_floats(N,
+ * heads) floats, 16-byte aligned) = dsvt_attn_window_bias_frag(bias [heads][N][N]), built once per
+ * bias table; out columns heads*32..ldo-1 are zeroed.  Bitwise the same out as dsvt_attn_window_fwd. */
+int64_t dsvt_attn_window_bias_frag_floats(int64_t N, int64_t heads);
+int dsvt_attn_window_bias_frag(const float *bias, int64_t N, int64_t heads, float *frag, void *stream);
+int dsvt_attn_window_frag_fwd(const void *qkv, void *out, int64_t ldo, const float *frag, const int32_t *region,
+                              int64_t nwin, int64_t nwc, int64_t N, int64_t heads, float scale, void *stream);
 /* y [N, ldk] = x [N, K] cast to the storage dtype with zero columns K..ldk-1. */
 int dsvt_cast_pad_fwd(int dtype, const float *x, void *y, int64_t N, int64_t K, int64_t ldk, void *stream);
 

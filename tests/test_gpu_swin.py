@@ -296,6 +296,31 @@ def test_attn_window_bwd_vs_autograd(dtype, N, shifted):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,shifted,ldo", [(98, True, 128), (98, False, 96), (49, True, 128), (25, False, 96),
+                                           (128, True, 96), (17, True, 128)])
+def test_attn_window_frag_matches_plain(N, shifted, ldo):
+    """dsvt_attn_window_frag_fwd (bias in MFMA-fragment order, region ids in LDS) against
+    dsvt_attn_window_fwd: BITWISE equal out (same arithmetic), the K-padding columns heads*32..ldo-1
+    zeroed (the plain kernel leaves them), ragged N (17, 25, 49) and a full 128-row window."""
+    from dsvt import ops
+    torch.manual_seed(N + ldo)
+    heads, nwin, nwc, C = 3, 10, 4, 96
+    dev = torch.device("cuda")
+    qkv = torch.randn(nwin * N, 3 * C, device=dev).to(torch.bfloat16)
+    reg = torch.randint(0, 4, (nwc, N), device=dev, dtype=torch.int32) if shifted else \
+        torch.zeros(nwc, N, device=dev, dtype=torch.int32)
+    bias = torch.randn(heads, N, N, device=dev)
+    scale = 32 ** -0.5
+    o1 = torch.zeros(nwin * N, ldo, device=dev, dtype=torch.bfloat16)
+    ops.attn_window(qkv, o1, bias, reg, nwin, nwc, N, heads, scale)
+    frag = ops.attn_window_bias_frag(bias, N, heads)
+    o2 = torch.full((nwin * N, ldo), 3.0, device=dev, dtype=torch.bfloat16)
+    ops.attn_window_frag(qkv, o2, frag, reg, nwin, nwc, N, heads, scale)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+
+
+@pytest.mark.gpu
 def test_swin_trainer_steps_bf16():
     """DINOTrainer steps (train_ssl.py:466-573 loop body: student forward + teacher forward, DINO
     loss, backward into the persistent gradient buffers -- the Swin student goes through one
