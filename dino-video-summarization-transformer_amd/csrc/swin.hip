@@ -229,6 +229,7 @@ hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, co
     if (C == 96) DSVT_SLN(96, 16)
     if (C == 192) DSVT_SLN(192, 16)
     if (C == 384) DSVT_SLN(384, 32)
+    if (C == 768) DSVT_SLN(768, 64)   // stage 4 and the final norm: 9.5 us per call on the wave-per-row kernel
   }
 #undef DSVT_SLN
   const unsigned blocks = (unsigned)((rows + 3) / 4);
@@ -284,9 +285,87 @@ __global__ __launch_bounds__(256) void swin_merge_ln_kernel(const float* __restr
   }
 }
 
+// The same with LPR lanes per output row (as swin_ln_rows_small_kernel): lane `sub` owns VPL
+// contiguous columns of the 4C row, all inside one of the four gathered parts (C % VPL == 0).
+// The wave-per-row kernel above left 3/4 of its lanes idle at C = 96: 14 us per call at stage 1.
+template <typename T, int C4, int LPR>
+__global__ __launch_bounds__(256) void swin_merge_ln_small_kernel(const float* __restrict__ x,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ beta, T* __restrict__ out,
+                                                                  int64_t rows, int D, int H, int W, float eps) {
+  constexpr int C = C4 / 4, VPL = C4 / LPR, RPW = 64 / LPR;
+  static_assert(C4 % LPR == 0 && C % VPL == 0 && VPL % 2 == 0 && 64 % LPR == 0, "row split");
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t m = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool live = m < rows;
+  const int H2 = (H + 1) / 2, W2 = (W + 1) / 2;
+  const int64_t mm = live ? m : 0;
+  const int w2 = (int)(mm % W2), h2 = (int)((mm / W2) % H2);
+  const int64_t bd = mm / ((int64_t)W2 * H2);
+  const int c0 = sub * VPL, part = c0 / C, cc = c0 % C;
+  const int hh = 2 * h2 + (part & 1), ww = 2 * w2 + (part >> 1);
+  const bool in = hh < H && ww < W;                  // zero taps past odd H / W (F.pad, :302-310)
+  float v[VPL];
+  float s = 0.f;
+  if (in) {
+    const float2* xr = reinterpret_cast<const float2*>(x + ((bd * H + hh) * W + ww) * C + cc);
+#pragma unroll
+    for (int i = 0; i < VPL / 2; ++i) {
+      const float2 t = xr[i];
+      v[2 * i] = t.x;
+      v[2 * i + 1] = t.y;
+      s += t.x + t.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] = 0.f;
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o);
+  const float mean = s * (1.0f / C4);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    v[i] -= mean;
+    q += v[i] * v[i];
+  }
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) q += __shfl_xor(q, o);
+  const float rstd = 1.0f / sqrtf(q * (1.0f / C4) + eps);
+  if (!live) return;
+  T* o = out + m * C4 + c0;
+#pragma unroll
+  for (int i = 0; i < VPL; i += 2) {
+    const float a = v[i] * rstd * gamma[c0 + i] + beta[c0 + i];
+    const float b = v[i + 1] * rstd * gamma[c0 + i + 1] + beta[c0 + i + 1];
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<unsigned*>(o + i) = pack_bf16x2(a, b);
+    } else {
+      *reinterpret_cast<float2*>(o + i) = make_float2(a, b);
+    }
+  }
+}
+
 hipError_t launch_swin_merge_ln(int dtype, const float* x, const float* gamma, const float* beta, void* out, int64_t B,
                                 int64_t D, int64_t H, int64_t W, int64_t C, float eps, hipStream_t s) {
   const int64_t rows = B * D * ((H + 1) / 2) * ((W + 1) / 2);
+#define DSVT_SMLN(CC4, LPR)                                                                                    \
+  {                                                                                                             \
+    const unsigned nb = (unsigned)((rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR)));                           \
+    if (dtype == 0)                                                                                             \
+      swin_merge_ln_small_kernel<bf16_t, CC4, LPR><<<nb, 256, 0, s>>>(x, gamma, beta, (bf16_t*)out, rows,      \
+                                                                       (int)D, (int)H, (int)W, eps);           \
+    else                                                                                                        \
+      swin_merge_ln_small_kernel<float, CC4, LPR><<<nb, 256, 0, s>>>(x, gamma, beta, (float*)out, rows, (int)D, \
+                                                                      (int)H, (int)W, eps);                    \
+    return hipGetLastError();                                                                                   \
+  }
+  if (((uintptr_t)x & 7) == 0 && ((uintptr_t)out & (dtype == 0 ? 3 : 7)) == 0) {
+    if (C == 96) DSVT_SMLN(384, 32)
+    if (C == 192) DSVT_SMLN(768, 64)
+    if (C == 384) DSVT_SMLN(1536, 64)
+  }
+#undef DSVT_SMLN
   const unsigned blocks = (unsigned)((rows + 3) / 4);
   if (dtype == 0)
     swin_merge_ln_kernel<bf16_t><<<blocks, 256, 0, s>>>(x, gamma, beta, (bf16_t*)out, B, (int)D, (int)H, (int)W,

@@ -146,6 +146,32 @@ def test_gemm_resid_rows_matches_two_call_form(M, N, K):
     assert (X1 - ref).abs().max().item() < 2e-3
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,H,W", [(96, 14, 14), (96, 7, 9), (192, 5, 6), (384, 3, 3), (64, 5, 5)])
+def test_swin_merge_ln(dtype, C, H, W):
+    """dsvt_swin_merge_ln_fwd (PatchMerging, swin_transformer.py:293-315: the 2x2 gather x0..x3 with
+    zero taps past odd H / W, then LayerNorm(4C)) against torch -- the lane-group kernel (C = 96 /
+    192 / 384) and the wave-per-row one (C = 64)."""
+    from dsvt import ops
+    g = torch.Generator(device="cuda").manual_seed(C + H)
+    B, D = 2, 2
+    x = torch.randn(B, D, H, W, C, device="cuda", generator=g) * 2 + 0.3
+    ln = torch.nn.LayerNorm(4 * C).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(torch.rand(4 * C, device="cuda", generator=g) + 0.5)
+        ln.bias.copy_(torch.randn(4 * C, device="cuda", generator=g) * 0.1)
+    H2, W2 = (H + 1) // 2, (W + 1) // 2
+    out = torch.full((B * D * H2 * W2, 4 * C), 7.0, device="cuda", dtype=dtype)
+    ops.swin_merge_ln(x.reshape(-1, C), ln, out, B, D, H, W)
+    with torch.no_grad():
+        xp = torch.nn.functional.pad(x, (0, 0, 0, W % 2, 0, H % 2))
+        cat = torch.cat([xp[:, :, 0::2, 0::2], xp[:, :, 1::2, 0::2], xp[:, :, 0::2, 1::2], xp[:, :, 1::2, 1::2]], -1)
+        ref = ln(cat).reshape(-1, 4 * C)
+    err = (out.float() - ref).abs().max().item()
+    assert err < (3e-5 if dtype == torch.float32 else 3e-2), err
+
+
 # ------------------------------------------------------------------------------ Swin training
 SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
 SWIN_TRAIN96 = dict(embed_dim=96, depths=[2], num_heads=[3])
