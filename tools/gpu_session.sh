@@ -2,7 +2,7 @@
 # One GPU-box session: each stage under its own time limit; stop at the first crash, abort,
 # fault or timeout (exit status other than 0 = pass / 1 = test failures or Python error).
 # usage: tools/gpu_session.sh stage [stage ...]
-#   stages: kernels model gputests smoke bench prof graphprof trainprof c4prof c5prof pmc
+#   stages: kernels model gputests smoke bench prof graphprof trainprof c4prof c5prof c5pmc pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
@@ -40,6 +40,11 @@ for stage in "$@"; do
                "$(date -u +%Y-%m-%d) bench.py --steps 3 --warmup 1 --serial --no-graph (libdsvt $(md5sum dino-video-summarization-transformer_amd/dsvt/libdsvt.so | cut -c1-12))" \
                > "$OUT/pmc_summary.txt" &&
              cp "$OUT/pmc_traffic.json" profiles/pmc_traffic.json ;;
+    c5pmc)   run c5pmc 300 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/c5pmc_fetch" -o run -- python3 tools/cfg_bench.py c5 --reps 2 --warm 1 &&
+             run c5pmc2 300 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/c5pmc_write" -o run -- python3 tools/cfg_bench.py c5 --reps 2 --warm 1 &&
+             python tools/pmc_summary.py "$OUT/c5pmc_fetch" "$OUT/c5pmc_write" "$OUT/c5_pmc_traffic.json" \
+               "$(date -u +%Y-%m-%d) tools/cfg_bench.py c5 --reps 2 --warm 1" > "$OUT/c5_pmc_summary.txt" &&
+             run c5probe 300 python3 tools/swin_probe.py 3 ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done
