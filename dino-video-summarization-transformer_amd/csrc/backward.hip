@@ -480,9 +480,12 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 
 // out[c] (+)= sum_p partial[p*stride + c]: block = 32 columns x 8 part lanes, LDS combine
 // (fixed order -> deterministic)
+// (out2: columns >= split go to out2[c - split] -- the LayerNorm backward's [dgamma | dbeta]
+// partial rows reduced in one pass, each column in the same order as alone)
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ partial, int64_t nparts,
                                                               int64_t width, int64_t stride, float* __restrict__ out,
-                                                              int accumulate) {
+                                                              int accumulate, float* __restrict__ out2 = nullptr,
+                                                              int64_t split = INT64_MAX) {
   __shared__ float red[8][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int64_t c = (int64_t)blockIdx.x * 32 + tx;
@@ -495,7 +498,8 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += red[k][tx];
-    out[c] = accumulate ? out[c] + s : s;
+    float* o = c < split ? out + c : out2 + (c - split);
+    *o = accumulate ? *o + s : s;
   }
 }
 
@@ -514,7 +518,7 @@ __global__ __launch_bounds__(256) void reduce_slices_kernel(float* __restrict__ 
 // fixed-order sum of nparts partial rows: one kernel for few parts; otherwise 64 slices summed
 // in parallel first (the single-kernel form ran on width/32 = 24 workgroups: ~12 us per call)
 static hipError_t reduce_parts(const float* partial, int64_t nparts, int64_t width, int64_t stride, float* out,
-                               int accumulate, hipStream_t s) {
+                               int accumulate, hipStream_t s, float* out2 = nullptr, int64_t split = INT64_MAX) {
   if (nparts > 128) {
     const int64_t slices = 64, chunk = (nparts + slices - 1) / slices;
     const int64_t used = (nparts + chunk - 1) / chunk;
@@ -522,11 +526,11 @@ static hipError_t reduce_parts(const float* partial, int64_t nparts, int64_t wid
     reduce_slices_kernel<<<g1, 256, 0, s>>>(const_cast<float*>(partial), nparts, width, stride, chunk);
     if (hipError_t e = hipGetLastError()) return e;
     reduce_partials_kernel<<<(unsigned)((width + 31) / 32), 256, 0, s>>>(partial, used, width, chunk * stride, out,
-                                                                         accumulate);
+                                                                         accumulate, out2, split);
     return hipGetLastError();
   }
   reduce_partials_kernel<<<(unsigned)((width + 31) / 32), 256, 0, s>>>(partial, nparts, width, stride, out,
-                                                                       accumulate);
+                                                                       accumulate, out2, split);
   return hipGetLastError();
 }
 
@@ -555,6 +559,11 @@ hipError_t launch_colsum_rows(int dtype, const void* y, int64_t rows, int64_t C,
 hipError_t launch_reduce_partials(const float* partial, int64_t nparts, int64_t width, int64_t stride, float* out,
                                   int accumulate, hipStream_t s) {
   return reduce_parts(partial, nparts, width, stride, out, accumulate, s);
+}
+
+hipError_t launch_ln_params_reduce(const float* partial, int64_t nparts, int64_t C, float* dgamma, float* dbeta,
+                                   int accumulate, hipStream_t s) {
+  return reduce_parts(partial, nparts, 2 * C, 2 * C, dgamma, accumulate, s, dbeta, C);
 }
 
 // ================================================================ temporal attention backward

@@ -719,8 +719,7 @@ int dsvt_layernorm_bwd(int dy_dtype, const float* x, const void* dy, const float
                   if ((e = launch_ln_bwd(dy_dtype, x, dy, gamma, dx, rows, C, rpg, gstride, goff, eps, part, s)))
                     return e;
                   if (!dgamma) return hipSuccess;            // partials left for dsvt_layernorm_bwd_params
-                  if ((e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s))) return e;
-                  return launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
+                  return launch_ln_params_reduce(part, nb, C, dgamma, dbeta, accumulate, s);
                 });
 }
 
@@ -746,8 +745,7 @@ int dsvt_layernorm_bwd_cast(int dy_dtype, const float* x, const void* dy, const 
                                               dxb, og, osk, s)))
                     return e;
                   if (!dgamma) return hipSuccess;
-                  if ((e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s))) return e;
-                  return launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
+                  return launch_ln_params_reduce(part, nb, C, dgamma, dbeta, accumulate, s);
                 });
 }
 
@@ -758,8 +756,7 @@ int dsvt_layernorm_bwd_params(int64_t rows, int64_t C, const void* workspace, in
   const float* part = (const float*)workspace;
   const int nb = ln_bwd_blocks(rows);
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = launch_reduce_partials(part, nb, C, 2 * C, dgamma, accumulate, s);
-  if (e == hipSuccess) e = launch_reduce_partials(part + C, nb, C, 2 * C, dbeta, accumulate, s);
+  hipError_t e = launch_ln_params_reduce(part, nb, C, dgamma, dbeta, accumulate, s);
   return e == hipSuccess ? 0 : hip_fail(e, "layernorm_bwd_params");
 }
 

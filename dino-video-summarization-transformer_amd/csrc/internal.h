@@ -179,6 +179,10 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
                          hipStream_t s);
 hipError_t launch_reduce_partials(const float* partial, int64_t nparts, int64_t width, int64_t stride, float* out,
                                   int accumulate, hipStream_t s);
+// the LayerNorm backward's partial rows [nparts][dgamma C | dbeta C] -> dgamma, dbeta in one pass (per column the
+// order of launch_reduce_partials)
+hipError_t launch_ln_params_reduce(const float* partial, int64_t nparts, int64_t C, float* dgamma, float* dbeta,
+                                   int accumulate, hipStream_t s);
 hipError_t launch_ln_bwd_cast(int dy_dtype, const float* x, const void* dy, const float* gamma, float* dx,
                               int64_t rows, int64_t rpg, int64_t gstride, int64_t goff, float eps, float* partial,
                               void* dxb, int64_t og, int64_t osk, hipStream_t s);

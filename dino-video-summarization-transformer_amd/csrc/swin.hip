@@ -551,7 +551,8 @@ __global__ __launch_bounds__(256) void attn_window_bf16(WinAttnParams p) {
 // 4(l/16) .. +3] (attn_window_bias_frag builds it once per table): 8 coalesced 16-byte loads per
 // lane per tile.  Same arithmetic as attn_window_bf16 (bitwise-equal outputs).  The workgroups
 // of head 0 also zero the out columns C..ldo-1 (the proj GEMM's K padding).
-__global__ __launch_bounds__(256) void attn_window_frag_bf16(WinAttnParams p) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_window_frag_bf16(WinAttnParams p) {
   constexpr int SN = 8, LPW = 128;
   __shared__ __attribute__((aligned(16))) bf16_t kv[2][LPW * WROW];
   __shared__ __attribute__((aligned(16))) int rg[LPW];
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(256) void attn_window_frag_bf16(WinAttnParams p) {
   const int64_t C = p.C;
   const bf16_t* qkv = (const bf16_t*)p.qkv + win * N * 3 * C;
   const int32_t* reg = p.region + (win % p.nwc) * N;
-  for (int pc = tid; pc < LPW * 4; pc += 256) {
+  for (int pc = tid; pc < LPW * 4; pc += 64 * NW) {
     const int r = pc >> 2, ch = pc & 3;
     uint4 k4 = make_uint4(0, 0, 0, 0), v4 = k4;
     if (r < N) {
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(256) void attn_window_frag_bf16(WinAttnParams p) {
   if (tid < LPW) rg[tid] = reg[tid < N ? tid : N - 1];
   if (h == 0 && p.ldo > C) {                       // zero K padding of the window's out rows
     const int pad8 = (int)((p.ldo - C) >> 3);
-    for (int e = tid; e < N * pad8; e += 256)
+    for (int e = tid; e < N * pad8; e += 64 * NW)
       *reinterpret_cast<uint4*>((bf16_t*)p.out + (win * N + e / pad8) * p.ldo + C + (e % pad8) * 8) =
           make_uint4(0, 0, 0, 0);
   }
@@ -587,7 +588,7 @@ __global__ __launch_bounds__(256) void attn_window_frag_bf16(WinAttnParams p) {
   const int nqt = (N + 15) >> 4;
   const float4* fb = reinterpret_cast<const float4*>(p.bias) + (int64_t)h * nqt * SN * 64;
   const float l2e = 1.4426950408889634f;
-  for (int qt = wave; qt < nqt; qt += 4) {
+  for (int qt = wave; qt < nqt; qt += NW) {
     int qi = qt * 16 + r16;
     const int qc = qi < N ? qi : N - 1;
     const sv8 qf = *reinterpret_cast<const sv8*>(qkv + (int64_t)qc * 3 * C + h * 32 + g * 8);
@@ -691,7 +692,15 @@ hipError_t launch_attn_window_frag(const void* qkv, void* out, int64_t ldo, cons
                                    int64_t nwin, int64_t nwc, int64_t N, int64_t heads, int64_t C, float scale,
                                    hipStream_t s) {
   WinAttnParams p{qkv, out, frag, region, nwin, nwc, N, heads, C, scale, ldo};
-  attn_window_frag_bf16<<<dim3((unsigned)heads, (unsigned)nwin), 256, 0, s>>>(p);
+#ifndef DSVT_WIN_NW
+#define DSVT_WIN_NW 8
+#endif
+  // one wave per 16-query tile (N = 98: 7 tiles) instead of two tiles each for 3 of 4 waves: config 5
+  // 7980 / 8145 vs 7884 / 8059 clips/s (tools/r6_g11.sh, interleaved, same box)
+  if (DSVT_WIN_NW == 8 && N > 64)
+    attn_window_frag_bf16<8><<<dim3((unsigned)heads, (unsigned)nwin), 512, 0, s>>>(p);
+  else
+    attn_window_frag_bf16<4><<<dim3((unsigned)heads, (unsigned)nwin), 256, 0, s>>>(p);
   return hipGetLastError();
 }
 
