@@ -112,7 +112,8 @@ int check_gemm(int dtype, int epi, const void* A, int64_t lda, const void* W, in
   REQUIRE(epi >= 0 && epi <= 5, "gemm: bad epilogue %d", epi);
   REQUIRE(A && W && out, "gemm: null pointer");
   REQUIRE(M > 0 && N > 0 && K > 0, "gemm: empty problem M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
-  REQUIRE((K * esize(dtype)) % 128 == 0, "gemm: K=%lld must be a multiple of %d", (long long)K, dtype == DSVT_BF16 ? 64 : 32);
+  // K % 32: one K step of the bf16 persistent kernels (K % 64 != 0 routes there) / the fp32 MFMA K tile
+  REQUIRE(K % 32 == 0, "gemm: K=%lld must be a multiple of 32", (long long)K);
   REQUIRE(N % 4 == 0, "gemm: N=%lld must be a multiple of 4", (long long)N);
   REQUIRE(lda >= K && ldw >= K && (lda * esize(dtype)) % 16 == 0 && (ldw * esize(dtype)) % 16 == 0,
           "gemm: lda/ldw must be >= K and 16-byte multiples");

@@ -429,6 +429,12 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
   // the index-mapped residual epilogue (dsvt_gemm_resid_rows_fwd): the 64x64 persistent kernel
   if (p.row_idx) return (dtype == 0 && epi == EPI_RESID && p.K % 32 == 0 && !p.stats_out && !p.ln_stats) ? 12 : -1;
   if (dtype != 0) return 0;
+  // K % 64 != 0 (Video Swin's C = 96 stage without K padding): only the persistent kernels step K
+  // by 32 -- the 64x64 one, or the 256x128 one where a variant of that family is forced
+  if (p.K % 64) {
+    if (p.ln_stats || p.stats_out) return -1;
+    return (g_gemm_variant >= 10 && g_gemm_variant <= 15) ? g_gemm_variant : 12;
+  }
   if (epi == EPI_PATCH) return 1;
   int gv = g_gemm_variant;
   if (gv == 30 && !(!p.ln_stats && gemm_192_ok(p, epi) && (epi == EPI_RESID || !out_f32))) gv = 0;   // forced, ineligible: auto

@@ -13,7 +13,8 @@ one per branch per block, the reference's call order), drawn for a whole forward
 PatchMerging (:293-315): the 2x2 gather (an index map), LayerNorm(4C), the reduction GEMM.
 Backward: the GEMM / wgrad / LayerNorm-backward kernels of the TimeSformer path plus
 csrc/swin_bwd.hip (window attention backward with the bias gradient, the relative-position table
-gradient, row gathers); K dimensions the MFMA tile does not divide (C = 96) are zero-padded.
+gradient, row gathers); K dimensions that are not multiples of the GEMM K step (32) are zero-padded
+(r06: C = 96 no longer is -- the persistent GEMM steps K by 32).
 """
 from functools import lru_cache
 
@@ -30,8 +31,8 @@ class _S:
 
 
 def _pad_to(n, mode):
-    q = 64 if mode == torch.bfloat16 else 32
-    return (n + q - 1) // q * q
+    """n rounded up to the GEMM K step (32; WeightCache.padded's quantum)."""
+    return (n + 31) // 32 * 32
 
 
 @lru_cache(maxsize=64)

@@ -86,13 +86,14 @@ class WeightCache:
 
     def padded(self, mode):
         """W [N, K] as [N, ldk] in the storage dtype with zero columns K..ldk-1 (ldk = K rounded
-        up to the MFMA K tile: 64 bf16 / 32 fp32), cached like the casts.  Returns (w, ldk)."""
+        up to 32 elements: one K step of the bf16 persistent GEMM / the fp32 MFMA K tile), cached
+        like the casts.  Returns (w, ldk)."""
         def get(p, flat=False):
             t = p.detach()
             if flat:
                 t = t.reshape(t.shape[0], -1)
             K = t.shape[1]
-            q = 64 if mode == torch.bfloat16 else 32
+            q = 32
             ldk = (K + q - 1) // q * q
             key = (id(p), "pad", mode, flat)
             ent = self._c.get(key)
@@ -112,7 +113,7 @@ class WeightCache:
         def get(p):
             t = p.detach()
             N = t.shape[0]
-            q = 64 if mode == torch.bfloat16 else 32
+            q = 32
             ldn = (N + q - 1) // q * q
             key = (id(p), "padT", mode)
             ent = self._c.get(key)

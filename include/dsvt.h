@@ -91,8 +91,8 @@ int64_t dsvt_workspace_bytes(int op, int dtype, int64_t M, int64_t N, int64_t K)
 /* K4/K7/K9/K12: MFMA GEMM with fused epilogue.
  * Replaces nn.Linear in Attention.qkv/proj (models/timesformer.py:63-64, 71, 83),
  * temporal_fc (:108, :133), Mlp.fc1/act/fc2 (:41-52) and DINOHead.mlp / last_layer
- * (vision_transformer.py:255-281).  Requires K % 64 == 0 (bf16) / K % 32 == 0 (f32),
- * N % 4 == 0.  A rows are contiguous with stride lda (elements of dtype); W [N,K]
+ * (vision_transformer.py:255-281).  Requires K % 32 == 0 (bf16 calls with K % 64 != 0 -- Video
+ * Swin's C = 96 -- run on the persistent kernel; r06, was K % 64), N % 4 == 0.  A rows are contiguous with stride lda (elements of dtype); W [N,K]
  * contiguous with stride ldw; out stride ldo (elements). out_f32 selects fp32 output for
  * EPI_BIAS / EPI_BIAS_GELU (otherwise dtype). */
 int dsvt_gemm_fwd(int dtype, int epilogue, int out_f32, const void *A, int64_t lda, const void *W,

@@ -66,9 +66,9 @@ def test_version_and_workspace(L):
 def test_validation_rejects_before_launch(L):
     from dsvt import _lib
     fake = ctypes.c_void_p(256)
-    # K not a multiple of 64 (bf16)
+    # K not a multiple of 32 (r06: K % 64 != 0 runs on the persistent kernels' 32-wide K steps)
     rc = L.dsvt_gemm_fwd(_lib.BF16, 0, 0, fake, 100, fake, 100, None, fake, 64, 16, 64, 100, 0, 0, 0, None)
-    assert rc == 1 and b"multiple of 64" in L.dsvt_last_error()
+    assert rc == 1 and b"multiple of 32" in L.dsvt_last_error()
     # LayerNorm-folded GEMM: K must be 768, N a multiple of 256, stats / wsum required
     rc = L.dsvt_gemm_lnx_fwd(0, fake, 512, 0, 0, 0, fake, ctypes.c_float(1e-6), fake, fake, fake, fake, 768, 100, 768,
                              512, 0, 0, 0, None)
