@@ -483,7 +483,10 @@ int gemm_variant_for(const GemmParams& p, int dtype, int epi, int out_f32) {
 #ifndef DSVT_SMALL_GEMM
 #define DSVT_SMALL_GEMM 1
 #endif
-  if (DSVT_SMALL_GEMM && gv == 0 && !p.row_scale && p.K % 32 == 0 && p.M >= 512 && (p.M < 4096 || p.N <= 576) &&
+#ifndef DSVT_SMALL_MIN_M
+#define DSVT_SMALL_MIN_M 512
+#endif
+  if (DSVT_SMALL_GEMM && gv == 0 && !p.row_scale && p.K % 32 == 0 && p.M >= DSVT_SMALL_MIN_M && (p.M < 4096 || p.N <= 576) &&
       (epi == EPI_BIAS || epi == EPI_GELU || epi == EPI_RESID))
     return 12;
   // training fc1 (GELU with the pre-activation saved, DropPath row scales or not) and the dX of

@@ -344,7 +344,8 @@ class SwinTransformer3D(nn.Module):
         self.avg_pool = torch.nn.AdaptiveAvgPool3d((1, 1, 1))
         self._freeze_stages()
         self.dsvt_dtype = _DEFAULT_DTYPE[0]
-        self.dsvt_streams = "auto"       # inference: clip chunks on concurrent streams (_split_count)
+        self.dsvt_streams = "auto"       # inference: clip chunks on concurrent streams (_split_plan)
+        self.dsvt_split_stage = 2        # ... from this stage on
         self._wcache = WeightCache()
         self._aux = {}
         self._drop = (drop_rate, attn_drop_rate, drop_path_rate)
@@ -435,32 +436,42 @@ class SwinTransformer3D(nn.Module):
         x = x.float().contiguous()
         B = x.shape[0]
         out = torch.empty(B, self.num_features, device=x.device, dtype=torch.float32)
-        k = self._split_count(B)
+        k, s0 = self._split_plan(B)
         from ..utils import fork_depth
-        if k > 1 and fork_depth() == 0:
-            # the clips are independent: k chunks on k HIP streams, one chunk's small, latency-bound
-            # kernels (stages 3-4: 784-3136 rows) beside another's (opt-in, see _split_count)
-            from ..utils import run_concurrent, stream_slot
-            bounds = [B * i // k for i in range(k + 1)]
-            for b0, b1 in zip(bounds[:-1], bounds[1:]):
-                self._prepare_chunk(ctx, b1 - b0, x.shape[2:])    # caches filled before the fork
-            run_concurrent([(lambda b0=b0, b1=b1: self._forward_chunk(ctx, x[b0:b1], out[b0:b1]))
-                            for b0, b1 in zip(bounds[:-1], bounds[1:])], x.device,
-                           slot0=("swin", stream_slot(x.device)))
-            return out
-        return self._forward_chunk(ctx, x, out)
+        if k <= 1 or fork_depth() > 0:
+            X, D, H, W = self._run_head(ctx, x, len(self.layers))
+            return self._run_tail(ctx, X, B, D, H, W, len(self.layers), out)
+        # the clips are independent: stages s0.. run as k clip chunks on k HIP streams, so one
+        # chunk's small, latency-bound kernels (stages 3-4: 784-3136 rows per 8 clips) run beside
+        # another's; the stages before s0 run on the whole batch (their kernels fill the chip)
+        from ..utils import run_concurrent, stream_slot
+        X, D, H, W = self._run_head(ctx, x, s0)
+        rpc = X.shape[0] // B                                    # token rows per clip at stage s0
+        bounds = [B * i // k for i in range(k + 1)]
+        dims = self._stage_geometry(*x.shape[2:])[1]
+        for b0, b1 in zip(bounds[:-1], bounds[1:]):              # caches filled before the fork
+            self._prepare_stages(ctx, b1 - b0, D, dims, s0)
+        run_concurrent([(lambda b0=b0, b1=b1: self._run_tail(ctx, X[b0 * rpc:b1 * rpc], b1 - b0, D, H, W, s0,
+                                                             out[b0:b1]))
+                        for b0, b1 in zip(bounds[:-1], bounds[1:])], x.device,
+                       slot0=("swin", stream_slot(x.device)))
+        return out
 
-    def _split_count(self, B):
-        """Streams of one inference forward: dsvt_streams, at most B ("auto": env DSVT_SWIN_STREAMS,
-        else 1)."""
+    def _split_plan(self, B):
+        """(k, s0): the clips of one inference forward as k chunks on k streams from stage s0 on.
+        dsvt_streams ("auto": env DSVT_SWIN_STREAMS, else 1) and dsvt_split_stage (env
+        DSVT_SWIN_SPLIT_STAGE overrides; 0 = the whole forward).  "auto" is ONE stream: config 5
+        (8 clips, HIP graph, same box, tools/r6_g9.sh / r6_g13.sh / r6_g14.sh) replays at 8 142 /
+        8 050 clips/s unsplit vs 7 427 / 7 425 split in two from stage 2, 7 040 / 7 019 from stage 3,
+        7 487 / 7 343 the whole forward, 5 924 / 6 155 in four -- and 7 954 / 8 002 vs 8 092 / 8 142
+        from stage 2 even with the small-GEMM route extended to the chunks' 392-row stage-4 GEMMs
+        (-DDSVT_SMALL_MIN_M=128): the chunks' kernels share the CUs rather than filling idle ones."""
         k = self.dsvt_streams
         if k == "auto":
             k = os.environ.get("DSVT_SWIN_STREAMS", "auto")
-        # auto = ONE stream: config 5 (8 clips) replays at 7044-7110 clips/s unsplit vs 6908-6928 in two
-        # chunks and 5734-6474 in four (tools/r6_g9.sh, HIP graph, same box) -- the chunks' halved
-        # GEMMs lose more than the overlap recovers
         k = 1 if k == "auto" else int(k)
-        return max(1, min(k, B))
+        s0 = int(os.environ.get("DSVT_SWIN_SPLIT_STAGE", self.dsvt_split_stage))
+        return max(1, min(k, B)), max(0, min(s0, len(self.layers)))
 
     def _stage_geometry(self, D0, H0, W0):
         """(D, H, W) of the token grid after the patch embedding, and of each stage."""
@@ -473,24 +484,26 @@ class SwinTransformer3D(nn.Module):
                 H, W = (H + 1) // 2, (W + 1) // 2
         return D, dims
 
-    def _prepare_chunk(self, ctx, B, spatial):
-        """The bf16 weight copies, window maps and relative-position biases a chunk of B clips
-        reads, made on the current stream (a chunk forked onto another stream must not be the
-        first to build a cache entry that a concurrent chunk reads)."""
-        ctx.wp(self.patch_embed.proj.weight, flat=True)
-        D, dims = self._stage_geometry(*spatial)
-        for layer, (H, W) in zip(self.layers, dims):
+    def _prepare_stages(self, ctx, B, D, dims, s0):
+        """The bf16 weight copies, window maps and relative-position biases that stages s0.. of a
+        chunk of B clips read, made on the current stream (a chunk forked onto another stream must
+        not be the first to build a cache entry that a concurrent chunk reads)."""
+        for layer, (H, W) in list(zip(self.layers, dims))[s0:]:
             for blk in layer.blocks:
                 ws, ss = get_window_size((D, H, W), blk.window_size, blk.shift_size)
                 _, _, _, N = ctx.maps(B, D, H, W, ws, ss)
-                ctx.bias(blk.attn, N)
+                ctx.no_pad(B, D, H, W, ws, ss)
+                if ctx.mode == torch.bfloat16:
+                    ctx.bias_frag(blk.attn, N)
+                else:
+                    ctx.bias(blk.attn, N)
                 for lin in (blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2):
                     ctx.wp(lin.weight)
             if layer.downsample is not None:
                 ctx.wp(layer.downsample.reduction.weight)
 
-    def _forward_chunk(self, ctx, x, out):
-        """The inference forward of clips x [B, Cin, D0, H0, W0] fp32 into out [B, num_features]."""
+    def _run_head(self, ctx, x, s1):
+        """Patch embedding and stages 0..s1-1 of clips x [B, Cin, D0, H0, W0] fp32 -> (X, D, H, W)."""
         mode = ctx.mode
         B, Cin, D0, H0, W0 = x.shape
         pd, ph, pw = self.patch_size
@@ -501,7 +514,13 @@ class SwinTransformer3D(nn.Module):
                          dtype=torch.float32)
         X = torch.empty(B * D * H * W, C, device=x.device, dtype=torch.float32)
         ops.swin_patch_embed(x, wpe, ldk, self.patch_embed.proj.bias, self.patch_size, X, ws)
-        for layer in self.layers:
+        for layer in self.layers[:s1]:
+            X, H, W = layer.run(X, B, D, H, W, ctx)
+        return X, D, H, W
+
+    def _run_tail(self, ctx, X, B, D, H, W, s0, out):
+        """Stages s0.. of B clips' token rows X, the final norm and the average pool into out [B, C]."""
+        for layer in self.layers[s0:]:
             X, H, W = layer.run(X, B, D, H, W, ctx)
         C = X.shape[1]
         Y = torch.empty_like(X)
