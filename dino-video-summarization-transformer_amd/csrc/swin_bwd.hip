@@ -175,6 +175,34 @@ __global__ __launch_bounds__(256) void relpos_bias_bwd_kernel(const float* __res
   dtable[t] = accumulate ? dtable[t] + s : s;
 }
 
+// The same with the head's dbias [N][N] and the index slice staged in LDS once per workgroup
+// (grid: entry chunks x heads; the index as int16, 6 bytes per pair: 56 KiB at N = 98): every
+// thread's scan reads broadcast LDS words instead of an int64 index and an fp32 value through the
+// cache per pair (9.6k pairs at N = 98).  Pairs in the same (i, j) order as above:
+// bitwise-equal sums.
+__global__ __launch_bounds__(256) void relpos_bias_bwd_lds_kernel(const float* __restrict__ dbias,
+                                                                  const int64_t* __restrict__ index, int nmax, int N,
+                                                                  int heads, int64_t entries,
+                                                                  float* __restrict__ dtable, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) char rb_smem[];
+  const int nn = N * N;
+  float* sd = reinterpret_cast<float*>(rb_smem);
+  short* si = reinterpret_cast<short*>(rb_smem + (size_t)nn * 4);      // entries < 32768
+  const int h = blockIdx.y;
+  for (int p = threadIdx.x; p < nn; p += 256) {
+    si[p] = (short)index[(int64_t)(p / N) * nmax + p % N];
+    sd[p] = dbias[(int64_t)h * nn + p];
+  }
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= entries) return;
+  float s = 0.f;
+  for (int p = 0; p < nn; ++p)
+    if (si[p] == (int)e) s += sd[p];
+  const int64_t t = e * heads + h;
+  dtable[t] = accumulate ? dtable[t] + s : s;
+}
+
 }  // namespace
 
 int64_t attn_window_bwd_groups(int64_t nwin, int64_t heads) {
@@ -212,6 +240,12 @@ hipError_t launch_attn_window_bwd(int dtype, const void* qkv, const void* o, int
 
 hipError_t launch_relpos_bias_bwd(const float* dbias, const int64_t* index, int64_t nmax, int64_t N, int64_t heads,
                                   int64_t entries, float* dtable, int accumulate, hipStream_t s) {
+  const int64_t lds = N * N * 6;
+  if (lds <= 64 * 1024 && entries < 32768) {
+    relpos_bias_bwd_lds_kernel<<<dim3((unsigned)((entries + 255) / 256), (unsigned)heads), 256, lds, s>>>(
+        dbias, index, (int)nmax, (int)N, (int)heads, entries, dtable, accumulate);
+    return hipGetLastError();
+  }
   const int64_t n = entries * heads;
   relpos_bias_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dbias, index, (int)nmax, (int)N, (int)heads,
                                                                        entries, dtable, accumulate);
