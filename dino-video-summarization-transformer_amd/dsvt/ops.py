@@ -20,7 +20,16 @@ def _dt(mode):
     raise ValueError("dsvt storage dtype must be torch.bfloat16 or torch.float32, got %s" % (mode,))
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream():
+    """The current HIP stream's handle: torch's raw getter (0.19 us per call on the MI355X box vs
+    2.6 us for torch.cuda.current_stream().cuda_stream, which builds a Stream object; the same
+    handle on side streams and under graph capture -- tools/stream_cost.py)."""
+    if _RAW_STREAM is not None and _CUR_DEVICE is not None:
+        return _RAW_STREAM(_CUR_DEVICE())
     return torch.cuda.current_stream().cuda_stream
 
 

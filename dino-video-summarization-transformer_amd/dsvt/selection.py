@@ -13,10 +13,7 @@ import torch
 
 from . import _lib
 from ._lib import call
-
-
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+from .ops import _stream  # noqa: F401  (the raw current-stream handle)
 
 
 def adaptive_frame_indices(loss_list, n_frames, n_unsampled, pre_sampling_rate, N, device=None, return_cdf=False):
