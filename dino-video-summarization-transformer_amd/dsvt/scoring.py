@@ -102,12 +102,18 @@ class FrameScorer:
     model(zeros, 60 frames)) -- whatever the video's length."""
 
     def __init__(self, model, local_clip_size=3, global_clip_size=30, teacher_temp=0.02, student_temp=0.3,
-                 frames_per_call=16, crop_size=None):
+                 frames_per_call=8, crop_size=None):
         self.model = model
         self.local_clip_size = local_clip_size
         self.global_clip_size = global_clip_size
         self.loss = PairwiseDINOLoss(model.embed_dim, teacher_temp, student_temp).to(model.pos_embed.device)
         self.frames_per_call = frames_per_call
+        # frame chunks on concurrent HIP streams (env DSVT_SCORE_STREAMS).  Bench video (64 frames, local 3 /
+        # global 30), HIP graph, same box: 16 frames per call 376.4 / 377.5 frames/s on 2 streams vs
+        # 367.4 / 367.5 on 1 and 373.7 / 374.1 on 4 (tools/r6_g15.sh); on 2 streams 8 frames per call
+        # 383.5 / 384.0 vs 12: 379.9 / 383.5, 16: 374.9 / 376.6, 32: 380.6 / 381.5, 4: 338.2, and 8 on 3
+        # streams 380.9 / 382.1 (tools/r6_g16.sh, r6_g17.sh)
+        self.streams = 2
         self.crop_size = crop_size if crop_size is not None else model.patch_embed.img_size[0]
         self._views = {}
         # no LayerNorm folding: a frame's score is a difference of two close losses (the pairwise
@@ -145,12 +151,29 @@ class FrameScorer:
         frames = frames.float().contiguous()
         scores = torch.empty(F, device=dev, dtype=torch.float32)
         n = self.frames_per_call
-        for s0 in range(0, F, n):
+
+        def chunk(s0):
             s1 = min(F, s0 + n)
             b = s1 - s0
             st = self.model.forward_frame_bank(frames, li_t[s0:s1].reshape(-1), b, ts, lnx=self.lnx)
             te = self.model.forward_frame_bank(frames, gi_t[s0:s1].reshape(-1), b, G, lnx=self.lnx)
             scores[s0:s1] = self.loss.per_row(st, te)
+        starts = list(range(0, F, n))
+        k = max(1, min(int(os.environ.get("DSVT_SCORE_STREAMS", self.streams)), len(starts)))
+        from .utils import fork_depth
+        if k > 1 and fork_depth() == 0:
+            # the frame chunks are independent: k HIP streams, chunk i on stream i % k, so one
+            # chunk's partly-filled last round of tiles runs beside another's full ones
+            from .utils import prepare_weights, run_concurrent, stream_slot
+            prepare_weights(self.model)           # weight copies and index maps made before the fork
+            for t in (ts, G):
+                self.model._indices(frames.shape[-2] // 16, frames.shape[-1] // 16, t, dev)
+            groups = [starts[i::k] for i in range(k)]
+            run_concurrent([(lambda g=g: [chunk(s0) for s0 in g]) for g in groups], dev,
+                           slot0=("score", stream_slot(dev)))
+        else:
+            for s0 in starts:
+                chunk(s0)
         return scores
 
 

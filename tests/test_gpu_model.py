@@ -372,6 +372,21 @@ def test_frame_scores_vs_oracle(dtype, tol):
     assert np.max(np.abs(scores - ref)) / np.max(np.abs(ref)) < tol, (scores, ref)
 
 
+def test_frame_scores_streams_bitwise():
+    """FrameScorer.streams > 1 (the frame chunks on concurrent HIP streams) returns the same scores,
+    bitwise, as the serial loop: the chunks run the same kernels on the same shapes."""
+    from dsvt.scoring import FrameScorer
+    sd = P.timesformer_state(31, embed_dim=192, depth=2, num_heads=3, img_size=32, num_frames=4)
+    m = tsf(sd, torch.bfloat16, embed_dim=192, depth=2, num_heads=3, img_size=32, num_frames=4)
+    frames = cu(P.clip(33, (18, 3, 32, 32)))
+    sc = FrameScorer(m, 3, 10, frames_per_call=4)
+    s1 = sc.score(frames).clone()
+    sc.streams = 3
+    s3 = sc.score(frames).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s3)
+
+
 def _ref_scores(fwd, frames, F_, local, glob):
     """Scores the reference's loop (dino_similarity.py:73-90) computes on the views its loader
     builds (oracle view_index_map), with `fwd` the oracle forward; windows deduplicated."""

@@ -21,18 +21,33 @@ from bench import PEAK_TFLOPS, joint_flops, swin_t_flops, vit_fwd_flops  # noqa:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cfg", choices=["c2bb", "c4", "c5"])
+    ap.add_argument("cfg", choices=["c2bb", "c4", "c5", "fs"])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--warm", type=int, default=2)
     ap.add_argument("--streams", default=None)
     ap.add_argument("--ln-fold", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--graph", action="store_true", help="also time HIP-graph replays (as bench.py does)")
+    ap.add_argument("--fpc", type=int, default=16, help="fs: frames per backbone call")
     args = ap.parse_args()
     from dsvt.models import SwinTransformer3D
     from dsvt.models.timesformer import VisionTransformer
     dev = torch.device("cuda")
     torch.manual_seed(1)
-    if args.cfg == "c5":
+    if args.cfg == "fs":                # frame scoring: one 64-frame 224^2 video, local 3 / global 30 (bench.py)
+        from dsvt.scoring import FrameScorer
+        torch.manual_seed(2)
+        fm = VisionTransformer(img_size=224, num_classes=0, embed_dim=768, depth=12, num_heads=12, qkv_bias=True,
+                               norm_layer=partial(nn.LayerNorm, eps=1e-6), num_frames=8,
+                               attention_type="divided_space_time").to(dev).eval()
+        fm.dsvt_dtype = torch.bfloat16
+        sc = FrameScorer(fm, local_clip_size=3, global_clip_size=30, frames_per_call=args.fpc)
+        video = torch.randn(64, 3, 224, 224, device=dev)
+
+        class _M:                       # the scorer as a "model" of 64 "clips" (frames)
+            def __call__(self, v):
+                return sc.score(v)
+        m, x, n, gf = _M(), video, 64, (vit_fwd_flops(3, 224) + vit_fwd_flops(30, 224)) / 1e9
+    elif args.cfg == "c5":
         m = SwinTransformer3D().to(dev)
         m.eval()                        # returns None, as the reference's (swin_transformer.py:684-687)
         x = torch.randn(8, 3, 8, 224, 224, device=dev)
