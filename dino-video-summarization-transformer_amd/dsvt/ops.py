@@ -566,6 +566,33 @@ def wgrad(dy, x, out, accumulate=False, db=None):
     return out
 
 
+def gemm_tn_f32(a, b, out, accumulate=False):
+    """out [N, K] (+)= a^T . b for fp32 a [M, N], b [M, K] (the reduction over the rows: a weight
+    gradient dY^T . X) on the dsvt fp32 MFMA GEMM -- the parity mode's dW (was
+    torch.mm): both operands transposed by the cast-transpose kernel into [., Mp] rows (M zero-padded
+    to the fp32 K step of 32), then out = A . W^T with A = a^T, W = b^T, accumulated in place through
+    the residual epilogue."""
+    _check(a, torch.float32, "a")
+    _check(b, torch.float32, "b")
+    _check(out, torch.float32, "out")
+    M, N = a.shape
+    K = b.shape[1]
+    if b.shape[0] != M or tuple(out.shape) != (N, K):
+        raise _lib.DsvtError("gemm_tn_f32: a %s, b %s, out %s do not match" % (tuple(a.shape), tuple(b.shape),
+                                                                               tuple(out.shape)))
+    Mp = (M + 31) // 32 * 32
+    if Mp != M:                          # zero rows: the padded K columns of the transposed operands
+        a = torch.cat([a, a.new_zeros(Mp - M, N)])
+        b = torch.cat([b, b.new_zeros(Mp - M, K)])
+    at = torch.empty(N, Mp, device=a.device, dtype=torch.float32)
+    bt = torch.empty(K, Mp, device=a.device, dtype=torch.float32)
+    cast_transpose(a, at)
+    cast_transpose(b, bt)
+    if accumulate:
+        return gemm_resid(at, bt, None, out, out)
+    return gemm(at, bt, None, out, out_f32=True)
+
+
 def cast_transpose(x, out):
     _check(x, torch.float32, "x")
     call("dsvt_cast_transpose", _dt(out.dtype), _ptr(x), _ptr(out), x.shape[0], x.shape[1], _stream())

@@ -87,7 +87,8 @@ def _wgrad(G, p, dy, x, bias=None, view=None):
         tdb = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32) if dbuf is not None else None
         ops.wgrad(dy, x, tmp, db=tdb)
     else:
-        tmp = torch.mm(dy.t(), x)
+        tmp = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
+        ops.gemm_tn_f32(dy, x, tmp)                            # fp32 parity mode: the dsvt fp32 GEMM
         tdb = None
         if dbuf is not None:
             tdb = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)

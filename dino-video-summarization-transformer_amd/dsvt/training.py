@@ -39,8 +39,8 @@ from ._lib import EPI_BIAS, EPI_BIAS_RESID, EPI_DGELU, EPI_GELU_SAVE, WS_ATTN_SP
 def wgrad(dy, x, G, p, view=None, bias=None):
     """grad(p) (+)= dy^T [N, M] . x [M, K] and, with `bias`, grad(bias) (+)= colsum(dy): the
     dsvt weight-gradient kernel in bf16 (fp32 results written / accumulated in place, the
-    column sum fused into it); the fp32 parity mode takes a plain library GEMM and the dsvt
-    column-sum kernel.  The first write of a gradient buffer is a copy (no zero fill)."""
+    column sum fused into it); the fp32 parity mode the dsvt fp32 MFMA GEMM (ops.gemm_tn_f32) and
+    the dsvt column-sum kernel.  The first write of a gradient buffer is a copy (no zero fill)."""
     buf, acc = G.acc(p)
     if view is not None:
         buf = buf.view(view)
@@ -53,11 +53,7 @@ def wgrad(dy, x, G, p, view=None, bias=None):
         if dy.dtype == torch.bfloat16:
             ops.wgrad(dy, x, buf, accumulate=acc, db=dbuf)
             return
-        r = torch.mm(dy.t(), x)
-        if acc:
-            buf.add_(r)
-        else:
-            buf.copy_(r)
+        ops.gemm_tn_f32(dy, x, buf, accumulate=acc)          # fp32 parity mode: the dsvt fp32 MFMA GEMM
         if dbuf is not None:
             ops.colsum(dy, dbuf, accumulate=acc)
     G.run_side(run, (dy, x))
@@ -1083,7 +1079,8 @@ def _head_backward(head, st, dlogits):
         dW = torch.empty(ll.out_features, ll.in_features, device=dev, dtype=torch.float32)
         ops.wgrad(dl, st.z, dW)                               # d(effective weight) [out, bottleneck]
     else:
-        dW = torch.mm(dl.t(), st.z)
+        dW = torch.empty(ll.out_features, ll.in_features, device=dev, dtype=torch.float32)
+        ops.gemm_tn_f32(dl, st.z, dW)
     ops.weight_norm_bwd(ll.weight_v.detach(), ll.weight_g.detach(), dW, G.acc(ll.weight_v)[0],
                         G.acc(ll.weight_g)[0].view(-1) if ll.weight_g.requires_grad else None, accumulate=False)
     if mode == torch.bfloat16:
@@ -1096,8 +1093,11 @@ def _head_backward(head, st, dlogits):
         dz = torch.empty(R8, ll.in_features, device=dev, dtype=torch.float32)
         ops.wgrad(dlT, st.wn, dz)
         dz = dz[:R]
-    else:
-        dz = torch.mm(dl, st.wn)                              # [R, bottleneck]
+    else:                                                     # dz [R, bottleneck] = dl . wn on the fp32 GEMM
+        wnT = torch.empty(st.wn.shape[1], st.wn.shape[0], device=dev, dtype=torch.float32)
+        ops.cast_transpose(st.wn.contiguous(), wnT)
+        dz = torch.empty(R, ll.in_features, device=dev, dtype=torch.float32)
+        ops.gemm(dl, wnT, None, dz, out_f32=True)
     dy = ops.head_norm_bwd(st.y, dz.contiguous())
     from .vision_transformer import bn_sync_group
     lins = _head_linears(head)
