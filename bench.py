@@ -292,6 +292,47 @@ def train_bench(args, device, rank, world, steps, warmup):
                                            "sequential after the student (RNG order)"}}
 
 
+def swin_train_bench(dtype, device, clips, steps, warmup):
+    """DINOTrainer steps with the Video Swin-T student / teacher (--arch swin)."""
+    from dsvt.loss import DINOLoss
+    from dsvt.models import SwinTransformer3D
+    from dsvt.trainer import DINOTrainer
+    from dsvt.utils import MultiCropWrapper
+    from dsvt.vision_transformer import DINOHead
+
+    def net():
+        bb = SwinTransformer3D(drop_path_rate=0.1)
+        hd = DINOHead(768, 65536, norm_last_layer=True)
+        bb.dsvt_dtype = hd.dsvt_dtype = dtype
+        return MultiCropWrapper(bb, hd).to(device)
+    torch.manual_seed(0)
+    student = net()
+    teacher = net()
+    teacher.load_state_dict(student.state_dict())
+    for p in teacher.parameters():
+        p.requires_grad_(False)
+    student.train()
+    teacher.eval()
+    loss_fn = DINOLoss(65536, 8, 0.04, 0.04, 0, 100).to(device)
+    trainer = DINOTrainer(student, teacher, loss_fn, niter_per_ep=1000, epochs=100, batch_size_per_gpu=clips,
+                          world_size=1)
+    crops = synthetic_crops(clips, device, seed=777)
+    for i in range(warmup):
+        trainer.step(crops, 2000 + i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = trainer.step(crops, 2000 + warmup + i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    lv = float(loss.item())
+    del trainer, student, teacher
+    return {"value": round(clips * steps / el, 3), "unit": "clips/s", "ms_per_step": round(el / steps * 1e3, 2),
+            "clips_per_step": clips, "steps": steps, "loss": round(lv, 5), "finite": bool(np.isfinite(lv)),
+            "crops": "2 x 8x224^2 + 6 x 8x96^2", "drop_path": 0.1,
+            "note": "Swin-T DINO SSL step (not a BASELINE metric); window-attention backward on the VALU"}
+
+
 # ----------------------------------------------------------------- configs 4 / 5: other backbones
 def joint_flops(T=16, S=224, C=768, depth=12, heads=12, mlp=4, patch=16, cls_tail=False):
     """ViT-B/16 joint space-time forward: 899.35 GFLOP at 16x224^2.  cls_tail: what
@@ -443,6 +484,12 @@ def other_configs(args, device):
                              "gflop_per_clip": round(swin_t_flops() / 1e9, 2),
                              "tflops": round(8 * swin_t_flops() / t / 1e12, 1)}
     del sm, xs
+    # the --arch swin SSL step (train_ssl.py:237-239 with the config-3 loop body): Swin-T student
+    # (DropPath 0.1 as the reference's swin default 0.2 is the Swin-B one) and teacher with the
+    # DINOHead(768, 65536), DINOLoss(ncrops 8), 8 clips of 2 global 8x224^2 + 6 local 8x96^2 crops --
+    # not a BASELINE metric: evidence that the Swin training path runs at full size
+    if not getattr(args, "no_swin_train", False):
+        res["config5_swin_t_train"] = swin_train_bench(dtype, device, clips=8, steps=3, warmup=1)
     # frame scoring (a18 / a19): one F = 64-frame 224^2 video, local 3 / global 30
     # views per frame (dino_similarity.py:66-93), pairwise DINO loss per frame
     from dsvt.scoring import FrameScorer
