@@ -330,7 +330,7 @@ def swin_train_bench(dtype, device, clips, steps, warmup):
     return {"value": round(clips * steps / el, 3), "unit": "clips/s", "ms_per_step": round(el / steps * 1e3, 2),
             "clips_per_step": clips, "steps": steps, "loss": round(lv, 5), "finite": bool(np.isfinite(lv)),
             "crops": "2 x 8x224^2 + 6 x 8x96^2", "drop_path": 0.1,
-            "note": "Swin-T DINO SSL step (not a BASELINE metric); window-attention backward on the VALU"}
+            "note": "Swin-T DINO SSL step (not a BASELINE metric; the --arch swin student)"}
 
 
 # ----------------------------------------------------------------- configs 4 / 5: other backbones
