@@ -182,6 +182,108 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
+// The narrow Video Swin widths (C = 96 / 192 / 384): LPR lanes per row, 64 / LPR rows per wave,
+// lane `sub` owns the VPL = C / LPR contiguous columns sub*VPL.. (8-byte loads, gamma held in
+// registers), the row sums over the LPR-lane group by xor shuffles, dgamma / dbeta partials in
+// registers per lane and combined over (wave, row group) in a fixed order through LDS.  One wave
+// per row (ln_bwd_wide_kernel at C = 96) left a third of the lanes idle and ran the four
+// reductions of each row one after another: ~270 us per call at Swin stage 1.
+template <typename DyT, int C, int LPR>
+__global__ __launch_bounds__(256) void ln_bwd_small_kernel(const float* __restrict__ x, const DyT* __restrict__ dy,
+                                                           const float* __restrict__ gamma, float* __restrict__ dx,
+                                                           int64_t rows, int64_t rpg, int64_t gstride, int64_t goff,
+                                                           float eps, float* __restrict__ partial) {
+  constexpr int VPL = C / LPR, RPW = 64 / LPR;
+  static_assert(C % LPR == 0 && VPL % 2 == 0 && 64 % LPR == 0, "row split");
+  __shared__ float red[4][RPW][2][C];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane % LPR, rsub = lane / LPR;
+  const int c0 = sub * VPL;
+  float gm[VPL], dg[VPL], db[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) { gm[i] = gamma[c0 + i]; dg[i] = 0.f; db[i] = 0.f; }
+  const int64_t step = (int64_t)gridDim.x * 4 * RPW;
+  for (int64_t rb = ((int64_t)blockIdx.x * 4 + wave) * RPW; rb < rows; rb += step) {
+    const int64_t r = rb + rsub;
+    const bool live = r < rows;                         // uniform over the lane's LPR group
+    const int64_t xr = live ? map_row(r, rpg, gstride, goff) * C : 0;
+    float v[VPL], d[VPL];
+    float s = 0.f;
+    if (live) {
+      const float2* xp = reinterpret_cast<const float2*>(x + xr + c0);
+#pragma unroll
+      for (int i = 0; i < VPL / 2; ++i) {
+        const float2 t = xp[i];
+        v[2 * i] = t.x; v[2 * i + 1] = t.y;
+        s += t.x + t.y;
+      }
+      if constexpr (sizeof(DyT) == 2) {
+        const unsigned* dp = reinterpret_cast<const unsigned*>(dy + r * C + c0);
+#pragma unroll
+        for (int i = 0; i < VPL / 2; ++i) {
+          const unsigned w = dp[i];
+          d[2 * i] = __uint_as_float(w << 16);
+          d[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+        }
+      } else {
+        const float2* dp = reinterpret_cast<const float2*>(dy + r * C + c0);
+#pragma unroll
+        for (int i = 0; i < VPL / 2; ++i) {
+          const float2 t = dp[i];
+          d[2 * i] = t.x; d[2 * i + 1] = t.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) { v[i] = 0.f; d[i] = 0.f; }
+    }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o);
+    const float mean = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) { v[i] -= mean; q += v[i] * v[i]; }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) q += __shfl_xor(q, o);
+    const float rstd = 1.0f / sqrtf(q / C + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const float xh = v[i] * rstd, gd = gm[i] * d[i];
+      v[i] = xh;
+      s1 += gd;
+      s2 += gd * xh;
+      dg[i] += d[i] * xh;
+      db[i] += d[i];
+    }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) { s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); }
+    s1 /= C;
+    s2 /= C;
+    if (live) {
+      float2* op = reinterpret_cast<float2*>(dx + xr + c0);
+#pragma unroll
+      for (int i = 0; i < VPL / 2; ++i) {
+        float2 t = op[i];
+        t.x += rstd * (gm[2 * i] * d[2 * i] - s1 - v[2 * i] * s2);
+        t.y += rstd * (gm[2 * i + 1] * d[2 * i + 1] - s1 - v[2 * i + 1] * s2);
+        op[i] = t;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) { red[wave][rsub][0][c0 + i] = dg[i]; red[wave][rsub][1][c0 + i] = db[i]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int k = 0; k < RPW; ++k) { a += red[w][k][0][c]; b += red[w][k][1][c]; }
+    partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+    partial[(int64_t)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
 // Any C % 32 == 0 up to 2048 (the Video Swin widths: 96 / 192 / 384 / 768, 128 ... 1024, and the
 // PatchMerging norms over 4C up to 2048): one wave per row, lane owns columns k*64 + lane.
 template <typename DyT>
@@ -406,6 +508,23 @@ hipError_t launch_ln_bwd(int dy_dtype, const float* x, const void* dy, const flo
 #define DSVT_LNB3(T) ln_bwd_kernel<T, true, 3><<<nb, 256, 0, s>>>(x, (const T*)dy, gamma, dx, rows, (int)C, rpg, \
                                                                   gstride, goff, eps, partial)
   const int lnb_v = lnb_variant();
+#define DSVT_LNBS(CC, LPR)                                                                                       \
+  {                                                                                                               \
+    if (dy_dtype == 0)                                                                                            \
+      ln_bwd_small_kernel<bf16_t, CC, LPR><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, rpg, gstride,  \
+                                                              goff, eps, partial);                                \
+    else                                                                                                          \
+      ln_bwd_small_kernel<float, CC, LPR><<<nb, 256, 0, s>>>(x, (const float*)dy, gamma, dx, rows, rpg, gstride,    \
+                                                             goff, eps, partial);                                 \
+    return hipGetLastError();                                                                                     \
+  }
+  // the narrow Video Swin widths (8-byte aligned rows)
+  if (((uintptr_t)x & 7) == 0 && ((uintptr_t)dx & 7) == 0 && ((uintptr_t)dy & 7) == 0) {
+    if (C == 96) DSVT_LNBS(96, 16)
+    if (C == 192) DSVT_LNBS(192, 16)
+    if (C == 384) DSVT_LNBS(384, 32)
+  }
+#undef DSVT_LNBS
   if (C == 768 && lnb_v == 2) {        // two rows of look-ahead: 2 blocks per CU (224 VGPRs)
     if (dy_dtype == 0)
       ln_bwd768_kernel<bf16_t><<<nb, 256, 0, s>>>(x, (const bf16_t*)dy, gamma, dx, rows, rpg, gstride, goff, eps, partial);
