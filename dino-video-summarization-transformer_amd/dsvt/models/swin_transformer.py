@@ -296,9 +296,10 @@ class _SwinCtx:
         if ent is None:
             b = torch.empty(attn.num_heads, N, N, device=self.device, dtype=torch.float32)
             ent = [None, b, None]
-            if self.mode == torch.bfloat16:
-                ent[2] = torch.empty(_lib_frag_floats(N, attn.num_heads), device=self.device, dtype=torch.float32)
             self.model._aux[key] = ent
+        if self.mode == torch.bfloat16 and ent[2] is None:     # first bf16 use (the entry may predate it)
+            ent[2] = torch.empty(_lib_frag_floats(N, attn.num_heads), device=self.device, dtype=torch.float32)
+            ent[0] = None
         if ent[0] != stamp:
             ops.relpos_bias(t.detach().contiguous(), attn.relative_position_index.contiguous(), N, ent[1])
             if ent[2] is not None:

@@ -172,6 +172,27 @@ def test_swin_merge_ln(dtype, C, H, W):
     assert err < (3e-5 if dtype == torch.float32 else 3e-2), err
 
 
+@pytest.mark.gpu
+def test_swin_dtype_switch_reuses_caches():
+    """A Swin model run in fp32, then switched to bf16 (its cache entries made under fp32 have no
+    fragment-order bias yet), then back: no error, bf16 within the bf16 bar of fp32, fp32 repeatable."""
+    from dsvt.models import SwinTransformer3D
+    torch.manual_seed(5)
+    m = SwinTransformer3D(**SMALL).cuda()
+    m.eval()                              # returns None, as the reference's
+    x = torch.randn(2, 3, 8, 64, 64, device="cuda")
+    with torch.no_grad():
+        m.dsvt_dtype = torch.float32
+        a = m(x).clone()
+        m.dsvt_dtype = torch.bfloat16
+        b = m(x).clone()
+        m.dsvt_dtype = torch.float32
+        c = m(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, c)
+    assert (a - b).abs().max().item() / a.abs().max().item() < 3e-2
+
+
 # ------------------------------------------------------------------------------ Swin training
 SWIN_TRAIN = dict(embed_dim=64, depths=[2, 2], num_heads=[2, 4])
 SWIN_TRAIN96 = dict(embed_dim=96, depths=[2], num_heads=[3])
