@@ -66,8 +66,17 @@ __global__ __launch_bounds__(256) void im2col3d_strip_kernel(const float* __rest
     if (z < D && y < H)
       v = *reinterpret_cast<const float4*>(x + ((((int64_t)b * Cin + c) * D + z) * H + y) * (int64_t)W + ow * 4);
     T* dst = tile + ow * ldl + tap * 4;
-    dst[0] = Elem<T>::from_f(v.x); dst[1] = Elem<T>::from_f(v.y);
-    dst[2] = Elem<T>::from_f(v.z); dst[3] = Elem<T>::from_f(v.w);
+#ifndef DSVT_I2C_VEC
+#define DSVT_I2C_VEC 1   // config 5: 8 217 / 8 181 / 8 196 vs 8 065 / 8 128 / 8 170 clips/s (tools/r6_g23.sh, same box)
+#endif
+    if constexpr (!DSVT_I2C_VEC) {
+      dst[0] = Elem<T>::from_f(v.x); dst[1] = Elem<T>::from_f(v.y);
+      dst[2] = Elem<T>::from_f(v.z); dst[3] = Elem<T>::from_f(v.w);
+    } else if constexpr (sizeof(T) == 2) {            // one 8-byte LDS write (ldl, 4 tap columns: aligned)
+      *reinterpret_cast<uint2*>(dst) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+    } else {
+      *reinterpret_cast<float4*>(dst) = v;
+    }
   }
   for (int e = threadIdx.x; e < Wo * (ldk - K); e += 256)    // zero K padding
     tile[(e / (ldk - K)) * ldl + K + e % (ldk - K)] = Elem<T>::from_f(0.f);
