@@ -235,7 +235,10 @@ hipError_t launch_swin_ln_rows(int dtype, const float* x, const int32_t* idx, co
   }
   // the small kernel stores column pairs: 4-byte bf16 / 8-byte fp32 aligned out
   if (((uintptr_t)x & 7) == 0 && ((uintptr_t)out & (dtype == 0 ? 3 : 7)) == 0 && ldo % 2 == 0) {
-    if (C == 96) DSVT_SLN(96, 16)
+#ifndef DSVT_SLN96_LPR
+#define DSVT_SLN96_LPR 8   // config 5: 8 139 / 8 144 / 8 160 vs 8 145 / 8 094 / 8 090 clips/s with 16 (tools/r6_g24.sh)
+#endif
+    if (C == 96) DSVT_SLN(96, DSVT_SLN96_LPR)
     if (C == 192) DSVT_SLN(192, 16)
     if (C == 384) DSVT_SLN(384, 32)
     if (C == 768) DSVT_SLN(768, 64)   // stage 4 and the final norm: 9.5 us per call on the wave-per-row kernel
