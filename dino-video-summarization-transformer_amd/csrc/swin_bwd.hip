@@ -431,7 +431,8 @@ __global__ __launch_bounds__(256) void relpos_bias_bwd_lds_kernel(const float* _
   if (e >= entries) return;
   const short es = (short)e;
   float s = 0.f;
-  for (int p = 0; p < nn8; p += 8) {
+#pragma unroll 4
+  for (int p = 0; p < nn8; p += 8) {               // (unrolled: four steps' LDS loads in flight)
     const uint4 iv = *reinterpret_cast<const uint4*>(si + p);
     const float4 va = *reinterpret_cast<const float4*>(sd + p);
     const float4 vb = *reinterpret_cast<const float4*>(sd + p + 4);
